@@ -1,0 +1,243 @@
+#!/usr/bin/env python3
+"""FM mini-batch SGD throughput on MI355X (BASELINE.json metric: train samples/s at k=16).
+
+One "step" = one fm_step over one device-resident synthetic mini-batch: forward + loss,
+stable sort of the entries by feature, segmented gradient reduction and the fused
+update + L1 over the model tables.  Workload (default) = config c3 of BASELINE.json:
+100M hashed features, k = 16, 256K rows per mini-batch (per GPU), 39 active entries per
+row (Criteo-shaped synthetic data); stepSize 0.1, regParam 1e-6.
+
+  python bench.py [--gpus N --steps K --warmup W]
+  python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (one rank per GPU)
+
+N = 1 runs the fused single-table path.  N > 1 row-shards the table (owner = id mod N) and
+exchanges ids / rows / gradients with RCCL all-to-all (weak scaling: every rank steps its own
+256K-row batch each iteration).  Rank 0 prints one JSON line.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+CONFIGS = {
+    # name: (num_features, k, rows per batch, zipf_s, description)
+    "c2": (1_000_000, 8, 65_536, 1.05, "synthetic Criteo-shaped 1M features, 39 nnz/row, k=8, batch 64K"),
+    "c3": (100_000_000, 16, 262_144, 1.05, "synthetic hashed 100M features, 39 nnz/row, k=16, batch 256K"),
+    "c4": (2_147_483_647, 32, 262_144, 1.05, "Int.MaxValue features, 39 nnz/row, k=32, batch 256K"),
+}
+STEP_SIZE = 0.1
+REG_PARAM = 1e-6
+INIT_SD = 0.01
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    p.add_argument("--batches", type=int, default=4, help="distinct resident mini-batches cycled through")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-steps", type=int, default=2)
+    p.add_argument("--profile-kernels", type=int, default=1, help="HIP-event timing of each kernel phase")
+    return p.parse_args()
+
+
+def log(msg):
+    print(msg, file=sys.stderr, flush=True)
+
+
+def algorithmic_bytes(F, k, B, z, U):
+    """A = 8z + 12 + 4z(k+1) + 8(k+1) U/B bytes per sample, split by kernel."""
+    fwd = B * (8 * z + 12 + 4 * z * (k + 1))  # CSR col+val, row_ptr+label, gather of w+V
+    upd = 8 * (k + 1) * U  # read + write of every touched row
+    return fwd, upd
+
+
+def cpu_baseline(cfg, batch, steps):
+    """The fp64 C restatement (oracle/fm_oracle.c, OpenMP) timed on this host's cores on a
+    bounded sample of the same workload: `steps` mini-batch steps over the full table."""
+    import ctypes as C
+
+    from oracle import oracle_c
+
+    F, k, B, _, _ = cfg
+    lib = oracle_c.load()
+    threads = oracle_c.threads(lib)
+    m = oracle_c.create(lib, F, k)
+    try:
+        t0 = time.perf_counter()
+        lib.oracle_init_random(m, 12345, INIT_SD, 0, F)
+        t_init = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        for i in range(steps):
+            oracle_c.step(lib, m, batch, i + 1, STEP_SIZE, REG_PARAM)
+        dt = time.perf_counter() - t0
+    finally:
+        lib.oracle_destroy(m)
+    return {
+        "value": steps * B / dt,
+        "unit": "samples/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{steps} mini-batch steps x {B} rows on the full F={F} k={k} table (fp64, eager L1 over "
+                  f"every row as the reference; init {t_init:.1f}s excluded), oracle/fm_oracle.c",
+    }
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            log(f"--gpus {args.gpus} needs torch.distributed.run (one rank per GPU); running 1 rank")
+        args.gpus = world
+    import torch
+    import torch.distributed as dist
+
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    from fm_spark_amd.data import synthetic_batch
+    from fm_spark_amd.engine import FMContext
+    from fm_spark_amd._native import CSRHost
+
+    cfg = CONFIGS[args.config]
+    F, k, B, zipf_s, desc = cfg
+    t0 = time.perf_counter()
+    host_batches = [synthetic_batch(B, F, batch_index=rank * 1000 + i, zipf_s=zipf_s) for i in range(args.batches)]
+    log(f"[rank {rank}] generated {args.batches} batches in {time.perf_counter() - t0:.1f}s")
+    z = host_batches[0].nnz / B
+
+    if world == 1:
+        ctx = FMContext(F, k, device=local_rank, seed=20261015, init_sd=INIT_SD)
+        ctx.init_random_range(0, F)
+        dbatches = [ctx.batch(CSRHost(b.row_ptr, b.col, b.val, b.label)) for b in host_batches]
+        ctx.reserve(B, max(b.nnz for b in host_batches))
+        uniques = {}
+        t = 0
+        for i in range(args.warmup):
+            t += 1
+            o = ctx.step_batch(dbatches[i % len(dbatches)], t, STEP_SIZE, REG_PARAM, sync=True)
+            uniques[i % len(dbatches)] = o.n_unique
+        for j in range(len(dbatches)):
+            if j not in uniques:  # count U for every batch (untimed)
+                t += 1
+                uniques[j] = ctx.step_batch(dbatches[j], t, STEP_SIZE, REG_PARAM, sync=True).n_unique
+        torch.cuda.synchronize()
+        ctx.sync()
+        if args.profile_kernels:
+            ctx.profile_reset()
+            ctx.profile_enable(True)
+        t_start = time.perf_counter()
+        for i in range(args.steps):
+            t += 1
+            ctx.step_batch(dbatches[i % len(dbatches)], t, STEP_SIZE, REG_PARAM, sync=False)
+        ctx.sync()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t_start
+        prof = ctx.profile_read() if args.profile_kernels else {}
+        ctx.profile_enable(False)
+        losses = ctx.loss_history()
+        assert np.all(np.isfinite(losses)), "non-finite loss"
+        U_mean = float(np.mean([uniques[i % len(dbatches)] for i in range(args.steps)]))
+        parallelism = "single table"
+    else:
+        from fm_spark_amd.distributed import ShardedTrainer
+
+        tr = ShardedTrainer(F, k, rank=rank, world=world, device=local_rank, seed=20261015, init_sd=INIT_SD)
+        tr.init_random_range(0, F)
+        dbatches = [tr.batch(CSRHost(b.row_ptr, b.col, b.val, b.label)) for b in host_batches]
+        t = 0
+        uniques = []
+        for i in range(args.warmup):
+            t += 1
+            o = tr.step(dbatches[i % len(dbatches)], t, STEP_SIZE, REG_PARAM)
+            uniques.append(o.n_unique)
+        torch.cuda.synchronize()
+        dist.barrier()
+        if args.profile_kernels:
+            tr.ctx.profile_reset()
+            tr.ctx.profile_enable(True)
+        t_start = time.perf_counter()
+        for i in range(args.steps):
+            t += 1
+            tr.step(dbatches[i % len(dbatches)], t, STEP_SIZE, REG_PARAM, sync=False)
+        tr.ctx.sync()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t_start
+        prof = tr.ctx.profile_read() if args.profile_kernels else {}
+        U_mean = float(np.mean(uniques)) if uniques else 0.0
+        parallelism = f"row-sharded x{world} (RCCL all-to-all)"
+
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+        dist.barrier()
+
+    if rank == 0:
+        ms_per_step = 1000.0 * elapsed / args.steps
+        value = world * B * args.steps / elapsed
+        fwd_b, upd_b = algorithmic_bytes(F, k, B, z, U_mean)
+        line = {
+            "metric": "FM SGD train samples/sec at k=16, 1/8 GPUs; % of HBM roofline" if k == 16 else
+                      f"FM SGD train samples/sec at k={k}",
+            "value": value,
+            "unit": "samples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (Criteo-shaped, Zipf(%.2f) hashed ids, seed 20261015), random-init tables" % zipf_s,
+            "config": {"workload": f"{args.config}: {desc}", "num_features": F, "k": k, "batch_rows_per_gpu": B,
+                       "global_batch": B * world, "nnz_per_row": z, "unique_ids_per_batch": U_mean,
+                       "step_size": STEP_SIZE, "reg_param": REG_PARAM, "parallelism": parallelism},
+        }
+        if prof:
+            kern = {name: {"avg_ms": ms / max(n, 1), "launches": n} for name, (ms, n) in prof.items()}
+            line["kernels"] = kern
+            algo = {"forward": fwd_b, "update": upd_b}
+            dom = max(kern, key=lambda n: kern[n]["avg_ms"])
+            if dom == "sort":
+                # the sort moves keys+payloads: per pass 4 B (count) + 8 B read + 8 B write per entry
+                passes = max(1, math.ceil(math.log2(max(F // world, 2)) / 8))
+                algo["sort"] = passes * 20 * z * B
+            ach = algo.get(dom, 0.0) / (kern[dom]["avg_ms"] * 1e-3) / 1e9
+            line["roofline"] = {"bound": "hbm", "kernel": dom, "achieved": ach, "peak": HBM_PEAK_GBS,
+                                "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "traffic": None}
+            step_bytes = fwd_b + upd_b
+            line["step_roofline"] = {"bytes_per_step": step_bytes,
+                                     "achieved_GBs": step_bytes / (ms_per_step * 1e-3) / 1e9,
+                                     "frac": step_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS}
+        if not args.no_cpu_baseline:
+            try:
+                line["cpu_baseline"] = cpu_baseline(cfg, host_batches[0], args.cpu_steps)
+            except Exception as e:  # reported, never silently replaced
+                line["cpu_baseline"] = {"value": None, "error": repr(e)}
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,59 @@
+"""Build libfm_hip.so (HIP for gfx950) in-tree with hipcc.  No JIT cache, no setuptools:
+the .so lands in fm_spark_amd/lib/ so it travels with the repo snapshot to the GPU box."""
+
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+CSRC = PKG / "csrc"
+LIB_DIR = PKG / "lib"
+LIB = LIB_DIR / "libfm_hip.so"
+INCLUDE = PKG.parent / "include"
+ARCH = os.environ.get("FM_HIP_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+SOURCES = ["fm_kernels.hip", "fm_sort.hip", "fm_capi.hip", "fm_shard.hip", "fm_sampler.cpp"]
+HEADERS = ["fm_internal.h"]
+
+CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function", "-Wno-unused-variable"]
+
+
+def _newer(target: Path, deps) -> bool:
+    if not target.exists():
+        return True
+    t = target.stat().st_mtime
+    return any(Path(d).stat().st_mtime > t for d in deps)
+
+
+def build(verbose: bool = False, force: bool = False) -> Path:
+    LIB_DIR.mkdir(parents=True, exist_ok=True)
+    objdir = LIB_DIR / "obj"
+    objdir.mkdir(exist_ok=True)
+    headers = [CSRC / h for h in HEADERS] + [INCLUDE / "fm_hip.h"]
+    objs = []
+    for src in SOURCES:
+        s = CSRC / src
+        o = objdir / (src + ".o")
+        objs.append(o)
+        if force or _newer(o, [s, *headers]):
+            if src.endswith(".hip"):
+                cmd = [HIPCC, f"--offload-arch={ARCH}", *CXXFLAGS, "-c", str(s), "-o", str(o)]
+            else:
+                cmd = [HIPCC, *CXXFLAGS, "-x", "c++", "-c", str(s), "-o", str(o)]
+            if verbose:
+                print(" ".join(cmd), file=sys.stderr)
+            subprocess.run(cmd, check=True)
+    if force or _newer(LIB, objs):
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", str(LIB)]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.run(cmd, check=True)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(verbose=True, force="--force" in sys.argv))

@@ -1,0 +1,739 @@
+// C-ABI implementation of include/fm_hip.h: contexts, device tables, mini-batch upload,
+// the step driver (forward -> sort -> segmented update) and the table import/export.
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <utility>
+
+#include "fm_internal.h"
+
+namespace fmhip {
+
+static thread_local std::string g_last_error;
+void set_error(const std::string& msg) { g_last_error = msg; }
+
+void DevBuf::ensure(size_t n) {
+  if (n <= bytes && p) return;
+  release();
+  if (n == 0) n = 16;
+  FM_HIP_CHECK(hipMalloc(&p, n));
+  bytes = n;
+}
+
+void DevBuf::release() {
+  if (p) (void)hipFree(p);
+  p = nullptr;
+  bytes = 0;
+}
+
+// Pinned host staging for small device->host reads.
+struct Pinned {
+  void* p = nullptr;
+  size_t bytes = 0;
+  void ensure(size_t n) {
+    if (n <= bytes && p) return;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    FM_HIP_CHECK(hipHostMalloc(&p, n, hipHostMallocDefault));
+    bytes = n;
+  }
+  ~Pinned() {
+    if (p) (void)hipHostFree(p);
+  }
+};
+
+struct ProfEntry {
+  double ms = 0.0;
+  int64_t n = 0;
+};
+
+}  // namespace fmhip
+
+using namespace fmhip;
+
+struct fm_batch {
+  fm_ctx* owner = nullptr;
+  int device = 0;
+  BatchDev dev;
+  int64_t max_id = -1;
+  ~fm_batch() {
+    (void)hipSetDevice(device);
+    dev.row_ptr.release();
+    dev.col.release();
+    dev.val.release();
+    dev.label.release();
+  }
+};
+
+struct fm_ctx {
+  std::mutex mu;
+  fm_config cfg{};
+  int32_t kp = 0;
+  int64_t rows = 0;  // local rows
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  DevBuf wt, V;
+  DevBuf cum;  // [cum_cap] double
+  int64_t cum_cap = 0;
+  std::vector<double> cum_host{0.0};
+  int32_t epoch = 0;
+  DevBuf loss_hist;  // [hist_cap][3] double {loss, n_loss, n_unique}
+  int64_t hist_cap = 0;
+  StepWork work;
+  Pinned pinned;
+  // profiling
+  bool prof = false;
+  std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> pending;
+  std::vector<hipEvent_t> free_events;
+  std::map<std::string, ProfEntry> prof_acc;
+  std::vector<std::string> prof_order;
+  // sharded step state
+  DevBuf plan_req;      // [U] int32 local slots, owner-major
+  DevBuf plan_uidx;     // [N] uint32 unique index per entry (CSR order)
+  DevBuf plan_ukey;     // [U] uint32 composite keys (sorted)
+  DevBuf plan_counts;   // [shard_count] int64
+  DevBuf rows_local;    // scratch
+  int64_t plan_unique = 0;
+  int64_t plan_nnz = 0;
+  double last_loss = 0.0;
+  int64_t last_nloss = 0;
+
+  TableView view() const {
+    TableView T;
+    T.wt = wt.as<WT>();
+    T.V = V.as<float>();
+    T.cum = cum.as<double>();
+    T.rows = rows;
+    T.k = cfg.k;
+    T.kp = kp;
+    T.shard_count = cfg.shard_count;
+    T.shard_index = cfg.shard_index;
+    return T;
+  }
+
+  hipEvent_t get_event() {
+    if (!free_events.empty()) {
+      hipEvent_t e = free_events.back();
+      free_events.pop_back();
+      return e;
+    }
+    hipEvent_t e;
+    FM_HIP_CHECK(hipEventCreate(&e));
+    return e;
+  }
+
+  // RAII-free helpers: begin() records a start event, end() the stop event for `name`.
+  hipEvent_t prof_begin() {
+    if (!prof) return nullptr;
+    hipEvent_t e = get_event();
+    FM_HIP_CHECK(hipEventRecord(e, stream));
+    return e;
+  }
+  void prof_end(const char* name, hipEvent_t e0) {
+    if (!prof || !e0) return;
+    hipEvent_t e1 = get_event();
+    FM_HIP_CHECK(hipEventRecord(e1, stream));
+    pending.push_back({name, {e0, e1}});
+    if (pending.size() > 4096) resolve_profile();
+  }
+  void resolve_profile() {
+    if (pending.empty()) return;
+    FM_HIP_CHECK(hipStreamSynchronize(stream));
+    for (auto& pe : pending) {
+      float ms = 0.f;
+      FM_HIP_CHECK(hipEventElapsedTime(&ms, pe.second.first, pe.second.second));
+      auto it = prof_acc.find(pe.first);
+      if (it == prof_acc.end()) {
+        prof_order.push_back(pe.first);
+        it = prof_acc.emplace(pe.first, ProfEntry{}).first;
+      }
+      it->second.ms += ms;
+      it->second.n += 1;
+      free_events.push_back(pe.second.first);
+      free_events.push_back(pe.second.second);
+    }
+    pending.clear();
+  }
+
+  void ensure_cum(int64_t need) {
+    if (need <= cum_cap) return;
+    int64_t c = std::max<int64_t>(4096, cum_cap);
+    while (c < need) c *= 2;
+    FM_HIP_CHECK(hipStreamSynchronize(stream));
+    cum.ensure(sizeof(double) * c);
+    cum_cap = c;
+    std::vector<double> tmp(c, 0.0);
+    std::copy(cum_host.begin(), cum_host.end(), tmp.begin());
+    FM_HIP_CHECK(hipMemcpy(cum.p, tmp.data(), sizeof(double) * c, hipMemcpyHostToDevice));
+  }
+
+  void ensure_hist(int64_t need) {
+    if (need <= hist_cap) return;
+    int64_t c = std::max<int64_t>(4096, hist_cap);
+    while (c < need) c *= 2;
+    FM_HIP_CHECK(hipStreamSynchronize(stream));
+    DevBuf nb;
+    nb.ensure(sizeof(double) * 3 * c);
+    FM_HIP_CHECK(hipMemset(nb.p, 0, sizeof(double) * 3 * c));
+    if (hist_cap > 0)
+      FM_HIP_CHECK(hipMemcpy(nb.p, loss_hist.p, sizeof(double) * 3 * hist_cap, hipMemcpyDeviceToDevice));
+    loss_hist.release();
+    loss_hist = nb;
+    nb.p = nullptr;
+    hist_cap = c;
+  }
+
+  ~fm_ctx() {
+    (void)hipSetDevice(cfg.device);
+    if (stream) (void)hipStreamSynchronize(stream);
+    for (auto& pe : pending) {
+      (void)hipEventDestroy(pe.second.first);
+      (void)hipEventDestroy(pe.second.second);
+    }
+    for (auto e : free_events) (void)hipEventDestroy(e);
+    wt.release();
+    V.release();
+    cum.release();
+    loss_hist.release();
+    DevBuf* bufs[] = {&work.S, &work.yl, &work.rec, &work.loss_part, &work.part, &work.stats,
+                      &work.sort.keys_a, &work.sort.keys_b, &work.sort.vals_a, &work.sort.vals_b,
+                      &work.sort.counts, &work.sort.digit_tot, &plan_req, &plan_uidx, &plan_ukey,
+                      &plan_counts, &rows_local};
+    for (auto* b : bufs) b->release();
+    if (own_stream && stream) (void)hipStreamDestroy(stream);
+  }
+};
+
+namespace {
+
+template <class F>
+int guarded(fm_ctx* ctx, F&& f) {
+  if (!ctx) {
+    set_error("null fm_ctx");
+    return FM_ERR_ARG;
+  }
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  try {
+    FM_HIP_CHECK(hipSetDevice(ctx->cfg.device));
+    return f();
+  } catch (const Error& e) {
+    set_error(e.msg);
+    return e.code;
+  } catch (const std::bad_alloc&) {
+    set_error("host allocation failed");
+    return FM_ERR_OOM;
+  } catch (const std::exception& e) {
+    set_error(e.what());
+    return FM_ERR_HIP;
+  } catch (...) {
+    set_error("unknown error");
+    return FM_ERR_HIP;
+  }
+}
+
+template <class F>
+int guarded_free(F&& f) {
+  try {
+    return f();
+  } catch (const Error& e) {
+    set_error(e.msg);
+    return e.code;
+  } catch (const std::bad_alloc&) {
+    set_error("host allocation failed");
+    return FM_ERR_OOM;
+  } catch (const std::exception& e) {
+    set_error(e.what());
+    return FM_ERR_HIP;
+  } catch (...) {
+    set_error("unknown error");
+    return FM_ERR_HIP;
+  }
+}
+
+int bits_for(int64_t max_value) {
+  int b = 1;
+  while (b < 63 && (int64_t(1) << b) <= max_value) ++b;
+  return b;
+}
+
+// Validates and uploads a host CSR.  check_range: ids must be owned by this context's
+// table (training); otherwise any non-negative int32 id is accepted (predict drops
+// unknown ids).
+void upload_batch(fm_ctx* ctx, const fm_csr* c, fm_batch* b, bool check_range) {
+  FM_REQUIRE(c != nullptr, "null fm_csr");
+  FM_REQUIRE(c->n_rows >= 0 && c->nnz >= 0, "negative n_rows / nnz");
+  FM_REQUIRE(c->n_rows < (int64_t(1) << 31), "n_rows must be < 2^31");
+  FM_REQUIRE(c->nnz < (int64_t(1) << 31), "nnz must be < 2^31 per batch");
+  FM_REQUIRE(c->n_rows == 0 || (c->row_ptr && c->label), "null row_ptr / label");
+  FM_REQUIRE(c->nnz == 0 || (c->col && c->val), "null col / val");
+  const int64_t B = c->n_rows, N = c->nnz;
+  if (B > 0) {
+    FM_REQUIRE(c->row_ptr[0] == 0, "row_ptr[0] must be 0");
+    FM_REQUIRE(c->row_ptr[B] == N, "row_ptr[n_rows] must equal nnz");
+    for (int64_t i = 0; i < B; ++i) FM_REQUIRE(c->row_ptr[i] <= c->row_ptr[i + 1], "row_ptr must be non-decreasing");
+  } else {
+    FM_REQUIRE(N == 0, "nnz > 0 with n_rows == 0");
+  }
+  std::vector<uint32_t> col(N);
+  std::vector<float> val(N), lab(B);
+  int64_t mx = -1;
+  const int64_t F = ctx->cfg.num_features;
+  for (int64_t e = 0; e < N; ++e) {
+    const int32_t id = c->col[e];
+    FM_REQUIRE(id >= 0, "negative feature id");
+    if (check_range) {
+      FM_REQUIRE(id < F, "feature id >= num_features");
+    }
+    col[e] = (uint32_t)id;
+    mx = std::max<int64_t>(mx, id);
+    val[e] = (float)c->val[e];
+  }
+  for (int64_t i = 0; i < B; ++i) lab[i] = (float)c->label[i];
+  b->owner = ctx;
+  b->device = ctx->cfg.device;
+  b->max_id = mx;
+  b->dev.n_rows = B;
+  b->dev.nnz = N;
+  b->dev.row_ptr.ensure(sizeof(int64_t) * (B + 1));
+  b->dev.col.ensure(sizeof(uint32_t) * std::max<int64_t>(N, 4) + 16);
+  b->dev.val.ensure(sizeof(float) * std::max<int64_t>(N, 4) + 16);
+  b->dev.label.ensure(sizeof(float) * std::max<int64_t>(B, 4) + 16);
+  if (B > 0) FM_HIP_CHECK(hipMemcpy(b->dev.row_ptr.p, c->row_ptr, sizeof(int64_t) * (B + 1), hipMemcpyHostToDevice));
+  else {
+    const int64_t z = 0;
+    FM_HIP_CHECK(hipMemcpy(b->dev.row_ptr.p, &z, sizeof(int64_t), hipMemcpyHostToDevice));
+  }
+  if (N > 0) {
+    FM_HIP_CHECK(hipMemcpy(b->dev.col.p, col.data(), sizeof(uint32_t) * N, hipMemcpyHostToDevice));
+    FM_HIP_CHECK(hipMemcpy(b->dev.val.p, val.data(), sizeof(float) * N, hipMemcpyHostToDevice));
+  }
+  if (B > 0) FM_HIP_CHECK(hipMemcpy(b->dev.label.p, lab.data(), sizeof(float) * B, hipMemcpyHostToDevice));
+}
+
+void reserve_work(fm_ctx* ctx, int64_t B, int64_t N) {
+  StepWork& w = ctx->work;
+  w.S.ensure(sizeof(float) * (size_t)std::max<int64_t>(B, 1) * ctx->kp);
+  w.yl.ensure(sizeof(float) * 2 * (size_t)std::max<int64_t>(B, 1));
+  w.rec.ensure(sizeof(int32_t) * 2 * (size_t)std::max<int64_t>(N, 1));
+  w.sort.ensure(std::max<int64_t>(N, 1));
+  const int64_t nchunks = (N + 63) / 64;
+  w.part.ensure(sizeof(double) * (size_t)std::max<int64_t>(nchunks, 1) * 2 * (ctx->kp + 1));
+  w.stats.ensure(64);
+  w.loss_part.ensure(sizeof(double) * 2 * 256 * 8);
+}
+
+int step_impl(fm_ctx* ctx, const fm_batch* b, int32_t t, double step_size, double reg_param, fm_step_out* out) {
+  FM_REQUIRE(b != nullptr, "null batch");
+  FM_REQUIRE(b->owner == ctx, "batch belongs to another context");
+  FM_REQUIRE(ctx->cfg.shard_count == 1, "sharded contexts step through the fm_shard_* entry points");
+  if (b->dev.n_rows == 0) return FM_NOTHING_TO_DO;  // SGD.scala:126-128
+  FM_REQUIRE(t >= 1, "iteration index t must be >= 1");
+  FM_REQUIRE(std::isfinite(step_size) && std::isfinite(reg_param), "non-finite step size / regParam");
+  const int64_t B = b->dev.n_rows, N = b->dev.nnz;
+  reserve_work(ctx, B, N);
+  ctx->ensure_cum(ctx->epoch + 2);
+  ctx->ensure_hist(ctx->epoch + 1);
+  StepParams p;
+  p.n_rows = B;
+  p.eta = step_size / std::sqrt((double)t);  // SGD.scala:121
+  p.lam = p.eta * reg_param;                 // SGD.scala:122
+  p.m = (double)B;                           // miniBatchSize, SGD.scala:124
+  p.scale_v = p.eta / (double)B;             // currentStepSize / miniBatchSize, SGD.scala:153
+  p.epoch = ctx->epoch;
+  p.cum_next = ctx->cum_host.back() + p.lam;
+  p.w0 = ctx->cfg.w0;
+  const TableView T = ctx->view();
+  int64_t nfwd = 0;
+  hipEvent_t e0 = ctx->prof_begin();
+  launch_forward(T, b->dev, ctx->work, p, ctx->stream, &nfwd);
+  ctx->prof_end("forward", e0);
+  e0 = ctx->prof_begin();
+  const uint32_t *skeys = nullptr, *svals = nullptr;
+  radix_sort_pairs(ctx->work.sort, b->dev.col.as<uint32_t>(), nullptr, N, bits_for(ctx->rows - 1), ctx->stream,
+                   &skeys, &svals);
+  ctx->prof_end("sort", e0);
+  e0 = ctx->prof_begin();
+  double* stats = ctx->loss_hist.as<double>() + 3 * (int64_t)ctx->epoch;
+  launch_segment_update(T, b->dev, ctx->work, p, skeys, svals, nfwd, ctx->cum.as<double>(), stats, ctx->stream);
+  ctx->prof_end("update", e0);
+  ctx->epoch += 1;
+  ctx->cum_host.push_back(p.cum_next);
+  if (out) {
+    ctx->pinned.ensure(64);
+    FM_HIP_CHECK(hipMemcpyAsync(ctx->pinned.p, stats, sizeof(double) * 3, hipMemcpyDeviceToHost, ctx->stream));
+    FM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    const double* h = reinterpret_cast<const double*>(ctx->pinned.p);
+    out->loss_sum = h[0];
+    out->n_loss_rows = (int64_t)h[1];
+    out->n_unique = (int64_t)h[2];
+    out->n_rows = B;
+  }
+  return FM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* fm_last_error(void) { return g_last_error.c_str(); }
+
+int fm_create(const fm_config* cfg, fm_ctx** out) {
+  return guarded_free([&]() -> int {
+    FM_REQUIRE(cfg && out, "null argument");
+    FM_REQUIRE(cfg->num_features >= 1 && cfg->num_features <= (int64_t(1) << 31), "num_features must be in [1, 2^31]");
+    FM_REQUIRE(cfg->k >= 1 && cfg->k <= 256, "dimFactorization must be in [1, 256]");
+    FM_REQUIRE(cfg->shard_count >= 1 && cfg->shard_index >= 0 && cfg->shard_index < cfg->shard_count,
+               "bad shard_index / shard_count");
+    FM_REQUIRE(cfg->init_sd >= 0.0, "init_sd must be >= 0");
+    int ndev = 0;
+    FM_HIP_CHECK(hipGetDeviceCount(&ndev));
+    FM_REQUIRE(cfg->device >= 0 && cfg->device < ndev, "device ordinal out of range");
+    FM_HIP_CHECK(hipSetDevice(cfg->device));
+    std::unique_ptr<fm_ctx> c(new fm_ctx());
+    c->cfg = *cfg;
+    c->kp = (cfg->k + 3) / 4 * 4;
+    c->rows = (cfg->num_features - cfg->shard_index + cfg->shard_count - 1) / cfg->shard_count;
+    FM_HIP_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    c->own_stream = true;
+    c->wt.ensure(sizeof(WT) * (size_t)std::max<int64_t>(c->rows, 1));
+    c->V.ensure(sizeof(float) * (size_t)std::max<int64_t>(c->rows, 1) * c->kp);
+    c->ensure_cum(4096);
+    c->ensure_hist(4096);
+    launch_table_reset(c->view(), c->stream);
+    FM_HIP_CHECK(hipStreamSynchronize(c->stream));
+    *out = c.release();
+    return FM_OK;
+  });
+}
+
+void fm_destroy(fm_ctx* ctx) {
+  if (!ctx) return;
+  try {
+    delete ctx;
+  } catch (...) {
+  }
+}
+
+int fm_set_stream(fm_ctx* ctx, void* s) {
+  return guarded(ctx, [&]() -> int {
+    FM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    if (ctx->own_stream && ctx->stream) FM_HIP_CHECK(hipStreamDestroy(ctx->stream));
+    if (s) {
+      ctx->stream = reinterpret_cast<hipStream_t>(s);
+      ctx->own_stream = false;
+    } else {
+      FM_HIP_CHECK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+      ctx->own_stream = true;
+    }
+    return FM_OK;
+  });
+}
+
+int fm_sync(fm_ctx* ctx) {
+  return guarded(ctx, [&]() -> int {
+    FM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    return FM_OK;
+  });
+}
+
+int fm_reserve(fm_ctx* ctx, int64_t max_rows, int64_t max_nnz) {
+  return guarded(ctx, [&]() -> int {
+    FM_REQUIRE(max_rows >= 0 && max_nnz >= 0, "negative reserve");
+    reserve_work(ctx, max_rows, max_nnz);
+    return FM_OK;
+  });
+}
+
+int fm_load_tables(fm_ctx* ctx, const int32_t* ids, int64_t n, const double* w, const double* V) {
+  return guarded(ctx, [&]() -> int {
+    FM_REQUIRE(n >= 0, "negative n");
+    if (n == 0) return FM_OK;
+    FM_REQUIRE(ids && w && V, "null argument");
+    for (int64_t i = 0; i < n; ++i)
+      FM_REQUIRE(ids[i] >= 0 && ids[i] < ctx->cfg.num_features, "id out of [0, num_features)");
+    DevBuf di, dw, dv;
+    di.ensure(sizeof(int32_t) * n);
+    dw.ensure(sizeof(double) * n);
+    dv.ensure(sizeof(double) * n * ctx->cfg.k);
+    FM_HIP_CHECK(hipMemcpy(di.p, ids, sizeof(int32_t) * n, hipMemcpyHostToDevice));
+    FM_HIP_CHECK(hipMemcpy(dw.p, w, sizeof(double) * n, hipMemcpyHostToDevice));
+    FM_HIP_CHECK(hipMemcpy(dv.p, V, sizeof(double) * n * ctx->cfg.k, hipMemcpyHostToDevice));
+    launch_load_rows(ctx->view(), di.as<int32_t>(), n, dw.as<double>(), dv.as<double>(), ctx->epoch, ctx->stream);
+    FM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    di.release();
+    dw.release();
+    dv.release();
+    return FM_OK;
+  });
+}
+
+int fm_init_random(fm_ctx* ctx, const int32_t* ids, int64_t n) {
+  return guarded(ctx, [&]() -> int {
+    FM_REQUIRE(n >= 0, "negative n");
+    if (n == 0) return FM_OK;
+    FM_REQUIRE(ids, "null ids");
+    for (int64_t i = 0; i < n; ++i)
+      FM_REQUIRE(ids[i] >= 0 && ids[i] < ctx->cfg.num_features, "id out of [0, num_features)");
+    DevBuf di;
+    di.ensure(sizeof(int32_t) * n);
+    FM_HIP_CHECK(hipMemcpy(di.p, ids, sizeof(int32_t) * n, hipMemcpyHostToDevice));
+    launch_init_random(ctx->view(), di.as<int32_t>(), n, 0, ctx->cfg.seed, ctx->cfg.init_sd, ctx->epoch, ctx->stream);
+    FM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    di.release();
+    return FM_OK;
+  });
+}
+
+int fm_init_random_range(fm_ctx* ctx, int64_t b, int64_t e) {
+  return guarded(ctx, [&]() -> int {
+    FM_REQUIRE(b >= 0 && e >= b && e <= ctx->cfg.num_features, "bad id range");
+    launch_init_random(ctx->view(), nullptr, e - b, b, ctx->cfg.seed, ctx->cfg.init_sd, ctx->epoch, ctx->stream);
+    FM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    return FM_OK;
+  });
+}
+
+int64_t fm_num_present(fm_ctx* ctx) {
+  int64_t n = -1;
+  int rc = guarded(ctx, [&]() -> int {
+    DevBuf d;
+    d.ensure(sizeof(int64_t));
+    launch_count_present(ctx->view(), d.as<int64_t>(), ctx->stream);
+    FM_HIP_CHECK(hipMemcpyAsync(&n, d.p, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+    FM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    d.release();
+    return FM_OK;
+  });
+  return rc == FM_OK ? n : rc;
+}
+
+int64_t fm_epoch(fm_ctx* ctx) { return ctx ? ctx->epoch : -1; }
+
+int fm_export_tables(fm_ctx* ctx, int32_t* ids, double* w, double* V, int64_t cap, int64_t* n) {
+  return guarded(ctx, [&]() -> int {
+    FM_REQUIRE(n != nullptr && cap >= 0, "bad arguments");
+    launch_flush(ctx->view(), ctx->epoch, ctx->stream);  // apply pending L1 to every row
+    std::vector<WT> hw(ctx->rows);
+    FM_HIP_CHECK(hipMemcpyAsync(hw.data(), ctx->wt.p, sizeof(WT) * ctx->rows, hipMemcpyDeviceToHost, ctx->stream));
+    FM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    int64_t cnt = 0;
+    for (int64_t i = 0; i < ctx->rows; ++i) cnt += hw[i].t >= 0;
+    *n = cnt;
+    if (cap == 0) return FM_OK;
+    FM_REQUIRE(cap >= cnt && ids && w && V, "export buffers too small or null");
+    const int k = ctx->cfg.k, kp = ctx->kp;
+    const int64_t chunk_rows = 1 << 20;
+    std::vector<float> hv;
+    int64_t o = 0;
+    for (int64_t r0 = 0; r0 < ctx->rows; r0 += chunk_rows) {
+      const int64_t r1 = std::min(ctx->rows, r0 + chunk_rows);
+      bool any = false;
+      for (int64_t i = r0; i < r1 && !any; ++i) any = hw[i].t >= 0;
+      if (!any) continue;
+      hv.resize((size_t)(r1 - r0) * kp);
+      FM_HIP_CHECK(hipMemcpy(hv.data(), ctx->V.as<float>() + r0 * kp, sizeof(float) * (r1 - r0) * kp,
+                             hipMemcpyDeviceToHost));
+      for (int64_t i = r0; i < r1; ++i) {
+        if (hw[i].t < 0) continue;
+        ids[o] = (int32_t)(i * ctx->cfg.shard_count + ctx->cfg.shard_index);
+        w[o] = hw[i].w;
+        for (int f = 0; f < k; ++f) V[o * k + f] = hv[(size_t)(i - r0) * kp + f];
+        ++o;
+      }
+    }
+    return FM_OK;
+  });
+}
+
+int fm_batch_create(fm_ctx* ctx, const fm_csr* csr, fm_batch** out) {
+  return guarded(ctx, [&]() -> int {
+    FM_REQUIRE(out != nullptr, "null out");
+    std::unique_ptr<fm_batch> b(new fm_batch());
+    upload_batch(ctx, csr, b.get(), true);
+    *out = b.release();
+    return FM_OK;
+  });
+}
+
+void fm_batch_destroy(fm_batch* b) {
+  if (!b) return;
+  try {
+    delete b;
+  } catch (...) {
+  }
+}
+
+int64_t fm_batch_rows(const fm_batch* b) { return b ? b->dev.n_rows : -1; }
+int64_t fm_batch_nnz(const fm_batch* b) { return b ? b->dev.nnz : -1; }
+
+int fm_step_batch(fm_ctx* ctx, const fm_batch* batch, int32_t t, double step_size, double reg_param,
+                  fm_step_out* out) {
+  return guarded(ctx, [&]() -> int { return step_impl(ctx, batch, t, step_size, reg_param, out); });
+}
+
+int fm_step(fm_ctx* ctx, const fm_csr* csr, int32_t t, double step_size, double reg_param, fm_step_out* out) {
+  return guarded(ctx, [&]() -> int {
+    FM_REQUIRE(csr != nullptr, "null batch");
+    if (csr->n_rows == 0) {
+      if (out) {
+        out->loss_sum = 0.0;
+        out->n_rows = 0;
+        out->n_loss_rows = 0;
+        out->n_unique = 0;
+      }
+      return FM_NOTHING_TO_DO;
+    }
+    std::unique_ptr<fm_batch> b(new fm_batch());
+    upload_batch(ctx, csr, b.get(), true);
+    fm_step_out tmp;
+    const int rc = step_impl(ctx, b.get(), t, step_size, reg_param, out ? out : &tmp);
+    return rc;
+  });
+}
+
+int fm_loss_history(fm_ctx* ctx, double* loss, int64_t cap, int64_t* n) {
+  return guarded(ctx, [&]() -> int {
+    FM_REQUIRE(n != nullptr, "null n");
+    *n = ctx->epoch;
+    if (cap == 0 || ctx->epoch == 0) return FM_OK;
+    FM_REQUIRE(loss != nullptr, "null loss buffer");
+    const int64_t m = std::min<int64_t>(cap, ctx->epoch);
+    std::vector<double> h(3 * m);
+    FM_HIP_CHECK(hipMemcpyAsync(h.data(), ctx->loss_hist.p, sizeof(double) * 3 * m, hipMemcpyDeviceToHost, ctx->stream));
+    FM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    for (int64_t i = 0; i < m; ++i) loss[i] = h[3 * i];
+    return FM_OK;
+  });
+}
+
+int fm_predict(fm_ctx* ctx, const fm_csr* csr, double lo, double hi, double* pred) {
+  return guarded(ctx, [&]() -> int {
+    FM_REQUIRE(csr != nullptr && (csr->n_rows == 0 || pred), "null argument");
+    if (csr->n_rows == 0) return FM_OK;
+    std::unique_ptr<fm_batch> b(new fm_batch());
+    upload_batch(ctx, csr, b.get(), false);
+    DevBuf dp;
+    dp.ensure(sizeof(double) * csr->n_rows);
+    launch_predict(ctx->view(), b->dev, ctx->epoch, ctx->cfg.num_features, ctx->cfg.w0, lo, hi, dp.as<double>(),
+                   ctx->stream);
+    FM_HIP_CHECK(hipMemcpyAsync(pred, dp.p, sizeof(double) * csr->n_rows, hipMemcpyDeviceToHost, ctx->stream));
+    FM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    dp.release();
+    return FM_OK;
+  });
+}
+
+int fm_loss_grad(fm_ctx* ctx, const fm_csr* csr, double* pred, double* loss, double* dw, double* dv) {
+  return guarded(ctx, [&]() -> int {
+    FM_REQUIRE(csr != nullptr, "null argument");
+    if (csr->n_rows == 0 || csr->nnz == 0) return FM_OK;
+    std::unique_ptr<fm_batch> b(new fm_batch());
+    upload_batch(ctx, csr, b.get(), true);
+    const int64_t N = csr->nnz;
+    const int k = ctx->cfg.k;
+    DevBuf dpred, dloss, ddw, ddv, dabs;
+    dpred.ensure(sizeof(double) * N);
+    dloss.ensure(sizeof(double) * N);
+    ddw.ensure(sizeof(double) * N);
+    ddv.ensure(sizeof(double) * N * k);
+    dabs.ensure(sizeof(int32_t));
+    FM_HIP_CHECK(hipMemsetAsync(dabs.p, 0, sizeof(int32_t), ctx->stream));
+    launch_loss_grad(ctx->view(), b->dev, ctx->epoch, ctx->cfg.w0, dpred.as<double>(), dloss.as<double>(),
+                     ddw.as<double>(), ddv.as<double>(), dabs.as<int32_t>(), ctx->stream);
+    int32_t absent = 0;
+    FM_HIP_CHECK(hipMemcpyAsync(&absent, dabs.p, sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
+    FM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    FM_REQUIRE(absent == 0, "batch references feature ids absent from the model");
+    if (pred) FM_HIP_CHECK(hipMemcpy(pred, dpred.p, sizeof(double) * N, hipMemcpyDeviceToHost));
+    if (loss) FM_HIP_CHECK(hipMemcpy(loss, dloss.p, sizeof(double) * N, hipMemcpyDeviceToHost));
+    if (dw) FM_HIP_CHECK(hipMemcpy(dw, ddw.p, sizeof(double) * N, hipMemcpyDeviceToHost));
+    if (dv) FM_HIP_CHECK(hipMemcpy(dv, ddv.p, sizeof(double) * N * k, hipMemcpyDeviceToHost));
+    return FM_OK;
+  });
+}
+
+int fm_vector_sum_by_key(fm_ctx* ctx, const int32_t* keys, int64_t n, const double* vecs, int32_t k,
+                         int32_t* out_keys, double* out_sums, int64_t* n_out) {
+  return guarded(ctx, [&]() -> int {
+    FM_REQUIRE(n >= 0 && k >= 1 && n_out, "bad arguments");
+    *n_out = 0;
+    if (n == 0) return FM_OK;
+    FM_REQUIRE(keys && vecs && out_keys && out_sums, "null argument");
+    int64_t mx = 0;
+    for (int64_t i = 0; i < n; ++i) {
+      FM_REQUIRE(keys[i] >= 0, "negative key");
+      mx = std::max<int64_t>(mx, keys[i]);
+    }
+    DevBuf dk, dvec, dok, dos, drun, dn;
+    SortWork sw;
+    dk.ensure(sizeof(uint32_t) * n);
+    dvec.ensure(sizeof(double) * n * k);
+    dok.ensure(sizeof(int32_t) * n);
+    dos.ensure(sizeof(double) * n * k);
+    drun.ensure(sizeof(uint32_t) * n);
+    dn.ensure(sizeof(int64_t));
+    FM_HIP_CHECK(hipMemcpy(dk.p, keys, sizeof(int32_t) * n, hipMemcpyHostToDevice));
+    FM_HIP_CHECK(hipMemcpy(dvec.p, vecs, sizeof(double) * n * k, hipMemcpyHostToDevice));
+    const uint32_t *sk = nullptr, *sv = nullptr;
+    radix_sort_pairs(sw, dk.as<uint32_t>(), nullptr, n, bits_for(mx), ctx->stream, &sk, &sv);
+    launch_segment_sum(sk, sv, n, dvec.as<double>(), k, drun.as<uint32_t>(), dok.as<int32_t>(), dos.as<double>(),
+                       dn.as<int64_t>(), ctx->stream);
+    int64_t nu = 0;
+    FM_HIP_CHECK(hipMemcpyAsync(&nu, dn.p, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+    FM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    FM_HIP_CHECK(hipMemcpy(out_keys, dok.p, sizeof(int32_t) * nu, hipMemcpyDeviceToHost));
+    FM_HIP_CHECK(hipMemcpy(out_sums, dos.p, sizeof(double) * nu * k, hipMemcpyDeviceToHost));
+    *n_out = nu;
+    DevBuf* bufs[] = {&dk, &dvec, &dok, &dos, &drun, &dn, &sw.keys_a, &sw.keys_b, &sw.vals_a, &sw.vals_b,
+                      &sw.counts, &sw.digit_tot};
+    for (auto* bb : bufs) bb->release();
+    return FM_OK;
+  });
+}
+
+int fm_profile_enable(fm_ctx* ctx, int32_t on) {
+  return guarded(ctx, [&]() -> int {
+    ctx->prof = on != 0;
+    return FM_OK;
+  });
+}
+
+int fm_profile_reset(fm_ctx* ctx) {
+  return guarded(ctx, [&]() -> int {
+    ctx->resolve_profile();
+    ctx->prof_acc.clear();
+    ctx->prof_order.clear();
+    return FM_OK;
+  });
+}
+
+int fm_profile_read(fm_ctx* ctx, char* names, int64_t names_cap, double* total_ms, int64_t* launches, int64_t cap,
+                    int64_t* n) {
+  return guarded(ctx, [&]() -> int {
+    FM_REQUIRE(n != nullptr, "null n");
+    ctx->resolve_profile();
+    *n = (int64_t)ctx->prof_order.size();
+    std::string joined;
+    int64_t i = 0;
+    for (const auto& nm : ctx->prof_order) {
+      if (i < cap) {
+        if (total_ms) total_ms[i] = ctx->prof_acc[nm].ms;
+        if (launches) launches[i] = ctx->prof_acc[nm].n;
+      }
+      if (!joined.empty()) joined += "\n";
+      joined += nm;
+      ++i;
+    }
+    if (names && names_cap > 0) {
+      const size_t m = std::min<size_t>((size_t)names_cap - 1, joined.size());
+      std::memcpy(names, joined.data(), m);
+      names[m] = '\0';
+    }
+    return FM_OK;
+  });
+}
+
+}  // extern "C"

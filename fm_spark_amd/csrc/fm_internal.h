@@ -1,0 +1,129 @@
+// Internal declarations shared by the HIP translation units of libfm_hip.so.
+// Nothing here crosses the C-ABI (include/fm_hip.h).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/fm_hip.h"
+
+namespace fmhip {
+
+// ------------------------------------------------------------------------ errors
+void set_error(const std::string& msg);
+
+struct Error {
+  int code;
+  std::string msg;
+};
+
+#define FM_HIP_CHECK(expr)                                                            \
+  do {                                                                                \
+    hipError_t _e = (expr);                                                           \
+    if (_e != hipSuccess)                                                             \
+      throw ::fmhip::Error{_e == hipErrorOutOfMemory ? FM_ERR_OOM : FM_ERR_HIP,        \
+                           std::string(#expr) + ": " + hipGetErrorString(_e)};        \
+  } while (0)
+
+#define FM_REQUIRE(cond, msg)                                \
+  do {                                                       \
+    if (!(cond)) throw ::fmhip::Error{FM_ERR_ARG, (msg)};    \
+  } while (0)
+
+// -------------------------------------------------------------------- device table
+// Per feature row: {w, t_r} packed in 8 bytes so the linear term and the row's L1 epoch
+// come from one sector; V is row-major with stride kp = roundup(k, 4) floats (16-byte
+// aligned rows; padding columns stay exactly 0 through every update).
+struct WT {
+  float w;
+  int32_t t;  // epoch of the last applied L1 (rows are current through step t); -1 = absent
+};
+
+struct TableView {
+  WT* wt;          // [rows]
+  float* V;        // [rows * kp]
+  const double* cum;  // [epoch+1] cumulative L1 shrink: cum[e] = sum of lambda over executed steps 1..e
+  int64_t rows;    // local rows
+  int32_t k;
+  int32_t kp;
+  int32_t shard_count;
+  int32_t shard_index;
+};
+
+// device buffer helper
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  void ensure(size_t n);
+  void release();
+  template <class T>
+  T* as() const { return reinterpret_cast<T*>(p); }
+};
+
+// ------------------------------------------------------------------- radix sort
+struct SortWork {
+  DevBuf keys_a, keys_b, vals_a, vals_b, counts, digit_tot;
+  int64_t cap = 0;
+  void ensure(int64_t n);
+};
+
+// Stable LSD sort of (key, index) pairs: keys_in[n] (uint32, < 2^key_bits) with payload
+// = original index (vals_in == nullptr) or vals_in[n].  Returns pointers to the sorted
+// keys / payloads (inside `w`).
+void radix_sort_pairs(SortWork& w, const uint32_t* keys_in, const uint32_t* vals_in, int64_t n,
+                      int key_bits, hipStream_t st, const uint32_t** keys_out,
+                      const uint32_t** vals_out);
+
+// ---------------------------------------------------------------- step kernels
+struct BatchDev {
+  int64_t n_rows = 0, nnz = 0;
+  DevBuf row_ptr, col, val, label;  // int64, uint32 (local slot), float, float
+};
+
+struct StepWork {
+  DevBuf S;         // [B * kp] float: per-sample vfxiSum
+  DevBuf yl;        // [B] float2 {yhat, y}
+  DevBuf rec;       // [N] int2 {s, x bits}
+  DevBuf loss_part; // [n_fwd_blocks] double2 {loss, n_loss}
+  DevBuf part;      // [nchunks * 2 * (kp+1)] double partial gradients
+  DevBuf stats;     // step statistics {loss, n_loss, n_unique}
+  SortWork sort;
+};
+
+struct StepParams {
+  int64_t n_rows;
+  double eta;        // stepSize / sqrt(t)
+  double lam;        // eta * regParam
+  double scale_v;    // eta / m
+  double m;          // miniBatchSize as double: (sum / m) * eta
+  int32_t epoch;     // steps executed before this one (E)
+  double cum_next;   // cum[E] + lam, stored into cum[E+1]
+  double w0;
+};
+
+void launch_forward(const TableView& T, const BatchDev& b, StepWork& w, const StepParams& p,
+                    hipStream_t st, int64_t* n_fwd_blocks);
+void launch_segment_update(const TableView& T, const BatchDev& b, StepWork& w, const StepParams& p,
+                           const uint32_t* skeys, const uint32_t* svals, int64_t n_fwd_blocks,
+                           double* cum_w, double* stats_out, hipStream_t st);
+
+void launch_init_random(const TableView& T, const int32_t* ids, int64_t n, int64_t id_begin,
+                        uint64_t seed, double sd, int32_t epoch, hipStream_t st);
+void launch_load_rows(const TableView& T, const int32_t* ids, int64_t n, const double* w,
+                      const double* V, int32_t epoch, hipStream_t st);
+void launch_flush(const TableView& T, int32_t epoch, hipStream_t st);
+void launch_table_reset(const TableView& T, hipStream_t st);
+void launch_predict(const TableView& T, const BatchDev& b, int32_t epoch, int64_t num_features,
+                    double w0, double lo, double hi, double* pred, hipStream_t st);
+void launch_loss_grad(const TableView& T, const BatchDev& b, int32_t epoch, double w0, double* pred,
+                      double* loss, double* dw, double* dv, int32_t* absent_flag, hipStream_t st);
+void launch_segment_sum(const uint32_t* skeys, const uint32_t* svals, int64_t n, const double* vecs,
+                        int32_t k, uint32_t* run_index, int32_t* out_keys, double* out_sums,
+                        int64_t* n_out_dev, hipStream_t st);
+void launch_count_present(const TableView& T, int64_t* out, hipStream_t st);
+
+}  // namespace fmhip

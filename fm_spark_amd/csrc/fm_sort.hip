@@ -1,0 +1,249 @@
+// Stable LSD radix sort of (uint32 key, uint32 payload) pairs for gfx950.
+//
+// Replaces the reference's shuffle-by-featureId groupBy (FactorizationMachinesSGD.scala:148,
+// FactorizationMachinesModel.scala:191 window) with a deterministic grouping: equal keys end
+// up contiguous and in their original (CSR) order, so every per-feature sum downstream runs
+// in a fixed order and the step is bitwise reproducible.
+//
+// Per pass (8-bit digit):
+//   count   : one 256-thread block per 4096-key tile, LDS histogram  -> counts[digit][tile]
+//   scan    : one block per digit, exclusive scan along tiles        -> counts, digit totals
+//   scatter : each wave ranks its 1024 keys with 8 ballots per round (wave64 match), the
+//             block stages the tile in LDS in digit order, then writes runs coalesced.
+// HBM traffic per pass: 4 B (count) + 8 B read + 8 B write per pair.
+#include "fm_internal.h"
+
+namespace fmhip {
+
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kWaves = kBlock / 64;
+constexpr int kRounds = 16;
+constexpr int kTile = kBlock * kRounds;  // 4096 keys per tile
+constexpr int kRadix = 256;
+
+__global__ __launch_bounds__(kBlock) void k_radix_count(const uint32_t* __restrict__ keys, int64_t n,
+                                                        int shift, uint32_t* __restrict__ counts,
+                                                        int64_t ntiles) {
+  __shared__ uint32_t hist[kRadix];
+  hist[threadIdx.x] = 0;
+  __syncthreads();
+  const int64_t base = (int64_t)blockIdx.x * kTile;
+  if (base + kTile <= n) {
+    const uint4* k4 = reinterpret_cast<const uint4*>(keys + base);
+#pragma unroll
+    for (int i = 0; i < kRounds / 4; ++i) {
+      const uint4 q = k4[i * kBlock + threadIdx.x];
+      atomicAdd(&hist[(q.x >> shift) & 255u], 1u);
+      atomicAdd(&hist[(q.y >> shift) & 255u], 1u);
+      atomicAdd(&hist[(q.z >> shift) & 255u], 1u);
+      atomicAdd(&hist[(q.w >> shift) & 255u], 1u);
+    }
+  } else {
+    for (int i = 0; i < kRounds; ++i) {
+      const int64_t idx = base + (int64_t)i * kBlock + threadIdx.x;
+      if (idx < n) atomicAdd(&hist[(keys[idx] >> shift) & 255u], 1u);
+    }
+  }
+  __syncthreads();
+  counts[(int64_t)threadIdx.x * ntiles + blockIdx.x] = hist[threadIdx.x];
+}
+
+__device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v, int lane) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t t = __shfl_up(v, o);
+    if (lane >= o) v += t;
+  }
+  return v;
+}
+
+// Exclusive scan of each digit's row counts[d][0..ntiles), row totals -> digit_tot[d].
+__global__ __launch_bounds__(kBlock) void k_radix_scan_rows(uint32_t* __restrict__ counts, int64_t ntiles,
+                                                            uint32_t* __restrict__ digit_tot) {
+  __shared__ uint32_t wsum[kWaves];
+  uint32_t* row = counts + (int64_t)blockIdx.x * ntiles;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t carry = 0;
+  for (int64_t b = 0; b < ntiles; b += kBlock) {
+    const int64_t i = b + threadIdx.x;
+    const uint32_t v = i < ntiles ? row[i] : 0u;
+    const uint32_t incl = wave_incl_scan_u32(v, lane);
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    uint32_t wpre = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) {
+      const uint32_t s = wsum[w];
+      wpre += (w < wave) ? s : 0u;
+      tot += s;
+    }
+    if (i < ntiles) row[i] = carry + wpre + incl - v;
+    carry += tot;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) digit_tot[blockIdx.x] = carry;
+}
+
+__global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint32_t* __restrict__ keys_in,
+                                                          const uint32_t* __restrict__ vals_in,
+                                                          uint32_t* __restrict__ keys_out,
+                                                          uint32_t* __restrict__ vals_out, int64_t n,
+                                                          int shift, const uint32_t* __restrict__ counts,
+                                                          const uint32_t* __restrict__ digit_tot,
+                                                          int64_t ntiles) {
+  __shared__ uint32_t s_keys[kTile];
+  __shared__ uint32_t s_vals[kTile];
+  __shared__ uint32_t wave_hist[kWaves][kRadix];
+  __shared__ uint32_t tile_start[kRadix];
+  __shared__ uint32_t glob_off[kRadix];
+  __shared__ uint32_t wsum[kWaves];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+  for (int w = 0; w < kWaves; ++w) wave_hist[w][tid] = 0u;
+
+  // global base of (digit = tid, this tile): exclusive scan of digit totals + row prefix.
+  {
+    const uint32_t v = digit_tot[tid];
+    const uint32_t incl = wave_incl_scan_u32(v, lane);
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    uint32_t wpre = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) wpre += (w < wave) ? wsum[w] : 0u;
+    glob_off[tid] = wpre + incl - v + counts[(int64_t)tid * ntiles + blockIdx.x];
+  }
+  __syncthreads();
+
+  const int64_t tile_base = (int64_t)blockIdx.x * kTile;
+  const int64_t wbase = tile_base + (int64_t)wave * (kTile / kWaves);
+  const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  uint32_t my_key[kRounds], my_val[kRounds], my_rank[kRounds];
+#pragma unroll
+  for (int r = 0; r < kRounds; ++r) {
+    const int64_t idx = wbase + (int64_t)r * 64 + lane;
+    const bool valid = idx < n;
+    const uint32_t key = valid ? keys_in[idx] : 0u;
+    const uint32_t val = valid ? (vals_in ? vals_in[idx] : (uint32_t)idx) : 0u;
+    const uint32_t d = (key >> shift) & 255u;
+    uint64_t peers = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      const bool bit = (d >> b) & 1u;
+      const uint64_t m = __ballot(bit);
+      peers &= bit ? m : ~m;
+    }
+    const uint32_t below = (uint32_t)__popcll(peers & lt_mask);
+    const uint32_t cnt = (uint32_t)__popcll(peers);
+    const uint32_t prev = wave_hist[wave][d];
+    __builtin_amdgcn_wave_barrier();
+    if (valid && below == 0) wave_hist[wave][d] = prev + cnt;
+    __builtin_amdgcn_wave_barrier();
+    my_key[r] = key;
+    my_val[r] = valid ? val : 0xFFFFFFFFu;
+    my_rank[r] = valid ? prev + below : 0xFFFFFFFFu;
+  }
+  __syncthreads();
+
+  // per-digit wave bases (exclusive over waves) and the tile's digit starts.
+  {
+    const int d = tid;
+    uint32_t acc = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) {
+      const uint32_t c = wave_hist[w][d];
+      wave_hist[w][d] = acc;
+      acc += c;
+    }
+    const uint32_t incl = wave_incl_scan_u32(acc, lane);
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    uint32_t wpre = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) wpre += (w < wave) ? wsum[w] : 0u;
+    tile_start[d] = wpre + incl - acc;
+  }
+  __syncthreads();
+
+#pragma unroll
+  for (int r = 0; r < kRounds; ++r) {
+    if (my_rank[r] != 0xFFFFFFFFu) {
+      const uint32_t d = (my_key[r] >> shift) & 255u;
+      const uint32_t pos = tile_start[d] + wave_hist[wave][d] + my_rank[r];
+      s_keys[pos] = my_key[r];
+      s_vals[pos] = my_val[r];
+    }
+  }
+  __syncthreads();
+
+  const int64_t rem = n - tile_base;
+  const int tile_n = rem < kTile ? (int)rem : kTile;
+  for (int j = tid; j < tile_n; j += kBlock) {
+    const uint32_t key = s_keys[j];
+    const uint32_t d = (key >> shift) & 255u;
+    const uint32_t dest = glob_off[d] + (uint32_t)j - tile_start[d];
+    keys_out[dest] = key;
+    vals_out[dest] = s_vals[j];
+  }
+}
+
+}  // namespace
+
+void SortWork::ensure(int64_t n) {
+  if (n <= cap) return;
+  const int64_t c = n + n / 8 + 4096;
+  keys_a.ensure(sizeof(uint32_t) * c);
+  keys_b.ensure(sizeof(uint32_t) * c);
+  vals_a.ensure(sizeof(uint32_t) * c);
+  vals_b.ensure(sizeof(uint32_t) * c);
+  const int64_t ntiles = (c + kTile - 1) / kTile;
+  counts.ensure(sizeof(uint32_t) * kRadix * ntiles);
+  digit_tot.ensure(sizeof(uint32_t) * kRadix);
+  cap = c;
+}
+
+void radix_sort_pairs(SortWork& w, const uint32_t* keys_in, const uint32_t* vals_in, int64_t n,
+                      int key_bits, hipStream_t st, const uint32_t** keys_out,
+                      const uint32_t** vals_out) {
+  FM_REQUIRE(n >= 0 && n < (int64_t(1) << 32) - 1, "sort size out of range");
+  w.ensure(n > 0 ? n : 1);
+  if (n == 0) {
+    *keys_out = w.keys_a.as<uint32_t>();
+    *vals_out = w.vals_a.as<uint32_t>();
+    return;
+  }
+  const int passes = key_bits <= 8 ? 1 : (key_bits + 7) / 8;
+  const int64_t ntiles = (n + kTile - 1) / kTile;
+  FM_REQUIRE(ntiles < (int64_t(1) << 31), "too many sort tiles");
+  const uint32_t* kin = keys_in;
+  const uint32_t* vin = vals_in;
+  uint32_t* kbuf[2] = {w.keys_a.as<uint32_t>(), w.keys_b.as<uint32_t>()};
+  uint32_t* vbuf[2] = {w.vals_a.as<uint32_t>(), w.vals_b.as<uint32_t>()};
+  int which = 0;
+  // the count kernel reads keys as uint4 when the tile is full: needs 16-byte alignment
+  const bool aligned = (reinterpret_cast<uintptr_t>(keys_in) & 15u) == 0;
+  for (int p = 0; p < passes; ++p) {
+    const int shift = 8 * p;
+    if (p == 0 && !aligned) {
+      FM_HIP_CHECK(hipMemcpyAsync(kbuf[1], keys_in, sizeof(uint32_t) * n, hipMemcpyDeviceToDevice, st));
+      kin = kbuf[1];
+    }
+    hipLaunchKernelGGL(k_radix_count, dim3((unsigned)ntiles), dim3(kBlock), 0, st, kin, n, shift,
+                       w.counts.as<uint32_t>(), ntiles);
+    hipLaunchKernelGGL(k_radix_scan_rows, dim3(kRadix), dim3(kBlock), 0, st, w.counts.as<uint32_t>(),
+                       ntiles, w.digit_tot.as<uint32_t>());
+    hipLaunchKernelGGL(k_radix_scatter, dim3((unsigned)ntiles), dim3(kBlock), 0, st, kin, vin,
+                       kbuf[which], vbuf[which], n, shift, w.counts.as<uint32_t>(),
+                       w.digit_tot.as<uint32_t>(), ntiles);
+    FM_HIP_CHECK(hipGetLastError());
+    kin = kbuf[which];
+    vin = vbuf[which];
+    which ^= 1;
+  }
+  *keys_out = kin;
+  *vals_out = vin;
+}
+
+}  // namespace fmhip

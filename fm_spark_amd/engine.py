@@ -1,0 +1,197 @@
+"""Pythonic handle over one fm_ctx (one device's FM tables) — thin, no arithmetic.
+
+Every method calls straight through the C-ABI of include/fm_hip.h; errors raise FMError.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _native as N
+
+
+@dataclass
+class StepOut:
+    loss_sum: float
+    n_rows: int
+    n_loss_rows: int
+    n_unique: int
+    executed: bool = True
+
+
+class DeviceBatch:
+    """A CSR mini-batch resident in HBM (fm_batch_create)."""
+
+    def __init__(self, ctx: "FMContext", csr: N.CSRHost):
+        self._lib = N.load()
+        self.ctx = ctx
+        h = C.c_void_p()
+        N.check(self._lib.fm_batch_create(ctx.handle, C.byref(csr.c), C.byref(h)), "fm_batch_create")
+        self.handle = h
+        self.n_rows = csr.n_rows
+        self.nnz = csr.nnz
+
+    def close(self):
+        if self.handle:
+            self._lib.fm_batch_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class FMContext:
+    def __init__(self, num_features: int, k: int, *, device: int = 0, seed: int = 0, init_sd: float = 0.01,
+                 w0: float = 0.0, shard_index: int = 0, shard_count: int = 1):
+        self._lib = N.load()
+        cfg = N.fm_config(num_features=int(num_features), k=int(k), device=int(device), seed=int(seed) & (2**64 - 1),
+                          init_sd=float(init_sd), w0=float(w0), shard_index=int(shard_index),
+                          shard_count=int(shard_count))
+        h = C.c_void_p()
+        N.check(self._lib.fm_create(C.byref(cfg), C.byref(h)), "fm_create")
+        self.handle = h
+        self.num_features = int(num_features)
+        self.k = int(k)
+        self.w0 = float(w0)
+        self.shard_index = int(shard_index)
+        self.shard_count = int(shard_count)
+
+    # ------------------------------------------------------------------ lifecycle
+    def close(self):
+        if getattr(self, "handle", None):
+            self._lib.fm_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_stream(self, stream_ptr: int | None):
+        N.check(self._lib.fm_set_stream(self.handle, C.c_void_p(stream_ptr or 0)), "fm_set_stream")
+
+    def sync(self):
+        N.check(self._lib.fm_sync(self.handle), "fm_sync")
+
+    def reserve(self, max_rows: int, max_nnz: int):
+        N.check(self._lib.fm_reserve(self.handle, int(max_rows), int(max_nnz)), "fm_reserve")
+
+    # --------------------------------------------------------------------- tables
+    def load_tables(self, ids, w, V):
+        ids = np.ascontiguousarray(ids, dtype=np.int32)
+        w = np.ascontiguousarray(w, dtype=np.float64)
+        V = np.ascontiguousarray(V, dtype=np.float64).reshape(len(ids), self.k)
+        N.check(self._lib.fm_load_tables(self.handle, N.ptr(ids, C.c_int32), len(ids), N.ptr(w, C.c_double),
+                                         N.ptr(V, C.c_double)), "fm_load_tables")
+
+    def init_random(self, ids):
+        ids = np.ascontiguousarray(ids, dtype=np.int32)
+        N.check(self._lib.fm_init_random(self.handle, N.ptr(ids, C.c_int32), len(ids)), "fm_init_random")
+
+    def init_random_range(self, begin: int, end: int):
+        N.check(self._lib.fm_init_random_range(self.handle, int(begin), int(end)), "fm_init_random_range")
+
+    def export_tables(self):
+        n = C.c_int64()
+        N.check(self._lib.fm_export_tables(self.handle, None, None, None, 0, C.byref(n)), "fm_export_tables")
+        cnt = n.value
+        ids = np.zeros(max(cnt, 1), dtype=np.int32)
+        w = np.zeros(max(cnt, 1))
+        V = np.zeros((max(cnt, 1), self.k))
+        if cnt:
+            N.check(self._lib.fm_export_tables(self.handle, N.ptr(ids, C.c_int32), N.ptr(w, C.c_double),
+                                               N.ptr(V, C.c_double), cnt, C.byref(n)), "fm_export_tables")
+        return ids[:cnt], w[:cnt], V[:cnt]
+
+    def num_present(self) -> int:
+        return N.check(self._lib.fm_num_present(self.handle), "fm_num_present")
+
+    @property
+    def epoch(self) -> int:
+        return int(self._lib.fm_epoch(self.handle))
+
+    # ------------------------------------------------------------------- stepping
+    def batch(self, csr: N.CSRHost) -> DeviceBatch:
+        return DeviceBatch(self, csr)
+
+    def step(self, csr: N.CSRHost, t: int, step_size: float, reg_param: float) -> StepOut:
+        out = N.fm_step_out()
+        rc = N.check(self._lib.fm_step(self.handle, C.byref(csr.c), int(t), float(step_size), float(reg_param),
+                                       C.byref(out)), "fm_step")
+        if rc == N.FM_NOTHING_TO_DO:
+            return StepOut(0.0, 0, 0, 0, executed=False)
+        return StepOut(out.loss_sum, out.n_rows, out.n_loss_rows, out.n_unique)
+
+    def step_batch(self, b: DeviceBatch, t: int, step_size: float, reg_param: float, sync: bool = True):
+        if sync:
+            out = N.fm_step_out()
+            rc = N.check(self._lib.fm_step_batch(self.handle, b.handle, int(t), float(step_size), float(reg_param),
+                                                 C.byref(out)), "fm_step_batch")
+            if rc == N.FM_NOTHING_TO_DO:
+                return StepOut(0.0, 0, 0, 0, executed=False)
+            return StepOut(out.loss_sum, out.n_rows, out.n_loss_rows, out.n_unique)
+        N.check(self._lib.fm_step_batch(self.handle, b.handle, int(t), float(step_size), float(reg_param), None),
+                "fm_step_batch")
+        return None
+
+    def loss_history(self) -> np.ndarray:
+        n = C.c_int64()
+        N.check(self._lib.fm_loss_history(self.handle, None, 0, C.byref(n)), "fm_loss_history")
+        out = np.zeros(max(n.value, 1))
+        if n.value:
+            N.check(self._lib.fm_loss_history(self.handle, N.ptr(out, C.c_double), n.value, C.byref(n)),
+                    "fm_loss_history")
+        return out[: n.value]
+
+    # ------------------------------------------------------------------- inference
+    def predict(self, csr: N.CSRHost, min_label: float, max_label: float) -> np.ndarray:
+        out = np.zeros(max(csr.n_rows, 1))
+        N.check(self._lib.fm_predict(self.handle, C.byref(csr.c), float(min_label), float(max_label),
+                                     N.ptr(out, C.c_double)), "fm_predict")
+        return out[: csr.n_rows]
+
+    def loss_grad(self, csr: N.CSRHost):
+        n = max(csr.nnz, 1)
+        pred, loss, dw = np.zeros(n), np.zeros(n), np.zeros(n)
+        dv = np.zeros((n, self.k))
+        N.check(self._lib.fm_loss_grad(self.handle, C.byref(csr.c), N.ptr(pred, C.c_double), N.ptr(loss, C.c_double),
+                                       N.ptr(dw, C.c_double), N.ptr(dv, C.c_double)), "fm_loss_grad")
+        m = csr.nnz
+        return pred[:m], loss[:m], dw[:m], dv[:m]
+
+    def vector_sum_by_key(self, keys, vecs):
+        keys = np.ascontiguousarray(keys, dtype=np.int32)
+        vecs = np.ascontiguousarray(vecs, dtype=np.float64)
+        n, k = vecs.shape
+        ok = np.zeros(max(n, 1), dtype=np.int32)
+        os_ = np.zeros((max(n, 1), k))
+        nout = C.c_int64()
+        N.check(self._lib.fm_vector_sum_by_key(self.handle, N.ptr(keys, C.c_int32), n, N.ptr(vecs, C.c_double), k,
+                                               N.ptr(ok, C.c_int32), N.ptr(os_, C.c_double), C.byref(nout)),
+                "fm_vector_sum_by_key")
+        return ok[: nout.value], os_[: nout.value]
+
+    # ------------------------------------------------------------------ profiling
+    def profile_enable(self, on: bool = True):
+        N.check(self._lib.fm_profile_enable(self.handle, 1 if on else 0), "fm_profile_enable")
+
+    def profile_reset(self):
+        N.check(self._lib.fm_profile_reset(self.handle), "fm_profile_reset")
+
+    def profile_read(self) -> dict:
+        n = C.c_int64()
+        cap = 64
+        names = C.create_string_buffer(4096)
+        ms = np.zeros(cap)
+        cnt = np.zeros(cap, dtype=np.int64)
+        N.check(self._lib.fm_profile_read(self.handle, names, 4096, N.ptr(ms, C.c_double), N.ptr(cnt, C.c_int64),
+                                          cap, C.byref(n)), "fm_profile_read")
+        keys = names.value.decode().split("\n") if n.value else []
+        return {k: (float(ms[i]), int(cnt[i])) for i, k in enumerate(keys)}

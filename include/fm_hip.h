@@ -1,0 +1,212 @@
+/*
+ * fm_hip.h — C-ABI of the MI355X factorization-machine SGD hot path.
+ *
+ * This is the drop-in seam for Rainbowboys/fm_spark.  The reference has no FFI of its
+ * own: the hot path is the fold body of FactorizationMachinesSGD.runMiniBatchSGD
+ * (src/main/scala/org/apache/spark/ml/fm/FactorizationMachinesSGD.scala:116-211) plus the
+ * DataFrame plan it builds through FactorizationMachinesModel.calcLossGrad
+ * (FactorizationMachinesModel.scala:135-234).  Each entry point below names the reference
+ * code it replaces.  A JNI binding for the Scala side is sketched in INTEGRATION.md.
+ *
+ * Conventions
+ *   - plain C types only; every pointer argument is caller-owned and only borrowed for
+ *     the duration of the call (host pointers unless the name says _device);
+ *   - return codes: FM_OK (0) success, FM_NOTHING_TO_DO (1) an empty mini-batch
+ *     (FactorizationMachinesSGD.scala:126-128), negative = error; the message is available
+ *     from fm_last_error() on the calling thread.  No C++ exception, abort or exit crosses
+ *     this boundary;
+ *   - one fm_ctx owns one device's tables (one process per GPU).  Calls on one context are
+ *     serialised by an internal mutex; independent contexts may run concurrently
+ *     (CrossValidator keeps several models alive at once).
+ *   - arithmetic: tables are fp32 on the device, accumulations fp64; inputs/outputs fp64.
+ */
+#ifndef FM_HIP_H
+#define FM_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FM_OK 0
+#define FM_NOTHING_TO_DO 1
+#define FM_ERR_ARG (-1)
+#define FM_ERR_OOM (-2)
+#define FM_ERR_HIP (-3)
+#define FM_ERR_STATE (-5)
+
+typedef struct fm_ctx fm_ctx;
+typedef struct fm_batch fm_batch;
+
+/* Model hyper-parameters fixed at creation.
+ * num_features : feature ids are int32 in [0, num_features) (README.md:7 "<= Int.MaxValue").
+ * k            : dimFactorization (FactorizationMachines.scala:26, >= 1).
+ * w0           : globalBias (FactorizationMachinesModel.scala:45); fit always uses 0.0
+ *                (FactorizationMachinesSGD.scala:246).
+ * init_sd/seed : createInitialModel's N(0, initialSd^2) draw (FactorizationMachinesSGD.scala:234-241),
+ *                made deterministic (the reference's draw is unseeded).
+ * shard_index/shard_count : row sharding by feature hash; this context owns the ids with
+ *                id % shard_count == shard_index (shard_count 1 = whole table). */
+typedef struct fm_config {
+  int64_t num_features;
+  int32_t k;
+  int32_t device;
+  uint64_t seed;
+  double init_sd;
+  double w0;
+  int32_t shard_index;
+  int32_t shard_count;
+} fm_config;
+
+/* One mini-batch in CSR form: the result of explode(udfVecToMap(features))
+ * (FactorizationMachinesModel.scala:148-153, 244-250).  Row i holds the active entries
+ * of sample i (explicit zeros kept, one entry per index).  n_rows counts every sampled
+ * row, including rows without active entries: it is miniBatchSize (SGD.scala:124). */
+typedef struct fm_csr {
+  int64_t n_rows;
+  int64_t nnz;
+  const int64_t* row_ptr; /* [n_rows + 1], row_ptr[0] == 0 */
+  const int32_t* col;     /* [nnz] feature ids */
+  const double* val;      /* [nnz] feature values */
+  const double* label;    /* [n_rows] */
+} fm_csr;
+
+/* What one SGD iteration reports (SGD.scala:134-139 logs lossSum). */
+typedef struct fm_step_out {
+  double loss_sum;      /* sum over samples with >= 1 active entry of (yhat - y)^2 */
+  int64_t n_rows;       /* miniBatchSize m */
+  int64_t n_loss_rows;  /* samples contributing to loss_sum */
+  int64_t n_unique;     /* distinct feature ids touched (U) */
+} fm_step_out;
+
+/* ---- context --------------------------------------------------------------------- */
+/* Replaces: new FactorizationMachinesModel(uid, k, globalBias, ...) (Model.scala:43-48). */
+int fm_create(const fm_config* cfg, fm_ctx** out);
+void fm_destroy(fm_ctx* ctx);
+const char* fm_last_error(void);
+/* Launch on an externally owned HIP stream (hipStream_t passed as void*); NULL = own stream. */
+int fm_set_stream(fm_ctx* ctx, void* hip_stream);
+int fm_sync(fm_ctx* ctx);
+/* Pre-size the per-step workspace so no step allocates. */
+int fm_reserve(fm_ctx* ctx, int64_t max_rows, int64_t max_nnz);
+
+/* ---- tables (C9: Strength / FactorizedInteraction, Model.scala:275-289) ------------ */
+/* Inject rows (id, w, V[k]) and mark them present: the M0 injection point. */
+int fm_load_tables(fm_ctx* ctx, const int32_t* ids, int64_t n, const double* w, const double* V);
+/* createInitialModel (SGD.scala:218-252): w, V ~ N(0, init_sd^2) for the given ids,
+ * counter-based (seed, id, factor) so the draw is independent of order and shard. */
+int fm_init_random(fm_ctx* ctx, const int32_t* ids, int64_t n);
+/* Same for every id in [id_begin, id_end) (ids this shard does not own are skipped). */
+int fm_init_random_range(fm_ctx* ctx, int64_t id_begin, int64_t id_end);
+/* Export every present row owned by this context, ascending id, after applying the
+ * pending L1 shrink.  cap = capacity in rows; *n receives the number of present rows
+ * (call with cap 0 to size).  V is row-major [n][k]. */
+int fm_export_tables(fm_ctx* ctx, int32_t* ids, double* w, double* V, int64_t cap, int64_t* n);
+int64_t fm_num_present(fm_ctx* ctx);
+/* Number of executed (non-empty) SGD steps. */
+int64_t fm_epoch(fm_ctx* ctx);
+
+/* ---- mini-batches --------------------------------------------------------------------- */
+/* Copy a CSR batch into device memory once (validated: ids in range, row_ptr monotone). */
+int fm_batch_create(fm_ctx* ctx, const fm_csr* csr, fm_batch** out);
+void fm_batch_destroy(fm_batch* b);
+int64_t fm_batch_rows(const fm_batch* b);
+int64_t fm_batch_nnz(const fm_batch* b);
+
+/* ---- the hot path ------------------------------------------------------------------- */
+/* One mini-batch SGD iteration = the foldLeft body, SGD.scala:116-211:
+ *   eta = step_size / sqrt(t); lambda = eta * reg_param (SGD.scala:121-122)
+ *   forward + loss                      (Model.scala:148-233; SGD.scala:134-138)
+ *   per-feature gradient sums           (SGD.scala:142-155; note SURVEY P1: g_w = x*yhat - y)
+ *   w -= (sum g_w / m) * eta; V -= (sum g_V) * (eta / m)      (SGD.scala:150-154,171-175)
+ *   soft-threshold S_lambda on EVERY present row              (SGD.scala:177-181)
+ * t is the 1-based iteration index (tuple._2 + 1, SGD.scala:119).  Returns
+ * FM_NOTHING_TO_DO for n_rows == 0 without touching the model (SGD.scala:126-128).
+ * fm_step copies the host batch first; fm_step_batch uses a device-resident batch and,
+ * when out == NULL, only enqueues (no host synchronisation; losses are kept on the device,
+ * see fm_loss_history). */
+int fm_step(fm_ctx* ctx, const fm_csr* batch, int32_t t, double step_size, double reg_param,
+            fm_step_out* out);
+int fm_step_batch(fm_ctx* ctx, const fm_batch* batch, int32_t t, double step_size,
+                  double reg_param, fm_step_out* out);
+/* Per-step loss sums of every executed step so far (SGD.scala:139 log line). */
+int fm_loss_history(fm_ctx* ctx, double* loss, int64_t cap, int64_t* n);
+
+/* ---- inference & diagnostics ------------------------------------------------------- */
+/* FactorizationMachinesModel.transform/predict (Model.scala:69-133): ids absent from the
+ * model (or >= num_features) are dropped (inner joins, :103-112); a row with no learned
+ * feature gets w0 unclamped (na.fill, :86); otherwise clamp(yhat, min_label, max_label)
+ * (:129-132).  Pass -inf/+inf for the unclamped score. */
+int fm_predict(fm_ctx* ctx, const fm_csr* csr, double min_label, double max_label, double* pred);
+/* calcLossGrad (Model.scala:135-234), per active entry e in CSR order:
+ * pred[e] = yhat of its row (unclamped), loss[e] = (yhat - y)^2, delta_w[e] = x,
+ * delta_v[e*k + f] = vfxiSum_f * x - (v_f * x) * x.  Any output may be NULL.
+ * Ids absent from the model are an error here (the reference fills them with an
+ * unseeded random draw, Model.scala:170-171, which is never reached from fit). */
+int fm_loss_grad(fm_ctx* ctx, const fm_csr* csr, double* pred, double* loss, double* delta_w,
+                 double* delta_v);
+/* VectorSum UDAF + groupBy (FactorizationMachines.scala:45-81): for every distinct key,
+ * the element-wise fp64 sum of its k-vectors in input order.  Output ascending by key;
+ * *n_out = number of distinct keys (<= n).  Runs the device sort + segmented reduction. */
+int fm_vector_sum_by_key(fm_ctx* ctx, const int32_t* keys, int64_t n, const double* vecs,
+                         int32_t k, int32_t* out_keys, double* out_sums, int64_t* n_out);
+
+/* Per-kernel device time of the last fm_step_batch calls, measured with HIP events on the
+ * launch stream when enabled (names: "forward", "sort", "update", ...). */
+int fm_profile_enable(fm_ctx* ctx, int32_t on);
+/* Writes up to cap entries: names as a '\n'-joined string into names (size names_cap),
+ * total milliseconds and launch counts per kernel; *n = number of kernels. */
+int fm_profile_read(fm_ctx* ctx, char* names, int64_t names_cap, double* total_ms,
+                    int64_t* launches, int64_t cap, int64_t* n);
+int fm_profile_reset(fm_ctx* ctx);
+
+/* ---- mini-batch sampler: Dataset.randomSplit replay (SGD.scala:111-112) --------------- */
+/* Host-side replay of Spark 2.1.0 randomSplit(weights, seed) on a cached DataFrame whose
+ * rows are given partition by partition (part_ptr[n_parts+1]).  Each partition is sorted
+ * ascending by all columns in schema order (column_order: 'L' label double, 'F' features
+ * vector, 'I' int64 column extra[] ; sampleId is appended last), then split i keeps the
+ * rows whose XORShiftRandom(seed + partition).nextDouble() falls in
+ * [cumw[i], cumw[i+1]).  Features: vec_type (0 sparse, 1 dense), vec_size,
+ * vec_ptr[n+1], vec_idx (sparse only; ignored for dense), vec_val.
+ * Outputs: split_of[n] (-1 = in no split), sample_id[n] = (partition << 33) + row index
+ * (monotonically_increasing_id, Model.scala:268-272), order[n] = row indices in sorted
+ * (per-partition) order. */
+int fm_random_split(int32_t n_parts, const int64_t* part_ptr, const char* column_order,
+                    const double* label, const int8_t* vec_type, const int32_t* vec_size,
+                    const int64_t* vec_ptr, const int32_t* vec_idx, const double* vec_val,
+                    const int64_t* extra, int32_t n_weights, const double* weights,
+                    int64_t seed, int32_t* split_of, int64_t* sample_id, int64_t* order);
+/* The building blocks, exported for the parity tests. */
+int64_t fm_xorshift_hash_seed(int64_t seed);
+int32_t fm_murmur3_bytes_hash(const uint8_t* data, int64_t len, int32_t seed);
+/* n successive nextDouble() of XORShiftRandom(seed). */
+int fm_xorshift_next_doubles(int64_t seed, int64_t n, double* out);
+
+/* ---- sharded multi-GPU step (one context per rank; exchange done by the caller over
+ *      RCCL all-to-all).  See DESIGN.md "Multi-GPU". --------------------------------- */
+/* Phase 1 on the requesting rank: sort the batch's ids by (owner, slot), dedupe.
+ * Writes into the context's workspace; returns per-owner unique-id counts
+ * (send_counts[shard_count], host) . */
+int fm_shard_plan(fm_ctx* ctx, const fm_batch* batch, int64_t* send_counts);
+/* Copy the plan's request list (int32 local slots, owner-major, U entries) to dst. */
+int fm_shard_request_copy(fm_ctx* ctx, void* dst_device);
+/* Phase 2 on the owner: rows for n requested local slots -> rows_out[n][k+1] fp32 (w, V)
+ * with pending L1 applied.  Device pointers. */
+int fm_shard_serve_device(fm_ctx* ctx, const void* req_slots, int64_t n, void* rows_out);
+/* Phase 3 on the requester: forward + per-unique-id partial gradient using the rows
+ * received for its plan.  grads_out[U][k+1] fp64 (device).  Loss is accumulated. */
+int fm_shard_local_grad_device(fm_ctx* ctx, const fm_batch* batch, const void* rows_in,
+                               void* grads_out, int64_t global_rows);
+/* Phase 4 on the owner: sum the received partial gradients per slot in fixed rank order,
+ * apply the update + L1 (t, step_size, reg_param as fm_step), advance the epoch. */
+int fm_shard_apply_device(fm_ctx* ctx, const void* req_slots, const void* grads, int64_t n,
+                          int32_t t, double step_size, double reg_param, int64_t global_rows);
+/* Loss of the last sharded step on this rank (partial; the caller all-reduces). */
+int fm_shard_last_loss(fm_ctx* ctx, double* loss_sum, int64_t* n_loss_rows);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FM_HIP_H */

@@ -1,0 +1,253 @@
+"""GPU parity: the HIP path (through the C-ABI) against the fp64 oracle on the same inputs.
+
+Inputs that cross the boundary are rounded to fp32 first (the device keeps fp32 tables and
+values), so the comparison measures the device arithmetic only.  Tolerance: north_star's
+1e-5 relative, with an absolute floor of 1e-8 for values that the L1 soft-threshold drives
+to (near) zero.
+"""
+
+import math
+
+import numpy as np
+import pytest
+
+from oracle import fm_ref as R
+
+pytestmark = pytest.mark.gpu
+
+RTOL = 1e-5
+ATOL = 1e-8
+
+
+def f32(a):
+    return np.asarray(a, dtype=np.float32).astype(np.float64)
+
+
+def make_problem(seed, n_rows, F, k, mean_nnz, *, empty_frac=0.1, zero_frac=0.05, hot=None, labels="binary"):
+    rng = np.random.default_rng(seed)
+    row_ptr = [0]
+    cols, vals = [], []
+    for _ in range(n_rows):
+        if rng.random() < empty_frac:
+            row_ptr.append(len(cols))
+            continue
+        z = int(rng.integers(1, 2 * mean_nnz))
+        z = min(z, F)
+        ids = rng.choice(F, size=z, replace=False)
+        if hot is not None and rng.random() < 0.9 and hot not in ids:
+            ids[0] = hot
+        ids = np.sort(ids)
+        v = f32(rng.normal(0.0, 1.0, size=z))
+        v[rng.random(z) < zero_frac] = 0.0  # explicit zeros stay active
+        cols.extend(ids.tolist())
+        vals.extend(v.tolist())
+        row_ptr.append(len(cols))
+    if labels == "binary":
+        y = (rng.random(n_rows) < 0.25).astype(np.float64)
+    else:
+        y = f32(rng.normal(0.0, 1.0, n_rows))
+    csr = R.CSR(row_ptr=np.asarray(row_ptr, np.int64), col=np.asarray(cols, np.int32),
+                val=np.asarray(vals, np.float64), label=y)
+    ids = np.arange(F, dtype=np.int32)
+    w = f32(rng.normal(0.0, 0.1, F))
+    V = f32(rng.normal(0.0, 0.1, (F, k)))
+    return csr, ids, w, V
+
+
+def to_host(csr):
+    from fm_spark_amd._native import CSRHost
+
+    return CSRHost(csr.row_ptr, csr.col, csr.val, csr.label)
+
+
+def run_both(csr_list, F, k, ids, w, V, step_size, reg_param, t0=1):
+    from fm_spark_amd.engine import FMContext
+
+    model = R.Model.empty(F, k)
+    model.load(ids, w, V)
+    ctx = FMContext(F, k)
+    ctx.load_tables(ids, w, V)
+    losses = []
+    for i, csr in enumerate(csr_list):
+        t = t0 + i
+        ro = R.sgd_step_fast(model, csr, t, step_size, reg_param)
+        go = ctx.step(to_host(csr), t, step_size, reg_param)
+        assert go.executed == ro.executed
+        if ro.executed:
+            losses.append((go.loss_sum, ro.loss_sum))
+            assert go.n_loss_rows == ro.n_loss_rows
+            assert go.n_unique == ro.n_unique
+            assert go.n_rows == ro.n_rows
+    gids, gw, gV = ctx.export_tables()
+    ctx.close()
+    return model, (gids, gw, gV), losses
+
+
+def assert_tables(model, g):
+    gids, gw, gV = g
+    pids = np.nonzero(model.present)[0]
+    np.testing.assert_array_equal(gids, pids)
+    np.testing.assert_allclose(gw, model.w[pids], rtol=RTOL, atol=ATOL)
+    np.testing.assert_allclose(gV, model.V[pids], rtol=RTOL, atol=ATOL)
+
+
+def test_predict_kat(gpu):
+    """FactorizationMachinesSuite.scala:30-68 (pinned KAT), unclamped."""
+    from fm_spark_amd.engine import FMContext
+
+    csr = R.explode([0, 0, 0, 0], [R.dense(1.0, 2.0, 1.5, -1.0), R.sparse(4, [(0, 0.5), (2, -1.5)]),
+                                   R.sparse(5, [(0, 2.0), (4, 1.5)]), R.sparse(4, [])])
+    ctx = FMContext(4, 3, w0=5.0)
+    ctx.load_tables([0, 1, 2, 3], [0.1, 0.2, 0.3, 0.4],
+                    [[1.0, 2.0, 3.0], [3.0, 2.0, 1.0], [-0.1, -0.1, -0.2], [-0.5, 0.3, 0.0]])
+    p = ctx.predict(to_host(csr), -math.inf, math.inf)
+    np.testing.assert_allclose(p, [23.77, 5.275, 5.2, 5.0], rtol=1e-6)
+    # default [minLabel, maxLabel] = [0, 1] clamp (Model.scala:54-61,129-132); the empty row
+    # is na.fill(globalBias) unclamped (:86)
+    p = ctx.predict(to_host(csr), 0.0, 1.0)
+    np.testing.assert_allclose(p, [1.0, 1.0, 1.0, 5.0], rtol=1e-6)
+
+
+def test_vector_sum_kat(gpu):
+    """FactorizationMachinesSuite.scala:77-100 (pinned KAT): exact (111.11, 222.22, 333.33)."""
+    from fm_spark_amd.engine import FMContext
+
+    ctx = FMContext(4, 3)
+    vecs = np.array([[0.01, 0.02, 0.03], [0.1, 0.2, 0.3], [1.0, 2.0, 3.0], [10.0, 20.0, 30.0],
+                     [100.0, 200.0, 300.0]])
+    keys, sums = ctx.vector_sum_by_key([1, 1, 1, 1, 1], vecs)
+    np.testing.assert_array_equal(keys, [1])
+    assert sums[0].tolist() == [111.11, 222.22, 333.33]
+
+
+def test_vector_sum_by_key_many(gpu):
+    from fm_spark_amd.engine import FMContext
+
+    rng = np.random.default_rng(3)
+    keys = rng.integers(0, 3000, 20000).astype(np.int32)
+    vecs = rng.normal(size=(20000, 5))
+    ctx = FMContext(4, 3)
+    gk, gs = ctx.vector_sum_by_key(keys, vecs)
+    rk, rs = R.vector_sum_by_key(keys, vecs)
+    np.testing.assert_array_equal(gk, rk)
+    assert np.array_equal(gs, rs)  # same sequential order -> bitwise
+
+
+def test_loss_grad_matches_oracle(gpu):
+    from fm_spark_amd.engine import FMContext
+
+    csr, ids, w, V = make_problem(5, 300, 60, 5, 6)
+    model = R.Model.empty(60, 5)
+    model.load(ids, w, V)
+    ctx = FMContext(60, 5)
+    ctx.load_tables(ids, w, V)
+    gp, gl, gdw, gdv = ctx.loss_grad(to_host(csr))
+    rp, rl, rdw, rdv = R.loss_grad(model, csr)
+    np.testing.assert_allclose(gp, rp, rtol=1e-6, atol=1e-9)
+    np.testing.assert_allclose(gl, rl, rtol=1e-5, atol=1e-9)
+    np.testing.assert_array_equal(gdw, rdw)
+    np.testing.assert_allclose(gdv, rdv, rtol=1e-5, atol=1e-9)
+
+
+@pytest.mark.parametrize("k", [1, 3, 4, 8, 10, 16, 32])
+def test_step_parity_k(gpu, k):
+    F = 97
+    batches = []
+    for i in range(3):
+        csr, ids, w, V = make_problem(100 + i, 400, F, k, 8)
+        batches.append(csr)
+    _, ids, w, V = make_problem(7, 1, F, k, 1)
+    model, g, losses = run_both(batches, F, k, ids, w, V, step_size=0.5, reg_param=1e-4)
+    assert_tables(model, g)
+    for gl, rl in losses:
+        assert gl == pytest.approx(rl, rel=RTOL)
+
+
+@pytest.mark.parametrize("reg", [0.0, 1e-6, 3e-3])
+def test_step_parity_l1(gpu, reg):
+    """L1 on every present row (SGD.scala:177-181) incl. rows the batches never touch."""
+    F, k = 400, 8
+    batches = [make_problem(200 + i, 150, 120, k, 5)[0] for i in range(4)]  # ids < 120: rows 120..399 untouched
+    _, ids, w, V = make_problem(9, 1, F, k, 1)
+    model, g, losses = run_both(batches, F, k, ids, w, V, step_size=1.0, reg_param=reg)
+    assert_tables(model, g)
+
+
+def test_step_parity_hot_row(gpu):
+    """One id in ~90% of 5000 rows: its run crosses many 64-entry chunks (combine path)."""
+    F, k = 2000, 16
+    csr, ids, w, V = make_problem(11, 5000, F, k, 10, hot=17)
+    model, g, losses = run_both([csr], F, k, ids, w, V, step_size=0.1, reg_param=1e-6)
+    assert_tables(model, g)
+    assert losses[0][0] == pytest.approx(losses[0][1], rel=RTOL)
+
+
+def test_empty_batch_and_empty_rows(gpu):
+    from fm_spark_amd.engine import FMContext
+
+    F, k = 10, 4
+    _, ids, w, V = make_problem(1, 1, F, k, 1)
+    ctx = FMContext(F, k)
+    ctx.load_tables(ids, w, V)
+    empty = R.CSR(row_ptr=np.zeros(1, np.int64), col=np.zeros(0, np.int32), val=np.zeros(0), label=np.zeros(0))
+    assert not ctx.step(to_host(empty), 1, 1.0, 0.1).executed  # SGD.scala:126-128
+    assert ctx.epoch == 0
+    # rows but no entries: m = 3, no gradient, L1 still applies (SGD.scala:124, :157-181)
+    noent = R.CSR(row_ptr=np.zeros(4, np.int64), col=np.zeros(0, np.int32), val=np.zeros(0), label=np.ones(3))
+    model = R.Model.empty(F, k)
+    model.load(ids, w, V)
+    ro = R.sgd_step_fast(model, noent, 2, 1.0, 0.05)
+    go = ctx.step(to_host(noent), 2, 1.0, 0.05)
+    assert go.executed and go.n_rows == 3 and go.n_loss_rows == 0 and go.loss_sum == 0.0
+    assert_tables(model, ctx.export_tables())
+
+
+def test_determinism_bitwise(gpu):
+    from fm_spark_amd.engine import FMContext
+
+    F, k = 5000, 16
+    csr, ids, w, V = make_problem(21, 3000, F, k, 20, hot=3)
+    outs = []
+    for _ in range(2):
+        ctx = FMContext(F, k)
+        ctx.load_tables(ids, w, V)
+        for t in range(1, 4):
+            ctx.step(to_host(csr), t, 0.3, 1e-5)
+        outs.append(ctx.export_tables())
+        ctx.close()
+    for a, b in zip(outs[0], outs[1]):
+        assert np.array_equal(a, b)
+
+
+def test_device_batch_async(gpu):
+    from fm_spark_amd.engine import FMContext
+
+    F, k = 300, 8
+    csrs = [make_problem(300 + i, 200, F, k, 6)[0] for i in range(3)]
+    _, ids, w, V = make_problem(8, 1, F, k, 1)
+    model = R.Model.empty(F, k)
+    model.load(ids, w, V)
+    ctx = FMContext(F, k)
+    ctx.load_tables(ids, w, V)
+    dbs = [ctx.batch(to_host(c)) for c in csrs]
+    ref_losses = []
+    for i, (c, b) in enumerate(zip(csrs, dbs)):
+        ref_losses.append(R.sgd_step_fast(model, c, i + 1, 0.2, 1e-4).loss_sum)
+        ctx.step_batch(b, i + 1, 0.2, 1e-4, sync=False)
+    ctx.sync()
+    np.testing.assert_allclose(ctx.loss_history(), ref_losses, rtol=RTOL)
+    assert_tables(model, ctx.export_tables())
+
+
+def test_init_random_matches_oracle_draw(gpu):
+    from fm_spark_amd.engine import FMContext
+
+    ctx = FMContext(1000, 5, seed=1234, init_sd=0.01)
+    ids = np.array([0, 7, 999, 500], dtype=np.int32)
+    ctx.init_random(ids)
+    gids, gw, gV = ctx.export_tables()
+    rw, rV = R.init_draw(ids, 5, 1234, 0.01)
+    np.testing.assert_array_equal(gids, np.sort(ids))
+    order = np.argsort(ids)
+    np.testing.assert_allclose(gw, rw[order], rtol=1e-6)
+    np.testing.assert_allclose(gV, rV[order], rtol=1e-6)
