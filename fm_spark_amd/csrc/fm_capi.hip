@@ -2,6 +2,7 @@
 // the step driver (forward -> sort -> segmented update) and the table import/export.
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <map>
@@ -63,7 +64,7 @@ struct fm_batch {
     (void)hipSetDevice(device);
     dev.row_ptr.release();
     dev.col.release();
-    dev.val.release();
+    dev.ent.release();
     dev.label.release();
   }
 };
@@ -75,10 +76,10 @@ struct fm_ctx {
   int64_t rows = 0;  // local rows
   hipStream_t stream = nullptr;
   bool own_stream = false;
-  DevBuf wt, V;
-  DevBuf cum;  // [cum_cap] double
-  int64_t cum_cap = 0;
-  std::vector<double> cum_host{0.0};
+  hipStream_t side = nullptr;  // the entry sort runs here, overlapped with the forward
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  DevBuf hdr, V;
+  std::vector<double> cum_host{0.0};  // cum[e] = sum of lambda over executed steps 1..e
   int32_t epoch = 0;
   DevBuf loss_hist;  // [hist_cap][3] double {loss, n_loss, n_unique}
   int64_t hist_cap = 0;
@@ -103,9 +104,8 @@ struct fm_ctx {
 
   TableView view() const {
     TableView T;
-    T.wt = wt.as<WT>();
+    T.hdr = hdr.as<RowHdr>();
     T.V = V.as<float>();
-    T.cum = cum.as<double>();
     T.rows = rows;
     T.k = cfg.k;
     T.kp = kp;
@@ -126,22 +126,23 @@ struct fm_ctx {
   }
 
   // RAII-free helpers: begin() records a start event, end() the stop event for `name`.
-  hipEvent_t prof_begin() {
+  hipEvent_t prof_begin(hipStream_t s) {
     if (!prof) return nullptr;
     hipEvent_t e = get_event();
-    FM_HIP_CHECK(hipEventRecord(e, stream));
+    FM_HIP_CHECK(hipEventRecord(e, s));
     return e;
   }
-  void prof_end(const char* name, hipEvent_t e0) {
+  void prof_end(const char* name, hipEvent_t e0, hipStream_t s) {
     if (!prof || !e0) return;
     hipEvent_t e1 = get_event();
-    FM_HIP_CHECK(hipEventRecord(e1, stream));
+    FM_HIP_CHECK(hipEventRecord(e1, s));
     pending.push_back({name, {e0, e1}});
     if (pending.size() > 4096) resolve_profile();
   }
   void resolve_profile() {
     if (pending.empty()) return;
     FM_HIP_CHECK(hipStreamSynchronize(stream));
+    FM_HIP_CHECK(hipStreamSynchronize(side));
     for (auto& pe : pending) {
       float ms = 0.f;
       FM_HIP_CHECK(hipEventElapsedTime(&ms, pe.second.first, pe.second.second));
@@ -156,18 +157,6 @@ struct fm_ctx {
       free_events.push_back(pe.second.second);
     }
     pending.clear();
-  }
-
-  void ensure_cum(int64_t need) {
-    if (need <= cum_cap) return;
-    int64_t c = std::max<int64_t>(4096, cum_cap);
-    while (c < need) c *= 2;
-    FM_HIP_CHECK(hipStreamSynchronize(stream));
-    cum.ensure(sizeof(double) * c);
-    cum_cap = c;
-    std::vector<double> tmp(c, 0.0);
-    std::copy(cum_host.begin(), cum_host.end(), tmp.begin());
-    FM_HIP_CHECK(hipMemcpy(cum.p, tmp.data(), sizeof(double) * c, hipMemcpyHostToDevice));
   }
 
   void ensure_hist(int64_t need) {
@@ -194,11 +183,14 @@ struct fm_ctx {
       (void)hipEventDestroy(pe.second.second);
     }
     for (auto e : free_events) (void)hipEventDestroy(e);
-    wt.release();
+    if (side) (void)hipStreamSynchronize(side);
+    if (ev_fork) (void)hipEventDestroy(ev_fork);
+    if (ev_join) (void)hipEventDestroy(ev_join);
+    if (side) (void)hipStreamDestroy(side);
+    hdr.release();
     V.release();
-    cum.release();
     loss_hist.release();
-    DevBuf* bufs[] = {&work.S, &work.yl, &work.rec, &work.loss_part, &work.part, &work.stats,
+    DevBuf* bufs[] = {&work.S, &work.yl, &work.loss_part, &work.part, &work.ucnt,
                       &work.sort.keys_a, &work.sort.keys_b, &work.sort.vals_a, &work.sort.vals_b,
                       &work.sort.counts, &work.sort.digit_tot, &plan_req, &plan_uidx, &plan_ukey,
                       &plan_counts, &rows_local};
@@ -278,7 +270,8 @@ void upload_batch(fm_ctx* ctx, const fm_csr* c, fm_batch* b, bool check_range) {
     FM_REQUIRE(N == 0, "nnz > 0 with n_rows == 0");
   }
   std::vector<uint32_t> col(N);
-  std::vector<float> val(N), lab(B);
+  std::vector<uint32_t> ent(2 * N);  // exploded entries {sample, x bits}
+  std::vector<float> lab(B);
   int64_t mx = -1;
   const int64_t F = ctx->cfg.num_features;
   for (int64_t e = 0; e < N; ++e) {
@@ -289,8 +282,13 @@ void upload_batch(fm_ctx* ctx, const fm_csr* c, fm_batch* b, bool check_range) {
     }
     col[e] = (uint32_t)id;
     mx = std::max<int64_t>(mx, id);
-    val[e] = (float)c->val[e];
+    const float xf = (float)c->val[e];
+    uint32_t xb;
+    std::memcpy(&xb, &xf, 4);
+    ent[2 * e + 1] = xb;
   }
+  for (int64_t i = 0; i < B; ++i)
+    for (int64_t e = c->row_ptr[i]; e < c->row_ptr[i + 1]; ++e) ent[2 * e] = (uint32_t)i;
   for (int64_t i = 0; i < B; ++i) lab[i] = (float)c->label[i];
   b->owner = ctx;
   b->device = ctx->cfg.device;
@@ -299,7 +297,7 @@ void upload_batch(fm_ctx* ctx, const fm_csr* c, fm_batch* b, bool check_range) {
   b->dev.nnz = N;
   b->dev.row_ptr.ensure(sizeof(int64_t) * (B + 1));
   b->dev.col.ensure(sizeof(uint32_t) * std::max<int64_t>(N, 4) + 16);
-  b->dev.val.ensure(sizeof(float) * std::max<int64_t>(N, 4) + 16);
+  b->dev.ent.ensure(sizeof(uint32_t) * 2 * std::max<int64_t>(N, 4) + 16);
   b->dev.label.ensure(sizeof(float) * std::max<int64_t>(B, 4) + 16);
   if (B > 0) FM_HIP_CHECK(hipMemcpy(b->dev.row_ptr.p, c->row_ptr, sizeof(int64_t) * (B + 1), hipMemcpyHostToDevice));
   else {
@@ -308,7 +306,7 @@ void upload_batch(fm_ctx* ctx, const fm_csr* c, fm_batch* b, bool check_range) {
   }
   if (N > 0) {
     FM_HIP_CHECK(hipMemcpy(b->dev.col.p, col.data(), sizeof(uint32_t) * N, hipMemcpyHostToDevice));
-    FM_HIP_CHECK(hipMemcpy(b->dev.val.p, val.data(), sizeof(float) * N, hipMemcpyHostToDevice));
+    FM_HIP_CHECK(hipMemcpy(b->dev.ent.p, ent.data(), sizeof(uint32_t) * 2 * N, hipMemcpyHostToDevice));
   }
   if (B > 0) FM_HIP_CHECK(hipMemcpy(b->dev.label.p, lab.data(), sizeof(float) * B, hipMemcpyHostToDevice));
 }
@@ -317,11 +315,10 @@ void reserve_work(fm_ctx* ctx, int64_t B, int64_t N) {
   StepWork& w = ctx->work;
   w.S.ensure(sizeof(float) * (size_t)std::max<int64_t>(B, 1) * ctx->kp);
   w.yl.ensure(sizeof(float) * 2 * (size_t)std::max<int64_t>(B, 1));
-  w.rec.ensure(sizeof(int32_t) * 2 * (size_t)std::max<int64_t>(N, 1));
   w.sort.ensure(std::max<int64_t>(N, 1));
   const int64_t nchunks = (N + 63) / 64;
   w.part.ensure(sizeof(double) * (size_t)std::max<int64_t>(nchunks, 1) * 2 * (ctx->kp + 1));
-  w.stats.ensure(64);
+  w.ucnt.ensure(sizeof(uint32_t) * (size_t)std::max<int64_t>((nchunks + 3) / 4, 1));
   w.loss_part.ensure(sizeof(double) * 2 * 256 * 8);
 }
 
@@ -334,7 +331,6 @@ int step_impl(fm_ctx* ctx, const fm_batch* b, int32_t t, double step_size, doubl
   FM_REQUIRE(std::isfinite(step_size) && std::isfinite(reg_param), "non-finite step size / regParam");
   const int64_t B = b->dev.n_rows, N = b->dev.nnz;
   reserve_work(ctx, B, N);
-  ctx->ensure_cum(ctx->epoch + 2);
   ctx->ensure_hist(ctx->epoch + 1);
   StepParams p;
   p.n_rows = B;
@@ -343,22 +339,31 @@ int step_impl(fm_ctx* ctx, const fm_batch* b, int32_t t, double step_size, doubl
   p.m = (double)B;                           // miniBatchSize, SGD.scala:124
   p.scale_v = p.eta / (double)B;             // currentStepSize / miniBatchSize, SGD.scala:153
   p.epoch = ctx->epoch;
-  p.cum_next = ctx->cum_host.back() + p.lam;
+  p.cumE = ctx->cum_host.back();
+  p.cum_next = p.cumE + p.lam;
   p.w0 = ctx->cfg.w0;
   const TableView T = ctx->view();
   int64_t nfwd = 0;
-  hipEvent_t e0 = ctx->prof_begin();
+  // fork: the sort only reads the batch, so it runs on the side stream beside the forward
+  FM_HIP_CHECK(hipEventRecord(ctx->ev_fork, ctx->stream));
+  FM_HIP_CHECK(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
+  hipEvent_t es = ctx->prof_begin(ctx->side);
+  const uint32_t* skeys = nullptr;
+  const uint2* sents = nullptr;
+  radix_sort_pairs64(ctx->work.sort, b->dev.col.as<uint32_t>(), b->dev.ent.as<uint2>(), N, bits_for(ctx->rows - 1),
+                     ctx->side, &skeys, &sents);
+  ctx->prof_end("sort", es, ctx->side);
+  FM_HIP_CHECK(hipEventRecord(ctx->ev_join, ctx->side));
+  static const bool serial = getenv("FM_NO_OVERLAP") != nullptr;  // diagnostic: no sort/forward overlap
+  if (serial) FM_HIP_CHECK(hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));
+  hipEvent_t e0 = ctx->prof_begin(ctx->stream);
   launch_forward(T, b->dev, ctx->work, p, ctx->stream, &nfwd);
-  ctx->prof_end("forward", e0);
-  e0 = ctx->prof_begin();
-  const uint32_t *skeys = nullptr, *svals = nullptr;
-  radix_sort_pairs(ctx->work.sort, b->dev.col.as<uint32_t>(), nullptr, N, bits_for(ctx->rows - 1), ctx->stream,
-                   &skeys, &svals);
-  ctx->prof_end("sort", e0);
-  e0 = ctx->prof_begin();
+  ctx->prof_end("forward", e0, ctx->stream);
+  FM_HIP_CHECK(hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));
+  e0 = ctx->prof_begin(ctx->stream);
   double* stats = ctx->loss_hist.as<double>() + 3 * (int64_t)ctx->epoch;
-  launch_segment_update(T, b->dev, ctx->work, p, skeys, svals, nfwd, ctx->cum.as<double>(), stats, ctx->stream);
-  ctx->prof_end("update", e0);
+  launch_segment_update(T, b->dev, ctx->work, p, skeys, sents, nfwd, stats, ctx->stream);
+  ctx->prof_end("update", e0, ctx->stream);
   ctx->epoch += 1;
   ctx->cum_host.push_back(p.cum_next);
   if (out) {
@@ -398,9 +403,11 @@ int fm_create(const fm_config* cfg, fm_ctx** out) {
     c->rows = (cfg->num_features - cfg->shard_index + cfg->shard_count - 1) / cfg->shard_count;
     FM_HIP_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     c->own_stream = true;
-    c->wt.ensure(sizeof(WT) * (size_t)std::max<int64_t>(c->rows, 1));
+    FM_HIP_CHECK(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+    FM_HIP_CHECK(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
+    FM_HIP_CHECK(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
+    c->hdr.ensure(sizeof(RowHdr) * (size_t)std::max<int64_t>(c->rows, 1));
     c->V.ensure(sizeof(float) * (size_t)std::max<int64_t>(c->rows, 1) * c->kp);
-    c->ensure_cum(4096);
     c->ensure_hist(4096);
     launch_table_reset(c->view(), c->stream);
     FM_HIP_CHECK(hipStreamSynchronize(c->stream));
@@ -461,7 +468,8 @@ int fm_load_tables(fm_ctx* ctx, const int32_t* ids, int64_t n, const double* w, 
     FM_HIP_CHECK(hipMemcpy(di.p, ids, sizeof(int32_t) * n, hipMemcpyHostToDevice));
     FM_HIP_CHECK(hipMemcpy(dw.p, w, sizeof(double) * n, hipMemcpyHostToDevice));
     FM_HIP_CHECK(hipMemcpy(dv.p, V, sizeof(double) * n * ctx->cfg.k, hipMemcpyHostToDevice));
-    launch_load_rows(ctx->view(), di.as<int32_t>(), n, dw.as<double>(), dv.as<double>(), ctx->epoch, ctx->stream);
+    launch_load_rows(ctx->view(), di.as<int32_t>(), n, dw.as<double>(), dv.as<double>(), ctx->epoch,
+                     ctx->cum_host.back(), ctx->stream);
     FM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
     di.release();
     dw.release();
@@ -480,7 +488,8 @@ int fm_init_random(fm_ctx* ctx, const int32_t* ids, int64_t n) {
     DevBuf di;
     di.ensure(sizeof(int32_t) * n);
     FM_HIP_CHECK(hipMemcpy(di.p, ids, sizeof(int32_t) * n, hipMemcpyHostToDevice));
-    launch_init_random(ctx->view(), di.as<int32_t>(), n, 0, ctx->cfg.seed, ctx->cfg.init_sd, ctx->epoch, ctx->stream);
+    launch_init_random(ctx->view(), di.as<int32_t>(), n, 0, ctx->cfg.seed, ctx->cfg.init_sd, ctx->epoch,
+                       ctx->cum_host.back(), ctx->stream);
     FM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
     di.release();
     return FM_OK;
@@ -490,7 +499,8 @@ int fm_init_random(fm_ctx* ctx, const int32_t* ids, int64_t n) {
 int fm_init_random_range(fm_ctx* ctx, int64_t b, int64_t e) {
   return guarded(ctx, [&]() -> int {
     FM_REQUIRE(b >= 0 && e >= b && e <= ctx->cfg.num_features, "bad id range");
-    launch_init_random(ctx->view(), nullptr, e - b, b, ctx->cfg.seed, ctx->cfg.init_sd, ctx->epoch, ctx->stream);
+    launch_init_random(ctx->view(), nullptr, e - b, b, ctx->cfg.seed, ctx->cfg.init_sd, ctx->epoch,
+                       ctx->cum_host.back(), ctx->stream);
     FM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
     return FM_OK;
   });
@@ -515,9 +525,9 @@ int64_t fm_epoch(fm_ctx* ctx) { return ctx ? ctx->epoch : -1; }
 int fm_export_tables(fm_ctx* ctx, int32_t* ids, double* w, double* V, int64_t cap, int64_t* n) {
   return guarded(ctx, [&]() -> int {
     FM_REQUIRE(n != nullptr && cap >= 0, "bad arguments");
-    launch_flush(ctx->view(), ctx->epoch, ctx->stream);  // apply pending L1 to every row
-    std::vector<WT> hw(ctx->rows);
-    FM_HIP_CHECK(hipMemcpyAsync(hw.data(), ctx->wt.p, sizeof(WT) * ctx->rows, hipMemcpyDeviceToHost, ctx->stream));
+    launch_flush(ctx->view(), ctx->epoch, ctx->cum_host.back(), ctx->stream);  // apply pending L1 to every row
+    std::vector<RowHdr> hw(ctx->rows);
+    FM_HIP_CHECK(hipMemcpyAsync(hw.data(), ctx->hdr.p, sizeof(RowHdr) * ctx->rows, hipMemcpyDeviceToHost, ctx->stream));
     FM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
     int64_t cnt = 0;
     for (int64_t i = 0; i < ctx->rows; ++i) cnt += hw[i].t >= 0;
@@ -617,7 +627,7 @@ int fm_predict(fm_ctx* ctx, const fm_csr* csr, double lo, double hi, double* pre
     upload_batch(ctx, csr, b.get(), false);
     DevBuf dp;
     dp.ensure(sizeof(double) * csr->n_rows);
-    launch_predict(ctx->view(), b->dev, ctx->epoch, ctx->cfg.num_features, ctx->cfg.w0, lo, hi, dp.as<double>(),
+    launch_predict(ctx->view(), b->dev, ctx->cum_host.back(), ctx->cfg.num_features, ctx->cfg.w0, lo, hi, dp.as<double>(),
                    ctx->stream);
     FM_HIP_CHECK(hipMemcpyAsync(pred, dp.p, sizeof(double) * csr->n_rows, hipMemcpyDeviceToHost, ctx->stream));
     FM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
@@ -641,7 +651,7 @@ int fm_loss_grad(fm_ctx* ctx, const fm_csr* csr, double* pred, double* loss, dou
     ddv.ensure(sizeof(double) * N * k);
     dabs.ensure(sizeof(int32_t));
     FM_HIP_CHECK(hipMemsetAsync(dabs.p, 0, sizeof(int32_t), ctx->stream));
-    launch_loss_grad(ctx->view(), b->dev, ctx->epoch, ctx->cfg.w0, dpred.as<double>(), dloss.as<double>(),
+    launch_loss_grad(ctx->view(), b->dev, ctx->cum_host.back(), ctx->cfg.w0, dpred.as<double>(), dloss.as<double>(),
                      ddw.as<double>(), ddv.as<double>(), dabs.as<int32_t>(), ctx->stream);
     int32_t absent = 0;
     FM_HIP_CHECK(hipMemcpyAsync(&absent, dabs.p, sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));

@@ -35,18 +35,21 @@ struct Error {
   } while (0)
 
 // -------------------------------------------------------------------- device table
-// Per feature row: {w, t_r} packed in 8 bytes so the linear term and the row's L1 epoch
-// come from one sector; V is row-major with stride kp = roundup(k, 4) floats (16-byte
-// aligned rows; padding columns stay exactly 0 through every update).
-struct WT {
+// Per feature row: a 16-byte header {w, t, cum} and the V row (stride kp = roundup(k, 4)
+// floats, 16-byte aligned; padding columns stay exactly 0 through every update).
+//   t   : epoch (executed steps) through which the row is current; -1 = absent
+//   cum : sum of lambda over executed steps 1..t, i.e. the L1 shrink already applied.
+// A row read at epoch E is brought current by S_{cum[E] - cum} (lazy L1, see fm_kernels.hip);
+// keeping cum in the header avoids a dependent lookup of cum[t].
+struct alignas(16) RowHdr {
   float w;
-  int32_t t;  // epoch of the last applied L1 (rows are current through step t); -1 = absent
+  int32_t t;
+  double cum;
 };
 
 struct TableView {
-  WT* wt;          // [rows]
+  RowHdr* hdr;     // [rows]
   float* V;        // [rows * kp]
-  const double* cum;  // [epoch+1] cumulative L1 shrink: cum[e] = sum of lambda over executed steps 1..e
   int64_t rows;    // local rows
   int32_t k;
   int32_t kp;
@@ -77,20 +80,25 @@ struct SortWork {
 void radix_sort_pairs(SortWork& w, const uint32_t* keys_in, const uint32_t* vals_in, int64_t n,
                       int key_bits, hipStream_t st, const uint32_t** keys_out,
                       const uint32_t** vals_out);
+// Same with an 8-byte payload (e.g. the exploded entry {sample, x}).
+void radix_sort_pairs64(SortWork& w, const uint32_t* keys_in, const uint2* vals_in, int64_t n,
+                        int key_bits, hipStream_t st, const uint32_t** keys_out,
+                        const uint2** vals_out);
 
 // ---------------------------------------------------------------- step kernels
+// A device-resident mini-batch: the exploded (sampleId, featureId, featureValue) rows of
+// Model.scala:148-153 kept both as CSR (row_ptr) and as COO entries ent[e] = {sample, x bits}.
 struct BatchDev {
   int64_t n_rows = 0, nnz = 0;
-  DevBuf row_ptr, col, val, label;  // int64, uint32 (local slot), float, float
+  DevBuf row_ptr, col, ent, label;  // int64 [B+1], uint32 [N] feature slot, uint2 [N], float [B]
 };
 
 struct StepWork {
   DevBuf S;         // [B * kp] float: per-sample vfxiSum
   DevBuf yl;        // [B] float2 {yhat, y}
-  DevBuf rec;       // [N] int2 {s, x bits}
   DevBuf loss_part; // [n_fwd_blocks] double2 {loss, n_loss}
   DevBuf part;      // [nchunks * 2 * (kp+1)] double partial gradients
-  DevBuf stats;     // step statistics {loss, n_loss, n_unique}
+  DevBuf ucnt;      // [n_update_blocks] uint32 distinct-id counts per block
   SortWork sort;
 };
 
@@ -101,25 +109,26 @@ struct StepParams {
   double scale_v;    // eta / m
   double m;          // miniBatchSize as double: (sum / m) * eta
   int32_t epoch;     // steps executed before this one (E)
-  double cum_next;   // cum[E] + lam, stored into cum[E+1]
+  double cumE;       // cum[E]
+  double cum_next;   // cum[E] + lam = cum[E+1]
   double w0;
 };
 
 void launch_forward(const TableView& T, const BatchDev& b, StepWork& w, const StepParams& p,
                     hipStream_t st, int64_t* n_fwd_blocks);
 void launch_segment_update(const TableView& T, const BatchDev& b, StepWork& w, const StepParams& p,
-                           const uint32_t* skeys, const uint32_t* svals, int64_t n_fwd_blocks,
-                           double* cum_w, double* stats_out, hipStream_t st);
+                           const uint32_t* skeys, const uint2* sents, int64_t n_fwd_blocks,
+                           double* stats_out, hipStream_t st);
 
 void launch_init_random(const TableView& T, const int32_t* ids, int64_t n, int64_t id_begin,
-                        uint64_t seed, double sd, int32_t epoch, hipStream_t st);
+                        uint64_t seed, double sd, int32_t epoch, double cumE, hipStream_t st);
 void launch_load_rows(const TableView& T, const int32_t* ids, int64_t n, const double* w,
-                      const double* V, int32_t epoch, hipStream_t st);
-void launch_flush(const TableView& T, int32_t epoch, hipStream_t st);
+                      const double* V, int32_t epoch, double cumE, hipStream_t st);
+void launch_flush(const TableView& T, int32_t epoch, double cumE, hipStream_t st);
 void launch_table_reset(const TableView& T, hipStream_t st);
-void launch_predict(const TableView& T, const BatchDev& b, int32_t epoch, int64_t num_features,
+void launch_predict(const TableView& T, const BatchDev& b, double cumE, int64_t num_features,
                     double w0, double lo, double hi, double* pred, hipStream_t st);
-void launch_loss_grad(const TableView& T, const BatchDev& b, int32_t epoch, double w0, double* pred,
+void launch_loss_grad(const TableView& T, const BatchDev& b, double cumE, double w0, double* pred,
                       double* loss, double* dw, double* dv, int32_t* absent_flag, hipStream_t st);
 void launch_segment_sum(const uint32_t* skeys, const uint32_t* svals, int64_t n, const double* vecs,
                         int32_t k, uint32_t* run_index, int32_t* out_keys, double* out_sums,

@@ -5,24 +5,28 @@
 //
 //   k_forward          sample-major.  A team of TEAM lanes owns one sample; GS lanes hold one
 //                      k-wide V row as float4 quads (coalesced 16 B per lane), so a pass covers
-//                      TEAM/GS of the sample's entries.  Pending L1 is applied on the fly
-//                      (lazy soft-threshold, see below).  Computes vfxiSum (S), the linear and
-//                      v^2 x^2 terms with fp64 accumulation, yhat and the loss partial
-//                      (FactorizationMachinesModel.scala:173-233).
-//   radix sort         (fm_sort.hip) entries by feature slot -> CSC order, stable.
+//                      TEAM/GS of the sample's entries; four passes are issued before any is
+//                      consumed.  Pending L1 is applied on the fly (lazy soft-threshold, below).
+//                      fp64 accumulation of vfxiSum (S), the linear and v^2 x^2 terms, yhat and
+//                      the loss partial (FactorizationMachinesModel.scala:173-233).
+//   radix sort         (fm_sort.hip) entries by feature slot -> CSC order, stable; runs on a
+//                      second stream concurrently with k_forward (it only reads the batch).
 //   k_segment_update   feature-major.  One wave per 64 sorted entries, one lane per entry:
 //                      per-entry gradient (SGD.scala:145-146, keeping the reference's
 //                      x*yhat - y w-gradient), fixed-order segmented scan across lanes, and
 //                      the tail lane of every complete run applies the fused update + L1
 //                      (SGD.scala:150-181) to its row.  Runs that cross a 64-entry chunk write
 //                      fp64 partials instead.
-//   k_segment_combine  sums the partials of crossing runs in chunk order and applies the same
-//                      update; block 0 also closes the step (loss sum, epoch bookkeeping).
+//   k_segment_combine  one wave per crossing run sums its partials in chunk order (lanes over
+//                      the k+1 columns) and applies the same update; block 0 closes the step
+//                      (loss sum and distinct-id count, fixed-order reductions).
 //
 // Lazy L1.  The reference soft-thresholds EVERY model row every iteration (outer joins,
-// SGD.scala:157-181).  S_b(S_a(z)) = S_{a+b}(z) for a, b >= 0, so each row keeps the epoch t
-// through which it is current and cum[] holds the running sum of lambda over executed steps;
-// a row read at epoch E is first brought current by S_{cum[E]-cum[t]}.  Export flushes.
+// SGD.scala:157-181).  S_b(S_a(z)) = S_{a+b}(z) for a, b >= 0, so each row header keeps the
+// cumulative shrink `cum` it has received; a row read when the running total is cumE is first
+// brought current by S_{cumE - cum}.  Export flushes every row.
+#include <cstdlib>
+
 #include "fm_internal.h"
 
 namespace fmhip {
@@ -46,23 +50,18 @@ __device__ __forceinline__ float4 shrink4(float4 v, double a) {
   return make_float4(shrink_f(v.x, a), shrink_f(v.y, a), shrink_f(v.z, a), shrink_f(v.w, a));
 }
 
-// Row of `slot` brought current to epoch E (cumE = cum[E]).  Absent rows read as zero.
-__device__ __forceinline__ void load_row_quad(const TableView& T, uint32_t slot, int q, bool qok,
-                                              double cumE, float& w, float4& v, bool& present) {
-  const WT wt = T.wt[slot];
-  v = qok ? *reinterpret_cast<const float4*>(T.V + (int64_t)slot * T.kp + q * 4)
-          : make_float4(0.f, 0.f, 0.f, 0.f);
-  present = wt.t >= 0;
-  w = wt.w;
-  if (!present) {
+// The row header and one V quad brought current (absent rows read as zero).
+__device__ __forceinline__ void current_row(const RowHdr& h, float4& v, float& w, double cumE) {
+  if (h.t < 0) {
     w = 0.f;
     v = make_float4(0.f, 0.f, 0.f, 0.f);
-  } else {
-    const double a = cumE - T.cum[wt.t];
-    if (a > 0.0) {
-      w = shrink_f(w, a);
-      v = shrink4(v, a);
-    }
+    return;
+  }
+  w = h.w;
+  const double a = cumE - h.cum;
+  if (a > 0.0) {
+    w = shrink_f(w, a);
+    v = shrink4(v, a);
   }
 }
 
@@ -70,71 +69,65 @@ __device__ __forceinline__ void load_row_quad(const TableView& T, uint32_t slot,
 template <int GS, int TEAM>
 __global__ __launch_bounds__(kBlock) void k_forward(TableView T, const int64_t* __restrict__ row_ptr,
                                                     const uint32_t* __restrict__ col,
-                                                    const float* __restrict__ val,
+                                                    const uint2* __restrict__ ent,
                                                     const float* __restrict__ label, int64_t B,
-                                                    double w0, int32_t epoch, float* __restrict__ S_out,
-                                                    float2* __restrict__ yl_out, int2* __restrict__ rec_out,
-                                                    double2* __restrict__ loss_part) {
-  constexpr int RPP = TEAM / GS;  // rows (entries) per pass
+                                                    double w0, double cumE, float* __restrict__ S_out,
+                                                    float2* __restrict__ yl_out, double2* __restrict__ loss_part) {
+  constexpr int RPP = TEAM / GS;  // entries per pass
   constexpr int TPB = kBlock / TEAM;
+  constexpr int U = 4;            // passes in flight
   const int tid = threadIdx.x;
   const int tl = tid % TEAM;
   const int g = tl % GS;
   const int rs = tl / GS;
   const int kp = T.kp;
   const bool qok = g * 4 < kp;
-  const double cumE = T.cum[epoch];
+  const float4* __restrict__ V4 = reinterpret_cast<const float4*>(T.V);
+  const int nq = kp >> 2;
   double loss_acc = 0.0, nloss = 0.0;
 
   for (int64_t s = (int64_t)blockIdx.x * TPB + tid / TEAM; s < B; s += (int64_t)gridDim.x * TPB) {
     const int64_t e0 = row_ptr[s], e1 = row_ptr[s + 1];
     double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0, vv = 0.0, wx = 0.0;
-    int64_t e = e0 + rs;
-    // 2-deep unroll: issue both entries' gathers before consuming them
-    for (; e + RPP < e1; e += 2 * RPP) {
-      const uint32_t id0 = col[e], id1 = col[e + RPP];
-      const float x0 = val[e], x1 = val[e + RPP];
-      float w_0, w_1;
-      float4 v0, v1;
-      bool p0, p1;
-      load_row_quad(T, id0, g, qok, cumE, w_0, v0, p0);
-      load_row_quad(T, id1, g, qok, cumE, w_1, v1, p1);
-      {
-        const double x = x0;
-        a0 += (double)v0.x * x; a1 += (double)v0.y * x; a2 += (double)v0.z * x; a3 += (double)v0.w * x;
-        const double v2 = (double)v0.x * v0.x + (double)v0.y * v0.y + (double)v0.z * v0.z + (double)v0.w * v0.w;
-        vv += v2 * x * x;
-        if (g == 0) wx += (double)w_0 * x;
+    for (int64_t eb = e0 + rs; eb < e1; eb += U * RPP) {
+      uint32_t id[U];
+      float x[U];
+      bool ok[U];
+#pragma unroll
+      for (int j = 0; j < U; ++j) {
+        const int64_t e = eb + j * RPP;
+        ok[j] = e < e1;
+        id[j] = ok[j] ? col[e] : 0u;
+        x[j] = ok[j] ? __uint_as_float(ent[e].y) : 0.f;
       }
-      {
-        const double x = x1;
-        a0 += (double)v1.x * x; a1 += (double)v1.y * x; a2 += (double)v1.z * x; a3 += (double)v1.w * x;
-        const double v2 = (double)v1.x * v1.x + (double)v1.y * v1.y + (double)v1.z * v1.z + (double)v1.w * v1.w;
-        vv += v2 * x * x;
-        if (g == 0) wx += (double)w_1 * x;
+      RowHdr h[U];
+      float4 v[U];
+#pragma unroll
+      for (int j = 0; j < U; ++j) {
+        if (ok[j]) {
+          h[j] = T.hdr[id[j]];
+          v[j] = qok ? V4[(int64_t)id[j] * nq + g] : make_float4(0.f, 0.f, 0.f, 0.f);
+        } else {
+          h[j] = RowHdr{0.f, -1, 0.0};
+          v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
       }
-      if (g == 0) {
-        rec_out[e] = make_int2((int)s, __float_as_int(x0));
-        rec_out[e + RPP] = make_int2((int)s, __float_as_int(x1));
-      }
-    }
-    for (; e < e1; e += RPP) {
-      const uint32_t id0 = col[e];
-      const float x0 = val[e];
-      float w_0;
-      float4 v0;
-      bool p0;
-      load_row_quad(T, id0, g, qok, cumE, w_0, v0, p0);
-      const double x = x0;
-      a0 += (double)v0.x * x; a1 += (double)v0.y * x; a2 += (double)v0.z * x; a3 += (double)v0.w * x;
-      const double v2 = (double)v0.x * v0.x + (double)v0.y * v0.y + (double)v0.z * v0.z + (double)v0.w * v0.w;
-      vv += v2 * x * x;
-      if (g == 0) {
-        wx += (double)w_0 * x;
-        rec_out[e] = make_int2((int)s, __float_as_int(x0));
+#pragma unroll
+      for (int j = 0; j < U; ++j) {
+        float w;
+        current_row(h[j], v[j], w, cumE);
+        const double xd = x[j];
+        // vfxi = v * x (Model.scala:179), VectorSum over the sample (:191)
+        a0 += (double)v[j].x * xd; a1 += (double)v[j].y * xd;
+        a2 += (double)v[j].z * xd; a3 += (double)v[j].w * xd;
+        // vi2xi2 = (sum_f v_f^2) * x * x (Model.scala:256-258), this lane's factors
+        const double v2 = (double)v[j].x * v[j].x + (double)v[j].y * v[j].y + (double)v[j].z * v[j].z +
+                          (double)v[j].w * v[j].w;
+        vv += v2 * xd * xd;
+        if (g == 0) wx += (double)w * xd;  // wixi (Model.scala:178)
       }
     }
-    // sum the row slots (lanes with equal g), then the whole team for the scalars
+    // sum the entry slots (lanes with equal g), then the whole team for the scalars
 #pragma unroll
     for (int o = GS; o < TEAM; o <<= 1) {
       a0 += __shfl_xor(a0, o); a1 += __shfl_xor(a1, o);
@@ -187,202 +180,292 @@ __global__ __launch_bounds__(kBlock) void k_forward(TableView T, const int64_t* 
 // -------------------------------------------------------------- segmented update
 struct SegArgs {
   TableView T;
-  const uint32_t* skeys;
-  const uint32_t* svals;
+  const uint32_t* skeys;  // sorted feature slots
+  const uint2* sents;     // their entries {sample, x bits}, same order
   int64_t N;
-  const int2* rec;
   const float* S;
   const float2* yl;
   double* part;  // [nchunks][2][kp + 1]
   int64_t nchunks;
   StepParams p;
-  unsigned long long* n_unique;
+  uint32_t* ucnt;  // [update blocks]
+  int ablate;      // diagnostic ablation bits (FM_ABLATE); 0 in production
 };
 
-__device__ __forceinline__ double seg_scan(double v, int lane, int start_lane) {
-  // inclusive segmented scan over lanes [start_lane, lane]; fixed (tree) order
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
+// Inclusive segmented scan over lanes [start_lane, lane] in a fixed tree order.  nsteps is the
+// wave-uniform depth the longest piece needs; the skipped steps would add nothing, so the
+// result is bitwise that of the full 6-step scan.
+__device__ __forceinline__ double seg_scan(double v, int lane, int start_lane, int nsteps) {
+  for (int i = 0; i < nsteps; ++i) {
+    const int o = 1 << i;
     const double t = __shfl_up(v, o);
     if (lane - o >= start_lane) v += t;
   }
   return v;
 }
 
-// Row update of SGD.scala:150-181 for one factor quad, fp64:
-//   vec' = S_lambda(vec - sum * (eta / m))
+// Row update of SGD.scala:150-181, fp64:
+//   vec' = S_lambda(vec - sum * (eta / m));  strength' = S_lambda(strength - (sum / m) * eta)
 __device__ __forceinline__ float upd_v(float v, double g, const StepParams& p) {
   return (float)shrink_d((double)v - g * p.scale_v, p.lam);
 }
+__device__ __forceinline__ float upd_w(float w, double g, const StepParams& p) {
+  return (float)shrink_d((double)w - (g / p.m) * p.eta, p.lam);
+}
 
-template <int Q>
+// One wave per chunk of 64 sorted entries.
+//  Phase 1, one lane per entry: run structure (pieces of equal keys inside the chunk), the
+//    row header and the sample's (yhat, y); the linear gradient is scanned here and the tail
+//    lane of every complete run writes the row header.
+//  Phase 2, G lanes per entry (one float4 quad each), E = 64/G entries per round: S and V rows
+//    move as whole 64-byte rows (16 rows per wave-instruction for k = 16) -- gathers, the
+//    segmented scan (lane stride G, carry between rounds) and the write-back.
+template <int G>
 __global__ __launch_bounds__(kBlock) void k_segment_update(SegArgs a) {
-  const int lane = threadIdx.x & 63;
-  const int64_t chunk = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
-  if (chunk >= a.nchunks) return;  // wave-uniform
+  constexpr int E = 64 / G;  // entries per round
+  __shared__ uint32_t wcnt[kBlock / 64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t chunk = (int64_t)blockIdx.x * (kBlock / 64) + wave;
   const TableView& T = a.T;
   const int kp = T.kp, nq = kp >> 2;
   const int64_t p0 = chunk * 64;
   const int64_t pp = p0 + lane;
-  const bool valid = pp < a.N;
+  const bool valid = chunk < a.nchunks && pp < a.N;
   const uint32_t kNone = 0xFFFFFFFFu;
   const uint32_t key = valid ? a.skeys[pp] : kNone;
-  const uint32_t e = valid ? a.svals[pp] : 0u;
+  const uint2 en = valid ? a.sents[pp] : make_uint2(0u, 0u);
   uint32_t prev_key = __shfl_up(key, 1);
   uint32_t next_key = __shfl_down(key, 1);
-  if (lane == 0) prev_key = p0 > 0 ? a.skeys[p0 - 1] : kNone;
-  if (lane == 63) next_key = (p0 + 64 < a.N) ? a.skeys[p0 + 64] : kNone;
+  if (lane == 0) prev_key = (valid && p0 > 0) ? a.skeys[p0 - 1] : kNone;
+  if (lane == 63) next_key = (valid && p0 + 64 < a.N) ? a.skeys[p0 + 64] : kNone;
   if (pp == a.N - 1) next_key = kNone;
+  const int s = (int)en.x;
+  const float xf = __uint_as_float(en.y);
+  const double x = (double)xf;
+  const RowHdr h = valid ? T.hdr[key] : RowHdr{0.f, -1, 0.0};  // read before any write-back
+  const float2 yl = valid ? a.yl[s] : make_float2(0.f, 0.f);
+
   const bool seg_start = valid && key != prev_key;  // a run of this key starts here
   const bool seg_end = valid && key != next_key;     // ... ends here
   const bool piece_head = valid && (lane == 0 || seg_start);
   const bool piece_tail = valid && (lane == 63 || seg_end);
   const uint64_t heads = __ballot(piece_head);
   const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
-  const int start_lane = 63 - __clzll(heads & upto);
+  const uint64_t hm = heads & upto;
+  const int start_lane = hm ? 63 - __clzll(hm) : 0;
   const uint64_t starts = __ballot(seg_start);
-  if (lane == 0 && starts) atomicAdd(a.n_unique, (unsigned long long)__popcll(starts));
+  if (lane == 0) wcnt[wave] = (uint32_t)__popcll(starts);
+  const int dist = valid ? lane - start_lane : 0;
+  int nsteps = 0;
+  while (nsteps < 6 && __ballot(dist >= (1 << nsteps))) ++nsteps;
+  if (a.ablate & 1) nsteps = 0;
   // the piece is a whole run iff its head lane starts the run and its tail lane ends it
   const bool head_is_start = (starts >> start_lane) & 1ull;
   const bool complete = head_is_start && seg_end;
   // partial slot: 0 = the chunk's first piece continuing from the previous chunk (also used
   // when that piece spans the whole chunk), 1 = the last piece continuing into the next chunk
   const int slot = (start_lane == 0 && !head_is_start) ? 0 : 1;
-  double* prow = a.part + ((chunk * 2 + slot) * (int64_t)(kp + 1));
-
-  // per-entry inputs: (s, x) from the forward's record, (yhat, y) of its sample
-  int2 rc = valid ? a.rec[e] : make_int2(0, 0);
-  const int s = rc.x;
-  const double x = valid ? (double)__int_as_float(rc.y) : 0.0;
-  const float2 yl = valid ? a.yl[s] : make_float2(0.f, 0.f);
+  const bool present = h.t >= 0;
+  const double ac = present ? a.p.cumE - h.cum : 0.0;  // pending L1 of this row
   const double yhat = yl.x, y = yl.y;
   const double r = yhat - y;
-  const double cumE = T.cum[a.p.epoch];
 
   // ---- linear term: g_w = deltaWi * pred - label (SGD.scala:145)
   double gw = valid ? x * yhat - y : 0.0;
-  gw = seg_scan(gw, lane, start_lane);
-  WT wt = valid ? T.wt[key] : WT{0.f, -1};
-  if (piece_tail) {
+  gw = seg_scan(gw, lane, start_lane, nsteps);
+  const bool ab_w = a.ablate & 8;
+  if (piece_tail && !ab_w) {
     if (complete) {
-      float w = wt.w;
-      if (wt.t < 0) {
-        w = 0.f;
-      } else {
-        const double ac = cumE - T.cum[wt.t];
-        if (ac > 0.0) w = shrink_f(w, ac);
-      }
-      // strength - (sum/m)*eta, then S_lambda (SGD.scala:150, :171, :179)
-      const double wn = shrink_d((double)w - (gw / a.p.m) * a.p.eta, a.p.lam);
-      WT o;
-      o.w = (float)wn;
+      float w = present ? h.w : 0.f;
+      if (ac > 0.0) w = shrink_f(w, ac);
+      RowHdr o;
+      o.w = upd_w(w, gw, a.p);  // SGD.scala:150, :171, :179
       o.t = a.p.epoch + 1;
-      T.wt[key] = o;
+      o.cum = a.p.cum_next;
+      T.hdr[key] = o;
     } else {
-      prow[0] = gw;
+      a.part[(chunk * 2 + slot) * (int64_t)(kp + 1)] = gw;
     }
   }
+
   // ---- interaction term: g_V = (vfxiSum*x - (v*x)*x) * (pred - label) (Model.scala:201-204,
-  //      SGD.scala:146), in chunks of Q quads
-  for (int qc = 0; qc < nq; qc += Q) {
-    double c[4 * Q];
-    float4 vq[Q];
+  //      SGD.scala:146).  Per-entry scalars packed for the lane shuffles of phase 2.
+  const int flags = (valid ? 1 : 0) | (piece_tail ? 2 : 0) | (complete ? 4 : 0) | (present ? 8 : 0) |
+                    (slot << 4) | (start_lane << 8);
+  const float4* __restrict__ S4 = reinterpret_cast<const float4*>(a.S);
+  float4* __restrict__ V4 = reinterpret_cast<float4*>(T.V);
+  const int q_in = lane % G;   // this lane's quad inside a quad-chunk
+  const int j_in = lane / G;   // this lane's entry inside a round
+  const bool ab_s = a.ablate & 2, ab_v = a.ablate & 4;
+  for (int qc = 0; qc < nq; qc += G) {
+    const int q = qc + q_in;
+    const bool qok = q < nq;
+    double carry0 = 0.0, carry1 = 0.0, carry2 = 0.0, carry3 = 0.0;
+    for (int rd = 0; rd < G; ++rd) {  // 64 / E = G rounds
+      const int j = rd * E + j_in;    // entry (lane of phase 1) this lane serves
+      const int fl = __shfl(flags, j);
+      const uint32_t kj = __shfl(key, j);
+      const int sj = __shfl(s, j);
+      const float xj = __shfl(xf, j);
+      const double rj = __shfl(r, j);
+      const double acj = __shfl(ac, j);
+      const bool vj = (fl & 1) && qok;
+      const int sl = fl >> 8;
+      float4 sq = (vj && !ab_s) ? S4[(int64_t)sj * nq + q] : make_float4(xj, 0.f, 0.f, 0.f);
+      float4 v = (vj && !ab_v && (fl & 8)) ? V4[(int64_t)kj * nq + q] : make_float4(0.f, 0.f, 0.f, 0.f);
+      if (acj > 0.0) v = shrink4(v, acj);
+      const double xd = xj;
+      double c0 = vj ? ((double)sq.x * xd - ((double)v.x * xd) * xd) * rj : 0.0;
+      double c1 = vj ? ((double)sq.y * xd - ((double)v.y * xd) * xd) * rj : 0.0;
+      double c2 = vj ? ((double)sq.z * xd - ((double)v.z * xd) * xd) * rj : 0.0;
+      double c3 = vj ? ((double)sq.w * xd - ((double)v.w * xd) * xd) * rj : 0.0;
+      // segmented scan over this round's entries (lane stride G), fixed tree order
+      const int lo = sl > rd * E ? sl : rd * E;  // first entry of the piece inside this round
 #pragma unroll
-    for (int j = 0; j < Q; ++j) {
-      const int q = qc + j;
-      if (valid && q < nq) {
-        const float4 sq = *reinterpret_cast<const float4*>(a.S + (int64_t)s * kp + q * 4);
-        float w_unused;
-        bool pres;
-        load_row_quad(T, key, q, true, cumE, w_unused, vq[j], pres);
-        c[4 * j + 0] = ((double)sq.x * x - ((double)vq[j].x * x) * x) * r;
-        c[4 * j + 1] = ((double)sq.y * x - ((double)vq[j].y * x) * x) * r;
-        c[4 * j + 2] = ((double)sq.z * x - ((double)vq[j].z * x) * x) * r;
-        c[4 * j + 3] = ((double)sq.w * x - ((double)vq[j].w * x) * x) * r;
-      } else {
-        vq[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-        c[4 * j + 0] = c[4 * j + 1] = c[4 * j + 2] = c[4 * j + 3] = 0.0;
+      for (int o = 1; o < E; o <<= 1) {
+        if (o >= (1 << nsteps)) break;  // wave-uniform: no piece is that long
+        const double t0 = __shfl_up(c0, o * G), t1 = __shfl_up(c1, o * G);
+        const double t2 = __shfl_up(c2, o * G), t3 = __shfl_up(c3, o * G);
+        if (j - o >= lo) {
+          c0 += t0; c1 += t1; c2 += t2; c3 += t3;
+        }
       }
-    }
-#pragma unroll
-    for (int i = 0; i < 4 * Q; ++i) c[i] = seg_scan(c[i], lane, start_lane);
-    if (piece_tail) {
-#pragma unroll
-      for (int j = 0; j < Q; ++j) {
-        const int q = qc + j;
-        if (q >= nq) continue;
-        if (complete) {
-          float4 o;
-          o.x = upd_v(vq[j].x, c[4 * j + 0], a.p);
-          o.y = upd_v(vq[j].y, c[4 * j + 1], a.p);
-          o.z = upd_v(vq[j].z, c[4 * j + 2], a.p);
-          o.w = upd_v(vq[j].w, c[4 * j + 3], a.p);
-          *reinterpret_cast<float4*>(T.V + (int64_t)key * kp + q * 4) = o;
+      if (sl < rd * E) {  // the piece started in an earlier round: add its running sum
+        c0 += carry0; c1 += carry1; c2 += carry2; c3 += carry3;
+      }
+      const int last = (E - 1) * G + q_in;  // the round's last entry, same quad
+      carry0 = __shfl(c0, last); carry1 = __shfl(c1, last);
+      carry2 = __shfl(c2, last); carry3 = __shfl(c3, last);
+      if (ab_w) asm volatile("" ::"v"(c0), "v"(c1), "v"(c2), "v"(c3));
+      if (vj && (fl & 2) && !ab_w) {
+        if (fl & 4) {
+          V4[(int64_t)kj * nq + q] =
+              make_float4(upd_v(v.x, c0, a.p), upd_v(v.y, c1, a.p), upd_v(v.z, c2, a.p), upd_v(v.w, c3, a.p));
         } else {
-          prow[1 + 4 * q + 0] = c[4 * j + 0];
-          prow[1 + 4 * q + 1] = c[4 * j + 1];
-          prow[1 + 4 * q + 2] = c[4 * j + 2];
-          prow[1 + 4 * q + 3] = c[4 * j + 3];
+          double* prow = a.part + (((chunk * 2 + ((fl >> 4) & 1)) * (int64_t)(kp + 1)) + 1 + 4 * q);
+          prow[0] = c0;
+          prow[1] = c1;
+          prow[2] = c2;
+          prow[3] = c3;
         }
       }
     }
   }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+#pragma unroll
+    for (int w = 0; w < kBlock / 64; ++w) t += wcnt[w];
+    a.ucnt[blockIdx.x] = t;
+  }
 }
 
-// Runs that cross chunk boundaries: the chunk holding the run's first entry owns it and
-// adds the following chunks' head partials in chunk order.  Block 0 also closes the step.
+// Runs that cross chunk boundaries: the chunk holding the run's first entry owns it; one wave
+// per owner sums the following chunks' head partials in chunk order with lanes over the k+1
+// columns.  Block 0 also closes the step with fixed-order reductions.
 __global__ __launch_bounds__(kBlock) void k_segment_combine(SegArgs a, const double2* __restrict__ loss_part,
-                                                            int64_t n_loss_blocks,
-                                                            double* __restrict__ cum_w,
+                                                            int64_t n_loss_blocks, int64_t n_ucnt,
                                                             double* __restrict__ stats_out) {
+  const int tid = threadIdx.x, lane = tid & 63;
   const int kp = a.T.kp;
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    double l = 0.0, c = 0.0;
-    for (int64_t i = 0; i < n_loss_blocks; ++i) {
+  const int64_t W = kp + 1;
+  if (blockIdx.x == 0) {
+    __shared__ double rl[kBlock], rc[kBlock], ru[kBlock];
+    double l = 0.0, c = 0.0, u = 0.0;
+    for (int64_t i = tid; i < n_loss_blocks; i += kBlock) {
       l += loss_part[i].x;
       c += loss_part[i].y;
     }
-    stats_out[0] = l;
-    stats_out[1] = c;
-    stats_out[2] = (double)(*a.n_unique);
-    cum_w[a.p.epoch + 1] = a.p.cum_next;
+    for (int64_t i = tid; i < n_ucnt; i += kBlock) u += (double)a.ucnt[i];
+    rl[tid] = l;
+    rc[tid] = c;
+    ru[tid] = u;
+    __syncthreads();
+    for (int o = kBlock / 2; o > 0; o >>= 1) {
+      if (tid < o) {
+        rl[tid] += rl[tid + o];
+        rc[tid] += rc[tid + o];
+        ru[tid] += ru[tid + o];
+      }
+      __syncthreads();
+    }
+    if (tid == 0) {
+      stats_out[0] = rl[0];
+      stats_out[1] = rc[0];
+      stats_out[2] = ru[0];
+    }
   }
-  const int64_t chunk = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (chunk >= a.nchunks) return;
-  const int64_t p0 = chunk * 64;
-  const int64_t p1 = p0 + 64 < a.N ? p0 + 64 : a.N;
-  if (p1 >= a.N) return;                            // nothing continues past the last chunk
-  const uint32_t key = a.skeys[p1 - 1];
-  if (a.skeys[p1] != key) return;                   // last run ends inside this chunk
-  // does the last run start inside this chunk?  (otherwise an earlier chunk owns it)
-  if (a.skeys[p0] == key && p0 > 0 && a.skeys[p0 - 1] == key) return;
+  const int64_t chunk = (int64_t)blockIdx.x * kBlock + tid;
+  bool owner = false;
+  uint32_t key = 0;
+  if (chunk < a.nchunks) {
+    const int64_t p0 = chunk * 64;
+    const int64_t p1 = p0 + 64 < a.N ? p0 + 64 : a.N;
+    if (p1 < a.N) {
+      key = a.skeys[p1 - 1];
+      // the chunk's last run continues into the next chunk and starts inside this chunk
+      owner = a.skeys[p1] == key && !(a.skeys[p0] == key && p0 > 0 && a.skeys[p0 - 1] == key);
+    }
+  }
+  uint64_t owners = __ballot(owner);
   const TableView& T = a.T;
-  const double cumE = T.cum[a.p.epoch];
-  const double* tail = a.part + (chunk * 2 + 1) * (int64_t)(kp + 1);
-  // the owner chunk's piece was written to slot 1, unless it is also the chunk's first piece
-  // that continues from before (excluded above) -> always slot 1 here.
-  double gw = tail[0];
-  int64_t c2 = chunk + 1;
-  while (c2 < a.nchunks && a.skeys[c2 * 64] == key) {
-    gw += a.part[(c2 * 2 + 0) * (int64_t)(kp + 1)];
-    ++c2;
+  while (owners) {
+    const int l = __ffsll((unsigned long long)owners) - 1;
+    owners &= owners - 1;
+    const int64_t c0 = __shfl(chunk, l);
+    const uint32_t k0 = __shfl(key, l);
+    // end of the run: first chunk after c0 whose first key differs
+    int64_t cend = c0 + 1;
+    for (;;) {
+      const int64_t c = cend + lane;
+      const bool cont = c < a.nchunks && a.skeys[c * 64] == k0;
+      const uint64_t m = __ballot(cont);
+      if (m == ~0ull) {
+        cend += 64;
+        continue;
+      }
+      cend += __ffsll((unsigned long long)~m) - 1;
+      break;
+    }
+    const RowHdr h = T.hdr[k0];
+    const bool present = h.t >= 0;
+    const double ac = present ? a.p.cumE - h.cum : 0.0;
+    float wnew = 0.f;
+    for (int f0 = 0; f0 < W; f0 += 64) {
+      const int f = f0 + lane;
+      if (f < W) {
+        double g = a.part[(c0 * 2 + 1) * W + f];
+        int64_t c = c0 + 1;
+        for (; c + 4 <= cend; c += 4) {
+          const double g0 = a.part[((c + 0) * 2) * W + f];
+          const double g1 = a.part[((c + 1) * 2) * W + f];
+          const double g2 = a.part[((c + 2) * 2) * W + f];
+          const double g3 = a.part[((c + 3) * 2) * W + f];
+          g += g0;
+          g += g1;
+          g += g2;
+          g += g3;
+        }
+        for (; c < cend; ++c) g += a.part[(c * 2) * W + f];
+        if (f == 0) {
+          float w = present ? h.w : 0.f;
+          if (ac > 0.0) w = shrink_f(w, ac);
+          wnew = upd_w(w, g, a.p);
+        } else {
+          float v = present ? T.V[(int64_t)k0 * kp + (f - 1)] : 0.f;
+          if (ac > 0.0) v = shrink_f(v, ac);
+          T.V[(int64_t)k0 * kp + (f - 1)] = upd_v(v, g, a.p);
+        }
+      }
+    }
+    if (lane == 0) {
+      RowHdr o;
+      o.w = wnew;
+      o.t = a.p.epoch + 1;
+      o.cum = a.p.cum_next;
+      T.hdr[k0] = o;
+    }
   }
-  WT wt = T.wt[key];
-  const bool present = wt.t >= 0;
-  const double ac = present ? cumE - T.cum[wt.t] : 0.0;
-  float w = present ? wt.w : 0.f;
-  if (ac > 0.0) w = shrink_f(w, ac);
-  WT o;
-  o.w = (float)shrink_d((double)w - (gw / a.p.m) * a.p.eta, a.p.lam);
-  o.t = a.p.epoch + 1;
-  for (int f = 0; f < kp; ++f) {
-    double g = tail[1 + f];
-    for (int64_t c3 = chunk + 1; c3 < c2; ++c3) g += a.part[(c3 * 2 + 0) * (int64_t)(kp + 1) + 1 + f];
-    float v = present ? T.V[(int64_t)key * kp + f] : 0.f;
-    if (ac > 0.0) v = shrink_f(v, ac);
-    T.V[(int64_t)key * kp + f] = upd_v(v, g, a.p);
-  }
-  T.wt[key] = o;
 }
 
 // ---------------------------------------------------------------- table utilities
@@ -405,63 +488,61 @@ __device__ __forceinline__ float gauss_draw(uint64_t seed, int64_t id, int f, do
 }
 
 __global__ void k_init_random(TableView T, const int32_t* __restrict__ ids, int64_t n, int64_t id_begin,
-                              uint64_t seed, double sd, int32_t epoch) {
+                              uint64_t seed, double sd, int32_t epoch, double cumE) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t id = ids ? (int64_t)ids[i] : id_begin + i;
     if (id % T.shard_count != T.shard_index) continue;
     const int64_t slot = id / T.shard_count;
     if (slot >= T.rows) continue;
-    WT o;
+    RowHdr o;
     o.w = gauss_draw(seed, id, -1, sd);
     o.t = epoch;
+    o.cum = cumE;
     for (int f = 0; f < T.kp; ++f) T.V[slot * T.kp + f] = f < T.k ? gauss_draw(seed, id, f, sd) : 0.f;
-    T.wt[slot] = o;
+    T.hdr[slot] = o;
   }
 }
 
 __global__ void k_load_rows(TableView T, const int32_t* __restrict__ ids, int64_t n, const double* __restrict__ w,
-                            const double* __restrict__ V, int32_t epoch) {
+                            const double* __restrict__ V, int32_t epoch, double cumE) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t id = ids[i];
     if (id % T.shard_count != T.shard_index) continue;
     const int64_t slot = id / T.shard_count;
     if (slot >= T.rows) continue;
-    WT o;
+    RowHdr o;
     o.w = (float)w[i];
     o.t = epoch;
+    o.cum = cumE;
     for (int f = 0; f < T.kp; ++f) T.V[slot * T.kp + f] = f < T.k ? (float)V[i * T.k + f] : 0.f;
-    T.wt[slot] = o;
+    T.hdr[slot] = o;
   }
 }
 
 __global__ void k_table_reset(TableView T) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < T.rows; i += (int64_t)gridDim.x * blockDim.x) {
-    WT o;
-    o.w = 0.f;
-    o.t = -1;
-    T.wt[i] = o;
-  }
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < T.rows; i += (int64_t)gridDim.x * blockDim.x)
+    T.hdr[i] = RowHdr{0.f, -1, 0.0};
 }
 
-__global__ void k_flush(TableView T, int32_t epoch) {
-  const double cumE = T.cum[epoch];
+__global__ void k_flush(TableView T, int32_t epoch, double cumE) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < T.rows; i += (int64_t)gridDim.x * blockDim.x) {
-    WT wt = T.wt[i];
-    if (wt.t < 0 || wt.t == epoch) continue;
-    const double a = cumE - T.cum[wt.t];
+    RowHdr h = T.hdr[i];
+    if (h.t < 0) continue;
+    const double a = cumE - h.cum;
     if (a > 0.0) {
-      wt.w = shrink_f(wt.w, a);
+      h.w = shrink_f(h.w, a);
       for (int f = 0; f < T.kp; ++f) T.V[i * T.kp + f] = shrink_f(T.V[i * T.kp + f], a);
     }
-    wt.t = epoch;
-    T.wt[i] = wt;
+    h.t = epoch;
+    h.cum = cumE;
+    T.hdr[i] = h;
   }
 }
 
 __global__ void k_count_present(TableView T, unsigned long long* out) {
   unsigned long long c = 0;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < T.rows; i += (int64_t)gridDim.x * blockDim.x)
-    c += T.wt[i].t >= 0 ? 1ull : 0ull;
+    c += T.hdr[i].t >= 0 ? 1ull : 0ull;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
   if ((threadIdx.x & 63) == 0 && c) atomicAdd(out, c);
@@ -470,9 +551,8 @@ __global__ void k_count_present(TableView T, unsigned long long* out) {
 // FactorizationMachinesModel.predict/transform (Model.scala:69-133), one thread per sample.
 // Global ids arrive in b.col; ids >= num_features or absent from the model are dropped.
 __global__ void k_predict(TableView T, const int64_t* __restrict__ row_ptr, const uint32_t* __restrict__ col,
-                          const float* __restrict__ val, int64_t B, int64_t num_features, int32_t epoch,
+                          const uint2* __restrict__ ent, int64_t B, int64_t num_features, double cumE,
                           double w0, double lo, double hi, double* __restrict__ pred) {
-  const double cumE = T.cum[epoch];
   for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < B; s += (int64_t)gridDim.x * blockDim.x) {
     double acc[64];
     for (int f = 0; f < 64; ++f) acc[f] = 0.0;
@@ -481,11 +561,11 @@ __global__ void k_predict(TableView T, const int64_t* __restrict__ row_ptr, cons
     for (int64_t e = row_ptr[s]; e < row_ptr[s + 1]; ++e) {
       const int64_t id = col[e];
       if (id >= num_features) continue;
-      const WT wt = T.wt[id];
-      if (wt.t < 0) continue;
-      const double a = cumE - T.cum[wt.t];
-      const double x = val[e];
-      const float w = a > 0.0 ? shrink_f(wt.w, a) : wt.w;
+      const RowHdr h = T.hdr[id];
+      if (h.t < 0) continue;
+      const double a = cumE - h.cum;
+      const double x = (double)__uint_as_float(ent[e].y);
+      const float w = a > 0.0 ? shrink_f(h.w, a) : h.w;
       wx += (double)w * x;
       double v2 = 0.0;
       for (int f = 0; f < T.k; ++f) {
@@ -510,10 +590,9 @@ __global__ void k_predict(TableView T, const int64_t* __restrict__ row_ptr, cons
 
 // calcLossGrad per-entry outputs (Model.scala:135-234), one thread per sample.
 __global__ void k_loss_grad(TableView T, const int64_t* __restrict__ row_ptr, const uint32_t* __restrict__ col,
-                            const float* __restrict__ val, const float* __restrict__ label, int64_t B,
-                            int32_t epoch, double w0, double* pred, double* loss, double* dw, double* dv,
+                            const uint2* __restrict__ ent, const float* __restrict__ label, int64_t B,
+                            double cumE, double w0, double* pred, double* loss, double* dw, double* dv,
                             int32_t* absent) {
-  const double cumE = T.cum[epoch];
   for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < B; s += (int64_t)gridDim.x * blockDim.x) {
     double acc[64];
     for (int f = 0; f < 64; ++f) acc[f] = 0.0;
@@ -521,14 +600,14 @@ __global__ void k_loss_grad(TableView T, const int64_t* __restrict__ row_ptr, co
     const int64_t e0 = row_ptr[s], e1 = row_ptr[s + 1];
     for (int64_t e = e0; e < e1; ++e) {
       const int64_t id = col[e];
-      const WT wt = T.wt[id];
-      if (wt.t < 0) {
+      const RowHdr h = T.hdr[id];
+      if (h.t < 0) {
         *absent = 1;
         continue;
       }
-      const double a = cumE - T.cum[wt.t];
-      const double x = val[e];
-      const float w = a > 0.0 ? shrink_f(wt.w, a) : wt.w;
+      const double a = cumE - h.cum;
+      const double x = (double)__uint_as_float(ent[e].y);
+      const float w = a > 0.0 ? shrink_f(h.w, a) : h.w;
       wx += (double)w * x;
       double v2 = 0.0;
       for (int f = 0; f < T.k; ++f) {
@@ -545,15 +624,15 @@ __global__ void k_loss_grad(TableView T, const int64_t* __restrict__ row_ptr, co
     const double d = yhat - (double)label[s];
     for (int64_t e = e0; e < e1; ++e) {
       const int64_t id = col[e];
-      const WT wt = T.wt[id];
-      const double x = val[e];
+      const RowHdr h = T.hdr[id];
+      const double x = (double)__uint_as_float(ent[e].y);
       if (pred) pred[e] = yhat;
       if (loss) loss[e] = d * d;
       if (dw) dw[e] = x;
       if (dv) {
-        const double a = wt.t >= 0 ? cumE - T.cum[wt.t] : 0.0;
+        const double a = h.t >= 0 ? cumE - h.cum : 0.0;
         for (int f = 0; f < T.k; ++f) {
-          float v = wt.t >= 0 ? T.V[id * T.kp + f] : 0.f;
+          float v = h.t >= 0 ? T.V[id * T.kp + f] : 0.f;
           if (a > 0.0) v = shrink_f(v, a);
           dv[e * T.k + f] = acc[f & 63] * x - ((double)v * x) * x;
         }
@@ -625,9 +704,8 @@ void launch_fwd_t(const TableView& T, const BatchDev& b, StepWork& w, const Step
   *nblk = blocks;
   w.loss_part.ensure(sizeof(double2) * blocks);
   hipLaunchKernelGGL((k_forward<GS, TEAM>), dim3((unsigned)blocks), dim3(kBlock), 0, st, T,
-                     b.row_ptr.as<int64_t>(), b.col.as<uint32_t>(), b.val.as<float>(), b.label.as<float>(),
-                     b.n_rows, p.w0, p.epoch, w.S.as<float>(), w.yl.as<float2>(), w.rec.as<int2>(),
-                     w.loss_part.as<double2>());
+                     b.row_ptr.as<int64_t>(), b.col.as<uint32_t>(), b.ent.as<uint2>(), b.label.as<float>(),
+                     b.n_rows, p.w0, p.cumE, w.S.as<float>(), w.yl.as<float2>(), w.loss_part.as<double2>());
 }
 
 }  // namespace
@@ -647,52 +725,54 @@ void launch_forward(const TableView& T, const BatchDev& b, StepWork& w, const St
 }
 
 void launch_segment_update(const TableView& T, const BatchDev& b, StepWork& w, const StepParams& p,
-                           const uint32_t* skeys, const uint32_t* svals, int64_t n_fwd_blocks,
-                           double* cum_w, double* stats_out, hipStream_t st) {
+                           const uint32_t* skeys, const uint2* sents, int64_t n_fwd_blocks,
+                           double* stats_out, hipStream_t st) {
   const int64_t N = b.nnz;
   const int64_t nchunks = (N + 63) / 64;
   w.part.ensure(sizeof(double) * (size_t)(nchunks > 0 ? nchunks : 1) * 2 * (T.kp + 1));
-  w.stats.ensure(sizeof(unsigned long long));
-  unsigned long long* n_unique = w.stats.as<unsigned long long>();
-  FM_HIP_CHECK(hipMemsetAsync(n_unique, 0, sizeof(unsigned long long), st));
+  const int64_t ublocks = (nchunks + (kBlock / 64) - 1) / (kBlock / 64);
+  w.ucnt.ensure(sizeof(uint32_t) * (size_t)(ublocks > 0 ? ublocks : 1));
   SegArgs a;
   a.T = T;
   a.skeys = skeys;
-  a.svals = svals;
+  a.sents = sents;
   a.N = N;
-  a.rec = w.rec.as<int2>();
   a.S = w.S.as<float>();
   a.yl = w.yl.as<float2>();
   a.part = w.part.as<double>();
   a.nchunks = nchunks;
   a.p = p;
-  a.n_unique = n_unique;
+  a.ucnt = w.ucnt.as<uint32_t>();
+  static const int ablate = getenv("FM_ABLATE") ? atoi(getenv("FM_ABLATE")) : 0;
+  a.ablate = ablate;
   if (nchunks > 0) {
-    const unsigned blocks = (unsigned)((nchunks * 64 + kBlock - 1) / kBlock);
     const int nq = T.kp / 4;
-    if (nq <= 1) hipLaunchKernelGGL(k_segment_update<1>, dim3(blocks), dim3(kBlock), 0, st, a);
-    else if (nq <= 2) hipLaunchKernelGGL(k_segment_update<2>, dim3(blocks), dim3(kBlock), 0, st, a);
-    else hipLaunchKernelGGL(k_segment_update<4>, dim3(blocks), dim3(kBlock), 0, st, a);
+    if (nq <= 1) hipLaunchKernelGGL(k_segment_update<1>, dim3((unsigned)ublocks), dim3(kBlock), 0, st, a);
+    else if (nq <= 2) hipLaunchKernelGGL(k_segment_update<2>, dim3((unsigned)ublocks), dim3(kBlock), 0, st, a);
+    else if (nq <= 4) hipLaunchKernelGGL(k_segment_update<4>, dim3((unsigned)ublocks), dim3(kBlock), 0, st, a);
+    else if (nq <= 8) hipLaunchKernelGGL(k_segment_update<8>, dim3((unsigned)ublocks), dim3(kBlock), 0, st, a);
+    else hipLaunchKernelGGL(k_segment_update<16>, dim3((unsigned)ublocks), dim3(kBlock), 0, st, a);
     FM_HIP_CHECK(hipGetLastError());
   }
-  const unsigned cblocks = (unsigned)((nchunks + kBlock - 1) / kBlock) > 0 ? (unsigned)((nchunks + kBlock - 1) / kBlock) : 1u;
-  hipLaunchKernelGGL(k_segment_combine, dim3(cblocks), dim3(kBlock), 0, st, a,
-                     w.loss_part.as<double2>(), n_fwd_blocks, cum_w, stats_out);
+  int64_t cblocks = (nchunks + kBlock - 1) / kBlock;
+  if (cblocks < 1) cblocks = 1;
+  hipLaunchKernelGGL(k_segment_combine, dim3((unsigned)cblocks), dim3(kBlock), 0, st, a,
+                     w.loss_part.as<double2>(), n_fwd_blocks, nchunks > 0 ? ublocks : (int64_t)0, stats_out);
   FM_HIP_CHECK(hipGetLastError());
 }
 
 void launch_init_random(const TableView& T, const int32_t* ids, int64_t n, int64_t id_begin, uint64_t seed,
-                        double sd, int32_t epoch, hipStream_t st) {
+                        double sd, int32_t epoch, double cumE, hipStream_t st) {
   if (n <= 0) return;
   hipLaunchKernelGGL(k_init_random, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, st, T, ids, n, id_begin, seed, sd,
-                     epoch);
+                     epoch, cumE);
   FM_HIP_CHECK(hipGetLastError());
 }
 
 void launch_load_rows(const TableView& T, const int32_t* ids, int64_t n, const double* w, const double* V,
-                      int32_t epoch, hipStream_t st) {
+                      int32_t epoch, double cumE, hipStream_t st) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(k_load_rows, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, st, T, ids, n, w, V, epoch);
+  hipLaunchKernelGGL(k_load_rows, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, st, T, ids, n, w, V, epoch, cumE);
   FM_HIP_CHECK(hipGetLastError());
 }
 
@@ -703,9 +783,9 @@ void launch_table_reset(const TableView& T, hipStream_t st) {
   FM_HIP_CHECK(hipGetLastError());
 }
 
-void launch_flush(const TableView& T, int32_t epoch, hipStream_t st) {
+void launch_flush(const TableView& T, int32_t epoch, double cumE, hipStream_t st) {
   if (T.rows <= 0) return;
-  hipLaunchKernelGGL(k_flush, dim3(grid_for(T.rows, kBlock)), dim3(kBlock), 0, st, T, epoch);
+  hipLaunchKernelGGL(k_flush, dim3(grid_for(T.rows, kBlock)), dim3(kBlock), 0, st, T, epoch, cumE);
   FM_HIP_CHECK(hipGetLastError());
 }
 
@@ -717,24 +797,24 @@ void launch_count_present(const TableView& T, int64_t* out, hipStream_t st) {
   FM_HIP_CHECK(hipGetLastError());
 }
 
-void launch_predict(const TableView& T, const BatchDev& b, int32_t epoch, int64_t num_features, double w0,
+void launch_predict(const TableView& T, const BatchDev& b, double cumE, int64_t num_features, double w0,
                     double lo, double hi, double* pred, hipStream_t st) {
   FM_REQUIRE(T.k <= 64, "fm_predict supports dimFactorization <= 64");
   FM_REQUIRE(T.shard_count == 1, "fm_predict needs the whole table (shard_count == 1)");
   if (b.n_rows <= 0) return;
   hipLaunchKernelGGL(k_predict, dim3(grid_for(b.n_rows, kBlock)), dim3(kBlock), 0, st, T, b.row_ptr.as<int64_t>(),
-                     b.col.as<uint32_t>(), b.val.as<float>(), b.n_rows, num_features, epoch, w0, lo, hi, pred);
+                     b.col.as<uint32_t>(), b.ent.as<uint2>(), b.n_rows, num_features, cumE, w0, lo, hi, pred);
   FM_HIP_CHECK(hipGetLastError());
 }
 
-void launch_loss_grad(const TableView& T, const BatchDev& b, int32_t epoch, double w0, double* pred, double* loss,
+void launch_loss_grad(const TableView& T, const BatchDev& b, double cumE, double w0, double* pred, double* loss,
                       double* dw, double* dv, int32_t* absent_flag, hipStream_t st) {
   FM_REQUIRE(T.k <= 64, "fm_loss_grad supports dimFactorization <= 64");
   FM_REQUIRE(T.shard_count == 1, "fm_loss_grad needs the whole table (shard_count == 1)");
   if (b.n_rows <= 0) return;
   hipLaunchKernelGGL(k_loss_grad, dim3(grid_for(b.n_rows, kBlock)), dim3(kBlock), 0, st, T,
-                     b.row_ptr.as<int64_t>(), b.col.as<uint32_t>(), b.val.as<float>(), b.label.as<float>(),
-                     b.n_rows, epoch, w0, pred, loss, dw, dv, absent_flag);
+                     b.row_ptr.as<int64_t>(), b.col.as<uint32_t>(), b.ent.as<uint2>(), b.label.as<float>(),
+                     b.n_rows, cumE, w0, pred, loss, dw, dv, absent_flag);
   FM_HIP_CHECK(hipGetLastError());
 }
 

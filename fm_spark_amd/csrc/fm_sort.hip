@@ -86,15 +86,27 @@ __global__ __launch_bounds__(kBlock) void k_radix_scan_rows(uint32_t* __restrict
   if (threadIdx.x == 0) digit_tot[blockIdx.x] = carry;
 }
 
+template <class P>
+__device__ __forceinline__ P implicit_payload(int64_t idx);
+template <>
+__device__ __forceinline__ uint32_t implicit_payload<uint32_t>(int64_t idx) {
+  return (uint32_t)idx;
+}
+template <>
+__device__ __forceinline__ uint2 implicit_payload<uint2>(int64_t idx) {
+  return make_uint2((uint32_t)idx, 0u);
+}
+
+template <class P>
 __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint32_t* __restrict__ keys_in,
-                                                          const uint32_t* __restrict__ vals_in,
+                                                          const P* __restrict__ vals_in,
                                                           uint32_t* __restrict__ keys_out,
-                                                          uint32_t* __restrict__ vals_out, int64_t n,
+                                                          P* __restrict__ vals_out, int64_t n,
                                                           int shift, const uint32_t* __restrict__ counts,
                                                           const uint32_t* __restrict__ digit_tot,
                                                           int64_t ntiles) {
   __shared__ uint32_t s_keys[kTile];
-  __shared__ uint32_t s_vals[kTile];
+  __shared__ P s_vals[kTile];
   __shared__ uint32_t wave_hist[kWaves][kRadix];
   __shared__ uint32_t tile_start[kRadix];
   __shared__ uint32_t glob_off[kRadix];
@@ -120,13 +132,14 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint32_t* __rest
   const int64_t tile_base = (int64_t)blockIdx.x * kTile;
   const int64_t wbase = tile_base + (int64_t)wave * (kTile / kWaves);
   const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  uint32_t my_key[kRounds], my_val[kRounds], my_rank[kRounds];
+  uint32_t my_key[kRounds], my_rank[kRounds];
+  P my_val[kRounds];
 #pragma unroll
   for (int r = 0; r < kRounds; ++r) {
     const int64_t idx = wbase + (int64_t)r * 64 + lane;
     const bool valid = idx < n;
     const uint32_t key = valid ? keys_in[idx] : 0u;
-    const uint32_t val = valid ? (vals_in ? vals_in[idx] : (uint32_t)idx) : 0u;
+    const P val = valid ? (vals_in ? vals_in[idx] : implicit_payload<P>(idx)) : P{};
     const uint32_t d = (key >> shift) & 255u;
     uint64_t peers = __ballot(valid);
 #pragma unroll
@@ -142,7 +155,7 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint32_t* __rest
     if (valid && below == 0) wave_hist[wave][d] = prev + cnt;
     __builtin_amdgcn_wave_barrier();
     my_key[r] = key;
-    my_val[r] = valid ? val : 0xFFFFFFFFu;
+    my_val[r] = val;
     my_rank[r] = valid ? prev + below : 0xFFFFFFFFu;
   }
   __syncthreads();
@@ -196,31 +209,31 @@ void SortWork::ensure(int64_t n) {
   const int64_t c = n + n / 8 + 4096;
   keys_a.ensure(sizeof(uint32_t) * c);
   keys_b.ensure(sizeof(uint32_t) * c);
-  vals_a.ensure(sizeof(uint32_t) * c);
-  vals_b.ensure(sizeof(uint32_t) * c);
+  vals_a.ensure(sizeof(uint64_t) * c);  // payloads up to 8 bytes
+  vals_b.ensure(sizeof(uint64_t) * c);
   const int64_t ntiles = (c + kTile - 1) / kTile;
   counts.ensure(sizeof(uint32_t) * kRadix * ntiles);
   digit_tot.ensure(sizeof(uint32_t) * kRadix);
   cap = c;
 }
 
-void radix_sort_pairs(SortWork& w, const uint32_t* keys_in, const uint32_t* vals_in, int64_t n,
-                      int key_bits, hipStream_t st, const uint32_t** keys_out,
-                      const uint32_t** vals_out) {
+template <class P>
+static void radix_sort_impl(SortWork& w, const uint32_t* keys_in, const P* vals_in, int64_t n, int key_bits,
+                            hipStream_t st, const uint32_t** keys_out, const P** vals_out) {
   FM_REQUIRE(n >= 0 && n < (int64_t(1) << 32) - 1, "sort size out of range");
   w.ensure(n > 0 ? n : 1);
   if (n == 0) {
     *keys_out = w.keys_a.as<uint32_t>();
-    *vals_out = w.vals_a.as<uint32_t>();
+    *vals_out = w.vals_a.as<P>();
     return;
   }
   const int passes = key_bits <= 8 ? 1 : (key_bits + 7) / 8;
   const int64_t ntiles = (n + kTile - 1) / kTile;
   FM_REQUIRE(ntiles < (int64_t(1) << 31), "too many sort tiles");
   const uint32_t* kin = keys_in;
-  const uint32_t* vin = vals_in;
+  const P* vin = vals_in;
   uint32_t* kbuf[2] = {w.keys_a.as<uint32_t>(), w.keys_b.as<uint32_t>()};
-  uint32_t* vbuf[2] = {w.vals_a.as<uint32_t>(), w.vals_b.as<uint32_t>()};
+  P* vbuf[2] = {w.vals_a.as<P>(), w.vals_b.as<P>()};
   int which = 0;
   // the count kernel reads keys as uint4 when the tile is full: needs 16-byte alignment
   const bool aligned = (reinterpret_cast<uintptr_t>(keys_in) & 15u) == 0;
@@ -234,7 +247,7 @@ void radix_sort_pairs(SortWork& w, const uint32_t* keys_in, const uint32_t* vals
                        w.counts.as<uint32_t>(), ntiles);
     hipLaunchKernelGGL(k_radix_scan_rows, dim3(kRadix), dim3(kBlock), 0, st, w.counts.as<uint32_t>(),
                        ntiles, w.digit_tot.as<uint32_t>());
-    hipLaunchKernelGGL(k_radix_scatter, dim3((unsigned)ntiles), dim3(kBlock), 0, st, kin, vin,
+    hipLaunchKernelGGL(k_radix_scatter<P>, dim3((unsigned)ntiles), dim3(kBlock), 0, st, kin, vin,
                        kbuf[which], vbuf[which], n, shift, w.counts.as<uint32_t>(),
                        w.digit_tot.as<uint32_t>(), ntiles);
     FM_HIP_CHECK(hipGetLastError());
@@ -244,6 +257,16 @@ void radix_sort_pairs(SortWork& w, const uint32_t* keys_in, const uint32_t* vals
   }
   *keys_out = kin;
   *vals_out = vin;
+}
+
+void radix_sort_pairs(SortWork& w, const uint32_t* keys_in, const uint32_t* vals_in, int64_t n, int key_bits,
+                      hipStream_t st, const uint32_t** keys_out, const uint32_t** vals_out) {
+  radix_sort_impl<uint32_t>(w, keys_in, vals_in, n, key_bits, st, keys_out, vals_out);
+}
+
+void radix_sort_pairs64(SortWork& w, const uint32_t* keys_in, const uint2* vals_in, int64_t n, int key_bits,
+                        hipStream_t st, const uint32_t** keys_out, const uint2** vals_out) {
+  radix_sort_impl<uint2>(w, keys_in, vals_in, n, key_bits, st, keys_out, vals_out);
 }
 
 }  // namespace fmhip
