@@ -60,8 +60,19 @@ struct fm_batch {
   int device = 0;
   BatchDev dev;
   int64_t max_id = -1;
+  // feature-major view produced by fm_batch_prepare (consumed once by the next step)
+  DevBuf skeys, sents;
+  hipEvent_t ready = nullptr;     // recorded on the side stream after the prepared sort
+  hipEvent_t last_use = nullptr;  // recorded on the main stream after a step read skeys/sents
+  bool prepared = false;
   ~fm_batch() {
     (void)hipSetDevice(device);
+    if (ready) (void)hipEventSynchronize(ready);
+    if (last_use) (void)hipEventSynchronize(last_use);
+    if (ready) (void)hipEventDestroy(ready);
+    if (last_use) (void)hipEventDestroy(last_use);
+    skeys.release();
+    sents.release();
     dev.row_ptr.release();
     dev.col.release();
     dev.ent.release();
@@ -78,7 +89,9 @@ struct fm_ctx {
   bool own_stream = false;
   hipStream_t side = nullptr;  // the entry sort runs here, overlapped with the forward
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-  DevBuf hdr, V;
+  hipEvent_t ev_upd_done = nullptr;  // last main-stream read of the shared sort workspace
+  DevBuf rec;  // [rows * stride] float records (V row + header)
+  int32_t stride = 0;
   std::vector<double> cum_host{0.0};  // cum[e] = sum of lambda over executed steps 1..e
   int32_t epoch = 0;
   DevBuf loss_hist;  // [hist_cap][3] double {loss, n_loss, n_unique}
@@ -104,9 +117,9 @@ struct fm_ctx {
 
   TableView view() const {
     TableView T;
-    T.hdr = hdr.as<RowHdr>();
-    T.V = V.as<float>();
+    T.rec = rec.as<float>();
     T.rows = rows;
+    T.stride = stride;
     T.k = cfg.k;
     T.kp = kp;
     T.shard_count = cfg.shard_count;
@@ -186,9 +199,9 @@ struct fm_ctx {
     if (side) (void)hipStreamSynchronize(side);
     if (ev_fork) (void)hipEventDestroy(ev_fork);
     if (ev_join) (void)hipEventDestroy(ev_join);
+    if (ev_upd_done) (void)hipEventDestroy(ev_upd_done);
     if (side) (void)hipStreamDestroy(side);
-    hdr.release();
-    V.release();
+    rec.release();
     loss_hist.release();
     DevBuf* bufs[] = {&work.S, &work.yl, &work.loss_part, &work.part, &work.ucnt,
                       &work.sort.keys_a, &work.sort.keys_b, &work.sort.vals_a, &work.sort.vals_b,
@@ -322,7 +335,7 @@ void reserve_work(fm_ctx* ctx, int64_t B, int64_t N) {
   w.loss_part.ensure(sizeof(double) * 2 * 256 * 8);
 }
 
-int step_impl(fm_ctx* ctx, const fm_batch* b, int32_t t, double step_size, double reg_param, fm_step_out* out) {
+int step_impl(fm_ctx* ctx, fm_batch* b, int32_t t, double step_size, double reg_param, fm_step_out* out) {
   FM_REQUIRE(b != nullptr, "null batch");
   FM_REQUIRE(b->owner == ctx, "batch belongs to another context");
   FM_REQUIRE(ctx->cfg.shard_count == 1, "sharded contexts step through the fm_shard_* entry points");
@@ -344,25 +357,37 @@ int step_impl(fm_ctx* ctx, const fm_batch* b, int32_t t, double step_size, doubl
   p.w0 = ctx->cfg.w0;
   const TableView T = ctx->view();
   int64_t nfwd = 0;
-  // fork: the sort only reads the batch, so it runs on the side stream beside the forward
-  FM_HIP_CHECK(hipEventRecord(ctx->ev_fork, ctx->stream));
-  FM_HIP_CHECK(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
-  hipEvent_t es = ctx->prof_begin(ctx->side);
   const uint32_t* skeys = nullptr;
   const uint2* sents = nullptr;
-  radix_sort_pairs64(ctx->work.sort, b->dev.col.as<uint32_t>(), b->dev.ent.as<uint2>(), N, bits_for(ctx->rows - 1),
-                     ctx->side, &skeys, &sents);
-  ctx->prof_end("sort", es, ctx->side);
-  FM_HIP_CHECK(hipEventRecord(ctx->ev_join, ctx->side));
+  const bool prepared = b->prepared;
+  if (prepared) {
+    // sorted ahead of time by fm_batch_prepare on the side stream
+    skeys = b->skeys.as<uint32_t>();
+    sents = b->sents.as<uint2>();
+  } else {
+    // fork: the sort only reads the batch, so it runs on the side stream beside the forward
+    FM_HIP_CHECK(hipEventRecord(ctx->ev_fork, ctx->stream));
+    FM_HIP_CHECK(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
+    hipEvent_t es = ctx->prof_begin(ctx->side);
+    radix_sort_pairs64(ctx->work.sort, b->dev.col.as<uint32_t>(), b->dev.ent.as<uint2>(), N,
+                       bits_for(ctx->rows - 1), ctx->side, &skeys, &sents);
+    ctx->prof_end("sort", es, ctx->side);
+    FM_HIP_CHECK(hipEventRecord(ctx->ev_join, ctx->side));
+  }
   static const bool serial = getenv("FM_NO_OVERLAP") != nullptr;  // diagnostic: no sort/forward overlap
-  if (serial) FM_HIP_CHECK(hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));
+  if (serial) FM_HIP_CHECK(hipStreamWaitEvent(ctx->stream, prepared ? b->ready : ctx->ev_join, 0));
   hipEvent_t e0 = ctx->prof_begin(ctx->stream);
   launch_forward(T, b->dev, ctx->work, p, ctx->stream, &nfwd);
   ctx->prof_end("forward", e0, ctx->stream);
-  FM_HIP_CHECK(hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));
+  FM_HIP_CHECK(hipStreamWaitEvent(ctx->stream, prepared ? b->ready : ctx->ev_join, 0));
   e0 = ctx->prof_begin(ctx->stream);
   double* stats = ctx->loss_hist.as<double>() + 3 * (int64_t)ctx->epoch;
   launch_segment_update(T, b->dev, ctx->work, p, skeys, sents, nfwd, stats, ctx->stream);
+  FM_HIP_CHECK(hipEventRecord(ctx->ev_upd_done, ctx->stream));
+  if (prepared) {
+    FM_HIP_CHECK(hipEventRecord(b->last_use, ctx->stream));
+    b->prepared = false;
+  }
   ctx->prof_end("update", e0, ctx->stream);
   ctx->epoch += 1;
   ctx->cum_host.push_back(p.cum_next);
@@ -406,8 +431,10 @@ int fm_create(const fm_config* cfg, fm_ctx** out) {
     FM_HIP_CHECK(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
     FM_HIP_CHECK(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
     FM_HIP_CHECK(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
-    c->hdr.ensure(sizeof(RowHdr) * (size_t)std::max<int64_t>(c->rows, 1));
-    c->V.ensure(sizeof(float) * (size_t)std::max<int64_t>(c->rows, 1) * c->kp);
+    FM_HIP_CHECK(hipEventCreateWithFlags(&c->ev_upd_done, hipEventDisableTiming));
+    FM_HIP_CHECK(hipEventRecord(c->ev_upd_done, c->stream));
+    c->stride = record_stride(c->kp);
+    c->rec.ensure(sizeof(float) * (size_t)std::max<int64_t>(c->rows, 1) * c->stride);
     c->ensure_hist(4096);
     launch_table_reset(c->view(), c->stream);
     FM_HIP_CHECK(hipStreamSynchronize(c->stream));
@@ -526,34 +553,32 @@ int fm_export_tables(fm_ctx* ctx, int32_t* ids, double* w, double* V, int64_t ca
   return guarded(ctx, [&]() -> int {
     FM_REQUIRE(n != nullptr && cap >= 0, "bad arguments");
     launch_flush(ctx->view(), ctx->epoch, ctx->cum_host.back(), ctx->stream);  // apply pending L1 to every row
-    std::vector<RowHdr> hw(ctx->rows);
-    FM_HIP_CHECK(hipMemcpyAsync(hw.data(), ctx->hdr.p, sizeof(RowHdr) * ctx->rows, hipMemcpyDeviceToHost, ctx->stream));
     FM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
-    int64_t cnt = 0;
-    for (int64_t i = 0; i < ctx->rows; ++i) cnt += hw[i].t >= 0;
-    *n = cnt;
-    if (cap == 0) return FM_OK;
-    FM_REQUIRE(cap >= cnt && ids && w && V, "export buffers too small or null");
-    const int k = ctx->cfg.k, kp = ctx->kp;
-    const int64_t chunk_rows = 1 << 20;
+    const int k = ctx->cfg.k, kp = ctx->kp, S = ctx->stride;
+    const int64_t chunk_rows = std::max<int64_t>(1, (int64_t(64) << 20) / (4 * S));
     std::vector<float> hv;
-    int64_t o = 0;
+    int64_t cnt = 0, o = 0;
+    const bool fill = cap > 0;
     for (int64_t r0 = 0; r0 < ctx->rows; r0 += chunk_rows) {
       const int64_t r1 = std::min(ctx->rows, r0 + chunk_rows);
-      bool any = false;
-      for (int64_t i = r0; i < r1 && !any; ++i) any = hw[i].t >= 0;
-      if (!any) continue;
-      hv.resize((size_t)(r1 - r0) * kp);
-      FM_HIP_CHECK(hipMemcpy(hv.data(), ctx->V.as<float>() + r0 * kp, sizeof(float) * (r1 - r0) * kp,
+      hv.resize((size_t)(r1 - r0) * S);
+      FM_HIP_CHECK(hipMemcpy(hv.data(), ctx->rec.as<float>() + r0 * S, sizeof(float) * (r1 - r0) * S,
                              hipMemcpyDeviceToHost));
       for (int64_t i = r0; i < r1; ++i) {
-        if (hw[i].t < 0) continue;
+        const float* row = hv.data() + (size_t)(i - r0) * S;
+        RowHdr hd;
+        std::memcpy(&hd, row + kp, sizeof(RowHdr));
+        if (hd.t < 0) continue;
+        ++cnt;
+        if (!fill) continue;
+        FM_REQUIRE(o < cap && ids && w && V, "export buffers too small or null");
         ids[o] = (int32_t)(i * ctx->cfg.shard_count + ctx->cfg.shard_index);
-        w[o] = hw[i].w;
-        for (int f = 0; f < k; ++f) V[o * k + f] = hv[(size_t)(i - r0) * kp + f];
+        w[o] = hd.w;
+        for (int f = 0; f < k; ++f) V[o * k + f] = row[f];
         ++o;
       }
     }
+    *n = cnt;
     return FM_OK;
   });
 }
@@ -576,10 +601,38 @@ void fm_batch_destroy(fm_batch* b) {
   }
 }
 
+int fm_batch_prepare(fm_ctx* ctx, fm_batch* b) {
+  return guarded(ctx, [&]() -> int {
+    FM_REQUIRE(b != nullptr && b->owner == ctx, "batch belongs to another context");
+    FM_REQUIRE(ctx->cfg.shard_count == 1, "fm_batch_prepare is for single-table contexts");
+    const int64_t N = b->dev.nnz;
+    if (N == 0) return FM_OK;
+    if (!b->ready) {
+      FM_HIP_CHECK(hipEventCreateWithFlags(&b->ready, hipEventDisableTiming));
+      FM_HIP_CHECK(hipEventCreateWithFlags(&b->last_use, hipEventDisableTiming));
+      FM_HIP_CHECK(hipEventRecord(b->last_use, ctx->stream));
+    }
+    b->skeys.ensure(sizeof(uint32_t) * N);
+    b->sents.ensure(sizeof(uint2) * N);
+    // the shared sort workspace and this batch's view may still be read by an enqueued step
+    FM_HIP_CHECK(hipStreamWaitEvent(ctx->side, ctx->ev_upd_done, 0));
+    FM_HIP_CHECK(hipStreamWaitEvent(ctx->side, b->last_use, 0));
+    hipEvent_t es = ctx->prof_begin(ctx->side);
+    const uint32_t* sk = nullptr;
+    const uint2* sv = nullptr;
+    radix_sort_pairs64(ctx->work.sort, b->dev.col.as<uint32_t>(), b->dev.ent.as<uint2>(), N, bits_for(ctx->rows - 1),
+                       ctx->side, &sk, &sv, b->skeys.as<uint32_t>(), b->sents.as<uint2>());
+    ctx->prof_end("sort", es, ctx->side);
+    FM_HIP_CHECK(hipEventRecord(b->ready, ctx->side));
+    b->prepared = true;
+    return FM_OK;
+  });
+}
+
 int64_t fm_batch_rows(const fm_batch* b) { return b ? b->dev.n_rows : -1; }
 int64_t fm_batch_nnz(const fm_batch* b) { return b ? b->dev.nnz : -1; }
 
-int fm_step_batch(fm_ctx* ctx, const fm_batch* batch, int32_t t, double step_size, double reg_param,
+int fm_step_batch(fm_ctx* ctx, fm_batch* batch, int32_t t, double step_size, double reg_param,
                   fm_step_out* out) {
   return guarded(ctx, [&]() -> int { return step_impl(ctx, batch, t, step_size, reg_param, out); });
 }

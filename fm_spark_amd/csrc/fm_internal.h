@@ -35,12 +35,13 @@ struct Error {
   } while (0)
 
 // -------------------------------------------------------------------- device table
-// Per feature row: a 16-byte header {w, t, cum} and the V row (stride kp = roundup(k, 4)
-// floats, 16-byte aligned; padding columns stay exactly 0 through every update).
+// Per feature row, one record aligned to a 64- or 128-byte line so that a random row access
+// costs one line (random gathers on MI355X are bound by 128-byte line requests):
+//   float V[kp]          kp = roundup(k, 4); padding columns stay exactly 0 through updates
+//   RowHdr {w, t, cum}   at float offset kp (16-byte aligned)
 //   t   : epoch (executed steps) through which the row is current; -1 = absent
 //   cum : sum of lambda over executed steps 1..t, i.e. the L1 shrink already applied.
-// A row read at epoch E is brought current by S_{cum[E] - cum} (lazy L1, see fm_kernels.hip);
-// keeping cum in the header avoids a dependent lookup of cum[t].
+// A row read at epoch E is brought current by S_{cum[E] - cum} (lazy L1, see fm_kernels.hip).
 struct alignas(16) RowHdr {
   float w;
   int32_t t;
@@ -48,14 +49,27 @@ struct alignas(16) RowHdr {
 };
 
 struct TableView {
-  RowHdr* hdr;     // [rows]
-  float* V;        // [rows * kp]
+  float* rec;      // [rows * stride]
   int64_t rows;    // local rows
   int32_t k;
   int32_t kp;
+  int32_t stride;  // record stride in floats (16 or 32, or a multiple of 32)
   int32_t shard_count;
   int32_t shard_index;
+  __host__ __device__ float* v(int64_t slot) const { return rec + slot * stride; }
+  __host__ __device__ RowHdr* hdr(int64_t slot) const {
+    return reinterpret_cast<RowHdr*>(rec + slot * stride + kp);
+  }
 };
+
+// record stride (floats) for k factors: the smallest 64 B / 128 B line that holds V + header,
+// else a multiple of 128 B
+inline int32_t record_stride(int32_t kp) {
+  const int32_t need = kp + 4;
+  if (need <= 16) return 16;
+  if (need <= 32) return 32;
+  return (need + 31) / 32 * 32;
+}
 
 // device buffer helper
 struct DevBuf {
@@ -80,10 +94,12 @@ struct SortWork {
 void radix_sort_pairs(SortWork& w, const uint32_t* keys_in, const uint32_t* vals_in, int64_t n,
                       int key_bits, hipStream_t st, const uint32_t** keys_out,
                       const uint32_t** vals_out);
-// Same with an 8-byte payload (e.g. the exploded entry {sample, x}).
+// Same with an 8-byte payload (e.g. the exploded entry {sample, x}).  When final_keys /
+// final_vals are given, the last pass writes there (a batch's own sorted view).
 void radix_sort_pairs64(SortWork& w, const uint32_t* keys_in, const uint2* vals_in, int64_t n,
                         int key_bits, hipStream_t st, const uint32_t** keys_out,
-                        const uint2** vals_out);
+                        const uint2** vals_out, uint32_t* final_keys = nullptr,
+                        uint2* final_vals = nullptr);
 
 // ---------------------------------------------------------------- step kernels
 // A device-resident mini-batch: the exploded (sampleId, featureId, featureValue) rows of

@@ -82,8 +82,6 @@ __global__ __launch_bounds__(kBlock) void k_forward(TableView T, const int64_t* 
   const int rs = tl / GS;
   const int kp = T.kp;
   const bool qok = g * 4 < kp;
-  const float4* __restrict__ V4 = reinterpret_cast<const float4*>(T.V);
-  const int nq = kp >> 2;
   double loss_acc = 0.0, nloss = 0.0;
 
   for (int64_t s = (int64_t)blockIdx.x * TPB + tid / TEAM; s < B; s += (int64_t)gridDim.x * TPB) {
@@ -105,8 +103,8 @@ __global__ __launch_bounds__(kBlock) void k_forward(TableView T, const int64_t* 
 #pragma unroll
       for (int j = 0; j < U; ++j) {
         if (ok[j]) {
-          h[j] = T.hdr[id[j]];
-          v[j] = qok ? V4[(int64_t)id[j] * nq + g] : make_float4(0.f, 0.f, 0.f, 0.f);
+          h[j] = *T.hdr(id[j]);
+          v[j] = qok ? reinterpret_cast<const float4*>(T.v(id[j]))[g] : make_float4(0.f, 0.f, 0.f, 0.f);
         } else {
           h[j] = RowHdr{0.f, -1, 0.0};
           v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -242,7 +240,7 @@ __global__ __launch_bounds__(kBlock) void k_segment_update(SegArgs a) {
   const int s = (int)en.x;
   const float xf = __uint_as_float(en.y);
   const double x = (double)xf;
-  const RowHdr h = valid ? T.hdr[key] : RowHdr{0.f, -1, 0.0};  // read before any write-back
+  const RowHdr h = valid ? (*T.hdr(key)) : RowHdr{0.f, -1, 0.0};  // read before any write-back
   const float2 yl = valid ? a.yl[s] : make_float2(0.f, 0.f);
 
   const bool seg_start = valid && key != prev_key;  // a run of this key starts here
@@ -282,7 +280,7 @@ __global__ __launch_bounds__(kBlock) void k_segment_update(SegArgs a) {
       o.w = upd_w(w, gw, a.p);  // SGD.scala:150, :171, :179
       o.t = a.p.epoch + 1;
       o.cum = a.p.cum_next;
-      T.hdr[key] = o;
+      (*T.hdr(key)) = o;
     } else {
       a.part[(chunk * 2 + slot) * (int64_t)(kp + 1)] = gw;
     }
@@ -293,7 +291,6 @@ __global__ __launch_bounds__(kBlock) void k_segment_update(SegArgs a) {
   const int flags = (valid ? 1 : 0) | (piece_tail ? 2 : 0) | (complete ? 4 : 0) | (present ? 8 : 0) |
                     (slot << 4) | (start_lane << 8);
   const float4* __restrict__ S4 = reinterpret_cast<const float4*>(a.S);
-  float4* __restrict__ V4 = reinterpret_cast<float4*>(T.V);
   const int q_in = lane % G;   // this lane's quad inside a quad-chunk
   const int j_in = lane / G;   // this lane's entry inside a round
   const bool ab_s = a.ablate & 2, ab_v = a.ablate & 4;
@@ -312,7 +309,8 @@ __global__ __launch_bounds__(kBlock) void k_segment_update(SegArgs a) {
       const bool vj = (fl & 1) && qok;
       const int sl = fl >> 8;
       float4 sq = (vj && !ab_s) ? S4[(int64_t)sj * nq + q] : make_float4(xj, 0.f, 0.f, 0.f);
-      float4 v = (vj && !ab_v && (fl & 8)) ? V4[(int64_t)kj * nq + q] : make_float4(0.f, 0.f, 0.f, 0.f);
+      float4 v = (vj && !ab_v && (fl & 8)) ? reinterpret_cast<const float4*>(T.v(kj))[q]
+                                           : make_float4(0.f, 0.f, 0.f, 0.f);
       if (acj > 0.0) v = shrink4(v, acj);
       const double xd = xj;
       double c0 = vj ? ((double)sq.x * xd - ((double)v.x * xd) * xd) * rj : 0.0;
@@ -339,7 +337,7 @@ __global__ __launch_bounds__(kBlock) void k_segment_update(SegArgs a) {
       if (ab_w) asm volatile("" ::"v"(c0), "v"(c1), "v"(c2), "v"(c3));
       if (vj && (fl & 2) && !ab_w) {
         if (fl & 4) {
-          V4[(int64_t)kj * nq + q] =
+          reinterpret_cast<float4*>(T.v(kj))[q] =
               make_float4(upd_v(v.x, c0, a.p), upd_v(v.y, c1, a.p), upd_v(v.z, c2, a.p), upd_v(v.w, c3, a.p));
         } else {
           double* prow = a.part + (((chunk * 2 + ((fl >> 4) & 1)) * (int64_t)(kp + 1)) + 1 + 4 * q);
@@ -407,8 +405,40 @@ __global__ __launch_bounds__(kBlock) void k_segment_combine(SegArgs a, const dou
       owner = a.skeys[p1] == key && !(a.skeys[p0] == key && p0 > 0 && a.skeys[p0 - 1] == key);
     }
   }
-  uint64_t owners = __ballot(owner);
   const TableView& T = a.T;
+  // common case: the run ends inside the next chunk -> this lane combines the two partials
+  bool two = false;
+  if (owner) {
+    const int64_t c2 = chunk + 2;
+    two = !(c2 < a.nchunks && a.skeys[c2 * 64] == key);
+  }
+  if (owner && two) {
+    const double* pt = a.part + (chunk * 2 + 1) * W;
+    const double* ph = a.part + ((chunk + 1) * 2) * W;
+    const RowHdr h = *T.hdr(key);
+    const bool present = h.t >= 0;
+    const double ac = present ? a.p.cumE - h.cum : 0.0;
+    float w = present ? h.w : 0.f;
+    if (ac > 0.0) w = shrink_f(w, ac);
+    float* vrow = T.v(key);
+    for (int q = 0; q < (kp >> 2); ++q) {
+      float4 v = present ? reinterpret_cast<const float4*>(vrow)[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+      if (ac > 0.0) v = shrink4(v, ac);
+      const double g0 = pt[1 + 4 * q + 0] + ph[1 + 4 * q + 0];
+      const double g1 = pt[1 + 4 * q + 1] + ph[1 + 4 * q + 1];
+      const double g2 = pt[1 + 4 * q + 2] + ph[1 + 4 * q + 2];
+      const double g3 = pt[1 + 4 * q + 3] + ph[1 + 4 * q + 3];
+      reinterpret_cast<float4*>(vrow)[q] =
+          make_float4(upd_v(v.x, g0, a.p), upd_v(v.y, g1, a.p), upd_v(v.z, g2, a.p), upd_v(v.w, g3, a.p));
+    }
+    RowHdr o;
+    o.w = upd_w(w, pt[0] + ph[0], a.p);
+    o.t = a.p.epoch + 1;
+    o.cum = a.p.cum_next;
+    *T.hdr(key) = o;
+  }
+  // long runs (hot features): one wave per run, lanes over the k+1 columns, chunk order
+  uint64_t owners = __ballot(owner && !two);
   while (owners) {
     const int l = __ffsll((unsigned long long)owners) - 1;
     owners &= owners - 1;
@@ -427,7 +457,7 @@ __global__ __launch_bounds__(kBlock) void k_segment_combine(SegArgs a, const dou
       cend += __ffsll((unsigned long long)~m) - 1;
       break;
     }
-    const RowHdr h = T.hdr[k0];
+    const RowHdr h = *T.hdr(k0);
     const bool present = h.t >= 0;
     const double ac = present ? a.p.cumE - h.cum : 0.0;
     float wnew = 0.f;
@@ -452,9 +482,9 @@ __global__ __launch_bounds__(kBlock) void k_segment_combine(SegArgs a, const dou
           if (ac > 0.0) w = shrink_f(w, ac);
           wnew = upd_w(w, g, a.p);
         } else {
-          float v = present ? T.V[(int64_t)k0 * kp + (f - 1)] : 0.f;
+          float v = present ? T.v(k0)[f - 1] : 0.f;
           if (ac > 0.0) v = shrink_f(v, ac);
-          T.V[(int64_t)k0 * kp + (f - 1)] = upd_v(v, g, a.p);
+          T.v(k0)[f - 1] = upd_v(v, g, a.p);
         }
       }
     }
@@ -463,7 +493,7 @@ __global__ __launch_bounds__(kBlock) void k_segment_combine(SegArgs a, const dou
       o.w = wnew;
       o.t = a.p.epoch + 1;
       o.cum = a.p.cum_next;
-      T.hdr[k0] = o;
+      *T.hdr(k0) = o;
     }
   }
 }
@@ -498,8 +528,8 @@ __global__ void k_init_random(TableView T, const int32_t* __restrict__ ids, int6
     o.w = gauss_draw(seed, id, -1, sd);
     o.t = epoch;
     o.cum = cumE;
-    for (int f = 0; f < T.kp; ++f) T.V[slot * T.kp + f] = f < T.k ? gauss_draw(seed, id, f, sd) : 0.f;
-    T.hdr[slot] = o;
+    for (int f = 0; f < T.kp; ++f) T.v(slot)[f] = f < T.k ? gauss_draw(seed, id, f, sd) : 0.f;
+    (*T.hdr(slot)) = o;
   }
 }
 
@@ -514,35 +544,35 @@ __global__ void k_load_rows(TableView T, const int32_t* __restrict__ ids, int64_
     o.w = (float)w[i];
     o.t = epoch;
     o.cum = cumE;
-    for (int f = 0; f < T.kp; ++f) T.V[slot * T.kp + f] = f < T.k ? (float)V[i * T.k + f] : 0.f;
-    T.hdr[slot] = o;
+    for (int f = 0; f < T.kp; ++f) T.v(slot)[f] = f < T.k ? (float)V[i * T.k + f] : 0.f;
+    (*T.hdr(slot)) = o;
   }
 }
 
 __global__ void k_table_reset(TableView T) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < T.rows; i += (int64_t)gridDim.x * blockDim.x)
-    T.hdr[i] = RowHdr{0.f, -1, 0.0};
+    (*T.hdr(i)) = RowHdr{0.f, -1, 0.0};
 }
 
 __global__ void k_flush(TableView T, int32_t epoch, double cumE) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < T.rows; i += (int64_t)gridDim.x * blockDim.x) {
-    RowHdr h = T.hdr[i];
+    RowHdr h = (*T.hdr(i));
     if (h.t < 0) continue;
     const double a = cumE - h.cum;
     if (a > 0.0) {
       h.w = shrink_f(h.w, a);
-      for (int f = 0; f < T.kp; ++f) T.V[i * T.kp + f] = shrink_f(T.V[i * T.kp + f], a);
+      for (int f = 0; f < T.kp; ++f) T.v(i)[f] = shrink_f(T.v(i)[f], a);
     }
     h.t = epoch;
     h.cum = cumE;
-    T.hdr[i] = h;
+    (*T.hdr(i)) = h;
   }
 }
 
 __global__ void k_count_present(TableView T, unsigned long long* out) {
   unsigned long long c = 0;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < T.rows; i += (int64_t)gridDim.x * blockDim.x)
-    c += T.hdr[i].t >= 0 ? 1ull : 0ull;
+    c += (*T.hdr(i)).t >= 0 ? 1ull : 0ull;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
   if ((threadIdx.x & 63) == 0 && c) atomicAdd(out, c);
@@ -561,7 +591,7 @@ __global__ void k_predict(TableView T, const int64_t* __restrict__ row_ptr, cons
     for (int64_t e = row_ptr[s]; e < row_ptr[s + 1]; ++e) {
       const int64_t id = col[e];
       if (id >= num_features) continue;
-      const RowHdr h = T.hdr[id];
+      const RowHdr h = (*T.hdr(id));
       if (h.t < 0) continue;
       const double a = cumE - h.cum;
       const double x = (double)__uint_as_float(ent[e].y);
@@ -569,7 +599,7 @@ __global__ void k_predict(TableView T, const int64_t* __restrict__ row_ptr, cons
       wx += (double)w * x;
       double v2 = 0.0;
       for (int f = 0; f < T.k; ++f) {
-        float v = T.V[id * T.kp + f];
+        float v = T.v(id)[f];
         if (a > 0.0) v = shrink_f(v, a);
         acc[f & 63] += (double)v * x;  // k <= 64 on this path (checked on the host)
         v2 += (double)v * v;
@@ -600,7 +630,7 @@ __global__ void k_loss_grad(TableView T, const int64_t* __restrict__ row_ptr, co
     const int64_t e0 = row_ptr[s], e1 = row_ptr[s + 1];
     for (int64_t e = e0; e < e1; ++e) {
       const int64_t id = col[e];
-      const RowHdr h = T.hdr[id];
+      const RowHdr h = (*T.hdr(id));
       if (h.t < 0) {
         *absent = 1;
         continue;
@@ -611,7 +641,7 @@ __global__ void k_loss_grad(TableView T, const int64_t* __restrict__ row_ptr, co
       wx += (double)w * x;
       double v2 = 0.0;
       for (int f = 0; f < T.k; ++f) {
-        float v = T.V[id * T.kp + f];
+        float v = T.v(id)[f];
         if (a > 0.0) v = shrink_f(v, a);
         acc[f & 63] += (double)v * x;
         v2 += (double)v * v;
@@ -624,7 +654,7 @@ __global__ void k_loss_grad(TableView T, const int64_t* __restrict__ row_ptr, co
     const double d = yhat - (double)label[s];
     for (int64_t e = e0; e < e1; ++e) {
       const int64_t id = col[e];
-      const RowHdr h = T.hdr[id];
+      const RowHdr h = (*T.hdr(id));
       const double x = (double)__uint_as_float(ent[e].y);
       if (pred) pred[e] = yhat;
       if (loss) loss[e] = d * d;
@@ -632,7 +662,7 @@ __global__ void k_loss_grad(TableView T, const int64_t* __restrict__ row_ptr, co
       if (dv) {
         const double a = h.t >= 0 ? cumE - h.cum : 0.0;
         for (int f = 0; f < T.k; ++f) {
-          float v = h.t >= 0 ? T.V[id * T.kp + f] : 0.f;
+          float v = h.t >= 0 ? T.v(id)[f] : 0.f;
           if (a > 0.0) v = shrink_f(v, a);
           dv[e * T.k + f] = acc[f & 63] * x - ((double)v * x) * x;
         }
@@ -778,7 +808,7 @@ void launch_load_rows(const TableView& T, const int32_t* ids, int64_t n, const d
 
 void launch_table_reset(const TableView& T, hipStream_t st) {
   if (T.rows <= 0) return;
-  FM_HIP_CHECK(hipMemsetAsync(T.V, 0, sizeof(float) * (size_t)T.rows * T.kp, st));
+  FM_HIP_CHECK(hipMemsetAsync(T.rec, 0, sizeof(float) * (size_t)T.rows * T.stride, st));
   hipLaunchKernelGGL(k_table_reset, dim3(grid_for(T.rows, kBlock)), dim3(kBlock), 0, st, T);
   FM_HIP_CHECK(hipGetLastError());
 }

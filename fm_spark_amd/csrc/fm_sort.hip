@@ -219,7 +219,8 @@ void SortWork::ensure(int64_t n) {
 
 template <class P>
 static void radix_sort_impl(SortWork& w, const uint32_t* keys_in, const P* vals_in, int64_t n, int key_bits,
-                            hipStream_t st, const uint32_t** keys_out, const P** vals_out) {
+                            hipStream_t st, const uint32_t** keys_out, const P** vals_out,
+                            uint32_t* final_keys = nullptr, P* final_vals = nullptr) {
   FM_REQUIRE(n >= 0 && n < (int64_t(1) << 32) - 1, "sort size out of range");
   w.ensure(n > 0 ? n : 1);
   if (n == 0) {
@@ -247,12 +248,14 @@ static void radix_sort_impl(SortWork& w, const uint32_t* keys_in, const P* vals_
                        w.counts.as<uint32_t>(), ntiles);
     hipLaunchKernelGGL(k_radix_scan_rows, dim3(kRadix), dim3(kBlock), 0, st, w.counts.as<uint32_t>(),
                        ntiles, w.digit_tot.as<uint32_t>());
-    hipLaunchKernelGGL(k_radix_scatter<P>, dim3((unsigned)ntiles), dim3(kBlock), 0, st, kin, vin,
-                       kbuf[which], vbuf[which], n, shift, w.counts.as<uint32_t>(),
-                       w.digit_tot.as<uint32_t>(), ntiles);
+    const bool last = p == passes - 1 && final_keys != nullptr;
+    uint32_t* ko = last ? final_keys : kbuf[which];
+    P* vo = last ? final_vals : vbuf[which];
+    hipLaunchKernelGGL(k_radix_scatter<P>, dim3((unsigned)ntiles), dim3(kBlock), 0, st, kin, vin, ko, vo, n,
+                       shift, w.counts.as<uint32_t>(), w.digit_tot.as<uint32_t>(), ntiles);
     FM_HIP_CHECK(hipGetLastError());
-    kin = kbuf[which];
-    vin = vbuf[which];
+    kin = ko;
+    vin = vo;
     which ^= 1;
   }
   *keys_out = kin;
@@ -265,8 +268,9 @@ void radix_sort_pairs(SortWork& w, const uint32_t* keys_in, const uint32_t* vals
 }
 
 void radix_sort_pairs64(SortWork& w, const uint32_t* keys_in, const uint2* vals_in, int64_t n, int key_bits,
-                        hipStream_t st, const uint32_t** keys_out, const uint2** vals_out) {
-  radix_sort_impl<uint2>(w, keys_in, vals_in, n, key_bits, st, keys_out, vals_out);
+                        hipStream_t st, const uint32_t** keys_out, const uint2** vals_out, uint32_t* final_keys,
+                        uint2* final_vals) {
+  radix_sort_impl<uint2>(w, keys_in, vals_in, n, key_bits, st, keys_out, vals_out, final_keys, final_vals);
 }
 
 }  // namespace fmhip

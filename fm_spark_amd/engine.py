@@ -34,6 +34,10 @@ class DeviceBatch:
         self.n_rows = csr.n_rows
         self.nnz = csr.nnz
 
+    def prepare(self):
+        """Sort this batch by feature on the side stream ahead of its step (fm_batch_prepare)."""
+        N.check(self._lib.fm_batch_prepare(self.ctx.handle, self.handle), "fm_batch_prepare")
+
     def close(self):
         if self.handle:
             self._lib.fm_batch_destroy(self.handle)

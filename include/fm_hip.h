@@ -111,6 +111,12 @@ int64_t fm_epoch(fm_ctx* ctx);
 /* Copy a CSR batch into device memory once (validated: ids in range, row_ptr monotone). */
 int fm_batch_create(fm_ctx* ctx, const fm_csr* csr, fm_batch** out);
 void fm_batch_destroy(fm_batch* b);
+/* Sort the batch's entries by feature (the grouping the gradient reduction consumes) ahead
+ * of its step, on the context's side stream, so the sort overlaps whatever the previous step
+ * still runs (input prefetch).  The prepared order is consumed by the next fm_step_batch on
+ * this batch; a batch that was not prepared is sorted inside its step.  Stream-ordered, no
+ * host synchronisation. */
+int fm_batch_prepare(fm_ctx* ctx, fm_batch* batch);
 int64_t fm_batch_rows(const fm_batch* b);
 int64_t fm_batch_nnz(const fm_batch* b);
 
@@ -128,7 +134,7 @@ int64_t fm_batch_nnz(const fm_batch* b);
  * see fm_loss_history). */
 int fm_step(fm_ctx* ctx, const fm_csr* batch, int32_t t, double step_size, double reg_param,
             fm_step_out* out);
-int fm_step_batch(fm_ctx* ctx, const fm_batch* batch, int32_t t, double step_size,
+int fm_step_batch(fm_ctx* ctx, fm_batch* batch, int32_t t, double step_size,
                   double reg_param, fm_step_out* out);
 /* Per-step loss sums of every executed step so far (SGD.scala:139 log line). */
 int fm_loss_history(fm_ctx* ctx, double* loss, int64_t cap, int64_t* n);

@@ -219,3 +219,30 @@ def test_init_random_matches_oracle_draw(gpu):
     order = np.argsort(ids)
     np.testing.assert_allclose(gw, rw[order], rtol=1e-6)
     np.testing.assert_allclose(gV, rV[order], rtol=1e-6)
+
+
+def test_prepared_batches_bitwise_equal(gpu):
+    """fm_batch_prepare (sort ahead on the side stream) changes scheduling only."""
+    from fm_spark_amd.engine import FMContext
+
+    F, k = 3000, 16
+    csrs = [make_problem(400 + i, 1500, F, k, 12, hot=5)[0] for i in range(3)]
+    _, ids, w, V = make_problem(10, 1, F, k, 1)
+    outs = []
+    for prep in (False, True):
+        ctx = FMContext(F, k)
+        ctx.load_tables(ids, w, V)
+        dbs = [ctx.batch(to_host(c)) for c in csrs]
+        if prep:
+            dbs[0].prepare()
+        for i in range(6):
+            if prep and i + 1 < 6:
+                dbs[(i + 1) % 3].prepare()
+            ctx.step_batch(dbs[i % 3], i + 1, 0.2, 1e-5, sync=False)
+        ctx.sync()
+        outs.append((ctx.export_tables(), ctx.loss_history()))
+        ctx.close()
+    (a, la), (b, lb) = outs
+    for x, y in zip(a, b):
+        assert np.array_equal(x, y)
+    assert np.array_equal(la, lb)

@@ -1,0 +1,74 @@
+// Measurement tool (not product): time the library's radix_sort_pairs64 against rocPRIM's
+// device radix sort on the same 10M (uint32 key, uint64 payload) pairs, 27-bit keys.
+#include <hip/hip_runtime.h>
+#include <cstring>
+#include <rocprim/device/device_radix_sort.hpp>
+
+#include <cstdio>
+#include <cstdlib>
+#include <random>
+#include <vector>
+
+#include "../fm_spark_amd/csrc/fm_internal.h"
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s line %d\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)
+
+int main(int argc, char** argv) {
+  const int64_t n = argc > 1 ? atoll(argv[1]) : 10223616;
+  const int bits = argc > 2 ? atoi(argv[2]) : 27;
+  std::mt19937_64 rng(1);
+  std::vector<uint32_t> keys(n);
+  std::vector<uint2> vals(n);
+  for (int64_t i = 0; i < n; ++i) {
+    // 40% of keys from a small hot set (Zipf-like skew), the rest uniform
+    uint64_t r = rng();
+    keys[i] = (r % 10 < 4) ? (uint32_t)((r >> 8) % 1000) * 99991u % (1u << bits) : (uint32_t)((r >> 8) % (1u << bits));
+    vals[i] = make_uint2((uint32_t)i, (uint32_t)(r >> 32));
+  }
+  uint32_t *dk, *dk2;
+  uint2 *dv, *dv2;
+  CK(hipMalloc(&dk, 4 * n)); CK(hipMalloc(&dk2, 4 * n));
+  CK(hipMalloc(&dv, 8 * n)); CK(hipMalloc(&dv2, 8 * n));
+  CK(hipMemcpy(dk, keys.data(), 4 * n, hipMemcpyHostToDevice));
+  CK(hipMemcpy(dv, vals.data(), 8 * n, hipMemcpyHostToDevice));
+  hipStream_t st;
+  CK(hipStreamCreate(&st));
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
+  // rocPRIM
+  size_t tmp = 0;
+  CK(rocprim::radix_sort_pairs(nullptr, tmp, dk, dk2, dv, dv2, (size_t)n, 0, bits, st));
+  void* dtmp;
+  CK(hipMalloc(&dtmp, tmp));
+  for (int w = 0; w < 3; ++w) CK(rocprim::radix_sort_pairs(dtmp, tmp, dk, dk2, dv, dv2, (size_t)n, 0, bits, st));
+  const int R = 20;
+  CK(hipEventRecord(a, st));
+  for (int r = 0; r < R; ++r) CK(rocprim::radix_sort_pairs(dtmp, tmp, dk, dk2, dv, dv2, (size_t)n, 0, bits, st));
+  CK(hipEventRecord(b, st));
+  CK(hipEventSynchronize(b));
+  float ms;
+  CK(hipEventElapsedTime(&ms, a, b));
+  printf("rocprim radix_sort_pairs n=%lld bits=%d: %.3f ms\n", (long long)n, bits, ms / R);
+  // ours
+  fmhip::SortWork sw;
+  const uint32_t* ok;
+  const uint2* ov;
+  for (int w = 0; w < 3; ++w) fmhip::radix_sort_pairs64(sw, dk, dv, n, bits, st, &ok, &ov);
+  CK(hipEventRecord(a, st));
+  for (int r = 0; r < R; ++r) fmhip::radix_sort_pairs64(sw, dk, dv, n, bits, st, &ok, &ov);
+  CK(hipEventRecord(b, st));
+  CK(hipEventSynchronize(b));
+  CK(hipEventElapsedTime(&ms, a, b));
+  printf("fm_hip radix_sort_pairs64 n=%lld bits=%d: %.3f ms\n", (long long)n, bits, ms / R);
+  // check equality
+  std::vector<uint32_t> k1(n), k2(n);
+  std::vector<uint2> v1(n), v2(n);
+  CK(hipMemcpy(k1.data(), dk2, 4 * n, hipMemcpyDeviceToHost));
+  CK(hipMemcpy(k2.data(), ok, 4 * n, hipMemcpyDeviceToHost));
+  CK(hipMemcpy(v1.data(), dv2, 8 * n, hipMemcpyDeviceToHost));
+  CK(hipMemcpy(v2.data(), ov, 8 * n, hipMemcpyDeviceToHost));
+  int64_t bad = 0;
+  for (int64_t i = 0; i < n; ++i) bad += (k1[i] != k2[i]) || (v1[i].x != v2[i].x) || (v1[i].y != v2[i].y);
+  printf("mismatches vs rocprim (both stable): %lld\n", (long long)bad);
+  return 0;
+}
