@@ -99,7 +99,7 @@ SIGNATURES = {
     "fm_shard_plan": (C.c_int, [_P, _P, _I64P]),
     "fm_shard_request_copy": (C.c_int, [_P, _P]),
     "fm_shard_serve_device": (C.c_int, [_P, _P, C.c_int64, _P]),
-    "fm_shard_local_grad_device": (C.c_int, [_P, _P, _P, _P, C.c_int64]),
+    "fm_shard_local_grad_device": (C.c_int, [_P, _P, _P, _P]),
     "fm_shard_apply_device": (
         C.c_int, [_P, _P, _P, C.c_int64, C.c_int32, C.c_double, C.c_double, C.c_int64]),
     "fm_shard_last_loss": (C.c_int, [_P, _DP, _I64P]),

@@ -9,7 +9,7 @@
 #include <memory>
 #include <utility>
 
-#include "fm_internal.h"
+#include "fm_context.h"
 
 namespace fmhip {
 
@@ -28,240 +28,6 @@ void DevBuf::release() {
   if (p) (void)hipFree(p);
   p = nullptr;
   bytes = 0;
-}
-
-// Pinned host staging for small device->host reads.
-struct Pinned {
-  void* p = nullptr;
-  size_t bytes = 0;
-  void ensure(size_t n) {
-    if (n <= bytes && p) return;
-    if (p) (void)hipHostFree(p);
-    p = nullptr;
-    FM_HIP_CHECK(hipHostMalloc(&p, n, hipHostMallocDefault));
-    bytes = n;
-  }
-  ~Pinned() {
-    if (p) (void)hipHostFree(p);
-  }
-};
-
-struct ProfEntry {
-  double ms = 0.0;
-  int64_t n = 0;
-};
-
-}  // namespace fmhip
-
-using namespace fmhip;
-
-struct fm_batch {
-  fm_ctx* owner = nullptr;
-  int device = 0;
-  BatchDev dev;
-  int64_t max_id = -1;
-  // feature-major view produced by fm_batch_prepare (consumed once by the next step)
-  DevBuf skeys, sents;
-  hipEvent_t ready = nullptr;     // recorded on the side stream after the prepared sort
-  hipEvent_t last_use = nullptr;  // recorded on the main stream after a step read skeys/sents
-  bool prepared = false;
-  ~fm_batch() {
-    (void)hipSetDevice(device);
-    if (ready) (void)hipEventSynchronize(ready);
-    if (last_use) (void)hipEventSynchronize(last_use);
-    if (ready) (void)hipEventDestroy(ready);
-    if (last_use) (void)hipEventDestroy(last_use);
-    skeys.release();
-    sents.release();
-    dev.row_ptr.release();
-    dev.col.release();
-    dev.ent.release();
-    dev.label.release();
-  }
-};
-
-struct fm_ctx {
-  std::mutex mu;
-  fm_config cfg{};
-  int32_t kp = 0;
-  int64_t rows = 0;  // local rows
-  hipStream_t stream = nullptr;
-  bool own_stream = false;
-  hipStream_t side = nullptr;  // the entry sort runs here, overlapped with the forward
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-  hipEvent_t ev_upd_done = nullptr;  // last main-stream read of the shared sort workspace
-  DevBuf rec;  // [rows * stride] float records (V row + header)
-  int32_t stride = 0;
-  std::vector<double> cum_host{0.0};  // cum[e] = sum of lambda over executed steps 1..e
-  int32_t epoch = 0;
-  DevBuf loss_hist;  // [hist_cap][3] double {loss, n_loss, n_unique}
-  int64_t hist_cap = 0;
-  StepWork work;
-  Pinned pinned;
-  // profiling
-  bool prof = false;
-  std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> pending;
-  std::vector<hipEvent_t> free_events;
-  std::map<std::string, ProfEntry> prof_acc;
-  std::vector<std::string> prof_order;
-  // sharded step state
-  DevBuf plan_req;      // [U] int32 local slots, owner-major
-  DevBuf plan_uidx;     // [N] uint32 unique index per entry (CSR order)
-  DevBuf plan_ukey;     // [U] uint32 composite keys (sorted)
-  DevBuf plan_counts;   // [shard_count] int64
-  DevBuf rows_local;    // scratch
-  int64_t plan_unique = 0;
-  int64_t plan_nnz = 0;
-  double last_loss = 0.0;
-  int64_t last_nloss = 0;
-
-  TableView view() const {
-    TableView T;
-    T.rec = rec.as<float>();
-    T.rows = rows;
-    T.stride = stride;
-    T.k = cfg.k;
-    T.kp = kp;
-    T.shard_count = cfg.shard_count;
-    T.shard_index = cfg.shard_index;
-    return T;
-  }
-
-  hipEvent_t get_event() {
-    if (!free_events.empty()) {
-      hipEvent_t e = free_events.back();
-      free_events.pop_back();
-      return e;
-    }
-    hipEvent_t e;
-    FM_HIP_CHECK(hipEventCreate(&e));
-    return e;
-  }
-
-  // RAII-free helpers: begin() records a start event, end() the stop event for `name`.
-  hipEvent_t prof_begin(hipStream_t s) {
-    if (!prof) return nullptr;
-    hipEvent_t e = get_event();
-    FM_HIP_CHECK(hipEventRecord(e, s));
-    return e;
-  }
-  void prof_end(const char* name, hipEvent_t e0, hipStream_t s) {
-    if (!prof || !e0) return;
-    hipEvent_t e1 = get_event();
-    FM_HIP_CHECK(hipEventRecord(e1, s));
-    pending.push_back({name, {e0, e1}});
-    if (pending.size() > 4096) resolve_profile();
-  }
-  void resolve_profile() {
-    if (pending.empty()) return;
-    FM_HIP_CHECK(hipStreamSynchronize(stream));
-    FM_HIP_CHECK(hipStreamSynchronize(side));
-    for (auto& pe : pending) {
-      float ms = 0.f;
-      FM_HIP_CHECK(hipEventElapsedTime(&ms, pe.second.first, pe.second.second));
-      auto it = prof_acc.find(pe.first);
-      if (it == prof_acc.end()) {
-        prof_order.push_back(pe.first);
-        it = prof_acc.emplace(pe.first, ProfEntry{}).first;
-      }
-      it->second.ms += ms;
-      it->second.n += 1;
-      free_events.push_back(pe.second.first);
-      free_events.push_back(pe.second.second);
-    }
-    pending.clear();
-  }
-
-  void ensure_hist(int64_t need) {
-    if (need <= hist_cap) return;
-    int64_t c = std::max<int64_t>(4096, hist_cap);
-    while (c < need) c *= 2;
-    FM_HIP_CHECK(hipStreamSynchronize(stream));
-    DevBuf nb;
-    nb.ensure(sizeof(double) * 3 * c);
-    FM_HIP_CHECK(hipMemset(nb.p, 0, sizeof(double) * 3 * c));
-    if (hist_cap > 0)
-      FM_HIP_CHECK(hipMemcpy(nb.p, loss_hist.p, sizeof(double) * 3 * hist_cap, hipMemcpyDeviceToDevice));
-    loss_hist.release();
-    loss_hist = nb;
-    nb.p = nullptr;
-    hist_cap = c;
-  }
-
-  ~fm_ctx() {
-    (void)hipSetDevice(cfg.device);
-    if (stream) (void)hipStreamSynchronize(stream);
-    for (auto& pe : pending) {
-      (void)hipEventDestroy(pe.second.first);
-      (void)hipEventDestroy(pe.second.second);
-    }
-    for (auto e : free_events) (void)hipEventDestroy(e);
-    if (side) (void)hipStreamSynchronize(side);
-    if (ev_fork) (void)hipEventDestroy(ev_fork);
-    if (ev_join) (void)hipEventDestroy(ev_join);
-    if (ev_upd_done) (void)hipEventDestroy(ev_upd_done);
-    if (side) (void)hipStreamDestroy(side);
-    rec.release();
-    loss_hist.release();
-    DevBuf* bufs[] = {&work.S, &work.yl, &work.loss_part, &work.part, &work.ucnt,
-                      &work.sort.keys_a, &work.sort.keys_b, &work.sort.vals_a, &work.sort.vals_b,
-                      &work.sort.counts, &work.sort.digit_tot, &plan_req, &plan_uidx, &plan_ukey,
-                      &plan_counts, &rows_local};
-    for (auto* b : bufs) b->release();
-    if (own_stream && stream) (void)hipStreamDestroy(stream);
-  }
-};
-
-namespace {
-
-template <class F>
-int guarded(fm_ctx* ctx, F&& f) {
-  if (!ctx) {
-    set_error("null fm_ctx");
-    return FM_ERR_ARG;
-  }
-  std::lock_guard<std::mutex> lk(ctx->mu);
-  try {
-    FM_HIP_CHECK(hipSetDevice(ctx->cfg.device));
-    return f();
-  } catch (const Error& e) {
-    set_error(e.msg);
-    return e.code;
-  } catch (const std::bad_alloc&) {
-    set_error("host allocation failed");
-    return FM_ERR_OOM;
-  } catch (const std::exception& e) {
-    set_error(e.what());
-    return FM_ERR_HIP;
-  } catch (...) {
-    set_error("unknown error");
-    return FM_ERR_HIP;
-  }
-}
-
-template <class F>
-int guarded_free(F&& f) {
-  try {
-    return f();
-  } catch (const Error& e) {
-    set_error(e.msg);
-    return e.code;
-  } catch (const std::bad_alloc&) {
-    set_error("host allocation failed");
-    return FM_ERR_OOM;
-  } catch (const std::exception& e) {
-    set_error(e.what());
-    return FM_ERR_HIP;
-  } catch (...) {
-    set_error("unknown error");
-    return FM_ERR_HIP;
-  }
-}
-
-int bits_for(int64_t max_value) {
-  int b = 1;
-  while (b < 63 && (int64_t(1) << b) <= max_value) ++b;
-  return b;
 }
 
 // Validates and uploads a host CSR.  check_range: ids must be owned by this context's
@@ -334,6 +100,10 @@ void reserve_work(fm_ctx* ctx, int64_t B, int64_t N) {
   w.ucnt.ensure(sizeof(uint32_t) * (size_t)std::max<int64_t>((nchunks + 3) / 4, 1));
   w.loss_part.ensure(sizeof(double) * 2 * 256 * 8);
 }
+
+}  // namespace fmhip
+
+namespace {
 
 int step_impl(fm_ctx* ctx, fm_batch* b, int32_t t, double step_size, double reg_param, fm_step_out* out) {
   FM_REQUIRE(b != nullptr, "null batch");
@@ -455,13 +225,9 @@ int fm_set_stream(fm_ctx* ctx, void* s) {
   return guarded(ctx, [&]() -> int {
     FM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
     if (ctx->own_stream && ctx->stream) FM_HIP_CHECK(hipStreamDestroy(ctx->stream));
-    if (s) {
-      ctx->stream = reinterpret_cast<hipStream_t>(s);
-      ctx->own_stream = false;
-    } else {
-      FM_HIP_CHECK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
-      ctx->own_stream = true;
-    }
+    // NULL selects the device's default (null) stream, which is what torch's default stream is
+    ctx->stream = reinterpret_cast<hipStream_t>(s);
+    ctx->own_stream = false;
     return FM_OK;
   });
 }

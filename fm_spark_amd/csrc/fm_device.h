@@ -1,0 +1,45 @@
+// Device helpers shared by the step kernels (fm_kernels.hip) and the sharded path
+// (fm_shard.hip).
+#pragma once
+
+#include "fm_internal.h"
+
+namespace fmhip {
+
+__device__ __forceinline__ float shrink_f(float z, double a) {
+  // signum(z) * max(0, |z| - a) (FactorizationMachinesSGD.scala:104, :179), in fp64.
+  const double az = fabs((double)z) - a;
+  return az > 0.0 ? (float)copysign(az, (double)z) : 0.0f * z;
+}
+
+__device__ __forceinline__ double shrink_d(double z, double a) {
+  const double az = fabs(z) - a;
+  return az > 0.0 ? copysign(az, z) : 0.0 * z;
+}
+
+__device__ __forceinline__ float4 shrink4(float4 v, double a) {
+  return make_float4(shrink_f(v.x, a), shrink_f(v.y, a), shrink_f(v.z, a), shrink_f(v.w, a));
+}
+
+// Inclusive segmented scan over lanes [start_lane, lane] in a fixed tree order.  nsteps is the
+// wave-uniform depth the longest piece needs; the skipped steps would add nothing, so the
+// result is bitwise that of the full 6-step scan.
+__device__ __forceinline__ double seg_scan(double v, int lane, int start_lane, int nsteps) {
+  for (int i = 0; i < nsteps; ++i) {
+    const int o = 1 << i;
+    const double t = __shfl_up(v, o);
+    if (lane - o >= start_lane) v += t;
+  }
+  return v;
+}
+
+// Row update of SGD.scala:150-181, fp64:
+//   vec' = S_lambda(vec - sum * (eta / m));  strength' = S_lambda(strength - (sum / m) * eta)
+__device__ __forceinline__ float upd_v(float v, double g, const StepParams& p) {
+  return (float)shrink_d((double)v - g * p.scale_v, p.lam);
+}
+__device__ __forceinline__ float upd_w(float w, double g, const StepParams& p) {
+  return (float)shrink_d((double)w - (g / p.m) * p.eta, p.lam);
+}
+
+}  // namespace fmhip

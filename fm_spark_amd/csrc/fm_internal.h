@@ -131,7 +131,8 @@ struct StepParams {
 };
 
 void launch_forward(const TableView& T, const BatchDev& b, StepWork& w, const StepParams& p,
-                    hipStream_t st, int64_t* n_fwd_blocks);
+                    hipStream_t st, int64_t* n_fwd_blocks, const float* rows = nullptr,
+                    const uint32_t* uidx = nullptr);
 void launch_segment_update(const TableView& T, const BatchDev& b, StepWork& w, const StepParams& p,
                            const uint32_t* skeys, const uint2* sents, int64_t n_fwd_blocks,
                            double* stats_out, hipStream_t st);

@@ -27,28 +27,13 @@
 // brought current by S_{cumE - cum}.  Export flushes every row.
 #include <cstdlib>
 
-#include "fm_internal.h"
+#include "fm_device.h"
 
 namespace fmhip {
 
 namespace {
 
 constexpr int kBlock = 256;
-
-__device__ __forceinline__ float shrink_f(float z, double a) {
-  // signum(z) * max(0, |z| - a) (FactorizationMachinesSGD.scala:104, :179), in fp64.
-  const double az = fabs((double)z) - a;
-  return az > 0.0 ? (float)copysign(az, (double)z) : 0.0f * z;
-}
-
-__device__ __forceinline__ double shrink_d(double z, double a) {
-  const double az = fabs(z) - a;
-  return az > 0.0 ? copysign(az, z) : 0.0 * z;
-}
-
-__device__ __forceinline__ float4 shrink4(float4 v, double a) {
-  return make_float4(shrink_f(v.x, a), shrink_f(v.y, a), shrink_f(v.z, a), shrink_f(v.w, a));
-}
 
 // The row header and one V quad brought current (absent rows read as zero).
 __device__ __forceinline__ void current_row(const RowHdr& h, float4& v, float& w, double cumE) {
@@ -66,8 +51,13 @@ __device__ __forceinline__ void current_row(const RowHdr& h, float4& v, float& w
 }
 
 // ------------------------------------------------------------------------ forward
-template <int GS, int TEAM>
-__global__ __launch_bounds__(kBlock) void k_forward(TableView T, const int64_t* __restrict__ row_ptr,
+// FROM_ROWS: the sharded step's forward; entry e's row is rows[uidx[e]] of the rows this rank
+// received from the owners (already current, wire layout [V(kp) | w | pad]) instead of the
+// local table.
+template <int GS, int TEAM, bool FROM_ROWS>
+__global__ __launch_bounds__(kBlock) void k_forward(TableView T, const float* __restrict__ rows,
+                                                    const uint32_t* __restrict__ uidx,
+                                                    const int64_t* __restrict__ row_ptr,
                                                     const uint32_t* __restrict__ col,
                                                     const uint2* __restrict__ ent,
                                                     const float* __restrict__ label, int64_t B,
@@ -100,9 +90,14 @@ __global__ __launch_bounds__(kBlock) void k_forward(TableView T, const int64_t* 
       }
       RowHdr h[U];
       float4 v[U];
+      float wr[U];
 #pragma unroll
       for (int j = 0; j < U; ++j) {
-        if (ok[j]) {
+        if (FROM_ROWS) {
+          const float* row = rows + (int64_t)(ok[j] ? uidx[eb + j * RPP] : 0u) * (kp + 4);
+          v[j] = (ok[j] && qok) ? reinterpret_cast<const float4*>(row)[g] : make_float4(0.f, 0.f, 0.f, 0.f);
+          wr[j] = ok[j] ? row[kp] : 0.f;
+        } else if (ok[j]) {
           h[j] = *T.hdr(id[j]);
           v[j] = qok ? reinterpret_cast<const float4*>(T.v(id[j]))[g] : make_float4(0.f, 0.f, 0.f, 0.f);
         } else {
@@ -113,7 +108,8 @@ __global__ __launch_bounds__(kBlock) void k_forward(TableView T, const int64_t* 
 #pragma unroll
       for (int j = 0; j < U; ++j) {
         float w;
-        current_row(h[j], v[j], w, cumE);
+        if (FROM_ROWS) w = wr[j];
+        else current_row(h[j], v[j], w, cumE);
         const double xd = x[j];
         // vfxi = v * x (Model.scala:179), VectorSum over the sample (:191)
         a0 += (double)v[j].x * xd; a1 += (double)v[j].y * xd;
@@ -189,27 +185,6 @@ struct SegArgs {
   uint32_t* ucnt;  // [update blocks]
   int ablate;      // diagnostic ablation bits (FM_ABLATE); 0 in production
 };
-
-// Inclusive segmented scan over lanes [start_lane, lane] in a fixed tree order.  nsteps is the
-// wave-uniform depth the longest piece needs; the skipped steps would add nothing, so the
-// result is bitwise that of the full 6-step scan.
-__device__ __forceinline__ double seg_scan(double v, int lane, int start_lane, int nsteps) {
-  for (int i = 0; i < nsteps; ++i) {
-    const int o = 1 << i;
-    const double t = __shfl_up(v, o);
-    if (lane - o >= start_lane) v += t;
-  }
-  return v;
-}
-
-// Row update of SGD.scala:150-181, fp64:
-//   vec' = S_lambda(vec - sum * (eta / m));  strength' = S_lambda(strength - (sum / m) * eta)
-__device__ __forceinline__ float upd_v(float v, double g, const StepParams& p) {
-  return (float)shrink_d((double)v - g * p.scale_v, p.lam);
-}
-__device__ __forceinline__ float upd_w(float w, double g, const StepParams& p) {
-  return (float)shrink_d((double)w - (g / p.m) * p.eta, p.lam);
-}
 
 // One wave per chunk of 64 sorted entries.
 //  Phase 1, one lane per entry: run structure (pieces of equal keys inside the chunk), the
@@ -726,14 +701,19 @@ inline unsigned grid_for(int64_t n, int block, int64_t cap = 256 * 16) {
 
 template <int GS, int TEAM>
 void launch_fwd_t(const TableView& T, const BatchDev& b, StepWork& w, const StepParams& p, hipStream_t st,
-                  int64_t* nblk) {
+                  int64_t* nblk, const float* rows, const uint32_t* uidx) {
   constexpr int TPB = kBlock / TEAM;
   int64_t blocks = (b.n_rows + TPB - 1) / TPB;
   if (blocks > 256 * 8) blocks = 256 * 8;
   if (blocks < 1) blocks = 1;
   *nblk = blocks;
   w.loss_part.ensure(sizeof(double2) * blocks);
-  hipLaunchKernelGGL((k_forward<GS, TEAM>), dim3((unsigned)blocks), dim3(kBlock), 0, st, T,
+  if (rows)
+    hipLaunchKernelGGL((k_forward<GS, TEAM, true>), dim3((unsigned)blocks), dim3(kBlock), 0, st, T, rows, uidx,
+                       b.row_ptr.as<int64_t>(), b.col.as<uint32_t>(), b.ent.as<uint2>(), b.label.as<float>(),
+                       b.n_rows, p.w0, p.cumE, w.S.as<float>(), w.yl.as<float2>(), w.loss_part.as<double2>());
+  else
+  hipLaunchKernelGGL((k_forward<GS, TEAM, false>), dim3((unsigned)blocks), dim3(kBlock), 0, st, T, rows, uidx,
                      b.row_ptr.as<int64_t>(), b.col.as<uint32_t>(), b.ent.as<uint2>(), b.label.as<float>(),
                      b.n_rows, p.w0, p.cumE, w.S.as<float>(), w.yl.as<float2>(), w.loss_part.as<double2>());
 }
@@ -741,15 +721,15 @@ void launch_fwd_t(const TableView& T, const BatchDev& b, StepWork& w, const Step
 }  // namespace
 
 void launch_forward(const TableView& T, const BatchDev& b, StepWork& w, const StepParams& p, hipStream_t st,
-                    int64_t* n_fwd_blocks) {
+                    int64_t* n_fwd_blocks, const float* rows, const uint32_t* uidx) {
   const int nq = T.kp / 4;
-  if (nq <= 1) launch_fwd_t<1, 16>(T, b, w, p, st, n_fwd_blocks);
-  else if (nq <= 2) launch_fwd_t<2, 16>(T, b, w, p, st, n_fwd_blocks);
-  else if (nq <= 4) launch_fwd_t<4, 16>(T, b, w, p, st, n_fwd_blocks);
-  else if (nq <= 8) launch_fwd_t<8, 16>(T, b, w, p, st, n_fwd_blocks);
-  else if (nq <= 16) launch_fwd_t<16, 16>(T, b, w, p, st, n_fwd_blocks);
-  else if (nq <= 32) launch_fwd_t<32, 32>(T, b, w, p, st, n_fwd_blocks);
-  else if (nq <= 64) launch_fwd_t<64, 64>(T, b, w, p, st, n_fwd_blocks);
+  if (nq <= 1) launch_fwd_t<1, 16>(T, b, w, p, st, n_fwd_blocks, rows, uidx);
+  else if (nq <= 2) launch_fwd_t<2, 16>(T, b, w, p, st, n_fwd_blocks, rows, uidx);
+  else if (nq <= 4) launch_fwd_t<4, 16>(T, b, w, p, st, n_fwd_blocks, rows, uidx);
+  else if (nq <= 8) launch_fwd_t<8, 16>(T, b, w, p, st, n_fwd_blocks, rows, uidx);
+  else if (nq <= 16) launch_fwd_t<16, 16>(T, b, w, p, st, n_fwd_blocks, rows, uidx);
+  else if (nq <= 32) launch_fwd_t<32, 32>(T, b, w, p, st, n_fwd_blocks, rows, uidx);
+  else if (nq <= 64) launch_fwd_t<64, 64>(T, b, w, p, st, n_fwd_blocks, rows, uidx);
   else FM_REQUIRE(false, "dimFactorization > 256 is not supported");
   FM_HIP_CHECK(hipGetLastError());
 }

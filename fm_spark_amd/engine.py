@@ -79,7 +79,9 @@ class FMContext:
             pass
 
     def set_stream(self, stream_ptr: int | None):
-        N.check(self._lib.fm_set_stream(self.handle, C.c_void_p(stream_ptr or 0)), "fm_set_stream")
+        """Launch on this hipStream_t (an int handle, e.g. torch.cuda.current_stream().cuda_stream);
+        0 / None = the device's default (null) stream."""
+        N.check(self._lib.fm_set_stream(self.handle, C.c_void_p(stream_ptr or None)), "fm_set_stream")
 
     def sync(self):
         N.check(self._lib.fm_sync(self.handle), "fm_sync")

@@ -85,7 +85,8 @@ typedef struct fm_step_out {
 int fm_create(const fm_config* cfg, fm_ctx** out);
 void fm_destroy(fm_ctx* ctx);
 const char* fm_last_error(void);
-/* Launch on an externally owned HIP stream (hipStream_t passed as void*); NULL = own stream. */
+/* Launch on an externally owned HIP stream (hipStream_t passed as void*); NULL = the device's
+ * default (null) stream.  A new context launches on a non-blocking stream of its own. */
 int fm_set_stream(fm_ctx* ctx, void* hip_stream);
 int fm_sync(fm_ctx* ctx);
 /* Pre-size the per-step workspace so no step allocates. */
@@ -189,26 +190,31 @@ int32_t fm_murmur3_bytes_hash(const uint8_t* data, int64_t len, int32_t seed);
 /* n successive nextDouble() of XORShiftRandom(seed). */
 int fm_xorshift_next_doubles(int64_t seed, int64_t n, double* out);
 
-/* ---- sharded multi-GPU step (one context per rank; exchange done by the caller over
- *      RCCL all-to-all).  See DESIGN.md "Multi-GPU". --------------------------------- */
-/* Phase 1 on the requesting rank: sort the batch's ids by (owner, slot), dedupe.
- * Writes into the context's workspace; returns per-owner unique-id counts
- * (send_counts[shard_count], host) . */
+/* ---- row-sharded multi-GPU step ---------------------------------------------------------
+ * One context per rank (fm_config.shard_index / shard_count = rank / R); the caller exchanges
+ * the device buffers between phases with all-to-all (RCCL over xGMI; see
+ * fm_spark_amd/distributed.py).  Replaces the feature-keyed shuffles S1/S2/S5/S6 of the
+ * reference plan (Model.scala:155-164, SGD.scala:148-166).  Wire rows and
+ * gradients are fp32, kp + 4 floats per distinct id (kp = roundup(k, 4)):
+ *   row  = [V(kp) | w | 0 0 0]        gradient = [sum gV (kp) | sum gw | 0 0 0]
+ * Phase 1 (requester): sort the batch's entries by (owner, slot) and dedupe.  send_counts[R]
+ * receives the number of distinct ids requested from each owner (their sum is U).
+ * Synchronises the context's stream. */
 int fm_shard_plan(fm_ctx* ctx, const fm_batch* batch, int64_t* send_counts);
-/* Copy the plan's request list (int32 local slots, owner-major, U entries) to dst. */
+/* Copy the plan's request list (U int32 local slots, owner-major) to a device buffer. */
 int fm_shard_request_copy(fm_ctx* ctx, void* dst_device);
-/* Phase 2 on the owner: rows for n requested local slots -> rows_out[n][k+1] fp32 (w, V)
- * with pending L1 applied.  Device pointers. */
+/* Phase 2 (owner): rows for n requested local slots, pending L1 applied. */
 int fm_shard_serve_device(fm_ctx* ctx, const void* req_slots, int64_t n, void* rows_out);
-/* Phase 3 on the requester: forward + per-unique-id partial gradient using the rows
- * received for its plan.  grads_out[U][k+1] fp64 (device).  Loss is accumulated. */
-int fm_shard_local_grad_device(fm_ctx* ctx, const fm_batch* batch, const void* rows_in,
-                               void* grads_out, int64_t global_rows);
-/* Phase 4 on the owner: sum the received partial gradients per slot in fixed rank order,
- * apply the update + L1 (t, step_size, reg_param as fm_step), advance the epoch. */
+/* Phase 3 (requester): forward from the U received rows (ordered as the request list) and the
+ * per-distinct-id gradient sums of this rank's entries -> grads_out[U].  The rank's loss sum
+ * is kept for fm_shard_last_loss / fm_loss_history. */
+int fm_shard_local_grad_device(fm_ctx* ctx, fm_batch* batch, const void* rows_in, void* grads_out);
+/* Phase 4 (owner): the n received (slot, gradient) pairs of all ranks, rank-major; sums per
+ * slot in rank order and applies the update + L1 with global miniBatchSize global_rows
+ * (the sum of every rank's rows).  Returns FM_NOTHING_TO_DO when global_rows == 0. */
 int fm_shard_apply_device(fm_ctx* ctx, const void* req_slots, const void* grads, int64_t n,
                           int32_t t, double step_size, double reg_param, int64_t global_rows);
-/* Loss of the last sharded step on this rank (partial; the caller all-reduces). */
+/* This rank's (loss_sum, n_loss_rows) of the last step; the caller all-reduces. */
 int fm_shard_last_loss(fm_ctx* ctx, double* loss_sum, int64_t* n_loss_rows);
 
 #ifdef __cplusplus

@@ -1,0 +1,91 @@
+"""CPU, world_size 2 over gloo: the sharded step's exchange protocol
+(fm_spark_amd.distributed.ShardedTrainer: plan -> a2a -> serve -> a2a -> local_grad -> a2a ->
+apply) with the NumPy phase engine equals one single-table oracle step over the ranks'
+batches concatenated in rank order."""
+
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+F, K, WORLD = 211, 5, 2
+STEPS = 3
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _problem_for(rank, step):
+    from problems import make_problem
+
+    return make_problem(1000 * rank + step, 60 + 13 * rank, F, K, 6, hot=7)[0]
+
+
+def _worker(rank, world, port, outdir):
+    sys.path.insert(0, HERE)
+    sys.path.insert(0, os.path.dirname(HERE))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+
+    from fm_spark_amd.distributed import ShardedTrainer
+    from problems import make_problem
+    from shard_ref_engine import NumpyShardEngine
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        _, ids, w, V = make_problem(5, 1, F, K, 1)
+        eng = NumpyShardEngine(F, K, rank, world)
+        tr = ShardedTrainer(F, K, rank=rank, world=world, engine=eng)
+        tr.load_tables(ids, w, V)
+        losses = []
+        for t in range(1, STEPS + 1):
+            b = tr.batch(_problem_for(rank, t))
+            o = tr.step(b, t, 0.4, 1e-3)
+            losses.append(o.loss_sum)
+        gi, gw, gV = tr.export_tables()
+        np.savez(os.path.join(outdir, f"r{rank}.npz"), ids=gi, w=gw, V=gV, losses=np.array(losses))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_two_ranks_match_single_table(tmp_path):
+    from oracle import fm_ref as R
+    from problems import make_problem
+
+    port = _free_port()
+    mp.spawn(_worker, args=(WORLD, port, str(tmp_path)), nprocs=WORLD, join=True)
+    _, ids, w, V = make_problem(5, 1, F, K, 1)
+    model = R.Model.empty(F, K)
+    model.load(ids, w, V)
+    ref_losses = []
+    for t in range(1, STEPS + 1):
+        parts = [_problem_for(r, t) for r in range(WORLD)]
+        row_ptr = [np.zeros(1, np.int64)]
+        off = 0
+        for p in parts:
+            row_ptr.append(p.row_ptr[1:] + off)
+            off += p.nnz
+        cat = R.CSR(np.concatenate(row_ptr), np.concatenate([p.col for p in parts]),
+                    np.concatenate([p.val for p in parts]), np.concatenate([p.label for p in parts]))
+        ref_losses.append(R.sgd_step_fast(model, cat, t, 0.4, 1e-3).loss_sum)
+    gids, gw, gV = [], [], []
+    for r in range(WORLD):
+        d = np.load(tmp_path / f"r{r}.npz")
+        gids.append(d["ids"])
+        gw.append(d["w"])
+        gV.append(d["V"])
+        np.testing.assert_allclose(d["losses"], ref_losses, rtol=1e-6)
+    gids = np.concatenate(gids)
+    order = np.argsort(gids)
+    np.testing.assert_array_equal(gids[order], np.nonzero(model.present)[0])
+    # fp32 wire for rows and gradients: 1e-6 relative
+    np.testing.assert_allclose(np.concatenate(gw)[order], model.w[gids[order]], rtol=1e-6, atol=1e-9)
+    np.testing.assert_allclose(np.concatenate(gV)[order], model.V[gids[order]], rtol=1e-6, atol=1e-9)
