@@ -1,0 +1,63 @@
+"""CPU: the drop-in boundary.  libfm_hip.so loads, exports every function include/fm_hip.h
+declares, the ctypes binding covers exactly that list, and without a GPU the context
+constructor fails loudly through the error channel (no crash, no CPU fallback)."""
+
+import ctypes as C
+import re
+import subprocess
+from pathlib import Path
+
+import pytest
+
+from fm_spark_amd import _native as N
+
+HEADER = Path(__file__).resolve().parents[1] / "include" / "fm_hip.h"
+
+
+def header_functions():
+    text = HEADER.read_text()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"^[A-Za-z_][\w\s\*]*?\b(fm_\w+)\s*\(", text, flags=re.M)))
+
+
+def test_header_declares_the_boundary():
+    names = header_functions()
+    for required in ["fm_create", "fm_destroy", "fm_last_error", "fm_step", "fm_step_batch", "fm_predict",
+                     "fm_export_tables", "fm_load_tables", "fm_random_split", "fm_shard_plan", "fm_shard_apply_device"]:
+        assert required in names
+
+
+def test_library_exports_every_declared_symbol():
+    lib = N.load()
+    missing = [n for n in header_functions() if not hasattr(lib, n)]
+    assert not missing, missing
+    out = subprocess.run(["nm", "-D", "--defined-only", str(N.lib_path())], capture_output=True, text=True,
+                         check=True).stdout
+    exported = set(re.findall(r"\bT (fm_\w+)$", out, flags=re.M))
+    assert set(header_functions()) <= exported
+
+
+def test_binding_matches_header():
+    assert sorted(N.SIGNATURES) == header_functions()
+
+
+def test_no_gpu_fails_loudly():
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    from fm_spark_amd.engine import FMContext
+
+    with pytest.raises(N.FMError) as ei:
+        FMContext(10, 4)
+    assert "fm_create failed" in str(ei.value)
+
+
+def test_null_arguments_are_errors_not_crashes():
+    lib = N.load()
+    assert lib.fm_create(None, None) == -1
+    assert b"null" in lib.fm_last_error()
+    assert lib.fm_step(None, None, 1, 1.0, 0.0, None) == -1
+    assert lib.fm_epoch(None) == -1
+    lib.fm_destroy(None)
+    lib.fm_batch_destroy(None)

@@ -1,0 +1,40 @@
+"""CPU: Params, defaults, copy and schema checks of the mirror API (no device needed)."""
+
+import pytest
+
+from fm_spark_amd.linalg import Vectors
+from fm_spark_amd.ml import DataFrame, FactorizationMachinesModel, FactorizationMachinesSGD, _check_schema
+
+
+def test_defaults_match_reference():
+    # FactorizationMachinesSGD.scala:61-74
+    fm = FactorizationMachinesSGD()
+    assert fm.getDimFactorization() == 10 and fm.getMaxIter() == 10
+    assert fm.getMiniBatchFraction() == 0.1 and fm.getRegParam() == 0.1 and fm.getStepSize() == 1.0
+    assert fm.getMinLabel() == 0.0 and fm.getMaxLabel() == 1.0 and fm.getInitialSd() == 0.01
+    assert fm.uid.startswith("fm_")
+
+
+def test_setters_chain_and_copy_keeps_uid():
+    fm = FactorizationMachinesSGD("fm_x").setMaxIter(5).setMiniBatchFraction(0.2).setRegParam(1e-6)
+    c = fm.copy({"regParam": 0.0})
+    assert c.uid == "fm_x" and c.getRegParam() == 0.0 and fm.getRegParam() == 1e-6
+    assert c.getMaxIter() == 5 and c.getMiniBatchFraction() == 0.2
+    with pytest.raises(ValueError):
+        fm.setDimFactorization(0)
+
+
+def test_schema_validation():
+    df = DataFrame({"label": [1.0], "features": [Vectors.dense(1.0)]})
+    _check_schema(df, "features", "label")
+    with pytest.raises(ValueError):
+        _check_schema(DataFrame({"label": [1], "features": [Vectors.dense(1.0)]}), "features", "label")
+    with pytest.raises(ValueError):
+        _check_schema(DataFrame({"label": [1.0], "features": [[1.0]]}), "features", "label")
+
+
+def test_from_rows_partitions_and_sample_ids():
+    df = DataFrame.from_rows([(i, Vectors.dense(float(i))) for i in range(10)], ["rowId", "features"], 4)
+    assert df.partition_sizes == [2, 3, 2, 3]  # ParallelCollectionRDD slicing
+    sid = FactorizationMachinesModel.addSampleId(df)["sampleId"]
+    assert sid[:3] == [0, 1, 1 << 33] and sid[-1] == (3 << 33) + 2
