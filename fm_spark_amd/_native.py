@@ -119,14 +119,16 @@ def load() -> C.CDLL:
     global _lib
     if _lib is not None:
         return _lib
-    if not _LIB_PATH.exists():
-        raise FMError(f"{_LIB_PATH} is missing: run __graft_entry__.build() (hipcc, gfx950)")
+    # FM_HIP_LIB: an experiment variant built by tools/variants.sh (same ABI)
+    path = Path(os.environ.get("FM_HIP_LIB") or _LIB_PATH)
+    if not path.exists():
+        raise FMError(f"{path} is missing: run __graft_entry__.build() (hipcc, gfx950)")
     if os.environ.get("FM_NO_TORCH_PRELOAD") != "1":
         try:
             import torch  # noqa: F401
         except Exception:
             pass
-    lib = C.CDLL(str(_LIB_PATH), mode=C.RTLD_GLOBAL)
+    lib = C.CDLL(str(path), mode=C.RTLD_GLOBAL)
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)
         fn.restype = res

@@ -29,10 +29,14 @@ def _newer(target: Path, deps) -> bool:
     return any(Path(d).stat().st_mtime > t for d in deps)
 
 
-def build(verbose: bool = False, force: bool = False) -> Path:
-    LIB_DIR.mkdir(parents=True, exist_ok=True)
-    objdir = LIB_DIR / "obj"
+def build(verbose: bool = False, force: bool = False, out: Path | None = None, defines=()) -> Path:
+    """Build the library (incrementally).  ``out``/``defines``: an experiment variant with
+    extra -D flags, built into its own object directory (tools/variants.sh)."""
+    lib = Path(out) if out else LIB
+    lib.parent.mkdir(parents=True, exist_ok=True)
+    objdir = (LIB_DIR / "obj") if out is None else lib.parent / (lib.stem + "_obj")
     objdir.mkdir(exist_ok=True)
+    dflags = [f"-D{d}" for d in defines]
     headers = [CSRC / h for h in HEADERS] + [INCLUDE / "fm_hip.h"]
     objs = []
     for src in SOURCES:
@@ -41,19 +45,26 @@ def build(verbose: bool = False, force: bool = False) -> Path:
         objs.append(o)
         if force or _newer(o, [s, *headers]):
             if src.endswith(".hip"):
-                cmd = [HIPCC, f"--offload-arch={ARCH}", *CXXFLAGS, "-c", str(s), "-o", str(o)]
+                cmd = [HIPCC, f"--offload-arch={ARCH}", *CXXFLAGS, *dflags, "-c", str(s), "-o", str(o)]
             else:
                 cmd = [HIPCC, *CXXFLAGS, "-x", "c++", "-c", str(s), "-o", str(o)]
             if verbose:
                 print(" ".join(cmd), file=sys.stderr)
             subprocess.run(cmd, check=True)
-    if force or _newer(LIB, objs):
-        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", str(LIB)]
+    if force or _newer(lib, objs):
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", str(lib)]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.run(cmd, check=True)
-    return LIB
+    return lib
 
 
 if __name__ == "__main__":
-    print(build(verbose=True, force="--force" in sys.argv))
+    import argparse
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("--out", default=None)
+    ap.add_argument("-D", dest="defines", action="append", default=[])
+    args = ap.parse_args()
+    print(build(verbose=True, force=args.force, out=args.out, defines=args.defines))

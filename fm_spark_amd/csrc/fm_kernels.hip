@@ -34,6 +34,16 @@ namespace fmhip {
 namespace {
 
 constexpr int kBlock = 256;
+#ifndef FM_UPD_PF
+#define FM_UPD_PF 4
+#endif
+#ifndef FM_HDR_PAD
+#define FM_HDR_PAD 1
+#endif
+#ifndef FM_UPD_CH
+#define FM_UPD_CH 4
+#endif
+constexpr int kUpdateChunks = FM_UPD_CH;  // 64-entry chunks per update wave
 
 // The row header and one V quad brought current (absent rows read as zero).
 __device__ __forceinline__ void current_row(const RowHdr& h, float4& v, float& w, double cumE) {
@@ -179,151 +189,230 @@ struct SegArgs {
   int64_t N;
   const float* S;
   const float2* yl;
-  double* part;  // [nchunks][2][kp + 1]
-  int64_t nchunks;
+  double* part;     // [nranges][2][kp + 1]
+  int64_t nranges;  // ranges of L sorted entries, one wave each
+  int64_t L;        // entries per range (64 * CH)
   StepParams p;
   uint32_t* ucnt;  // [update blocks]
-  int ablate;      // diagnostic ablation bits (FM_ABLATE); 0 in production
 };
 
-// One wave per chunk of 64 sorted entries.
+// Per-entry scalars of the current chunk, staged in LDS for the G-lanes-per-entry phase.
+struct EntInfo {
+  uint32_t key;
+  int32_t s;
+  float x;
+  int32_t flags;  // valid | writes<<1 | complete<<2 | present<<3 | slot<<4 | start_lane<<8
+  double r;       // yhat - y
+  double ac;      // pending L1 of the row
+};
+
+// One wave per range of CH consecutive chunks of 64 sorted entries (L = 64 * CH entries).
 //  Phase 1, one lane per entry: run structure (pieces of equal keys inside the chunk), the
-//    row header and the sample's (yhat, y); the linear gradient is scanned here and the tail
-//    lane of every complete run writes the row header.
+//    row header and the sample's (yhat, y); the linear gradient is scanned here.
 //  Phase 2, G lanes per entry (one float4 quad each), E = 64/G entries per round: S and V rows
-//    move as whole 64-byte rows (16 rows per wave-instruction for k = 16) -- gathers, the
-//    segmented scan (lane stride G, carry between rounds) and the write-back.
-template <int G>
+//    move as whole rows (16 rows per wave-instruction for k = 16); the loads of up to four
+//    rounds are in flight together, then the segmented scan (lane stride G, carries between
+//    rounds) and the write-back.
+//  Runs continue across the chunks of a range through register carries, so only runs crossing
+//    a range boundary leave fp64 partials (slot 0: the range's first piece when its run began
+//    before the range; slot 1: the last piece when its run continues past the range).  The
+//    next chunk's entries are loaded while the current chunk is processed.
+//  CH > 1 needs nq <= G (one quad-chunk), which the launcher guarantees.
+template <int G, int CH>
 __global__ __launch_bounds__(kBlock) void k_segment_update(SegArgs a) {
-  constexpr int E = 64 / G;  // entries per round
+  constexpr int E = 64 / G;           // entries per round
+  constexpr int PF = G < FM_UPD_PF ? G : FM_UPD_PF;  // rounds whose loads are issued together
+  __shared__ EntInfo info[kBlock / 64][64];
+  __shared__ float wnew_s[kBlock / 64][64];
   __shared__ uint32_t wcnt[kBlock / 64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t chunk = (int64_t)blockIdx.x * (kBlock / 64) + wave;
   const TableView& T = a.T;
   const int kp = T.kp, nq = kp >> 2;
-  const int64_t p0 = chunk * 64;
-  const int64_t pp = p0 + lane;
-  const bool valid = chunk < a.nchunks && pp < a.N;
+#if FM_HDR_PAD
+  const int hq_end = (nq + 4) & ~3;  // end of the 64-B granule holding the header (in quads)
+#else
+  const int hq_end = nq + 1;
+#endif
+  const int64_t rg = (int64_t)blockIdx.x * (kBlock / 64) + wave;
+  const int64_t r0 = rg * a.L;
   const uint32_t kNone = 0xFFFFFFFFu;
-  const uint32_t key = valid ? a.skeys[pp] : kNone;
-  const uint2 en = valid ? a.sents[pp] : make_uint2(0u, 0u);
-  uint32_t prev_key = __shfl_up(key, 1);
-  uint32_t next_key = __shfl_down(key, 1);
-  if (lane == 0) prev_key = (valid && p0 > 0) ? a.skeys[p0 - 1] : kNone;
-  if (lane == 63) next_key = (valid && p0 + 64 < a.N) ? a.skeys[p0 + 64] : kNone;
-  if (pp == a.N - 1) next_key = kNone;
-  const int s = (int)en.x;
-  const float xf = __uint_as_float(en.y);
-  const double x = (double)xf;
-  const RowHdr h = valid ? (*T.hdr(key)) : RowHdr{0.f, -1, 0.0};  // read before any write-back
-  const float2 yl = valid ? a.yl[s] : make_float2(0.f, 0.f);
-
-  const bool seg_start = valid && key != prev_key;  // a run of this key starts here
-  const bool seg_end = valid && key != next_key;     // ... ends here
-  const bool piece_head = valid && (lane == 0 || seg_start);
-  const bool piece_tail = valid && (lane == 63 || seg_end);
-  const uint64_t heads = __ballot(piece_head);
-  const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
-  const uint64_t hm = heads & upto;
-  const int start_lane = hm ? 63 - __clzll(hm) : 0;
-  const uint64_t starts = __ballot(seg_start);
-  if (lane == 0) wcnt[wave] = (uint32_t)__popcll(starts);
-  const int dist = valid ? lane - start_lane : 0;
-  int nsteps = 0;
-  while (nsteps < 6 && __ballot(dist >= (1 << nsteps))) ++nsteps;
-  if (a.ablate & 1) nsteps = 0;
-  // the piece is a whole run iff its head lane starts the run and its tail lane ends it
-  const bool head_is_start = (starts >> start_lane) & 1ull;
-  const bool complete = head_is_start && seg_end;
-  // partial slot: 0 = the chunk's first piece continuing from the previous chunk (also used
-  // when that piece spans the whole chunk), 1 = the last piece continuing into the next chunk
-  const int slot = (start_lane == 0 && !head_is_start) ? 0 : 1;
-  const bool present = h.t >= 0;
-  const double ac = present ? a.p.cumE - h.cum : 0.0;  // pending L1 of this row
-  const double yhat = yl.x, y = yl.y;
-  const double r = yhat - y;
-
-  // ---- linear term: g_w = deltaWi * pred - label (SGD.scala:145)
-  double gw = valid ? x * yhat - y : 0.0;
-  gw = seg_scan(gw, lane, start_lane, nsteps);
-  const bool ab_w = a.ablate & 8;
-  if (piece_tail && !ab_w) {
-    if (complete) {
-      float w = present ? h.w : 0.f;
-      if (ac > 0.0) w = shrink_f(w, ac);
-      RowHdr o;
-      o.w = upd_w(w, gw, a.p);  // SGD.scala:150, :171, :179
-      o.t = a.p.epoch + 1;
-      o.cum = a.p.cum_next;
-      (*T.hdr(key)) = o;
-    } else {
-      a.part[(chunk * 2 + slot) * (int64_t)(kp + 1)] = gw;
-    }
-  }
-
-  // ---- interaction term: g_V = (vfxiSum*x - (v*x)*x) * (pred - label) (Model.scala:201-204,
-  //      SGD.scala:146).  Per-entry scalars packed for the lane shuffles of phase 2.
-  const int flags = (valid ? 1 : 0) | (piece_tail ? 2 : 0) | (complete ? 4 : 0) | (present ? 8 : 0) |
-                    (slot << 4) | (start_lane << 8);
   const float4* __restrict__ S4 = reinterpret_cast<const float4*>(a.S);
-  const int q_in = lane % G;   // this lane's quad inside a quad-chunk
-  const int j_in = lane / G;   // this lane's entry inside a round
-  const bool ab_s = a.ablate & 2, ab_v = a.ablate & 4;
-  for (int qc = 0; qc < nq; qc += G) {
-    const int q = qc + q_in;
-    const bool qok = q < nq;
-    double carry0 = 0.0, carry1 = 0.0, carry2 = 0.0, carry3 = 0.0;
-    for (int rd = 0; rd < G; ++rd) {  // 64 / E = G rounds
-      const int j = rd * E + j_in;    // entry (lane of phase 1) this lane serves
-      const int fl = __shfl(flags, j);
-      const uint32_t kj = __shfl(key, j);
-      const int sj = __shfl(s, j);
-      const float xj = __shfl(xf, j);
-      const double rj = __shfl(r, j);
-      const double acj = __shfl(ac, j);
-      const bool vj = (fl & 1) && qok;
-      const int sl = fl >> 8;
-      float4 sq = (vj && !ab_s) ? S4[(int64_t)sj * nq + q] : make_float4(xj, 0.f, 0.f, 0.f);
-      float4 v = (vj && !ab_v && (fl & 8)) ? reinterpret_cast<const float4*>(T.v(kj))[q]
-                                           : make_float4(0.f, 0.f, 0.f, 0.f);
-      if (acj > 0.0) v = shrink4(v, acj);
-      const double xd = xj;
-      double c0 = vj ? ((double)sq.x * xd - ((double)v.x * xd) * xd) * rj : 0.0;
-      double c1 = vj ? ((double)sq.y * xd - ((double)v.y * xd) * xd) * rj : 0.0;
-      double c2 = vj ? ((double)sq.z * xd - ((double)v.z * xd) * xd) * rj : 0.0;
-      double c3 = vj ? ((double)sq.w * xd - ((double)v.w * xd) * xd) * rj : 0.0;
-      // segmented scan over this round's entries (lane stride G), fixed tree order
-      const int lo = sl > rd * E ? sl : rd * E;  // first entry of the piece inside this round
+  EntInfo* inf = info[wave];
+  const int q_in = lane % G;  // this lane's quad inside a quad-chunk
+  const int j_in = lane / G;  // this lane's entry inside a round
+
+  uint32_t ucount = 0;
+  double cw = 0.0;                                          // open piece's running w sum
+  double cv0 = 0.0, cv1 = 0.0, cv2 = 0.0, cv3 = 0.0;        // ... and V sums (this lane's quad)
+  bool open_started = false;  // the piece open at the previous chunk's end began in this range
+  uint32_t prev_last = (r0 > 0 && r0 < a.N) ? a.skeys[r0 - 1] : kNone;
+  int64_t pp = r0 + lane;
+  bool valid = r0 < a.N && pp < a.N;
+  uint32_t key = valid ? a.skeys[pp] : kNone;
+  uint2 en = valid ? a.sents[pp] : make_uint2(0u, 0u);
+
+  for (int c = 0; c < CH; ++c) {
+    const int64_t p0 = r0 + (int64_t)c * 64;
+    if (p0 >= a.N) break;  // wave-uniform
+    // prefetch the next chunk of the range
+    const int64_t pn = p0 + 64 + lane;
+    const bool nvalid = (c + 1 < CH) && pn < a.N;
+    const uint32_t nkey = nvalid ? a.skeys[pn] : kNone;
+    const uint2 nen = nvalid ? a.sents[pn] : make_uint2(0u, 0u);
+
+    uint32_t prev_key = __shfl_up(key, 1);
+    uint32_t next_key = __shfl_down(key, 1);
+    if (lane == 0) prev_key = prev_last;
+    if (lane == 63) next_key = (p0 + 64 < a.N) ? a.skeys[p0 + 64] : kNone;
+    if (pp == a.N - 1) next_key = kNone;
+    const int s = (int)en.x;
+    const float xf = __uint_as_float(en.y);
+    const double x = (double)xf;
+    const RowHdr h = valid ? (*T.hdr(key)) : RowHdr{0.f, -1, 0.0};  // read before any write-back
+    const float2 yl = valid ? a.yl[s] : make_float2(0.f, 0.f);
+
+    const bool last_chunk = (c == CH - 1) || (p0 + 64 >= a.N);
+    const bool seg_start = valid && key != prev_key;  // a run of this key starts here
+    const bool seg_end = valid && key != next_key;     // ... ends here
+    const bool piece_head = valid && (lane == 0 || seg_start);
+    const bool writes = valid && (seg_end || (lane == 63 && last_chunk));
+    const uint64_t heads = __ballot(piece_head);
+    const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
+    const uint64_t hm = heads & upto;
+    const int start_lane = hm ? 63 - __clzll(hm) : 0;
+    const uint64_t starts = __ballot(seg_start);
+    ucount += (uint32_t)__popcll(starts);
+    // the lane-0 piece continues a piece of the previous chunk of this range
+    const bool cont = c > 0 && !(starts & 1ull);
+    const int dist = valid ? lane - start_lane : 0;
+    int nsteps = 0;
+    while (nsteps < 6 && __ballot(dist >= (1 << nsteps))) ++nsteps;
+    const bool head_is_start = ((starts >> start_lane) & 1ull) || (start_lane == 0 && cont && open_started);
+    const bool complete = head_is_start && seg_end;
+    const int slot = head_is_start ? 1 : 0;
+    const bool present = h.t >= 0;
+    const double ac = present ? a.p.cumE - h.cum : 0.0;  // pending L1 of this row
+    const double yhat = yl.x, y = yl.y;
+
+    // ---- linear term: g_w = deltaWi * pred - label (SGD.scala:145)
+    double gw = valid ? x * yhat - y : 0.0;
+    gw = seg_scan(gw, lane, start_lane, nsteps);
+    if (cont && start_lane == 0) gw += cw;
+    cw = __shfl(gw, 63);
+    if (writes) {
+      if (complete) {  // the header is stored with the V row in phase 2
+        float w = present ? h.w : 0.f;
+        if (ac > 0.0) w = shrink_f(w, ac);
+        wnew_s[wave][lane] = upd_w(w, gw, a.p);  // SGD.scala:150, :171, :179
+      } else {
+        a.part[(rg * 2 + slot) * (int64_t)(kp + 1)] = gw;
+      }
+    }
+    open_started = __shfl((int)head_is_start, 63) != 0;
+    prev_last = __shfl(key, 63);
+
+    // ---- interaction term: g_V = (vfxiSum*x - (v*x)*x) * (pred - label) (Model.scala:201-204,
+    //      SGD.scala:146)
+    EntInfo me;
+    me.key = key;
+    me.s = s;
+    me.x = xf;
+    me.flags = (valid ? 1 : 0) | (writes ? 2 : 0) | (complete ? 4 : 0) | (present ? 8 : 0) | (slot << 4) |
+               (start_lane << 8);
+    me.r = yhat - y;
+    me.ac = ac;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    inf[lane] = me;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    for (int qc = 0; qc < nq; qc += G) {
+      const int q = qc + q_in;
+      const bool qok = q < nq;
+#pragma unroll 1
+      for (int rb = 0; rb < G; rb += PF) {
+        EntInfo ei[PF];
+        float4 sq[PF], v[PF];
 #pragma unroll
-      for (int o = 1; o < E; o <<= 1) {
-        if (o >= (1 << nsteps)) break;  // wave-uniform: no piece is that long
-        const double t0 = __shfl_up(c0, o * G), t1 = __shfl_up(c1, o * G);
-        const double t2 = __shfl_up(c2, o * G), t3 = __shfl_up(c3, o * G);
-        if (j - o >= lo) {
-          c0 += t0; c1 += t1; c2 += t2; c3 += t3;
+        for (int u = 0; u < PF; ++u) ei[u] = inf[(rb + u) * E + j_in];
+#pragma unroll
+        for (int u = 0; u < PF; ++u) {
+          const bool vj = (ei[u].flags & 1) && qok;
+          sq[u] = vj ? S4[(int64_t)ei[u].s * nq + q] : make_float4(0.f, 0.f, 0.f, 0.f);
+          v[u] = (vj && (ei[u].flags & 8)) ? reinterpret_cast<const float4*>(T.v(ei[u].key))[q]
+                                           : make_float4(0.f, 0.f, 0.f, 0.f);
         }
-      }
-      if (sl < rd * E) {  // the piece started in an earlier round: add its running sum
-        c0 += carry0; c1 += carry1; c2 += carry2; c3 += carry3;
-      }
-      const int last = (E - 1) * G + q_in;  // the round's last entry, same quad
-      carry0 = __shfl(c0, last); carry1 = __shfl(c1, last);
-      carry2 = __shfl(c2, last); carry3 = __shfl(c3, last);
-      if (ab_w) asm volatile("" ::"v"(c0), "v"(c1), "v"(c2), "v"(c3));
-      if (vj && (fl & 2) && !ab_w) {
-        if (fl & 4) {
-          reinterpret_cast<float4*>(T.v(kj))[q] =
-              make_float4(upd_v(v.x, c0, a.p), upd_v(v.y, c1, a.p), upd_v(v.z, c2, a.p), upd_v(v.w, c3, a.p));
-        } else {
-          double* prow = a.part + (((chunk * 2 + ((fl >> 4) & 1)) * (int64_t)(kp + 1)) + 1 + 4 * q);
-          prow[0] = c0;
-          prow[1] = c1;
-          prow[2] = c2;
-          prow[3] = c3;
+#pragma unroll
+        for (int u = 0; u < PF; ++u) {
+          const int rd = rb + u;
+          const int j = rd * E + j_in;  // entry (lane of phase 1) this lane serves
+          const int fl = ei[u].flags;
+          const bool vj = (fl & 1) && qok;
+          const int sl = fl >> 8;
+          if (ei[u].ac > 0.0) v[u] = shrink4(v[u], ei[u].ac);
+          const double xd = ei[u].x, rj = ei[u].r;
+          double c0 = vj ? ((double)sq[u].x * xd - ((double)v[u].x * xd) * xd) * rj : 0.0;
+          double c1 = vj ? ((double)sq[u].y * xd - ((double)v[u].y * xd) * xd) * rj : 0.0;
+          double c2 = vj ? ((double)sq[u].z * xd - ((double)v[u].z * xd) * xd) * rj : 0.0;
+          double c3 = vj ? ((double)sq[u].w * xd - ((double)v[u].w * xd) * xd) * rj : 0.0;
+          // segmented scan over this round's entries (lane stride G), fixed tree order
+          const int lo = sl > rd * E ? sl : rd * E;  // first entry of the piece inside this round
+#pragma unroll
+          for (int o = 1; o < E; o <<= 1) {
+            if (o < (1 << nsteps)) {  // wave-uniform: skip steps no piece is long enough for
+              const double t0 = __shfl_up(c0, o * G), t1 = __shfl_up(c1, o * G);
+              const double t2 = __shfl_up(c2, o * G), t3 = __shfl_up(c3, o * G);
+              if (j - o >= lo) {
+                c0 += t0; c1 += t1; c2 += t2; c3 += t3;
+              }
+            }
+          }
+          // the piece started in an earlier round, or continues from the previous chunk
+          if (sl < rd * E || (rd == 0 && sl == 0 && cont)) {
+            c0 += cv0; c1 += cv1; c2 += cv2; c3 += cv3;
+          }
+          const int last = (E - 1) * G + q_in;  // the round's last entry, same quad
+          cv0 = __shfl(c0, last); cv1 = __shfl(c1, last);
+          cv2 = __shfl(c2, last); cv3 = __shfl(c3, last);
+          if ((fl & 1) && (fl & 2)) {
+            if (fl & 4) {
+              float4* rec = reinterpret_cast<float4*>(T.v(ei[u].key));
+              if (qok)
+                rec[q] = make_float4(upd_v(v[u].x, c0, a.p), upd_v(v[u].y, c1, a.p), upd_v(v[u].z, c2, a.p),
+                                     upd_v(v[u].w, c3, a.p));
+              if (qc + G >= nq) {
+                // last quad-chunk: the header and the zero pad of its 64-B granule, stored by the
+                // same lanes so every granule of the record is written whole (see store_hdr)
+                for (int hq = nq + q_in; hq < hq_end; hq += G) {
+                  float4 hv = make_float4(0.f, 0.f, 0.f, 0.f);
+                  if (hq == nq) {
+                    RowHdr o;
+                    o.w = wnew_s[wave][j];
+                    o.t = a.p.epoch + 1;
+                    o.cum = a.p.cum_next;
+                    hv = *reinterpret_cast<const float4*>(&o);
+                  }
+                  rec[hq] = hv;
+                }
+              }
+            } else if (qok) {
+              double* prow = a.part + (((rg * 2 + ((fl >> 4) & 1)) * (int64_t)(kp + 1)) + 1 + 4 * q);
+              prow[0] = c0;
+              prow[1] = c1;
+              prow[2] = c2;
+              prow[3] = c3;
+            }
+          }
         }
       }
     }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    key = nkey;
+    en = nen;
+    pp += 64;
+    valid = nvalid;
   }
+  if (lane == 0) wcnt[wave] = ucount;
   __syncthreads();
   if (threadIdx.x == 0) {
     uint32_t t = 0;
@@ -333,9 +422,9 @@ __global__ __launch_bounds__(kBlock) void k_segment_update(SegArgs a) {
   }
 }
 
-// Runs that cross chunk boundaries: the chunk holding the run's first entry owns it; one wave
-// per owner sums the following chunks' head partials in chunk order with lanes over the k+1
-// columns.  Block 0 also closes the step with fixed-order reductions.
+// Runs that cross range boundaries: the range holding the run's first entry owns it; one wave
+// per owner sums the following ranges' head partials in range order with lanes over the k+1
+// columns (a lane alone when the run ends in the next range).  Block 0 also closes the step with fixed-order reductions.
 __global__ __launch_bounds__(kBlock) void k_segment_combine(SegArgs a, const double2* __restrict__ loss_part,
                                                             int64_t n_loss_blocks, int64_t n_ucnt,
                                                             double* __restrict__ stats_out) {
@@ -368,12 +457,13 @@ __global__ __launch_bounds__(kBlock) void k_segment_combine(SegArgs a, const dou
       stats_out[2] = ru[0];
     }
   }
-  const int64_t chunk = (int64_t)blockIdx.x * kBlock + tid;
+  const int64_t chunk = (int64_t)blockIdx.x * kBlock + tid;  // range index
+  const int64_t L = a.L;
   bool owner = false;
   uint32_t key = 0;
-  if (chunk < a.nchunks) {
-    const int64_t p0 = chunk * 64;
-    const int64_t p1 = p0 + 64 < a.N ? p0 + 64 : a.N;
+  if (chunk < a.nranges) {
+    const int64_t p0 = chunk * L;
+    const int64_t p1 = p0 + L < a.N ? p0 + L : a.N;
     if (p1 < a.N) {
       key = a.skeys[p1 - 1];
       // the chunk's last run continues into the next chunk and starts inside this chunk
@@ -385,7 +475,7 @@ __global__ __launch_bounds__(kBlock) void k_segment_combine(SegArgs a, const dou
   bool two = false;
   if (owner) {
     const int64_t c2 = chunk + 2;
-    two = !(c2 < a.nchunks && a.skeys[c2 * 64] == key);
+    two = !(c2 < a.nranges && a.skeys[c2 * L] == key);
   }
   if (owner && two) {
     const double* pt = a.part + (chunk * 2 + 1) * W;
@@ -410,7 +500,7 @@ __global__ __launch_bounds__(kBlock) void k_segment_combine(SegArgs a, const dou
     o.w = upd_w(w, pt[0] + ph[0], a.p);
     o.t = a.p.epoch + 1;
     o.cum = a.p.cum_next;
-    *T.hdr(key) = o;
+    store_hdr(T, key, o);
   }
   // long runs (hot features): one wave per run, lanes over the k+1 columns, chunk order
   uint64_t owners = __ballot(owner && !two);
@@ -423,7 +513,7 @@ __global__ __launch_bounds__(kBlock) void k_segment_combine(SegArgs a, const dou
     int64_t cend = c0 + 1;
     for (;;) {
       const int64_t c = cend + lane;
-      const bool cont = c < a.nchunks && a.skeys[c * 64] == k0;
+      const bool cont = c < a.nranges && a.skeys[c * L] == k0;
       const uint64_t m = __ballot(cont);
       if (m == ~0ull) {
         cend += 64;
@@ -468,7 +558,7 @@ __global__ __launch_bounds__(kBlock) void k_segment_combine(SegArgs a, const dou
       o.w = wnew;
       o.t = a.p.epoch + 1;
       o.cum = a.p.cum_next;
-      *T.hdr(k0) = o;
+      store_hdr(T, k0, o);
     }
   }
 }
@@ -504,7 +594,7 @@ __global__ void k_init_random(TableView T, const int32_t* __restrict__ ids, int6
     o.t = epoch;
     o.cum = cumE;
     for (int f = 0; f < T.kp; ++f) T.v(slot)[f] = f < T.k ? gauss_draw(seed, id, f, sd) : 0.f;
-    (*T.hdr(slot)) = o;
+    store_hdr(T, slot, o);
   }
 }
 
@@ -520,13 +610,13 @@ __global__ void k_load_rows(TableView T, const int32_t* __restrict__ ids, int64_
     o.t = epoch;
     o.cum = cumE;
     for (int f = 0; f < T.kp; ++f) T.v(slot)[f] = f < T.k ? (float)V[i * T.k + f] : 0.f;
-    (*T.hdr(slot)) = o;
+    store_hdr(T, slot, o);
   }
 }
 
 __global__ void k_table_reset(TableView T) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < T.rows; i += (int64_t)gridDim.x * blockDim.x)
-    (*T.hdr(i)) = RowHdr{0.f, -1, 0.0};
+    store_hdr(T, i, RowHdr{0.f, -1, 0.0});
 }
 
 __global__ void k_flush(TableView T, int32_t epoch, double cumE) {
@@ -540,7 +630,7 @@ __global__ void k_flush(TableView T, int32_t epoch, double cumE) {
     }
     h.t = epoch;
     h.cum = cumE;
-    (*T.hdr(i)) = h;
+    store_hdr(T, i, h);
   }
 }
 
@@ -738,9 +828,13 @@ void launch_segment_update(const TableView& T, const BatchDev& b, StepWork& w, c
                            const uint32_t* skeys, const uint2* sents, int64_t n_fwd_blocks,
                            double* stats_out, hipStream_t st) {
   const int64_t N = b.nnz;
-  const int64_t nchunks = (N + 63) / 64;
-  w.part.ensure(sizeof(double) * (size_t)(nchunks > 0 ? nchunks : 1) * 2 * (T.kp + 1));
-  const int64_t ublocks = (nchunks + (kBlock / 64) - 1) / (kBlock / 64);
+  const int nq = T.kp / 4;
+  const int G = nq <= 1 ? 1 : nq <= 2 ? 2 : nq <= 4 ? 4 : nq <= 8 ? 8 : 16;
+  const int CH = nq <= G ? kUpdateChunks : 1;  // carries across chunks need one quad-chunk
+  const int64_t L = 64 * (int64_t)CH;
+  const int64_t nranges = (N + L - 1) / L;
+  w.part.ensure(sizeof(double) * (size_t)(nranges > 0 ? nranges : 1) * 2 * (T.kp + 1));
+  const int64_t ublocks = (nranges + (kBlock / 64) - 1) / (kBlock / 64);
   w.ucnt.ensure(sizeof(uint32_t) * (size_t)(ublocks > 0 ? ublocks : 1));
   SegArgs a;
   a.T = T;
@@ -750,24 +844,31 @@ void launch_segment_update(const TableView& T, const BatchDev& b, StepWork& w, c
   a.S = w.S.as<float>();
   a.yl = w.yl.as<float2>();
   a.part = w.part.as<double>();
-  a.nchunks = nchunks;
+  a.nranges = nranges;
+  a.L = L;
   a.p = p;
   a.ucnt = w.ucnt.as<uint32_t>();
-  static const int ablate = getenv("FM_ABLATE") ? atoi(getenv("FM_ABLATE")) : 0;
-  a.ablate = ablate;
-  if (nchunks > 0) {
-    const int nq = T.kp / 4;
-    if (nq <= 1) hipLaunchKernelGGL(k_segment_update<1>, dim3((unsigned)ublocks), dim3(kBlock), 0, st, a);
-    else if (nq <= 2) hipLaunchKernelGGL(k_segment_update<2>, dim3((unsigned)ublocks), dim3(kBlock), 0, st, a);
-    else if (nq <= 4) hipLaunchKernelGGL(k_segment_update<4>, dim3((unsigned)ublocks), dim3(kBlock), 0, st, a);
-    else if (nq <= 8) hipLaunchKernelGGL(k_segment_update<8>, dim3((unsigned)ublocks), dim3(kBlock), 0, st, a);
-    else hipLaunchKernelGGL(k_segment_update<16>, dim3((unsigned)ublocks), dim3(kBlock), 0, st, a);
+  if (nranges > 0) {
+    const dim3 grid((unsigned)ublocks), blk(kBlock);
+    if (nq > G) {
+      hipLaunchKernelGGL((k_segment_update<16, 1>), grid, blk, 0, st, a);
+    } else if (G == 1) {
+      hipLaunchKernelGGL((k_segment_update<1, kUpdateChunks>), grid, blk, 0, st, a);
+    } else if (G == 2) {
+      hipLaunchKernelGGL((k_segment_update<2, kUpdateChunks>), grid, blk, 0, st, a);
+    } else if (G == 4) {
+      hipLaunchKernelGGL((k_segment_update<4, kUpdateChunks>), grid, blk, 0, st, a);
+    } else if (G == 8) {
+      hipLaunchKernelGGL((k_segment_update<8, kUpdateChunks>), grid, blk, 0, st, a);
+    } else {
+      hipLaunchKernelGGL((k_segment_update<16, kUpdateChunks>), grid, blk, 0, st, a);
+    }
     FM_HIP_CHECK(hipGetLastError());
   }
-  int64_t cblocks = (nchunks + kBlock - 1) / kBlock;
+  int64_t cblocks = (nranges + kBlock - 1) / kBlock;
   if (cblocks < 1) cblocks = 1;
   hipLaunchKernelGGL(k_segment_combine, dim3((unsigned)cblocks), dim3(kBlock), 0, st, a,
-                     w.loss_part.as<double2>(), n_fwd_blocks, nchunks > 0 ? ublocks : (int64_t)0, stats_out);
+                     w.loss_part.as<double2>(), n_fwd_blocks, nranges > 0 ? ublocks : (int64_t)0, stats_out);
   FM_HIP_CHECK(hipGetLastError());
 }
 

@@ -390,7 +390,7 @@ __global__ __launch_bounds__(kBlock) void k_shard_apply(TableView T, const uint3
     o.w = upd_w(w, gw, p);
     o.t = p.epoch + 1;
     o.cum = p.cum_next;
-    *T.hdr(slot) = o;
+    store_hdr(T, slot, o);
   }
 }
 
