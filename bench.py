@@ -202,8 +202,8 @@ def main():
         prof = tr.ctx.profile_read() if args.profile_kernels else {}
         losses = tr.ctx.loss_history()
         assert os.environ.get("FM_ABLATE") or np.all(np.isfinite(losses)), "non-finite loss"
-        U_mean = float(np.mean(uniques)) if uniques else 0.0
-        parallelism = f"row-sharded x{world} (RCCL all-to-all)"
+        U_mean = float(np.mean(uniques)) / world if uniques else 0.0  # rows one owner updates
+        parallelism = f"row-sharded x{world}, owner-computes (RCCL all-to-all of entries, partial sums, S)"
 
     if sharded:
         tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
@@ -230,14 +230,16 @@ def main():
             "dtype": "f32",
             "data": "synthetic (Criteo-shaped, Zipf(%.2f) hashed ids, seed 20261015), random-init tables" % zipf_s,
             "config": {"workload": f"{args.config}: {desc}", "num_features": F, "k": k, "batch_rows_per_gpu": B,
-                       "global_batch": B * world, "nnz_per_row": z, "unique_ids_per_batch": U_mean,
+                       "global_batch": B * world, "nnz_per_row": z, "rows_updated_per_gpu": U_mean,
                        "step_size": STEP_SIZE, "reg_param": REG_PARAM, "parallelism": parallelism},
         }
         if prof:
             kern = {name: {"avg_ms": ms / max(n, 1), "launches": n} for name, (ms, n) in prof.items()}
             line["kernels"] = kern
-            # the row read-modify-write happens in "update" (single table) or "apply" (sharded)
-            algo = {"forward": fwd_b, "update": upd_b, "apply": upd_b}
+            # single table: "forward" gathers, "update" does the row read-modify-write; sharded:
+            # "owner_forward" / "owner_update" do the same on the rank's own rows (per rank: the
+            # entries an owner receives ~ its own batch's, the rows it updates ~ U / world)
+            algo = {"forward": fwd_b, "update": upd_b, "owner_forward": fwd_b, "owner_update": upd_b}
             # dominant kernel among those that move the path's algorithmic bytes;
             # sort / plan / grad / serve bytes are implementation overhead, reported as times
             dom = max((n for n in kern if n in algo), key=lambda n: kern[n]["avg_ms"])

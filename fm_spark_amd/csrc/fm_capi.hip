@@ -105,10 +105,16 @@ void reserve_work(fm_ctx* ctx, int64_t B, int64_t N) {
 
 namespace {
 
-int step_impl(fm_ctx* ctx, fm_batch* b, int32_t t, double step_size, double reg_param, fm_step_out* out) {
+__global__ void k_store_count(const unsigned long long* c, double* dst) { *dst = (double)*c; }
+
+// One fused step.  emit != nullptr (replicated mode, fm_repl_grad): the per-slot gradient sums
+// are written to emit[rows][kp + 4] instead of being applied, and the epoch does not advance.
+int step_impl(fm_ctx* ctx, fm_batch* b, int32_t t, double step_size, double reg_param, fm_step_out* out,
+              float* emit = nullptr) {
   FM_REQUIRE(b != nullptr, "null batch");
   FM_REQUIRE(b->owner == ctx, "batch belongs to another context");
   FM_REQUIRE(ctx->cfg.shard_count == 1, "sharded contexts step through the fm_shard_* entry points");
+  if (emit) FM_HIP_CHECK(hipMemsetAsync(emit, 0, sizeof(float) * (size_t)ctx->rows * (ctx->kp + 4), ctx->stream));
   if (b->dev.n_rows == 0) return FM_NOTHING_TO_DO;  // SGD.scala:126-128
   FM_REQUIRE(t >= 1, "iteration index t must be >= 1");
   FM_REQUIRE(std::isfinite(step_size) && std::isfinite(reg_param), "non-finite step size / regParam");
@@ -152,13 +158,14 @@ int step_impl(fm_ctx* ctx, fm_batch* b, int32_t t, double step_size, double reg_
   FM_HIP_CHECK(hipStreamWaitEvent(ctx->stream, prepared ? b->ready : ctx->ev_join, 0));
   e0 = ctx->prof_begin(ctx->stream);
   double* stats = ctx->loss_hist.as<double>() + 3 * (int64_t)ctx->epoch;
-  launch_segment_update(T, b->dev, ctx->work, p, skeys, sents, nfwd, stats, ctx->stream);
+  launch_segment_update(T, b->dev, ctx->work, p, skeys, sents, nfwd, stats, ctx->stream, emit);
   FM_HIP_CHECK(hipEventRecord(ctx->ev_upd_done, ctx->stream));
   if (prepared) {
     FM_HIP_CHECK(hipEventRecord(b->last_use, ctx->stream));
     b->prepared = false;
   }
   ctx->prof_end("update", e0, ctx->stream);
+  if (emit) return FM_OK;
   ctx->epoch += 1;
   ctx->cum_host.push_back(p.cum_next);
   if (out) {
@@ -561,6 +568,70 @@ int fm_profile_read(fm_ctx* ctx, char* names, int64_t names_cap, double* total_m
       std::memcpy(names, joined.data(), m);
       names[m] = '\0';
     }
+    return FM_OK;
+  });
+}
+
+int fm_repl_grad(fm_ctx* ctx, fm_batch* batch, void* grad) {
+  return guarded(ctx, [&]() -> int {
+    FM_REQUIRE(grad != nullptr, "null gradient buffer");
+    FM_REQUIRE(!ctx->repl_pending, "fm_repl_apply must follow fm_repl_grad");
+    ctx->ensure_hist(ctx->epoch + 1);
+    double* stats = ctx->loss_hist.as<double>() + 3 * (int64_t)ctx->epoch;
+    FM_HIP_CHECK(hipMemsetAsync(stats, 0, sizeof(double) * 3, ctx->stream));
+    const int rc = step_impl(ctx, batch, 1, 0.0, 0.0, nullptr, reinterpret_cast<float*>(grad));
+    ctx->repl_pending = true;
+    return rc;
+  });
+}
+
+int fm_repl_apply(fm_ctx* ctx, const void* grad, int32_t t, double step_size, double reg_param,
+                  int64_t global_rows) {
+  return guarded(ctx, [&]() -> int {
+    FM_REQUIRE(ctx->repl_pending, "fm_repl_grad must run first");
+    FM_REQUIRE(global_rows >= 0, "negative global_rows");
+    ctx->repl_pending = false;
+    if (global_rows == 0) return FM_NOTHING_TO_DO;  // SGD.scala:126-128 (every rank skips)
+    FM_REQUIRE(grad != nullptr, "null gradient buffer");
+    FM_REQUIRE(t >= 1, "iteration index t must be >= 1");
+    FM_REQUIRE(std::isfinite(step_size) && std::isfinite(reg_param), "non-finite step size / regParam");
+    StepParams p{};
+    p.n_rows = global_rows;
+    p.eta = step_size / std::sqrt((double)t);  // SGD.scala:121
+    p.lam = p.eta * reg_param;                 // SGD.scala:122
+    p.m = (double)global_rows;                 // global miniBatchSize
+    p.scale_v = p.eta / (double)global_rows;
+    p.epoch = ctx->epoch;
+    p.cumE = ctx->cum_host.back();
+    p.cum_next = p.cumE + p.lam;
+    p.w0 = ctx->cfg.w0;
+    ctx->ensure_hist(ctx->epoch + 1);
+    ctx->repl_cnt.ensure(sizeof(unsigned long long));
+    hipEvent_t e0 = ctx->prof_begin(ctx->stream);
+    launch_repl_apply(ctx->view(), reinterpret_cast<const float*>(grad), p, ctx->repl_cnt.as<unsigned long long>(),
+                      ctx->stream);
+    double* stats = ctx->loss_hist.as<double>() + 3 * (int64_t)ctx->epoch;
+    hipLaunchKernelGGL(k_store_count, dim3(1), dim3(1), 0, ctx->stream, ctx->repl_cnt.as<unsigned long long>(),
+                       stats + 2);
+    FM_HIP_CHECK(hipGetLastError());
+    ctx->prof_end("apply", e0, ctx->stream);
+    ctx->epoch += 1;
+    ctx->cum_host.push_back(p.cum_next);
+    return FM_OK;
+  });
+}
+
+int fm_last_stats(fm_ctx* ctx, double* loss_sum, int64_t* n_loss_rows, int64_t* n_unique) {
+  return guarded(ctx, [&]() -> int {
+    FM_REQUIRE(loss_sum && n_loss_rows && n_unique, "null argument");
+    FM_REQUIRE(ctx->epoch >= 1, "no step executed");
+    double h[3];
+    FM_HIP_CHECK(hipMemcpyAsync(h, ctx->loss_hist.as<double>() + 3 * (int64_t)(ctx->epoch - 1), sizeof(h),
+                                hipMemcpyDeviceToHost, ctx->stream));
+    FM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    *loss_sum = h[0];
+    *n_loss_rows = (int64_t)h[1];
+    *n_unique = (int64_t)h[2];
     return FM_OK;
   });
 }

@@ -78,6 +78,7 @@ struct fm_ctx {
   int64_t hist_cap = 0;
   StepWork work;
   Pinned pinned;
+  Pinned sh_pin_off, sh_pin_poff;  // host staging of the sharded phases' small H2D copies
   // profiling
   bool prof = false;
   std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> pending;
@@ -85,17 +86,29 @@ struct fm_ctx {
   std::map<std::string, ProfEntry> prof_acc;
   std::vector<std::string> prof_order;
   // sharded step state (fm_shard.hip)
-  DevBuf plan_ck;        // [N] composite keys owner * rows_per_shard + slot
-  DevBuf plan_run;       // [N] distinct-id index per sorted position
-  DevBuf plan_uidx;      // [N] distinct-id index per entry (CSR order)
-  DevBuf plan_req;       // [U] int32 requested slots, owner-major
-  DevBuf plan_counts;    // [R] per-owner request counts, then U
-  DevBuf plan_bsum;      // run-index scan block sums
-  const uint32_t* plan_skeys = nullptr;  // sorted composite keys (in the sort workspace)
-  const uint32_t* plan_sidx = nullptr;   // entry index per sorted position
-  const fm_batch* plan_batch = nullptr;
-  int64_t plan_unique = 0;
-  int64_t plan_nnz = -1;
+  //  requester (route / combine)
+  DevBuf sh_okey;      // [N] owner of each entry (partition sort keys)
+  DevBuf sh_mask;      // [B] uint64 owners present in each sample
+  DevBuf sh_tcnt;      // [R][tiles] pair counts -> exclusive offsets
+  DevBuf sh_tot;       // [R] pairs per owner, then [R] entries per owner (uint64)
+  DevBuf sh_pairidx;   // [B][R] int32 pair index of (sample, owner), -1 if none
+  const fm_batch* sh_route_batch = nullptr;
+  int64_t sh_route_nnz = -1;
+  std::vector<int64_t> sh_pairs_out;  // pairs sent to each owner
+  int64_t sh_loss_blocks = 0;
+  bool sh_combined = false;
+  //  owner (owner_forward / owner_update)
+  const uint32_t* sh_recv_slot = nullptr;  // caller's buffer, valid until owner_update
+  int64_t sh_recv_n = -1;
+  int64_t sh_P = 0;                        // pairs received
+  DevBuf sh_src_off;   // [R+1] int64 source offsets of the received entries
+  DevBuf sh_bsum;      // pair-head scan block sums (+ total)
+  DevBuf sh_pair_ptr;  // [P+1] int64 entry offsets of the pairs
+  DevBuf sh_ent2;      // [n] uint2 {pair, x bits}
+  DevBuf sh_skeys, sh_sents;  // sorted slots / {pair, x}
+  // replicated step state (fm_repl_*)
+  DevBuf repl_cnt;            // touched-row counter (uint64)
+  bool repl_pending = false;  // fm_repl_grad ran, fm_repl_apply not yet
 
   TableView view() const {
     TableView T;
@@ -187,8 +200,9 @@ struct fm_ctx {
     loss_hist.release();
     DevBuf* bufs[] = {&work.S, &work.yl, &work.loss_part, &work.part, &work.ucnt,
                       &work.sort.keys_a, &work.sort.keys_b, &work.sort.vals_a, &work.sort.vals_b,
-                      &work.sort.counts, &work.sort.digit_tot, &plan_ck, &plan_run, &plan_uidx,
-                      &plan_req, &plan_counts, &plan_bsum};
+                      &work.sort.counts, &work.sort.digit_tot, &sh_okey, &sh_mask, &sh_tcnt, &sh_tot,
+                      &sh_pairidx, &sh_src_off, &sh_bsum, &sh_pair_ptr, &sh_ent2, &sh_skeys, &sh_sents,
+                      &repl_cnt};
     for (auto* b : bufs) b->release();
     if (own_stream && stream) (void)hipStreamDestroy(stream);
   }

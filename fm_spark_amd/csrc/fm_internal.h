@@ -130,12 +130,28 @@ struct StepParams {
   double w0;
 };
 
+// partial_out != nullptr: the sharded owner's partial pass (rows [kp + 4] per pair, fm_shard.hip)
 void launch_forward(const TableView& T, const BatchDev& b, StepWork& w, const StepParams& p,
-                    hipStream_t st, int64_t* n_fwd_blocks, const float* rows = nullptr,
-                    const uint32_t* uidx = nullptr);
+                    hipStream_t st, int64_t* n_fwd_blocks, float* partial_out = nullptr);
+// per-sample inputs of the segmented update: S rows of s_stride_q quads, {yhat, y} at yl[s * yl_stride]
+struct SegSource {
+  const float* S;
+  int s_stride_q;
+  const float2* yl;
+  int yl_stride;
+};
+// emit != nullptr (replicated mode): the per-slot gradient sums go to emit[rows][kp + 4] as
+// [sum g_V (kp) | sum g_w | 1 (touched) | 0] instead of being applied to the table
 void launch_segment_update(const TableView& T, const BatchDev& b, StepWork& w, const StepParams& p,
                            const uint32_t* skeys, const uint2* sents, int64_t n_fwd_blocks,
-                           double* stats_out, hipStream_t st);
+                           double* stats_out, hipStream_t st, float* emit = nullptr);
+void launch_segment_update(const TableView& T, int64_t N, const SegSource& src, StepWork& w, const StepParams& p,
+                           const uint32_t* skeys, const uint2* sents, int64_t n_loss_blocks, double* stats_out,
+                           hipStream_t st, float* emit = nullptr);
+// replicated mode: apply the all-reduced gradient sums grad[rows][kp + 4] to every touched row;
+// the number of touched rows -> *n_touched (device)
+void launch_repl_apply(const TableView& T, const float* grad, const StepParams& p, unsigned long long* n_touched,
+                       hipStream_t st);
 
 void launch_init_random(const TableView& T, const int32_t* ids, int64_t n, int64_t id_begin,
                         uint64_t seed, double sd, int32_t epoch, double cumE, hipStream_t st);

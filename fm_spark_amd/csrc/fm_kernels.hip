@@ -61,13 +61,11 @@ __device__ __forceinline__ void current_row(const RowHdr& h, float4& v, float& w
 }
 
 // ------------------------------------------------------------------------ forward
-// FROM_ROWS: the sharded step's forward; entry e's row is rows[uidx[e]] of the rows this rank
-// received from the owners (already current, wire layout [V(kp) | w | pad]) instead of the
-// local table.
-template <int GS, int TEAM, bool FROM_ROWS>
-__global__ __launch_bounds__(kBlock) void k_forward(TableView T, const float* __restrict__ rows,
-                                                    const uint32_t* __restrict__ uidx,
-                                                    const int64_t* __restrict__ row_ptr,
+// PARTIAL: the sharded owner's pass (fm_shard.hip).  "Samples" are (source rank, sample)
+// pairs of the entries this owner received; the output per pair is the partial row
+// [sum v*x (kp) | sum v^2 x^2 | sum w*x | 0 0] (fp32) instead of S / yhat / loss.
+template <int GS, int TEAM, bool PARTIAL>
+__global__ __launch_bounds__(kBlock) void k_forward(TableView T, const int64_t* __restrict__ row_ptr,
                                                     const uint32_t* __restrict__ col,
                                                     const uint2* __restrict__ ent,
                                                     const float* __restrict__ label, int64_t B,
@@ -100,14 +98,9 @@ __global__ __launch_bounds__(kBlock) void k_forward(TableView T, const float* __
       }
       RowHdr h[U];
       float4 v[U];
-      float wr[U];
 #pragma unroll
       for (int j = 0; j < U; ++j) {
-        if (FROM_ROWS) {
-          const float* row = rows + (int64_t)(ok[j] ? uidx[eb + j * RPP] : 0u) * (kp + 4);
-          v[j] = (ok[j] && qok) ? reinterpret_cast<const float4*>(row)[g] : make_float4(0.f, 0.f, 0.f, 0.f);
-          wr[j] = ok[j] ? row[kp] : 0.f;
-        } else if (ok[j]) {
+        if (ok[j]) {
           h[j] = *T.hdr(id[j]);
           v[j] = qok ? reinterpret_cast<const float4*>(T.v(id[j]))[g] : make_float4(0.f, 0.f, 0.f, 0.f);
         } else {
@@ -118,8 +111,7 @@ __global__ __launch_bounds__(kBlock) void k_forward(TableView T, const float* __
 #pragma unroll
       for (int j = 0; j < U; ++j) {
         float w;
-        if (FROM_ROWS) w = wr[j];
-        else current_row(h[j], v[j], w, cumE);
+        current_row(h[j], v[j], w, cumE);
         const double xd = x[j];
         // vfxi = v * x (Model.scala:179), VectorSum over the sample (:191)
         a0 += (double)v[j].x * xd; a1 += (double)v[j].y * xd;
@@ -142,6 +134,13 @@ __global__ __launch_bounds__(kBlock) void k_forward(TableView T, const float* __
       vv += __shfl_xor(vv, o);
       wx += __shfl_xor(wx, o);
     }
+    if (PARTIAL) {
+      const int W = kp + 4;
+      if (rs == 0 && qok)
+        *reinterpret_cast<float4*>(S_out + s * W + g * 4) = make_float4((float)a0, (float)a1, (float)a2, (float)a3);
+      if (tl == 0) *reinterpret_cast<float4*>(S_out + s * W + kp) = make_float4((float)vv, (float)wx, 0.f, 0.f);
+      continue;
+    }
     double ss = qok ? a0 * a0 + a1 * a1 + a2 * a2 + a3 * a3 : 0.0;
 #pragma unroll
     for (int o = 1; o < GS; o <<= 1) ss += __shfl_xor(ss, o);
@@ -159,6 +158,7 @@ __global__ __launch_bounds__(kBlock) void k_forward(TableView T, const float* __
       }
     }
   }
+  if (PARTIAL) return;
   // deterministic block reduction of the loss partials
   __shared__ double red[2][kBlock / 64];
 #pragma unroll
@@ -187,13 +187,16 @@ struct SegArgs {
   const uint32_t* skeys;  // sorted feature slots
   const uint2* sents;     // their entries {sample, x bits}, same order
   int64_t N;
-  const float* S;
-  const float2* yl;
+  const float* S;   // per-sample rows of s_stride_q quads (vfxiSum first)
+  const float2* yl; // {yhat, y} of sample s at yl[s * yl_stride]
+  int s_stride_q;
+  int yl_stride;
   double* part;     // [nranges][2][kp + 1]
   int64_t nranges;  // ranges of L sorted entries, one wave each
   int64_t L;        // entries per range (64 * CH)
   StepParams p;
   uint32_t* ucnt;  // [update blocks]
+  float* emit;     // replicated mode: per-slot gradient sums [rows][kp + 4] instead of the update
 };
 
 // Per-entry scalars of the current chunk, staged in LDS for the G-lanes-per-entry phase.
@@ -269,7 +272,7 @@ __global__ __launch_bounds__(kBlock) void k_segment_update(SegArgs a) {
     const float xf = __uint_as_float(en.y);
     const double x = (double)xf;
     const RowHdr h = valid ? (*T.hdr(key)) : RowHdr{0.f, -1, 0.0};  // read before any write-back
-    const float2 yl = valid ? a.yl[s] : make_float2(0.f, 0.f);
+    const float2 yl = valid ? a.yl[(int64_t)s * a.yl_stride] : make_float2(0.f, 0.f);
 
     const bool last_chunk = (c == CH - 1) || (p0 + 64 >= a.N);
     const bool seg_start = valid && key != prev_key;  // a run of this key starts here
@@ -300,7 +303,9 @@ __global__ __launch_bounds__(kBlock) void k_segment_update(SegArgs a) {
     if (cont && start_lane == 0) gw += cw;
     cw = __shfl(gw, 63);
     if (writes) {
-      if (complete) {  // the header is stored with the V row in phase 2
+      if (complete && a.emit) {  // [.. | sum g_w | touched]
+        *reinterpret_cast<float2*>(a.emit + (int64_t)key * (kp + 4) + kp) = make_float2((float)gw, 1.f);
+      } else if (complete) {  // the header is stored with the V row in phase 2
         float w = present ? h.w : 0.f;
         if (ac > 0.0) w = shrink_f(w, ac);
         wnew_s[wave][lane] = upd_w(w, gw, a.p);  // SGD.scala:150, :171, :179
@@ -337,7 +342,7 @@ __global__ __launch_bounds__(kBlock) void k_segment_update(SegArgs a) {
 #pragma unroll
         for (int u = 0; u < PF; ++u) {
           const bool vj = (ei[u].flags & 1) && qok;
-          sq[u] = vj ? S4[(int64_t)ei[u].s * nq + q] : make_float4(0.f, 0.f, 0.f, 0.f);
+          sq[u] = vj ? S4[(int64_t)ei[u].s * a.s_stride_q + q] : make_float4(0.f, 0.f, 0.f, 0.f);
           v[u] = (vj && (ei[u].flags & 8)) ? reinterpret_cast<const float4*>(T.v(ei[u].key))[q]
                                            : make_float4(0.f, 0.f, 0.f, 0.f);
         }
@@ -374,7 +379,11 @@ __global__ __launch_bounds__(kBlock) void k_segment_update(SegArgs a) {
           cv0 = __shfl(c0, last); cv1 = __shfl(c1, last);
           cv2 = __shfl(c2, last); cv3 = __shfl(c3, last);
           if ((fl & 1) && (fl & 2)) {
-            if (fl & 4) {
+            if ((fl & 4) && a.emit) {
+              if (qok)
+                reinterpret_cast<float4*>(a.emit + (int64_t)ei[u].key * (kp + 4))[q] =
+                    make_float4((float)c0, (float)c1, (float)c2, (float)c3);
+            } else if (fl & 4) {
               float4* rec = reinterpret_cast<float4*>(T.v(ei[u].key));
               if (qok)
                 rec[q] = make_float4(upd_v(v[u].x, c0, a.p), upd_v(v[u].y, c1, a.p), upd_v(v[u].z, c2, a.p),
@@ -477,7 +486,13 @@ __global__ __launch_bounds__(kBlock) void k_segment_combine(SegArgs a, const dou
     const int64_t c2 = chunk + 2;
     two = !(c2 < a.nranges && a.skeys[c2 * L] == key);
   }
-  if (owner && two) {
+  if (owner && two && a.emit) {
+    const double* pt = a.part + (chunk * 2 + 1) * W;
+    const double* ph = a.part + ((chunk + 1) * 2) * W;
+    float* gr = a.emit + (int64_t)key * (kp + 4);
+    for (int f = 0; f < kp; ++f) gr[f] = (float)(pt[1 + f] + ph[1 + f]);
+    *reinterpret_cast<float2*>(gr + kp) = make_float2((float)(pt[0] + ph[0]), 1.f);
+  } else if (owner && two) {
     const double* pt = a.part + (chunk * 2 + 1) * W;
     const double* ph = a.part + ((chunk + 1) * 2) * W;
     const RowHdr h = *T.hdr(key);
@@ -542,7 +557,11 @@ __global__ __launch_bounds__(kBlock) void k_segment_combine(SegArgs a, const dou
           g += g3;
         }
         for (; c < cend; ++c) g += a.part[(c * 2) * W + f];
-        if (f == 0) {
+        if (a.emit) {
+          float* gr = a.emit + (int64_t)k0 * (kp + 4);
+          if (f == 0) *reinterpret_cast<float2*>(gr + kp) = make_float2((float)g, 1.f);
+          else gr[f - 1] = (float)g;
+        } else if (f == 0) {
           float w = present ? h.w : 0.f;
           if (ac > 0.0) w = shrink_f(w, ac);
           wnew = upd_w(w, g, a.p);
@@ -553,7 +572,7 @@ __global__ __launch_bounds__(kBlock) void k_segment_combine(SegArgs a, const dou
         }
       }
     }
-    if (lane == 0) {
+    if (lane == 0 && !a.emit) {
       RowHdr o;
       o.w = wnew;
       o.t = a.p.epoch + 1;
@@ -561,6 +580,48 @@ __global__ __launch_bounds__(kBlock) void k_segment_combine(SegArgs a, const dou
       store_hdr(T, k0, o);
     }
   }
+}
+
+// ------------------------------------------------------------- replicated apply
+// Every rank holds the whole table; the gradient sums of all ranks were all-reduced into
+// grad[rows][kp + 4] = [sum g_V | sum g_w | touched | 0].  G lanes per row: the update + L1
+// of SGD.scala:150-181 on touched rows (untouched rows take their L1 lazily, as always).
+template <int G>
+__global__ __launch_bounds__(kBlock) void k_repl_apply(TableView T, const float* __restrict__ grad, StepParams p,
+                                                       unsigned long long* __restrict__ n_touched) {
+  const int g = threadIdx.x % G;
+  const int kp = T.kp, nq = kp >> 2, W = kp + 4;
+  uint32_t touched = 0;
+  for (int64_t i = ((int64_t)blockIdx.x * kBlock + threadIdx.x) / G; i < T.rows;
+       i += (int64_t)gridDim.x * kBlock / G) {
+    const float* gr = grad + i * W;
+    const float2 wt = *reinterpret_cast<const float2*>(gr + kp);
+    if (wt.y == 0.f) continue;
+    touched += g == 0 ? 1u : 0u;
+    const RowHdr h = *T.hdr(i);
+    const bool present = h.t >= 0;
+    const double ac = present ? p.cumE - h.cum : 0.0;
+    float4* rec = reinterpret_cast<float4*>(T.v(i));
+    for (int q = g; q < nq; q += G) {
+      float4 v = present ? rec[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+      if (ac > 0.0) v = shrink4(v, ac);
+      const float4 d = reinterpret_cast<const float4*>(gr)[q];
+      rec[q] = make_float4(upd_v(v.x, d.x, p), upd_v(v.y, d.y, p), upd_v(v.z, d.z, p), upd_v(v.w, d.w, p));
+    }
+    if (g == 0) {
+      float w = present ? h.w : 0.f;
+      if (ac > 0.0) w = shrink_f(w, ac);
+      RowHdr o;
+      o.w = upd_w(w, (double)wt.x, p);
+      o.t = p.epoch + 1;
+      o.cum = p.cum_next;
+      store_hdr(T, i, o);
+    }
+  }
+  // integer count: deterministic
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) touched += __shfl_xor(touched, o);
+  if ((threadIdx.x & 63) == 0 && touched) atomicAdd(n_touched, (unsigned long long)touched);
 }
 
 // ---------------------------------------------------------------- table utilities
@@ -791,43 +852,49 @@ inline unsigned grid_for(int64_t n, int block, int64_t cap = 256 * 16) {
 
 template <int GS, int TEAM>
 void launch_fwd_t(const TableView& T, const BatchDev& b, StepWork& w, const StepParams& p, hipStream_t st,
-                  int64_t* nblk, const float* rows, const uint32_t* uidx) {
+                  int64_t* nblk, float* partial_out) {
   constexpr int TPB = kBlock / TEAM;
   int64_t blocks = (b.n_rows + TPB - 1) / TPB;
   if (blocks > 256 * 8) blocks = 256 * 8;
   if (blocks < 1) blocks = 1;
   *nblk = blocks;
   w.loss_part.ensure(sizeof(double2) * blocks);
-  if (rows)
-    hipLaunchKernelGGL((k_forward<GS, TEAM, true>), dim3((unsigned)blocks), dim3(kBlock), 0, st, T, rows, uidx,
+  if (partial_out)
+    hipLaunchKernelGGL((k_forward<GS, TEAM, true>), dim3((unsigned)blocks), dim3(kBlock), 0, st, T,
+                       b.row_ptr.as<int64_t>(), b.col.as<uint32_t>(), b.ent.as<uint2>(), nullptr, b.n_rows, p.w0,
+                       p.cumE, partial_out, nullptr, nullptr);
+  else
+    hipLaunchKernelGGL((k_forward<GS, TEAM, false>), dim3((unsigned)blocks), dim3(kBlock), 0, st, T,
                        b.row_ptr.as<int64_t>(), b.col.as<uint32_t>(), b.ent.as<uint2>(), b.label.as<float>(),
                        b.n_rows, p.w0, p.cumE, w.S.as<float>(), w.yl.as<float2>(), w.loss_part.as<double2>());
-  else
-  hipLaunchKernelGGL((k_forward<GS, TEAM, false>), dim3((unsigned)blocks), dim3(kBlock), 0, st, T, rows, uidx,
-                     b.row_ptr.as<int64_t>(), b.col.as<uint32_t>(), b.ent.as<uint2>(), b.label.as<float>(),
-                     b.n_rows, p.w0, p.cumE, w.S.as<float>(), w.yl.as<float2>(), w.loss_part.as<double2>());
 }
 
 }  // namespace
 
 void launch_forward(const TableView& T, const BatchDev& b, StepWork& w, const StepParams& p, hipStream_t st,
-                    int64_t* n_fwd_blocks, const float* rows, const uint32_t* uidx) {
+                    int64_t* n_fwd_blocks, float* partial_out) {
   const int nq = T.kp / 4;
-  if (nq <= 1) launch_fwd_t<1, 16>(T, b, w, p, st, n_fwd_blocks, rows, uidx);
-  else if (nq <= 2) launch_fwd_t<2, 16>(T, b, w, p, st, n_fwd_blocks, rows, uidx);
-  else if (nq <= 4) launch_fwd_t<4, 16>(T, b, w, p, st, n_fwd_blocks, rows, uidx);
-  else if (nq <= 8) launch_fwd_t<8, 16>(T, b, w, p, st, n_fwd_blocks, rows, uidx);
-  else if (nq <= 16) launch_fwd_t<16, 16>(T, b, w, p, st, n_fwd_blocks, rows, uidx);
-  else if (nq <= 32) launch_fwd_t<32, 32>(T, b, w, p, st, n_fwd_blocks, rows, uidx);
-  else if (nq <= 64) launch_fwd_t<64, 64>(T, b, w, p, st, n_fwd_blocks, rows, uidx);
+  if (nq <= 1) launch_fwd_t<1, 16>(T, b, w, p, st, n_fwd_blocks, partial_out);
+  else if (nq <= 2) launch_fwd_t<2, 16>(T, b, w, p, st, n_fwd_blocks, partial_out);
+  else if (nq <= 4) launch_fwd_t<4, 16>(T, b, w, p, st, n_fwd_blocks, partial_out);
+  else if (nq <= 8) launch_fwd_t<8, 16>(T, b, w, p, st, n_fwd_blocks, partial_out);
+  else if (nq <= 16) launch_fwd_t<16, 16>(T, b, w, p, st, n_fwd_blocks, partial_out);
+  else if (nq <= 32) launch_fwd_t<32, 32>(T, b, w, p, st, n_fwd_blocks, partial_out);
+  else if (nq <= 64) launch_fwd_t<64, 64>(T, b, w, p, st, n_fwd_blocks, partial_out);
   else FM_REQUIRE(false, "dimFactorization > 256 is not supported");
   FM_HIP_CHECK(hipGetLastError());
 }
 
 void launch_segment_update(const TableView& T, const BatchDev& b, StepWork& w, const StepParams& p,
                            const uint32_t* skeys, const uint2* sents, int64_t n_fwd_blocks,
-                           double* stats_out, hipStream_t st) {
-  const int64_t N = b.nnz;
+                           double* stats_out, hipStream_t st, float* emit) {
+  SegSource src{w.S.as<float>(), T.kp / 4, w.yl.as<float2>(), 1};
+  launch_segment_update(T, b.nnz, src, w, p, skeys, sents, n_fwd_blocks, stats_out, st, emit);
+}
+
+void launch_segment_update(const TableView& T, int64_t N, const SegSource& src, StepWork& w, const StepParams& p,
+                           const uint32_t* skeys, const uint2* sents, int64_t n_fwd_blocks, double* stats_out,
+                           hipStream_t st, float* emit) {
   const int nq = T.kp / 4;
   const int G = nq <= 1 ? 1 : nq <= 2 ? 2 : nq <= 4 ? 4 : nq <= 8 ? 8 : 16;
   const int CH = nq <= G ? kUpdateChunks : 1;  // carries across chunks need one quad-chunk
@@ -841,13 +908,16 @@ void launch_segment_update(const TableView& T, const BatchDev& b, StepWork& w, c
   a.skeys = skeys;
   a.sents = sents;
   a.N = N;
-  a.S = w.S.as<float>();
-  a.yl = w.yl.as<float2>();
+  a.S = src.S;
+  a.yl = src.yl;
+  a.s_stride_q = src.s_stride_q;
+  a.yl_stride = src.yl_stride;
   a.part = w.part.as<double>();
   a.nranges = nranges;
   a.L = L;
   a.p = p;
   a.ucnt = w.ucnt.as<uint32_t>();
+  a.emit = emit;
   if (nranges > 0) {
     const dim3 grid((unsigned)ublocks), blk(kBlock);
     if (nq > G) {
@@ -891,6 +961,23 @@ void launch_table_reset(const TableView& T, hipStream_t st) {
   if (T.rows <= 0) return;
   FM_HIP_CHECK(hipMemsetAsync(T.rec, 0, sizeof(float) * (size_t)T.rows * T.stride, st));
   hipLaunchKernelGGL(k_table_reset, dim3(grid_for(T.rows, kBlock)), dim3(kBlock), 0, st, T);
+  FM_HIP_CHECK(hipGetLastError());
+}
+
+void launch_repl_apply(const TableView& T, const float* grad, const StepParams& p, unsigned long long* n_touched,
+                       hipStream_t st) {
+  FM_HIP_CHECK(hipMemsetAsync(n_touched, 0, sizeof(unsigned long long), st));
+  if (T.rows <= 0) return;
+  const int nq = T.kp / 4;
+  const int G = nq <= 1 ? 1 : nq <= 2 ? 2 : nq <= 4 ? 4 : nq <= 8 ? 8 : 16;
+  const unsigned grid = grid_for(T.rows * G, kBlock);
+  switch (G) {
+    case 1: hipLaunchKernelGGL(k_repl_apply<1>, dim3(grid), dim3(kBlock), 0, st, T, grad, p, n_touched); break;
+    case 2: hipLaunchKernelGGL(k_repl_apply<2>, dim3(grid), dim3(kBlock), 0, st, T, grad, p, n_touched); break;
+    case 4: hipLaunchKernelGGL(k_repl_apply<4>, dim3(grid), dim3(kBlock), 0, st, T, grad, p, n_touched); break;
+    case 8: hipLaunchKernelGGL(k_repl_apply<8>, dim3(grid), dim3(kBlock), 0, st, T, grad, p, n_touched); break;
+    default: hipLaunchKernelGGL(k_repl_apply<16>, dim3(grid), dim3(kBlock), 0, st, T, grad, p, n_touched); break;
+  }
   FM_HIP_CHECK(hipGetLastError());
 }
 

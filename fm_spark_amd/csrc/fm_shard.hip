@@ -1,25 +1,34 @@
-// Row-sharded FM SGD step (one context per rank, owner of feature id = id % R, local slot =
-// id / R).  The fused single-table step of fm_kernels.hip split at its two data-dependence
-// points so the caller can exchange over RCCL all-to-all between phases:
+// Row-sharded FM SGD step, owner-computes (one context per rank; the owner of feature id is
+// id % R, its local slot id / R).  Every rank holds 1/R of the table and steps its own
+// mini-batch; one iteration is four phases of the C-ABI joined by three all-to-alls:
 //
-//   fm_shard_plan        sort the batch's entries by (owner, slot); dedupe -> request list
-//                        (owner-major, one entry per distinct id) + each entry's unique index
-//   -- all-to-all requests -->
-//   fm_shard_serve       owner: gather the requested rows, pending L1 applied
-//   -- all-to-all rows <--
-//   fm_shard_local_grad  forward from the received rows + per-distinct-id partial gradient
-//                        (segmented reduction over the plan's sorted order; fp64 sums, fp32 wire)
-//   -- all-to-all gradients -->
-//   fm_shard_apply       owner: merge the <= R partials per slot in fixed rank order, apply the
-//                        update + L1 of SGD.scala:150-181, advance the epoch.
+//   fm_shard_route          requester: the batch's entries partitioned by owner (CSR order kept)
+//                           as {slot} and {sample, x}; per sample the owners it touches and the
+//                           pair index of every (sample, owner) pair
+//   -- all-to-all entries -->
+//   fm_shard_owner_forward  owner: per received (source, sample) pair, the partial forward sums
+//                           over the entries it owns: [sum v*x | sum v^2 x^2 | sum w*x], lazy L1
+//                           caught up on read (FactorizationMachinesModel.scala:173-221)
+//   -- all-to-all partials <--
+//   fm_shard_combine        requester: per sample, the owners' partials summed in owner order
+//                           (fp64) -> vfxiSum S, yhat, loss; S | yhat | y sent back per pair
+//   -- all-to-all S -->
+//   fm_shard_owner_update   owner: the received entries sorted by slot (stable: source rank
+//                           order, then CSR order) and the fused segmented gradient + update + L1
+//                           of fm_kernels.hip (SGD.scala:143-181) on its own rows
 //
 // Semantics equal the single-table step over the ranks' batches concatenated in rank order
-// (global miniBatchSize m = sum of the ranks' rows), up to fp summation order.
-// Wire formats: rows [V(kp) | w | 0 0 0] fp32, gradients [gV(kp) | gw | 0 0 0] fp32; kp + 4
-// floats per distinct id.
+// (global miniBatchSize m = sum of the ranks' rows), up to fp summation order: the forward
+// sums are split per owner (fp32 on the wire), the per-feature gradient sums run over the
+// same entries in the same order.  Deterministic for a given R.
+// Traffic per rank and step (k = 16, z = 39, R = 8): entries 12 B each, partials and S rows
+// (kp + 4) * 4 B per (sample, owner) pair -- about 400 MB, against about 1 GB when rows and
+// gradients of every distinct id travel instead.
+// Wire rows are kp + 4 floats: partial [sum vx (kp) | vv | wx | 0 0], S [S (kp) | yhat | y | 0 0].
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
+#include <cstring>
 
 #include "fm_context.h"
 #include "fm_device.h"
@@ -29,26 +38,144 @@ namespace fmhip {
 namespace {
 
 constexpr int kBlock = 256;
-constexpr int kTileS = 4096;  // entries per block in the run-index scan
+constexpr int kTileS = 4096;  // entries per block in the pair-head scan
+constexpr int kMaxR = 64;     // owner masks are uint64
 
-__global__ void k_shard_keys(const uint32_t* __restrict__ col, int64_t n, uint32_t R, uint32_t rpsh,
-                             uint32_t* __restrict__ ck) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const uint32_t id = col[i];
-    ck[i] = (id % R) * rpsh + id / R;
+__device__ __forceinline__ uint32_t incl_scan_u32(uint32_t v, int lane) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t t = __shfl_up(v, o);
+    if (lane >= o) v += t;
+  }
+  return v;
+}
+
+// ------------------------------------------------------------------ requester: route
+__global__ void k_owner_keys(const uint32_t* __restrict__ col, int64_t n, uint32_t R, uint32_t* __restrict__ okey) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    okey[i] = col[i] % R;
+}
+
+// per sample: the owners it touches (bit mask); per owner: entry counts
+__global__ __launch_bounds__(kBlock) void k_sample_mask(const int64_t* __restrict__ row_ptr,
+                                                        const uint32_t* __restrict__ col, int64_t B, uint32_t R,
+                                                        uint64_t* __restrict__ mask,
+                                                        unsigned long long* __restrict__ ecount) {
+  __shared__ uint32_t cnt[kMaxR];
+  if (threadIdx.x < kMaxR) cnt[threadIdx.x] = 0;
+  __syncthreads();
+  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < B; s += (int64_t)gridDim.x * blockDim.x) {
+    uint64_t m = 0;
+    for (int64_t e = row_ptr[s]; e < row_ptr[s + 1]; ++e) {
+      const uint32_t o = col[e] % R;
+      m |= 1ull << o;
+      atomicAdd(&cnt[o], 1u);
+    }
+    mask[s] = m;
+  }
+  __syncthreads();
+  if (threadIdx.x < R && cnt[threadIdx.x]) atomicAdd(&ecount[threadIdx.x], (unsigned long long)cnt[threadIdx.x]);
+}
+
+// pairs per (owner, tile of kBlock samples) -> tcnt[o][tile]
+__global__ __launch_bounds__(kBlock) void k_pair_count(const uint64_t* __restrict__ mask, int64_t B, int R,
+                                                       int64_t ntiles, uint32_t* __restrict__ tcnt) {
+  __shared__ uint32_t wc[kBlock / 64][kMaxR];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t s = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const uint64_t m = s < B ? mask[s] : 0ull;
+  for (int o = 0; o < R; ++o) {
+    const uint64_t b = __ballot((m >> o) & 1ull);
+    if (lane == 0) wc[wave][o] = (uint32_t)__popcll(b);
+  }
+  __syncthreads();
+  if (threadIdx.x < R) {
+    uint32_t t = 0;
+    for (int w = 0; w < kBlock / 64; ++w) t += wc[w][threadIdx.x];
+    tcnt[(int64_t)threadIdx.x * ntiles + blockIdx.x] = t;
   }
 }
 
-__device__ __forceinline__ uint32_t run_flag(const uint32_t* skeys, int64_t p, int64_t n) {
-  return (p < n && (p == 0 || skeys[p - 1] != skeys[p])) ? 1u : 0u;
+// one block per row: exclusive scan of rows[r][0..n) in place, row total -> tot[r]
+__global__ __launch_bounds__(kBlock) void k_rows_scan(uint32_t* __restrict__ rows, int64_t n,
+                                                      unsigned long long* __restrict__ tot) {
+  __shared__ uint32_t ws[kBlock / 64];
+  uint32_t* row = rows + (int64_t)blockIdx.x * n;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t carry = 0;
+  for (int64_t b = 0; b < n; b += kBlock) {
+    const int64_t i = b + threadIdx.x;
+    const uint32_t v = i < n ? row[i] : 0u;
+    const uint32_t inc = incl_scan_u32(v, lane);
+    if (lane == 63) ws[wave] = inc;
+    __syncthreads();
+    uint32_t pre = 0, t = 0;
+#pragma unroll
+    for (int w = 0; w < kBlock / 64; ++w) {
+      pre += w < wave ? ws[w] : 0u;
+      t += ws[w];
+    }
+    if (i < n) row[i] = carry + pre + inc - v;
+    carry += t;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) tot[blockIdx.x] = carry;
 }
 
-__global__ __launch_bounds__(kBlock) void k_runs_count(const uint32_t* __restrict__ skeys, int64_t n,
-                                                       uint32_t* __restrict__ bsum) {
+// pair index of every (sample, owner): owner o's pairs are numbered in sample order
+__global__ __launch_bounds__(kBlock) void k_pair_index(const uint64_t* __restrict__ mask, int64_t B, int R,
+                                                       int64_t ntiles, const uint32_t* __restrict__ toff,
+                                                       int32_t* __restrict__ pairidx) {
+  __shared__ uint32_t wc[kBlock / 64][kMaxR];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t s = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const uint64_t m = s < B ? mask[s] : 0ull;
+  const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+  for (int o = 0; o < R; ++o) {
+    const uint64_t b = __ballot((m >> o) & 1ull);
+    if (lane == 0) wc[wave][o] = (uint32_t)__popcll(b);
+  }
+  __syncthreads();
+  for (int o = 0; o < R; ++o) {
+    const bool bit = (m >> o) & 1ull;
+    const uint64_t b = __ballot(bit);
+    uint32_t pre = toff[(int64_t)o * ntiles + blockIdx.x] + (uint32_t)__popcll(b & lt);
+    for (int w = 0; w < wave; ++w) pre += wc[w][o];
+    if (s < B) pairidx[s * R + o] = bit ? (int32_t)pre : -1;
+  }
+}
+
+// entries in owner-partitioned order (sidx: stable partition of entry indices) -> wire
+__global__ void k_route_pack(const uint32_t* __restrict__ sidx, int64_t n, const uint32_t* __restrict__ col,
+                             const uint2* __restrict__ ent, uint32_t R, uint32_t* __restrict__ send_slot,
+                             uint2* __restrict__ send_ent) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t e = sidx[i];
+    send_slot[i] = col[e] / R;
+    send_ent[i] = ent[e];
+  }
+}
+
+// ------------------------------------------------------------------ owner: pairs
+// i starts a (source, sample) pair: first entry of a source's segment, or a new sample
+__device__ __forceinline__ bool pair_head(const uint2* __restrict__ ent, int64_t i, const int64_t* __restrict__ src_off,
+                                          int R) {
+  if (i == 0) return true;
+  for (int r = 1; r < R; ++r)
+    if (src_off[r] == i) return true;
+  return ent[i].x != ent[i - 1].x;
+}
+
+__global__ __launch_bounds__(kBlock) void k_heads_count(const uint2* __restrict__ ent, int64_t n,
+                                                        const int64_t* __restrict__ src_off, int R,
+                                                        uint32_t* __restrict__ bsum) {
   __shared__ uint32_t ws[kBlock / 64];
   const int64_t base = (int64_t)blockIdx.x * kTileS;
   uint32_t c = 0;
-  for (int i = threadIdx.x; i < kTileS; i += kBlock) c += run_flag(skeys, base + i, n);
+  for (int i = threadIdx.x; i < kTileS; i += kBlock) {
+    const int64_t p = base + i;
+    c += (p < n && pair_head(ent, p, src_off, R)) ? 1u : 0u;
+  }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
   if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = c;
@@ -60,349 +187,135 @@ __global__ __launch_bounds__(kBlock) void k_runs_count(const uint32_t* __restric
   }
 }
 
-// single block: exclusive scan of the block sums in place, total -> *total
-__global__ __launch_bounds__(kBlock) void k_runs_scan(uint32_t* __restrict__ bsum, int64_t nb,
-                                                      uint64_t* __restrict__ total) {
+// pair_ptr[pair] = its first entry; ent2[i] = {pair of i, x bits}
+__global__ __launch_bounds__(kBlock) void k_heads_apply(const uint2* __restrict__ ent, int64_t n,
+                                                        const int64_t* __restrict__ src_off, int R,
+                                                        const uint32_t* __restrict__ boff,
+                                                        int64_t* __restrict__ pair_ptr, uint2* __restrict__ ent2) {
   __shared__ uint32_t ws[kBlock / 64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  uint32_t carry = 0;
-  for (int64_t b = 0; b < nb; b += kBlock) {
-    const int64_t i = b + threadIdx.x;
-    const uint32_t v = i < nb ? bsum[i] : 0u;
-    uint32_t inc = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t t = __shfl_up(inc, o);
-      if (lane >= o) inc += t;
-    }
-    if (lane == 63) ws[wave] = inc;
-    __syncthreads();
-    uint32_t pre = 0, tot = 0;
-    for (int w = 0; w < kBlock / 64; ++w) {
-      pre += w < wave ? ws[w] : 0u;
-      tot += ws[w];
-    }
-    if (i < nb) bsum[i] = carry + pre + inc - v;
-    carry += tot;
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) *total = carry;
-}
-
-// Per sorted position: run index (= distinct-id index u), the request list, each entry's
-// unique index (CSR order) and the per-owner request counts.
-__global__ __launch_bounds__(kBlock) void k_plan_apply(const uint32_t* __restrict__ skeys,
-                                                       const uint32_t* __restrict__ sidx, int64_t n,
-                                                       const uint32_t* __restrict__ boff, uint32_t rpsh, int R,
-                                                       int32_t* __restrict__ req, uint32_t* __restrict__ run_of,
-                                                       uint32_t* __restrict__ uidx,
-                                                       unsigned long long* __restrict__ counts) {
-  __shared__ uint32_t ws[kBlock / 64];
-  __shared__ uint32_t ocount[1024];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int o = threadIdx.x; o < R; o += kBlock) ocount[o] = 0;
-  __syncthreads();
   const int64_t base = (int64_t)blockIdx.x * kTileS;
   uint32_t carry = boff[blockIdx.x];
   for (int r = 0; r < kTileS / kBlock; ++r) {
     const int64_t p = base + (int64_t)r * kBlock + threadIdx.x;
-    const uint32_t f = run_flag(skeys, p, n);
-    uint32_t inc = f;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t t = __shfl_up(inc, o);
-      if (lane >= o) inc += t;
-    }
+    const bool valid = p < n;
+    const uint32_t f = (valid && pair_head(ent, p, src_off, R)) ? 1u : 0u;
+    const uint32_t inc = incl_scan_u32(f, lane);
     if (lane == 63) ws[wave] = inc;
     __syncthreads();
     uint32_t pre = 0, tot = 0;
+#pragma unroll
     for (int w = 0; w < kBlock / 64; ++w) {
       pre += w < wave ? ws[w] : 0u;
       tot += ws[w];
     }
-    if (p < n) {
-      const uint32_t u = carry + pre + inc - 1u;  // run containing p
-      const uint32_t key = skeys[p];
-      run_of[p] = u;
-      uidx[sidx[p]] = u;
-      if (f) {
-        req[u] = (int32_t)(key % rpsh);
-        atomicAdd(&ocount[key / rpsh], 1u);
-      }
+    if (valid) {
+      const uint32_t u = carry + pre + inc - 1u;
+      if (f) pair_ptr[u] = p;
+      ent2[p] = make_uint2(u, ent[p].y);
     }
     carry += tot;
     __syncthreads();
   }
-  for (int o = threadIdx.x; o < R; o += kBlock)
-    if (ocount[o]) atomicAdd(&counts[o], (unsigned long long)ocount[o]);
 }
 
-// owner side: requested slots -> rows [V(kp) | w | 0 0 0], pending L1 applied
-template <int G>
-__global__ __launch_bounds__(kBlock) void k_shard_serve(TableView T, const int32_t* __restrict__ req, int64_t n,
-                                                        double cumE, float* __restrict__ rows) {
-  const int g = threadIdx.x % G;
-  const int64_t i = ((int64_t)blockIdx.x * kBlock + threadIdx.x) / G;
-  if (i >= n) return;
-  const int kp = T.kp, nq = kp >> 2, RW = kp + 4;
-  const int64_t slot = req[i];
-  const RowHdr h = *T.hdr(slot);
-  const bool present = h.t >= 0;
-  const double a = present ? cumE - h.cum : 0.0;
-  float* out = rows + i * RW;
-  for (int q = g; q < nq; q += G) {
-    float4 v = present ? reinterpret_cast<const float4*>(T.v(slot))[q] : make_float4(0.f, 0.f, 0.f, 0.f);
-    if (a > 0.0) v = shrink4(v, a);
-    reinterpret_cast<float4*>(out)[q] = v;
-  }
-  if (g == 0) {
-    float w = present ? h.w : 0.f;
-    if (a > 0.0) w = shrink_f(w, a);
-    reinterpret_cast<float4*>(out)[nq] = make_float4(w, 0.f, 0.f, 0.f);
-  }
-}
-
-struct EmitArgs {
-  const uint32_t* skeys;  // composite keys, sorted
-  const uint32_t* sidx;   // entry index e per sorted position
-  const uint32_t* run_of; // distinct-id index u per sorted position
-  const uint2* ent;       // batch entries {sample, x}
-  const float* rows;      // received rows [U][kp+4]
-  const float* S;
-  const float2* yl;
-  float* grads;           // [U][kp+4]
-  double* part;           // [nchunks][2][kp+1]
-  int64_t N, nchunks;
-  int kp;
-};
-
-// Per-distinct-id partial gradient of this rank's entries (the k_segment_update reduction
-// with the row taken from the received rows and the result written out instead of applied).
-template <int G>
-__global__ __launch_bounds__(kBlock) void k_segment_emit(EmitArgs a) {
-  constexpr int E = 64 / G;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t chunk = (int64_t)blockIdx.x * (kBlock / 64) + wave;
-  const int kp = a.kp, nq = kp >> 2, RW = kp + 4;
-  const int64_t p0 = chunk * 64;
-  const int64_t pp = p0 + lane;
-  const bool valid = chunk < a.nchunks && pp < a.N;
-  const uint32_t kNone = 0xFFFFFFFFu;
-  const uint32_t key = valid ? a.skeys[pp] : kNone;
-  const uint32_t e = valid ? a.sidx[pp] : 0u;
-  const uint32_t u = valid ? a.run_of[pp] : 0u;
-  uint32_t prev_key = __shfl_up(key, 1);
-  uint32_t next_key = __shfl_down(key, 1);
-  if (lane == 0) prev_key = (valid && p0 > 0) ? a.skeys[p0 - 1] : kNone;
-  if (lane == 63) next_key = (valid && p0 + 64 < a.N) ? a.skeys[p0 + 64] : kNone;
-  if (pp == a.N - 1) next_key = kNone;
-  const uint2 en = valid ? a.ent[e] : make_uint2(0u, 0u);
-  const int s = (int)en.x;
-  const float xf = __uint_as_float(en.y);
-  const double x = (double)xf;
-  const float2 yl = valid ? a.yl[s] : make_float2(0.f, 0.f);
-
-  const bool seg_start = valid && key != prev_key;
-  const bool seg_end = valid && key != next_key;
-  const bool piece_head = valid && (lane == 0 || seg_start);
-  const bool piece_tail = valid && (lane == 63 || seg_end);
-  const uint64_t heads = __ballot(piece_head);
-  const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
-  const uint64_t hm = heads & upto;
-  const int start_lane = hm ? 63 - __clzll(hm) : 0;
-  const uint64_t starts = __ballot(seg_start);
-  const int dist = valid ? lane - start_lane : 0;
-  int nsteps = 0;
-  while (nsteps < 6 && __ballot(dist >= (1 << nsteps))) ++nsteps;
-  const bool head_is_start = (starts >> start_lane) & 1ull;
-  const bool complete = head_is_start && seg_end;
-  const int slot = (start_lane == 0 && !head_is_start) ? 0 : 1;
-  const double yhat = yl.x, y = yl.y;
-  const double r = yhat - y;
-
-  double gw = valid ? x * yhat - y : 0.0;  // SGD.scala:145
-  gw = seg_scan(gw, lane, start_lane, nsteps);
-  if (piece_tail) {
-    if (complete) reinterpret_cast<float4*>(a.grads + (int64_t)u * RW)[nq] = make_float4((float)gw, 0.f, 0.f, 0.f);
-    else a.part[(chunk * 2 + slot) * (int64_t)(kp + 1)] = gw;
-  }
-  const int flags = (valid ? 1 : 0) | (piece_tail ? 2 : 0) | (complete ? 4 : 0) | (slot << 4) | (start_lane << 8);
-  const float4* __restrict__ S4 = reinterpret_cast<const float4*>(a.S);
-  const int q_in = lane % G, j_in = lane / G;
-  for (int qc = 0; qc < nq; qc += G) {
-    const int q = qc + q_in;
-    const bool qok = q < nq;
-    double carry0 = 0.0, carry1 = 0.0, carry2 = 0.0, carry3 = 0.0;
-    for (int rd = 0; rd < G; ++rd) {
-      const int j = rd * E + j_in;
-      const int fl = __shfl(flags, j);
-      const uint32_t uj = __shfl(u, j);
-      const int sj = __shfl(s, j);
-      const float xj = __shfl(xf, j);
-      const double rj = __shfl(r, j);
-      const bool vj = (fl & 1) && qok;
-      const int sl = fl >> 8;
-      const float4 sq = vj ? S4[(int64_t)sj * nq + q] : make_float4(0.f, 0.f, 0.f, 0.f);
-      const float4 v = vj ? reinterpret_cast<const float4*>(a.rows + (int64_t)uj * RW)[q] : make_float4(0.f, 0.f, 0.f, 0.f);
-      const double xd = xj;
-      double c0 = vj ? ((double)sq.x * xd - ((double)v.x * xd) * xd) * rj : 0.0;
-      double c1 = vj ? ((double)sq.y * xd - ((double)v.y * xd) * xd) * rj : 0.0;
-      double c2 = vj ? ((double)sq.z * xd - ((double)v.z * xd) * xd) * rj : 0.0;
-      double c3 = vj ? ((double)sq.w * xd - ((double)v.w * xd) * xd) * rj : 0.0;
-      const int lo = sl > rd * E ? sl : rd * E;
+// ------------------------------------------------------------------ requester: combine
+// Team of GS lanes per sample (one quad each): the owners' partials summed in owner order
+// in fp64 -> S = vfxiSum, yhat = 0.5 (|S|^2 - sum v^2 x^2) + sum w x + w0
+// (FactorizationMachinesModel.scala:221, :260-262), the loss partial (:230), and the S rows
+// sent back to every owner holding entries of the sample.
+template <int GS>
+__global__ __launch_bounds__(kBlock) void k_shard_combine(const int32_t* __restrict__ pairidx,
+                                                          const int64_t* __restrict__ poff, int R, int64_t B,
+                                                          const float* __restrict__ part_in,
+                                                          const float* __restrict__ label, int kp, double w0,
+                                                          float* __restrict__ s_send,
+                                                          double2* __restrict__ loss_part) {
+  constexpr int TPB = kBlock / GS;
+  const int tid = threadIdx.x, g = tid % GS;
+  const int nq = kp >> 2, W = kp + 4;
+  double loss_acc = 0.0, nloss = 0.0;
+  for (int64_t s = (int64_t)blockIdx.x * TPB + tid / GS; s < B; s += (int64_t)gridDim.x * TPB) {
+    const int32_t* pi = pairidx + s * R;
+    double vv = 0.0, wx = 0.0, ss = 0.0;
+    bool any = false;
+    for (int o = 0; o < R; ++o) {
+      const int32_t ix = pi[o];
+      if (ix >= 0) {
+        const float2 t = *reinterpret_cast<const float2*>(part_in + (poff[o] + ix) * W + kp);
+        vv += (double)t.x;
+        wx += (double)t.y;
+        any = true;
+      }
+    }
+    for (int qc = 0; qc < nq; qc += GS) {
+      const int q = qc + g;
+      double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+      if (q < nq) {
+        for (int o = 0; o < R; ++o) {
+          const int32_t ix = pi[o];
+          if (ix >= 0) {
+            const float4 t = reinterpret_cast<const float4*>(part_in + (poff[o] + ix) * W)[q];
+            a0 += (double)t.x; a1 += (double)t.y; a2 += (double)t.z; a3 += (double)t.w;
+          }
+        }
+        ss += a0 * a0 + a1 * a1 + a2 * a2 + a3 * a3;
+        const float4 sq = make_float4((float)a0, (float)a1, (float)a2, (float)a3);
+        for (int o = 0; o < R; ++o) {
+          const int32_t ix = pi[o];
+          if (ix >= 0) reinterpret_cast<float4*>(s_send + (poff[o] + ix) * W)[q] = sq;
+        }
+      }
+    }
 #pragma unroll
-      for (int o = 1; o < E; o <<= 1) {
-        if (o >= (1 << nsteps)) break;
-        const double t0 = __shfl_up(c0, o * G), t1 = __shfl_up(c1, o * G);
-        const double t2 = __shfl_up(c2, o * G), t3 = __shfl_up(c3, o * G);
-        if (j - o >= lo) {
-          c0 += t0; c1 += t1; c2 += t2; c3 += t3;
-        }
+    for (int o = 1; o < GS; o <<= 1) ss += __shfl_xor(ss, o);
+    const double yhat = 0.5 * (ss - vv) + wx + w0;
+    if (g == 0) {
+      const float y = label[s];
+      for (int o = 0; o < R; ++o) {
+        const int32_t ix = pi[o];
+        if (ix >= 0)
+          *reinterpret_cast<float4*>(s_send + (poff[o] + ix) * W + kp) = make_float4((float)yhat, y, 0.f, 0.f);
       }
-      if (sl < rd * E) {
-        c0 += carry0; c1 += carry1; c2 += carry2; c3 += carry3;
-      }
-      const int last = (E - 1) * G + q_in;
-      carry0 = __shfl(c0, last); carry1 = __shfl(c1, last);
-      carry2 = __shfl(c2, last); carry3 = __shfl(c3, last);
-      if (vj && (fl & 2)) {
-        if (fl & 4) {
-          reinterpret_cast<float4*>(a.grads + (int64_t)uj * RW)[q] = make_float4((float)c0, (float)c1, (float)c2, (float)c3);
-        } else {
-          double* prow = a.part + (((chunk * 2 + ((fl >> 4) & 1)) * (int64_t)(kp + 1)) + 1 + 4 * q);
-          prow[0] = c0;
-          prow[1] = c1;
-          prow[2] = c2;
-          prow[3] = c3;
-        }
+      if (any) {
+        const double d = yhat - (double)y;
+        loss_acc += d * d;
+        nloss += 1.0;
       }
     }
   }
-}
-
-// Crossing runs of the emit pass: chunk-order sums of the partials -> grads[u].  Block 0 also
-// closes the rank's loss statistics {loss, n_loss, U}.
-__global__ __launch_bounds__(kBlock) void k_segment_emit_combine(EmitArgs a, const double2* __restrict__ loss_part,
-                                                                 int64_t n_loss_blocks, const uint64_t* __restrict__ U,
-                                                                 double* __restrict__ stats_out) {
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int kp = a.kp, RW = kp + 4;
-  const int64_t W = kp + 1;
-  if (blockIdx.x == 0) {
-    __shared__ double rl[kBlock], rc[kBlock];
+  __shared__ double red[2][kBlock / 64];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    loss_acc += __shfl_xor(loss_acc, o);
+    nloss += __shfl_xor(nloss, o);
+  }
+  if ((tid & 63) == 0) {
+    red[0][tid >> 6] = loss_acc;
+    red[1][tid >> 6] = nloss;
+  }
+  __syncthreads();
+  if (tid == 0) {
     double l = 0.0, c = 0.0;
-    for (int64_t i = tid; i < n_loss_blocks; i += kBlock) {
-      l += loss_part[i].x;
-      c += loss_part[i].y;
+    for (int w = 0; w < kBlock / 64; ++w) {
+      l += red[0][w];
+      c += red[1][w];
     }
-    rl[tid] = l;
-    rc[tid] = c;
-    __syncthreads();
-    for (int o = kBlock / 2; o > 0; o >>= 1) {
-      if (tid < o) {
-        rl[tid] += rl[tid + o];
-        rc[tid] += rc[tid + o];
-      }
-      __syncthreads();
-    }
-    if (tid == 0) {
-      stats_out[0] = rl[0];
-      stats_out[1] = rc[0];
-      stats_out[2] = (double)*U;
-    }
-  }
-  const int64_t chunk = (int64_t)blockIdx.x * kBlock + tid;
-  bool owner = false;
-  uint32_t key = 0;
-  if (chunk < a.nchunks) {
-    const int64_t p0 = chunk * 64;
-    const int64_t p1 = p0 + 64 < a.N ? p0 + 64 : a.N;
-    if (p1 < a.N) {
-      key = a.skeys[p1 - 1];
-      owner = a.skeys[p1] == key && !(a.skeys[p0] == key && p0 > 0 && a.skeys[p0 - 1] == key);
-    }
-  }
-  uint64_t owners = __ballot(owner);
-  while (owners) {
-    const int l = __ffsll((unsigned long long)owners) - 1;
-    owners &= owners - 1;
-    const int64_t c0 = __shfl(chunk, l);
-    const uint32_t k0 = __shfl(key, l);
-    int64_t cend = c0 + 1;
-    for (;;) {
-      const int64_t c = cend + lane;
-      const bool cont = c < a.nchunks && a.skeys[c * 64] == k0;
-      const uint64_t m = __ballot(cont);
-      if (m == ~0ull) {
-        cend += 64;
-        continue;
-      }
-      cend += __ffsll((unsigned long long)~m) - 1;
-      break;
-    }
-    const uint32_t u0 = a.run_of[(c0 + 1) * 64 - 1];
-    for (int f0 = 0; f0 < W; f0 += 64) {
-      const int f = f0 + lane;
-      if (f < W) {
-        double g = a.part[(c0 * 2 + 1) * W + f];
-        for (int64_t c = c0 + 1; c < cend; ++c) g += a.part[(c * 2) * W + f];
-        // part column 0 is gw, 1.. are gV; the wire row is [gV(kp) | gw | pad]
-        a.grads[(int64_t)u0 * RW + (f == 0 ? kp : f - 1)] = (float)g;
-      }
-    }
+    loss_part[blockIdx.x] = make_double2(l, c);
   }
 }
 
-// owner side: received (slot, gradient) pairs grouped by slot (stable radix sort keeps the
-// rank order), summed in fp64 in that order, then the update + L1 of SGD.scala:150-181.
-template <int G>
-__global__ __launch_bounds__(kBlock) void k_shard_apply(TableView T, const uint32_t* __restrict__ sslots,
-                                                        const uint32_t* __restrict__ sidx, int64_t n,
-                                                        const float* __restrict__ grads, StepParams p) {
-  const int g = threadIdx.x % G;
-  const int64_t i = ((int64_t)blockIdx.x * kBlock + threadIdx.x) / G;
-  if (i >= n) return;
-  const uint32_t slot = sslots[i];
-  if (i > 0 && sslots[i - 1] == slot) return;  // not the first of its run
-  int64_t j1 = i + 1;
-  while (j1 < n && sslots[j1] == slot) ++j1;
-  const int kp = T.kp, nq = kp >> 2, RW = kp + 4;
-  const RowHdr h = *T.hdr(slot);
-  const bool present = h.t >= 0;
-  const double ac = present ? p.cumE - h.cum : 0.0;
-  for (int q = g; q < nq; q += G) {
-    double g0 = 0.0, g1 = 0.0, g2 = 0.0, g3 = 0.0;
-    for (int64_t j = i; j < j1; ++j) {
-      const float4 gr = reinterpret_cast<const float4*>(grads + (int64_t)sidx[j] * RW)[q];
-      g0 += gr.x; g1 += gr.y; g2 += gr.z; g3 += gr.w;
-    }
-    float4 v = present ? reinterpret_cast<const float4*>(T.v(slot))[q] : make_float4(0.f, 0.f, 0.f, 0.f);
-    if (ac > 0.0) v = shrink4(v, ac);
-    reinterpret_cast<float4*>(T.v(slot))[q] =
-        make_float4(upd_v(v.x, g0, p), upd_v(v.y, g1, p), upd_v(v.z, g2, p), upd_v(v.w, g3, p));
-  }
-  if (g == 0) {
-    double gw = 0.0;
-    for (int64_t j = i; j < j1; ++j) gw += grads[(int64_t)sidx[j] * RW + kp];
-    float w = present ? h.w : 0.f;
-    if (ac > 0.0) w = shrink_f(w, ac);
-    RowHdr o;
-    o.w = upd_w(w, gw, p);
-    o.t = p.epoch + 1;
-    o.cum = p.cum_next;
-    store_hdr(T, slot, o);
-  }
+inline unsigned blocks_for(int64_t threads, int64_t cap = 256 * 16) {
+  int64_t b = (threads + kBlock - 1) / kBlock;
+  if (b < 1) b = 1;
+  if (b > cap) b = cap;
+  return (unsigned)b;
 }
 
-inline int lanes_per_row(int nq) {
+inline int team_for(int nq) {
   int G = 1;
   while (G < nq && G < 16) G <<= 1;
   return G;
-}
-
-inline unsigned blocks_for(int64_t threads) {
-  int64_t b = (threads + kBlock - 1) / kBlock;
-  return (unsigned)(b < 1 ? 1 : b);
 }
 
 }  // namespace
@@ -413,209 +326,227 @@ using namespace fmhip;
 
 namespace {
 
-void require_plan(fm_ctx* ctx, const fm_batch* b) {
-  FM_REQUIRE(ctx->plan_batch == b && ctx->plan_nnz == (b ? b->dev.nnz : -1),
-             "fm_shard_plan must run on this batch first");
+// Owner-side step parameters (SGD.scala:121-124 with the global miniBatchSize).
+StepParams shard_params(fm_ctx* ctx, int32_t t, double step_size, double reg_param, int64_t global_rows) {
+  StepParams p{};
+  p.n_rows = global_rows;
+  p.eta = step_size / std::sqrt((double)t);  // SGD.scala:121
+  p.lam = p.eta * reg_param;                 // SGD.scala:122
+  p.m = (double)global_rows;
+  p.scale_v = p.eta / (double)global_rows;
+  p.epoch = ctx->epoch;
+  p.cumE = ctx->cum_host.back();
+  p.cum_next = p.cumE + p.lam;
+  p.w0 = ctx->cfg.w0;
+  return p;
 }
 
 }  // namespace
 
 extern "C" {
 
-int fm_shard_plan(fm_ctx* ctx, const fm_batch* b, int64_t* send_counts) {
+int fm_shard_route(fm_ctx* ctx, fm_batch* b, void* send_slot, void* send_ent, int64_t* counts) {
   return guarded(ctx, [&]() -> int {
-    FM_REQUIRE(b != nullptr && b->owner == ctx && send_counts != nullptr, "bad arguments");
+    FM_REQUIRE(b != nullptr && b->owner == ctx && counts != nullptr, "bad arguments");
     const int R = ctx->cfg.shard_count;
-    FM_REQUIRE(R <= 1024, "shard_count > 1024");
-    const int64_t N = b->dev.nnz;
-    const uint32_t rpsh = (uint32_t)((ctx->cfg.num_features + R - 1) / R);
-    ctx->plan_ck.ensure(sizeof(uint32_t) * std::max<int64_t>(N, 4) + 16);
-    ctx->plan_run.ensure(sizeof(uint32_t) * std::max<int64_t>(N, 1));
-    ctx->plan_uidx.ensure(sizeof(uint32_t) * std::max<int64_t>(N, 1));
-    ctx->plan_req.ensure(sizeof(int32_t) * std::max<int64_t>(N, 1));
-    ctx->plan_counts.ensure(sizeof(unsigned long long) * R + sizeof(uint64_t));
-    const int64_t nb = (N + kTileS - 1) / kTileS;
-    ctx->plan_bsum.ensure(sizeof(uint32_t) * std::max<int64_t>(nb, 1));
+    FM_REQUIRE(R <= kMaxR, "the owner-computes sharded step supports at most 64 ranks");
+    const int64_t B = b->dev.n_rows, N = b->dev.nnz;
+    FM_REQUIRE(N == 0 || (send_slot && send_ent), "null send buffer");
     hipStream_t st = ctx->stream;
     hipEvent_t e0 = ctx->prof_begin(st);
-    unsigned long long* counts = ctx->plan_counts.as<unsigned long long>();
-    uint64_t* total = reinterpret_cast<uint64_t*>(counts + R);
-    FM_HIP_CHECK(hipMemsetAsync(counts, 0, sizeof(unsigned long long) * R + sizeof(uint64_t), st));
-    if (N > 0) {
-      hipLaunchKernelGGL(k_shard_keys, dim3(blocks_for(N) > 4096 ? 4096 : blocks_for(N)), dim3(kBlock), 0, st,
-                         b->dev.col.as<uint32_t>(), N, (uint32_t)R, rpsh, ctx->plan_ck.as<uint32_t>());
-      const uint32_t *sk = nullptr, *si = nullptr;
-      radix_sort_pairs(ctx->work.sort, ctx->plan_ck.as<uint32_t>(), nullptr, N,
-                       bits_for((int64_t)R * rpsh - 1), st, &sk, &si);
-      ctx->plan_skeys = sk;
-      ctx->plan_sidx = si;
-      hipLaunchKernelGGL(k_runs_count, dim3((unsigned)nb), dim3(kBlock), 0, st, sk, N, ctx->plan_bsum.as<uint32_t>());
-      hipLaunchKernelGGL(k_runs_scan, dim3(1), dim3(kBlock), 0, st, ctx->plan_bsum.as<uint32_t>(), nb, total);
-      hipLaunchKernelGGL(k_plan_apply, dim3((unsigned)nb), dim3(kBlock), 0, st, sk, si, N,
-                         ctx->plan_bsum.as<uint32_t>(), rpsh, R, ctx->plan_req.as<int32_t>(),
-                         ctx->plan_run.as<uint32_t>(), ctx->plan_uidx.as<uint32_t>(), counts);
-      FM_HIP_CHECK(hipGetLastError());
+    const int64_t ntiles = std::max<int64_t>((B + kBlock - 1) / kBlock, 1);
+    ctx->sh_okey.ensure(sizeof(uint32_t) * std::max<int64_t>(N, 4) + 16);
+    ctx->sh_mask.ensure(sizeof(uint64_t) * std::max<int64_t>(B, 1));
+    ctx->sh_tcnt.ensure(sizeof(uint32_t) * R * ntiles);
+    ctx->sh_tot.ensure(sizeof(unsigned long long) * 2 * R);
+    ctx->sh_pairidx.ensure(sizeof(int32_t) * std::max<int64_t>(B, 1) * R);
+    unsigned long long* tot = ctx->sh_tot.as<unsigned long long>();  // [R] pairs, [R] entries
+    FM_HIP_CHECK(hipMemsetAsync(tot, 0, sizeof(unsigned long long) * 2 * R, st));
+    if (B > 0) {
+      hipLaunchKernelGGL(k_sample_mask, dim3(blocks_for(B)), dim3(kBlock), 0, st, b->dev.row_ptr.as<int64_t>(),
+                         b->dev.col.as<uint32_t>(), B, (uint32_t)R, ctx->sh_mask.as<uint64_t>(), tot + R);
+      hipLaunchKernelGGL(k_pair_count, dim3((unsigned)ntiles), dim3(kBlock), 0, st, ctx->sh_mask.as<uint64_t>(), B,
+                         R, ntiles, ctx->sh_tcnt.as<uint32_t>());
+      hipLaunchKernelGGL(k_rows_scan, dim3((unsigned)R), dim3(kBlock), 0, st, ctx->sh_tcnt.as<uint32_t>(), ntiles,
+                         tot);
+      hipLaunchKernelGGL(k_pair_index, dim3((unsigned)ntiles), dim3(kBlock), 0, st, ctx->sh_mask.as<uint64_t>(), B,
+                         R, ntiles, ctx->sh_tcnt.as<uint32_t>(), ctx->sh_pairidx.as<int32_t>());
     }
-    ctx->prof_end("plan", e0, st);
-    ctx->pinned.ensure(sizeof(unsigned long long) * (R + 1));
-    FM_HIP_CHECK(hipMemcpyAsync(ctx->pinned.p, counts, sizeof(unsigned long long) * (R + 1), hipMemcpyDeviceToHost, st));
+    if (N > 0) {
+      hipLaunchKernelGGL(k_owner_keys, dim3(blocks_for(N)), dim3(kBlock), 0, st, b->dev.col.as<uint32_t>(), N,
+                         (uint32_t)R, ctx->sh_okey.as<uint32_t>());
+      const uint32_t *sk = nullptr, *si = nullptr;
+      radix_sort_pairs(ctx->work.sort, ctx->sh_okey.as<uint32_t>(), nullptr, N, bits_for(R - 1), st, &sk, &si);
+      hipLaunchKernelGGL(k_route_pack, dim3(blocks_for(N)), dim3(kBlock), 0, st, si, N, b->dev.col.as<uint32_t>(),
+                         b->dev.ent.as<uint2>(), (uint32_t)R, reinterpret_cast<uint32_t*>(send_slot),
+                         reinterpret_cast<uint2*>(send_ent));
+    }
+    FM_HIP_CHECK(hipGetLastError());
+    ctx->prof_end("route", e0, st);
+    ctx->pinned.ensure(sizeof(unsigned long long) * 2 * R);
+    FM_HIP_CHECK(hipMemcpyAsync(ctx->pinned.p, tot, sizeof(unsigned long long) * 2 * R, hipMemcpyDeviceToHost, st));
     FM_HIP_CHECK(hipStreamSynchronize(st));
     const unsigned long long* hc = reinterpret_cast<const unsigned long long*>(ctx->pinned.p);
-    int64_t U = 0;
+    ctx->sh_pairs_out.assign(R, 0);
+    int64_t ne = 0;
     for (int o = 0; o < R; ++o) {
-      send_counts[o] = (int64_t)hc[o];
-      U += (int64_t)hc[o];
+      counts[o] = (int64_t)hc[R + o];      // entries to owner o
+      counts[R + o] = (int64_t)hc[o];      // (sample, owner) pairs to owner o
+      ctx->sh_pairs_out[o] = (int64_t)hc[o];
+      ne += (int64_t)hc[R + o];
     }
-    FM_REQUIRE(U == (int64_t)hc[R], "plan: inconsistent distinct-id count");
-    ctx->plan_unique = U;
-    ctx->plan_nnz = N;
-    ctx->plan_batch = b;
+    FM_REQUIRE(ne == N, "route: inconsistent entry count");
+    ctx->sh_route_batch = b;
+    ctx->sh_route_nnz = N;
+    ctx->sh_combined = false;
     return FM_OK;
   });
 }
 
-int fm_shard_request_copy(fm_ctx* ctx, void* dst) {
+int fm_shard_owner_forward(fm_ctx* ctx, const void* recv_slot, const void* recv_ent, int64_t n,
+                           const int64_t* src_entries, const int64_t* src_pairs, void* partials_out) {
   return guarded(ctx, [&]() -> int {
-    FM_REQUIRE(ctx->plan_batch != nullptr, "no plan");
-    if (ctx->plan_unique == 0) return FM_OK;
-    FM_REQUIRE(dst != nullptr, "null destination");
-    FM_HIP_CHECK(hipMemcpyAsync(dst, ctx->plan_req.p, sizeof(int32_t) * ctx->plan_unique, hipMemcpyDeviceToDevice,
-                                ctx->stream));
-    return FM_OK;
-  });
-}
-
-int fm_shard_serve_device(fm_ctx* ctx, const void* req, int64_t n, void* rows_out) {
-  return guarded(ctx, [&]() -> int {
-    FM_REQUIRE(n >= 0, "negative n");
-    if (n == 0) return FM_OK;
-    FM_REQUIRE(req && rows_out, "null buffer");
-    const TableView T = ctx->view();
-    const int G = lanes_per_row(ctx->kp / 4);
-    const unsigned blocks = blocks_for(n * G);
-    const double cumE = ctx->cum_host.back();
-    const int32_t* r = reinterpret_cast<const int32_t*>(req);
-    float* o = reinterpret_cast<float*>(rows_out);
-    hipEvent_t e0 = ctx->prof_begin(ctx->stream);
-    switch (G) {
-      case 1: hipLaunchKernelGGL(k_shard_serve<1>, dim3(blocks), dim3(kBlock), 0, ctx->stream, T, r, n, cumE, o); break;
-      case 2: hipLaunchKernelGGL(k_shard_serve<2>, dim3(blocks), dim3(kBlock), 0, ctx->stream, T, r, n, cumE, o); break;
-      case 4: hipLaunchKernelGGL(k_shard_serve<4>, dim3(blocks), dim3(kBlock), 0, ctx->stream, T, r, n, cumE, o); break;
-      case 8: hipLaunchKernelGGL(k_shard_serve<8>, dim3(blocks), dim3(kBlock), 0, ctx->stream, T, r, n, cumE, o); break;
-      default: hipLaunchKernelGGL(k_shard_serve<16>, dim3(blocks), dim3(kBlock), 0, ctx->stream, T, r, n, cumE, o); break;
+    const int R = ctx->cfg.shard_count;
+    FM_REQUIRE(n >= 0 && src_entries && src_pairs, "bad arguments");
+    std::vector<int64_t> off(R + 1, 0);
+    int64_t P = 0;
+    for (int r = 0; r < R; ++r) {
+      FM_REQUIRE(src_entries[r] >= 0 && src_pairs[r] >= 0 && src_pairs[r] <= src_entries[r], "bad source counts");
+      off[r + 1] = off[r] + src_entries[r];
+      P += src_pairs[r];
     }
-    FM_HIP_CHECK(hipGetLastError());
-    ctx->prof_end("serve", e0, ctx->stream);
-    return FM_OK;
-  });
-}
-
-int fm_shard_local_grad_device(fm_ctx* ctx, fm_batch* b, const void* rows_in, void* grads_out) {
-  return guarded(ctx, [&]() -> int {
-    FM_REQUIRE(b != nullptr, "null batch");
-    require_plan(ctx, b);
-    const int64_t B = b->dev.n_rows, N = b->dev.nnz;
-    const int64_t U = ctx->plan_unique;
-    FM_REQUIRE(U == 0 || (rows_in && grads_out), "null buffer");
-    reserve_work(ctx, B, N);
-    ctx->ensure_hist(ctx->epoch + 1);
-    double* stats = ctx->loss_hist.as<double>() + 3 * (int64_t)ctx->epoch;
-    StepParams p{};
-    p.w0 = ctx->cfg.w0;
-    p.cumE = ctx->cum_host.back();
-    int64_t nfwd = 0;
-    hipEvent_t e0 = ctx->prof_begin(ctx->stream);
-    if (B > 0)
-      launch_forward(ctx->view(), b->dev, ctx->work, p, ctx->stream, &nfwd, reinterpret_cast<const float*>(rows_in),
-                     ctx->plan_uidx.as<uint32_t>());
-    ctx->prof_end("forward", e0, ctx->stream);
-    e0 = ctx->prof_begin(ctx->stream);
-    EmitArgs a;
-    a.skeys = ctx->plan_skeys;
-    a.sidx = ctx->plan_sidx;
-    a.run_of = ctx->plan_run.as<uint32_t>();
-    a.ent = b->dev.ent.as<uint2>();
-    a.rows = reinterpret_cast<const float*>(rows_in);
-    a.S = ctx->work.S.as<float>();
-    a.yl = ctx->work.yl.as<float2>();
-    a.grads = reinterpret_cast<float*>(grads_out);
-    a.part = ctx->work.part.as<double>();
-    a.N = N;
-    a.nchunks = (N + 63) / 64;
-    a.kp = ctx->kp;
-    const int G = lanes_per_row(ctx->kp / 4);
-    if (a.nchunks > 0) {
-      const unsigned blocks = (unsigned)((a.nchunks + 3) / 4);
-      switch (G) {
-        case 1: hipLaunchKernelGGL(k_segment_emit<1>, dim3(blocks), dim3(kBlock), 0, ctx->stream, a); break;
-        case 2: hipLaunchKernelGGL(k_segment_emit<2>, dim3(blocks), dim3(kBlock), 0, ctx->stream, a); break;
-        case 4: hipLaunchKernelGGL(k_segment_emit<4>, dim3(blocks), dim3(kBlock), 0, ctx->stream, a); break;
-        case 8: hipLaunchKernelGGL(k_segment_emit<8>, dim3(blocks), dim3(kBlock), 0, ctx->stream, a); break;
-        default: hipLaunchKernelGGL(k_segment_emit<16>, dim3(blocks), dim3(kBlock), 0, ctx->stream, a); break;
-      }
-    }
-    const uint64_t* Ud = reinterpret_cast<const uint64_t*>(ctx->plan_counts.as<unsigned long long>() + ctx->cfg.shard_count);
-    hipLaunchKernelGGL(k_segment_emit_combine, dim3(blocks_for(std::max<int64_t>(a.nchunks, 1))), dim3(kBlock), 0,
-                       ctx->stream, a, ctx->work.loss_part.as<double2>(), B > 0 ? nfwd : (int64_t)0, Ud, stats);
-    FM_HIP_CHECK(hipGetLastError());
-    ctx->prof_end("grad", e0, ctx->stream);
-    return FM_OK;
-  });
-}
-
-int fm_shard_apply_device(fm_ctx* ctx, const void* req, const void* grads, int64_t n, int32_t t, double step_size,
-                          double reg_param, int64_t global_rows) {
-  return guarded(ctx, [&]() -> int {
-    FM_REQUIRE(n >= 0 && global_rows >= 0, "negative size");
-    if (global_rows == 0) return FM_NOTHING_TO_DO;  // SGD.scala:126-128 (every rank skips)
-    FM_REQUIRE(t >= 1, "iteration index t must be >= 1");
-    StepParams p{};
-    p.n_rows = global_rows;
-    p.eta = step_size / std::sqrt((double)t);  // SGD.scala:121
-    p.lam = p.eta * reg_param;                 // SGD.scala:122
-    p.m = (double)global_rows;                 // global miniBatchSize
-    p.scale_v = p.eta / (double)global_rows;
-    p.epoch = ctx->epoch;
-    p.cumE = ctx->cum_host.back();
-    p.cum_next = p.cumE + p.lam;
-    p.w0 = ctx->cfg.w0;
-    hipEvent_t e0 = ctx->prof_begin(ctx->stream);
+    FM_REQUIRE(off[R] == n, "source entry counts do not add up to n");
+    FM_REQUIRE(n == 0 || (recv_slot && recv_ent && partials_out), "null buffer");
+    hipStream_t st = ctx->stream;
+    hipEvent_t e0 = ctx->prof_begin(st);
+    const int64_t nb = std::max<int64_t>((n + kTileS - 1) / kTileS, 1);
+    ctx->sh_src_off.ensure(sizeof(int64_t) * (2 * R + 2));  // [R+1] source offsets, [R+1] owner offsets
+    ctx->sh_bsum.ensure(sizeof(uint32_t) * nb + sizeof(unsigned long long));
+    ctx->sh_pair_ptr.ensure(sizeof(int64_t) * (P + 1));
+    ctx->sh_ent2.ensure(sizeof(uint2) * std::max<int64_t>(n, 1));
+    // staging stays untouched until the next route synchronises the stream
+    ctx->sh_pin_off.ensure(sizeof(int64_t) * (R + 1));
+    std::memcpy(ctx->sh_pin_off.p, off.data(), sizeof(int64_t) * (R + 1));
+    FM_HIP_CHECK(hipMemcpyAsync(ctx->sh_src_off.p, ctx->sh_pin_off.p, sizeof(int64_t) * (R + 1), hipMemcpyHostToDevice, st));
+    int64_t* pair_ptr = ctx->sh_pair_ptr.as<int64_t>();
+    // the pair table closes with n (pair_ptr[P])
+    FM_HIP_CHECK(hipMemcpyAsync(pair_ptr + P, ctx->sh_src_off.as<int64_t>() + R, sizeof(int64_t),
+                                hipMemcpyDeviceToDevice, st));
     if (n > 0) {
-      FM_REQUIRE(req && grads, "null buffer");
-      const uint32_t *ss = nullptr, *si = nullptr;
-      radix_sort_pairs(ctx->work.sort, reinterpret_cast<const uint32_t*>(req), nullptr, n,
-                       bits_for(std::max<int64_t>(ctx->rows - 1, 1)), ctx->stream, &ss, &si);
-      const int G = lanes_per_row(ctx->kp / 4);
-      const unsigned blocks = blocks_for(n * G);
-      const TableView T = ctx->view();
-      const float* gr = reinterpret_cast<const float*>(grads);
-      switch (G) {
-        case 1: hipLaunchKernelGGL(k_shard_apply<1>, dim3(blocks), dim3(kBlock), 0, ctx->stream, T, ss, si, n, gr, p); break;
-        case 2: hipLaunchKernelGGL(k_shard_apply<2>, dim3(blocks), dim3(kBlock), 0, ctx->stream, T, ss, si, n, gr, p); break;
-        case 4: hipLaunchKernelGGL(k_shard_apply<4>, dim3(blocks), dim3(kBlock), 0, ctx->stream, T, ss, si, n, gr, p); break;
-        case 8: hipLaunchKernelGGL(k_shard_apply<8>, dim3(blocks), dim3(kBlock), 0, ctx->stream, T, ss, si, n, gr, p); break;
-        default: hipLaunchKernelGGL(k_shard_apply<16>, dim3(blocks), dim3(kBlock), 0, ctx->stream, T, ss, si, n, gr, p); break;
-      }
+      const uint2* ent = reinterpret_cast<const uint2*>(recv_ent);
+      uint32_t* bsum = ctx->sh_bsum.as<uint32_t>();
+      auto* total = reinterpret_cast<unsigned long long*>(bsum + nb);
+      hipLaunchKernelGGL(k_heads_count, dim3((unsigned)nb), dim3(kBlock), 0, st, ent, n,
+                         ctx->sh_src_off.as<int64_t>(), R, bsum);
+      hipLaunchKernelGGL(k_rows_scan, dim3(1), dim3(kBlock), 0, st, bsum, nb, total);
+      hipLaunchKernelGGL(k_heads_apply, dim3((unsigned)nb), dim3(kBlock), 0, st, ent, n,
+                         ctx->sh_src_off.as<int64_t>(), R, bsum, pair_ptr, ctx->sh_ent2.as<uint2>());
+      // partial forward over the pairs, rows of the local table (lazy L1 caught up on read)
+      BatchDev view;
+      view.n_rows = P;
+      view.nnz = n;
+      view.row_ptr.p = pair_ptr;
+      view.col.p = const_cast<void*>(recv_slot);
+      view.ent.p = const_cast<void*>(recv_ent);
+      StepParams p{};
+      p.cumE = ctx->cum_host.back();
+      int64_t nblk = 0;
+      if (P > 0) launch_forward(ctx->view(), view, ctx->work, p, st, &nblk, reinterpret_cast<float*>(partials_out));
       FM_HIP_CHECK(hipGetLastError());
     }
-    ctx->prof_end("apply", e0, ctx->stream);
-    ctx->epoch += 1;
-    ctx->cum_host.push_back(p.cum_next);
-    ctx->plan_batch = nullptr;
+    ctx->prof_end("owner_forward", e0, st);
+    ctx->sh_recv_slot = reinterpret_cast<const uint32_t*>(recv_slot);
+    ctx->sh_recv_n = n;
+    ctx->sh_P = P;
     return FM_OK;
   });
 }
 
-int fm_shard_last_loss(fm_ctx* ctx, double* loss_sum, int64_t* n_loss_rows) {
+int fm_shard_combine(fm_ctx* ctx, fm_batch* b, const void* partials_in, void* s_send) {
   return guarded(ctx, [&]() -> int {
-    FM_REQUIRE(loss_sum && n_loss_rows, "null argument");
-    FM_REQUIRE(ctx->epoch >= 1, "no step executed");
-    double h[3];
-    FM_HIP_CHECK(hipMemcpyAsync(h, ctx->loss_hist.as<double>() + 3 * (int64_t)(ctx->epoch - 1), sizeof(h),
-                                hipMemcpyDeviceToHost, ctx->stream));
-    FM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
-    *loss_sum = h[0];
-    *n_loss_rows = (int64_t)h[1];
+    FM_REQUIRE(b != nullptr && ctx->sh_route_batch == b && ctx->sh_route_nnz == b->dev.nnz,
+               "fm_shard_route must run on this batch first");
+    const int R = ctx->cfg.shard_count;
+    const int64_t B = b->dev.n_rows;
+    int64_t Ps = 0;
+    for (int o = 0; o < R; ++o) Ps += ctx->sh_pairs_out[o];
+    FM_REQUIRE(Ps == 0 || (partials_in && s_send), "null buffer");
+    hipStream_t st = ctx->stream;
+    hipEvent_t e0 = ctx->prof_begin(st);
+    // owner blocks of the partial / S buffers
+    ctx->sh_src_off.ensure(sizeof(int64_t) * (2 * R + 2));
+    int64_t* poff_dev = ctx->sh_src_off.as<int64_t>() + (R + 1);
+    ctx->sh_pin_poff.ensure(sizeof(int64_t) * (R + 1));
+    int64_t* hp = reinterpret_cast<int64_t*>(ctx->sh_pin_poff.p);
+    hp[0] = 0;
+    for (int o = 0; o < R; ++o) hp[o + 1] = hp[o] + ctx->sh_pairs_out[o];
+    FM_HIP_CHECK(hipMemcpyAsync(poff_dev, hp, sizeof(int64_t) * (R + 1), hipMemcpyHostToDevice, st));
+    const int nq = ctx->kp / 4;
+    const int GS = team_for(nq);
+    const int64_t tpb = kBlock / GS;
+    int64_t blocks = std::max<int64_t>((B + tpb - 1) / tpb, 1);
+    if (blocks > 256 * 8) blocks = 256 * 8;
+    ctx->work.loss_part.ensure(sizeof(double) * 2 * 256 * 8);  // reserve_work's size: no reallocation later
+    const int32_t* pi = ctx->sh_pairidx.as<int32_t>();
+    const float* pin = reinterpret_cast<const float*>(partials_in);
+    float* so = reinterpret_cast<float*>(s_send);
+    const float* lab = b->dev.label.as<float>();
+    double2* lp = ctx->work.loss_part.as<double2>();
+    const double w0 = ctx->cfg.w0;
+    const int kp = ctx->kp;
+    const dim3 grid((unsigned)blocks), blk(kBlock);
+    switch (GS) {
+      case 1: hipLaunchKernelGGL(k_shard_combine<1>, grid, blk, 0, st, pi, poff_dev, R, B, pin, lab, kp, w0, so, lp); break;
+      case 2: hipLaunchKernelGGL(k_shard_combine<2>, grid, blk, 0, st, pi, poff_dev, R, B, pin, lab, kp, w0, so, lp); break;
+      case 4: hipLaunchKernelGGL(k_shard_combine<4>, grid, blk, 0, st, pi, poff_dev, R, B, pin, lab, kp, w0, so, lp); break;
+      case 8: hipLaunchKernelGGL(k_shard_combine<8>, grid, blk, 0, st, pi, poff_dev, R, B, pin, lab, kp, w0, so, lp); break;
+      default: hipLaunchKernelGGL(k_shard_combine<16>, grid, blk, 0, st, pi, poff_dev, R, B, pin, lab, kp, w0, so, lp); break;
+    }
+    FM_HIP_CHECK(hipGetLastError());
+    ctx->prof_end("combine", e0, st);
+    ctx->sh_loss_blocks = blocks;
+    ctx->sh_combined = true;
+    return FM_OK;
+  });
+}
+
+int fm_shard_owner_update(fm_ctx* ctx, const void* s_recv, int32_t t, double step_size, double reg_param,
+                          int64_t global_rows) {
+  return guarded(ctx, [&]() -> int {
+    FM_REQUIRE(global_rows >= 0, "negative global_rows");
+    if (global_rows == 0) return FM_NOTHING_TO_DO;  // SGD.scala:126-128 (every rank skips)
+    FM_REQUIRE(t >= 1, "iteration index t must be >= 1");
+    FM_REQUIRE(ctx->sh_recv_n >= 0 && ctx->sh_combined, "owner_forward and combine must run first");
+    const int64_t n = ctx->sh_recv_n;
+    FM_REQUIRE(n == 0 || s_recv != nullptr, "null buffer");
+    hipStream_t st = ctx->stream;
+    StepParams p = shard_params(ctx, t, step_size, reg_param, global_rows);
+    ctx->ensure_hist(ctx->epoch + 1);
+    double* stats = ctx->loss_hist.as<double>() + 3 * (int64_t)ctx->epoch;
+    hipEvent_t e0 = ctx->prof_begin(st);
+    const uint32_t* skeys = nullptr;
+    const uint2* sents = nullptr;
+    if (n > 0) {
+      reserve_work(ctx, 1, n);
+      ctx->sh_skeys.ensure(sizeof(uint32_t) * n);
+      ctx->sh_sents.ensure(sizeof(uint2) * n);
+      radix_sort_pairs64(ctx->work.sort, ctx->sh_recv_slot, ctx->sh_ent2.as<uint2>(), n,
+                         bits_for(std::max<int64_t>(ctx->rows - 1, 1)), st, &skeys, &sents,
+                         ctx->sh_skeys.as<uint32_t>(), ctx->sh_sents.as<uint2>());
+    }
+    ctx->prof_end("owner_sort", e0, st);
+    e0 = ctx->prof_begin(st);
+    const float* S = reinterpret_cast<const float*>(s_recv);
+    const int W = ctx->kp + 4;
+    SegSource src{S, W / 4, reinterpret_cast<const float2*>(S + ctx->kp), W / 2};
+    launch_segment_update(ctx->view(), n, src, ctx->work, p, skeys, sents, ctx->sh_loss_blocks, stats, st);
+    ctx->prof_end("owner_update", e0, st);
+    ctx->epoch += 1;
+    ctx->cum_host.push_back(p.cum_next);
+    ctx->sh_recv_n = -1;
+    ctx->sh_recv_slot = nullptr;
+    ctx->sh_combined = false;
+    ctx->sh_route_batch = nullptr;
     return FM_OK;
   });
 }

@@ -5,49 +5,82 @@
 // up contiguous and in their original (CSR) order, so every per-feature sum downstream runs
 // in a fixed order and the step is bitwise reproducible.
 //
-// Per pass (8-bit digit):
+// Per pass (RB-bit digit, 8..10 bits: 27-bit feature slots take 3 passes of 9 bits):
 //   count   : one 256-thread block per 4096-key tile, LDS histogram  -> counts[digit][tile]
 //   scan    : one block per digit, exclusive scan along tiles        -> counts, digit totals
-//   scatter : each wave ranks its 1024 keys with 8 ballots per round (wave64 match), the
-//             block stages the tile in LDS in digit order, then writes runs coalesced.
-// HBM traffic per pass: 4 B (count) + 8 B read + 8 B write per pair.
+//   scatter : each wave ranks its 1024 keys with RB ballots per round (wave64 match), the
+//             block stages the tile in LDS in digit order, then writes runs coalesced; tiles
+//             are mapped to XCDs in contiguous groups.
+// HBM traffic per pass: 4 B (count) + (4 + P) B read + (4 + P) B write per pair.
 #include "fm_internal.h"
 
 namespace fmhip {
 
 namespace {
 
+#ifndef FM_SORT_MAXRB
+#define FM_SORT_MAXRB 10
+#endif
+#ifndef FM_SORT_XCD
+#define FM_SORT_XCD 1
+#endif
+
 constexpr int kBlock = 256;
 constexpr int kWaves = kBlock / 64;
 constexpr int kRounds = 16;
 constexpr int kTile = kBlock * kRounds;  // 4096 keys per tile
-constexpr int kRadix = 256;
+constexpr int kMaxRadix = 1 << 10;
 
+// Tile of a block.  With FM_SORT_XCD the tiles of one XCD (blocks b = x mod 8 are dispatched
+// to XCD x) are contiguous, so a digit's runs written by neighbouring tiles meet in the same L2
+// and leave it as whole 64-B granules (a partly written granule costs a read-modify-write in
+// HBM; tools/traffic_cal.hip).
+__device__ __forceinline__ int64_t tile_of_block(int64_t ntiles) {
+#if FM_SORT_XCD
+  const int64_t per = (ntiles + 7) / 8;
+  return (int64_t)(blockIdx.x % 8) * per + blockIdx.x / 8;
+#else
+  return blockIdx.x;
+#endif
+}
+
+inline int64_t blocks_for_tiles(int64_t ntiles) {
+#if FM_SORT_XCD
+  return (ntiles + 7) / 8 * 8;
+#else
+  return ntiles;
+#endif
+}
+
+template <int RB>
 __global__ __launch_bounds__(kBlock) void k_radix_count(const uint32_t* __restrict__ keys, int64_t n,
                                                         int shift, uint32_t* __restrict__ counts,
                                                         int64_t ntiles) {
-  __shared__ uint32_t hist[kRadix];
-  hist[threadIdx.x] = 0;
+  constexpr int R = 1 << RB;
+  constexpr uint32_t M = R - 1;
+  __shared__ uint32_t hist[R];
+  for (int d = threadIdx.x; d < R; d += kBlock) hist[d] = 0;
   __syncthreads();
-  const int64_t base = (int64_t)blockIdx.x * kTile;
+  const int64_t tile = blockIdx.x;
+  const int64_t base = tile * kTile;
   if (base + kTile <= n) {
     const uint4* k4 = reinterpret_cast<const uint4*>(keys + base);
 #pragma unroll
     for (int i = 0; i < kRounds / 4; ++i) {
       const uint4 q = k4[i * kBlock + threadIdx.x];
-      atomicAdd(&hist[(q.x >> shift) & 255u], 1u);
-      atomicAdd(&hist[(q.y >> shift) & 255u], 1u);
-      atomicAdd(&hist[(q.z >> shift) & 255u], 1u);
-      atomicAdd(&hist[(q.w >> shift) & 255u], 1u);
+      atomicAdd(&hist[(q.x >> shift) & M], 1u);
+      atomicAdd(&hist[(q.y >> shift) & M], 1u);
+      atomicAdd(&hist[(q.z >> shift) & M], 1u);
+      atomicAdd(&hist[(q.w >> shift) & M], 1u);
     }
   } else {
     for (int i = 0; i < kRounds; ++i) {
       const int64_t idx = base + (int64_t)i * kBlock + threadIdx.x;
-      if (idx < n) atomicAdd(&hist[(keys[idx] >> shift) & 255u], 1u);
+      if (idx < n) atomicAdd(&hist[(keys[idx] >> shift) & M], 1u);
     }
   }
   __syncthreads();
-  counts[(int64_t)threadIdx.x * ntiles + blockIdx.x] = hist[threadIdx.x];
+  for (int d = threadIdx.x; d < R; d += kBlock) counts[(int64_t)d * ntiles + tile] = hist[d];
 }
 
 __device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v, int lane) {
@@ -86,6 +119,26 @@ __global__ __launch_bounds__(kBlock) void k_radix_scan_rows(uint32_t* __restrict
   if (threadIdx.x == 0) digit_tot[blockIdx.x] = carry;
 }
 
+// Block-wide exclusive scan of R values held as D = R / kBlock consecutive values per thread.
+template <int D>
+__device__ __forceinline__ void block_excl_scan(uint32_t (&v)[D], uint32_t* wsum, int lane, int wave) {
+  uint32_t t = 0;
+#pragma unroll
+  for (int i = 0; i < D; ++i) t += v[i];
+  const uint32_t incl = wave_incl_scan_u32(t, lane);
+  if (lane == 63) wsum[wave] = incl;
+  __syncthreads();
+  uint32_t run = incl - t;
+#pragma unroll
+  for (int w = 0; w < kWaves; ++w) run += (w < wave) ? wsum[w] : 0u;
+#pragma unroll
+  for (int i = 0; i < D; ++i) {
+    const uint32_t c = v[i];
+    v[i] = run;
+    run += c;
+  }
+}
+
 template <class P>
 __device__ __forceinline__ P implicit_payload(int64_t idx);
 template <>
@@ -97,7 +150,7 @@ __device__ __forceinline__ uint2 implicit_payload<uint2>(int64_t idx) {
   return make_uint2((uint32_t)idx, 0u);
 }
 
-template <class P>
+template <class P, int RB>
 __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint32_t* __restrict__ keys_in,
                                                           const P* __restrict__ vals_in,
                                                           uint32_t* __restrict__ keys_out,
@@ -105,31 +158,35 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint32_t* __rest
                                                           int shift, const uint32_t* __restrict__ counts,
                                                           const uint32_t* __restrict__ digit_tot,
                                                           int64_t ntiles) {
+  constexpr int R = 1 << RB;
+  constexpr uint32_t M = R - 1;
+  constexpr int D = R / kBlock;  // digits per thread in the block scans
   __shared__ uint32_t s_keys[kTile];
   __shared__ P s_vals[kTile];
-  __shared__ uint32_t wave_hist[kWaves][kRadix];
-  __shared__ uint32_t tile_start[kRadix];
-  __shared__ uint32_t glob_off[kRadix];
+  __shared__ uint32_t wave_hist[kWaves][R];
+  __shared__ uint32_t tile_start[R];
+  __shared__ uint32_t glob_off[R];
   __shared__ uint32_t wsum[kWaves];
 
+  const int64_t tile = tile_of_block(ntiles);
+  if (tile >= ntiles) return;  // block-uniform
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 #pragma unroll
-  for (int w = 0; w < kWaves; ++w) wave_hist[w][tid] = 0u;
+  for (int w = 0; w < kWaves; ++w)
+    for (int d = tid; d < R; d += kBlock) wave_hist[w][d] = 0u;
 
-  // global base of (digit = tid, this tile): exclusive scan of digit totals + row prefix.
+  // global base of (digit, this tile): exclusive scan of digit totals + row prefix.
   {
-    const uint32_t v = digit_tot[tid];
-    const uint32_t incl = wave_incl_scan_u32(v, lane);
-    if (lane == 63) wsum[wave] = incl;
-    __syncthreads();
-    uint32_t wpre = 0;
+    uint32_t v[D];
 #pragma unroll
-    for (int w = 0; w < kWaves; ++w) wpre += (w < wave) ? wsum[w] : 0u;
-    glob_off[tid] = wpre + incl - v + counts[(int64_t)tid * ntiles + blockIdx.x];
+    for (int i = 0; i < D; ++i) v[i] = digit_tot[tid * D + i];
+    block_excl_scan<D>(v, wsum, lane, wave);
+#pragma unroll
+    for (int i = 0; i < D; ++i) glob_off[tid * D + i] = v[i] + counts[(int64_t)(tid * D + i) * ntiles + tile];
   }
   __syncthreads();
 
-  const int64_t tile_base = (int64_t)blockIdx.x * kTile;
+  const int64_t tile_base = tile * kTile;
   const int64_t wbase = tile_base + (int64_t)wave * (kTile / kWaves);
   const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   uint32_t my_key[kRounds], my_rank[kRounds];
@@ -138,12 +195,17 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint32_t* __rest
   for (int r = 0; r < kRounds; ++r) {
     const int64_t idx = wbase + (int64_t)r * 64 + lane;
     const bool valid = idx < n;
-    const uint32_t key = valid ? keys_in[idx] : 0u;
-    const P val = valid ? (vals_in ? vals_in[idx] : implicit_payload<P>(idx)) : P{};
-    const uint32_t d = (key >> shift) & 255u;
+    my_key[r] = valid ? keys_in[idx] : 0u;
+    my_val[r] = valid ? (vals_in ? vals_in[idx] : implicit_payload<P>(idx)) : P{};
+  }
+#pragma unroll
+  for (int r = 0; r < kRounds; ++r) {
+    const int64_t idx = wbase + (int64_t)r * 64 + lane;
+    const bool valid = idx < n;
+    const uint32_t d = (my_key[r] >> shift) & M;
     uint64_t peers = __ballot(valid);
 #pragma unroll
-    for (int b = 0; b < 8; ++b) {
+    for (int b = 0; b < RB; ++b) {
       const bool bit = (d >> b) & 1u;
       const uint64_t m = __ballot(bit);
       peers &= bit ? m : ~m;
@@ -154,36 +216,35 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint32_t* __rest
     __builtin_amdgcn_wave_barrier();
     if (valid && below == 0) wave_hist[wave][d] = prev + cnt;
     __builtin_amdgcn_wave_barrier();
-    my_key[r] = key;
-    my_val[r] = val;
     my_rank[r] = valid ? prev + below : 0xFFFFFFFFu;
   }
   __syncthreads();
 
   // per-digit wave bases (exclusive over waves) and the tile's digit starts.
   {
-    const int d = tid;
-    uint32_t acc = 0;
+    uint32_t v[D];
 #pragma unroll
-    for (int w = 0; w < kWaves; ++w) {
-      const uint32_t c = wave_hist[w][d];
-      wave_hist[w][d] = acc;
-      acc += c;
+    for (int i = 0; i < D; ++i) {
+      const int d = tid * D + i;
+      uint32_t acc = 0;
+#pragma unroll
+      for (int w = 0; w < kWaves; ++w) {
+        const uint32_t c = wave_hist[w][d];
+        wave_hist[w][d] = acc;
+        acc += c;
+      }
+      v[i] = acc;
     }
-    const uint32_t incl = wave_incl_scan_u32(acc, lane);
-    if (lane == 63) wsum[wave] = incl;
-    __syncthreads();
-    uint32_t wpre = 0;
+    block_excl_scan<D>(v, wsum, lane, wave);
 #pragma unroll
-    for (int w = 0; w < kWaves; ++w) wpre += (w < wave) ? wsum[w] : 0u;
-    tile_start[d] = wpre + incl - acc;
+    for (int i = 0; i < D; ++i) tile_start[tid * D + i] = v[i];
   }
   __syncthreads();
 
 #pragma unroll
   for (int r = 0; r < kRounds; ++r) {
     if (my_rank[r] != 0xFFFFFFFFu) {
-      const uint32_t d = (my_key[r] >> shift) & 255u;
+      const uint32_t d = (my_key[r] >> shift) & M;
       const uint32_t pos = tile_start[d] + wave_hist[wave][d] + my_rank[r];
       s_keys[pos] = my_key[r];
       s_vals[pos] = my_val[r];
@@ -195,7 +256,7 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint32_t* __rest
   const int tile_n = rem < kTile ? (int)rem : kTile;
   for (int j = tid; j < tile_n; j += kBlock) {
     const uint32_t key = s_keys[j];
-    const uint32_t d = (key >> shift) & 255u;
+    const uint32_t d = (key >> shift) & M;
     const uint32_t dest = glob_off[d] + (uint32_t)j - tile_start[d];
     keys_out[dest] = key;
     vals_out[dest] = s_vals[j];
@@ -212,9 +273,33 @@ void SortWork::ensure(int64_t n) {
   vals_a.ensure(sizeof(uint64_t) * c);  // payloads up to 8 bytes
   vals_b.ensure(sizeof(uint64_t) * c);
   const int64_t ntiles = (c + kTile - 1) / kTile;
-  counts.ensure(sizeof(uint32_t) * kRadix * ntiles);
-  digit_tot.ensure(sizeof(uint32_t) * kRadix);
+  counts.ensure(sizeof(uint32_t) * kMaxRadix * ntiles);
+  digit_tot.ensure(sizeof(uint32_t) * kMaxRadix);
   cap = c;
+}
+
+template <class P, int RB>
+static void radix_pass(const uint32_t* kin, const P* vin, uint32_t* ko, P* vo, int64_t n, int shift,
+                       SortWork& w, int64_t ntiles, hipStream_t st) {
+  hipLaunchKernelGGL(k_radix_count<RB>, dim3((unsigned)ntiles), dim3(kBlock), 0, st, kin, n, shift,
+                     w.counts.as<uint32_t>(), ntiles);
+  hipLaunchKernelGGL(k_radix_scan_rows, dim3(1u << RB), dim3(kBlock), 0, st, w.counts.as<uint32_t>(), ntiles,
+                     w.digit_tot.as<uint32_t>());
+  hipLaunchKernelGGL((k_radix_scatter<P, RB>), dim3((unsigned)blocks_for_tiles(ntiles)), dim3(kBlock), 0, st, kin,
+                     vin, ko, vo, n, shift, w.counts.as<uint32_t>(), w.digit_tot.as<uint32_t>(), ntiles);
+  FM_HIP_CHECK(hipGetLastError());
+}
+
+// Digit width: the fewest passes of at most FM_SORT_MAXRB bits, spread evenly (27-bit feature
+// slots: 3 passes of 9 bits), never narrower than 8 bits.
+inline int digit_bits(int key_bits, int* passes) {
+  const int kb = key_bits < 1 ? 1 : key_bits;
+  int p = (kb + FM_SORT_MAXRB - 1) / FM_SORT_MAXRB;
+  int rb = (kb + p - 1) / p;
+  if (rb < 8) rb = 8;
+  p = (kb + rb - 1) / rb;
+  *passes = p;
+  return rb;
 }
 
 template <class P>
@@ -228,7 +313,8 @@ static void radix_sort_impl(SortWork& w, const uint32_t* keys_in, const P* vals_
     *vals_out = w.vals_a.as<P>();
     return;
   }
-  const int passes = key_bits <= 8 ? 1 : (key_bits + 7) / 8;
+  int passes = 0;
+  const int rb = digit_bits(key_bits, &passes);
   const int64_t ntiles = (n + kTile - 1) / kTile;
   FM_REQUIRE(ntiles < (int64_t(1) << 31), "too many sort tiles");
   const uint32_t* kin = keys_in;
@@ -239,21 +325,19 @@ static void radix_sort_impl(SortWork& w, const uint32_t* keys_in, const P* vals_
   // the count kernel reads keys as uint4 when the tile is full: needs 16-byte alignment
   const bool aligned = (reinterpret_cast<uintptr_t>(keys_in) & 15u) == 0;
   for (int p = 0; p < passes; ++p) {
-    const int shift = 8 * p;
+    const int shift = rb * p;
     if (p == 0 && !aligned) {
       FM_HIP_CHECK(hipMemcpyAsync(kbuf[1], keys_in, sizeof(uint32_t) * n, hipMemcpyDeviceToDevice, st));
       kin = kbuf[1];
     }
-    hipLaunchKernelGGL(k_radix_count, dim3((unsigned)ntiles), dim3(kBlock), 0, st, kin, n, shift,
-                       w.counts.as<uint32_t>(), ntiles);
-    hipLaunchKernelGGL(k_radix_scan_rows, dim3(kRadix), dim3(kBlock), 0, st, w.counts.as<uint32_t>(),
-                       ntiles, w.digit_tot.as<uint32_t>());
     const bool last = p == passes - 1 && final_keys != nullptr;
     uint32_t* ko = last ? final_keys : kbuf[which];
     P* vo = last ? final_vals : vbuf[which];
-    hipLaunchKernelGGL(k_radix_scatter<P>, dim3((unsigned)ntiles), dim3(kBlock), 0, st, kin, vin, ko, vo, n,
-                       shift, w.counts.as<uint32_t>(), w.digit_tot.as<uint32_t>(), ntiles);
-    FM_HIP_CHECK(hipGetLastError());
+    switch (rb) {
+      case 8: radix_pass<P, 8>(kin, vin, ko, vo, n, shift, w, ntiles, st); break;
+      case 9: radix_pass<P, 9>(kin, vin, ko, vo, n, shift, w, ntiles, st); break;
+      default: radix_pass<P, 10>(kin, vin, ko, vo, n, shift, w, ntiles, st); break;
+    }
     kin = ko;
     vin = vo;
     which ^= 1;

@@ -1,19 +1,22 @@
-"""Row-sharded multi-GPU FM SGD step: one process per GPU, RCCL all-to-all over xGMI.
+"""Row-sharded multi-GPU FM SGD step, owner-computes: one process per GPU, RCCL all-to-all
+over xGMI.
 
 The reference shards its model implicitly: every join / groupBy on featureId shuffles the
 exploded entries and the model Datasets by feature hash (SURVEY §2b, S1/S2/S5/S6:
 FactorizationMachinesModel.scala:155-164, FactorizationMachinesSGD.scala:148-166).  Here the
-table is row-sharded by ``owner = id % R`` (slot ``id // R``) across R ranks and one SGD
-iteration is four phases of the C-ABI (include/fm_hip.h, fm_shard_*) joined by three
-all-to-alls:
+table is row-sharded by ``owner = id % R`` (slot ``id // R``) across R ranks and the work
+moves to the rows instead of the rows to the work.  One SGD iteration is four phases of the
+C-ABI (include/fm_hip.h, fm_shard_*) joined by three all-to-alls:
 
-    plan (requester)  -> a2a request ids -> serve (owner) -> a2a rows back ->
-    local_grad (requester) -> a2a gradients -> apply (owner: rank-ordered sums, update, L1)
+    route (requester: entries by owner) -> a2a entries -> owner_forward (partial sums per
+    (sample, owner) pair) -> a2a partials back -> combine (requester: S, yhat, loss) ->
+    a2a S to the owners -> owner_update (sort by slot, per-slot gradient sums, update + L1)
 
 Every rank steps its own mini-batch; the iteration's miniBatchSize is the sum over ranks
 (weak scaling: the global batch grows with R).  The result equals one single-table step over
-the ranks' batches concatenated in rank order, up to fp summation order (owners sum the <= R
-partials per feature in rank order, so the result is deterministic for a given R).
+the ranks' batches concatenated in rank order, up to fp summation order (deterministic for a
+given R).  Only entries (12 B) and two kp + 4 float rows per (sample, owner) pair cross xGMI
+-- no table row or per-id gradient does.
 """
 
 from __future__ import annotations
@@ -23,7 +26,7 @@ import ctypes as C
 import numpy as np
 
 from . import _native as N
-from .engine import DeviceBatch, FMContext, StepOut
+from .engine import FMContext, StepOut
 
 
 class HipShardEngine:
@@ -35,6 +38,7 @@ class HipShardEngine:
 
         self.torch = torch
         self.device = torch.device("cuda", device)
+        self.R = world
         self.ctx = FMContext(num_features, k, device=device, seed=seed, init_sd=init_sd, w0=w0, shard_index=rank,
                              shard_count=world)
         # launch on torch's stream so the C-ABI kernels and the collectives are stream-ordered
@@ -42,38 +46,55 @@ class HipShardEngine:
         self.kp = (k + 3) // 4 * 4
         self.width = self.kp + 4
         self._lib = N.load()
+        self._keep = None
 
-    def batch(self, csr: N.CSRHost) -> DeviceBatch:
+    def _empty(self, n, dtype):
+        return self.torch.empty(max(int(n), 1), dtype=dtype, device=self.device)[: int(n)]
+
+    @staticmethod
+    def _ptr(t):
+        return C.c_void_p(t.data_ptr() if t.numel() else 0)
+
+    def batch(self, csr: N.CSRHost):
         return self.ctx.batch(csr)
 
-    def plan(self, b: DeviceBatch) -> np.ndarray:
-        R = self.ctx.shard_count
-        counts = np.zeros(R, dtype=np.int64)
-        N.check(self._lib.fm_shard_plan(self.ctx.handle, b.handle, N.ptr(counts, C.c_int64)), "fm_shard_plan")
-        return counts
+    def route(self, b):
+        torch = self.torch
+        n = int(b.nnz)
+        send_slot = self._empty(n, torch.int32)
+        send_ent = self._empty(2 * n, torch.int32)
+        counts = np.zeros(2 * self.R, dtype=np.int64)
+        N.check(self._lib.fm_shard_route(self.ctx.handle, b.handle, self._ptr(send_slot), self._ptr(send_ent),
+                                         N.ptr(counts, C.c_int64)), "fm_shard_route")
+        return send_slot, send_ent, counts
 
-    def request_copy(self, dst):
-        N.check(self._lib.fm_shard_request_copy(self.ctx.handle, C.c_void_p(dst.data_ptr())), "fm_shard_request_copy")
+    def owner_forward(self, recv_slot, recv_ent, src_entries, src_pairs):
+        se = np.ascontiguousarray(src_entries, dtype=np.int64)
+        sp = np.ascontiguousarray(src_pairs, dtype=np.int64)
+        out = self._empty(int(sp.sum()) * self.width, self.torch.float32)
+        self._keep = (recv_slot, recv_ent)  # read again by owner_update
+        N.check(self._lib.fm_shard_owner_forward(self.ctx.handle, self._ptr(recv_slot), self._ptr(recv_ent),
+                                                 int(recv_slot.numel()), N.ptr(se, C.c_int64),
+                                                 N.ptr(sp, C.c_int64), self._ptr(out)), "fm_shard_owner_forward")
+        return out
 
-    def serve(self, req, n: int, rows_out):
-        N.check(self._lib.fm_shard_serve_device(self.ctx.handle, C.c_void_p(req.data_ptr()), int(n),
-                                                C.c_void_p(rows_out.data_ptr())), "fm_shard_serve_device")
+    def combine(self, b, partials_in, n_pairs_out: int):
+        s_send = self._empty(int(n_pairs_out) * self.width, self.torch.float32)
+        N.check(self._lib.fm_shard_combine(self.ctx.handle, b.handle, self._ptr(partials_in), self._ptr(s_send)),
+                "fm_shard_combine")
+        return s_send
 
-    def local_grad(self, b: DeviceBatch, rows_in, grads_out):
-        N.check(self._lib.fm_shard_local_grad_device(self.ctx.handle, b.handle, C.c_void_p(rows_in.data_ptr()),
-                                                     C.c_void_p(grads_out.data_ptr())), "fm_shard_local_grad_device")
+    def owner_update(self, s_recv, t: int, step_size: float, reg_param: float, global_rows: int) -> int:
+        rc = N.check(self._lib.fm_shard_owner_update(self.ctx.handle, self._ptr(s_recv), int(t), float(step_size),
+                                                     float(reg_param), int(global_rows)), "fm_shard_owner_update")
+        self._keep = None
+        return rc
 
-    def apply(self, req, grads, n: int, t: int, step_size: float, reg_param: float, global_rows: int) -> int:
-        return N.check(self._lib.fm_shard_apply_device(self.ctx.handle, C.c_void_p(req.data_ptr()),
-                                                       C.c_void_p(grads.data_ptr()), int(n), int(t),
-                                                       float(step_size), float(reg_param), int(global_rows)),
-                       "fm_shard_apply_device")
-
-    def last_loss(self):
-        loss = C.c_double()
-        nl = C.c_int64()
-        N.check(self._lib.fm_shard_last_loss(self.ctx.handle, C.byref(loss), C.byref(nl)), "fm_shard_last_loss")
-        return loss.value, nl.value
+    def last_stats(self):
+        """(loss_sum, n_loss_rows) of this rank's samples, distinct ids this rank owns."""
+        loss, nl, nu = C.c_double(), C.c_int64(), C.c_int64()
+        N.check(self._lib.fm_last_stats(self.ctx.handle, C.byref(loss), C.byref(nl), C.byref(nu)), "fm_last_stats")
+        return loss.value, nl.value, nu.value
 
     def init_random_range(self, begin: int, end: int):
         self.ctx.init_random_range(begin, end)
@@ -134,34 +155,138 @@ class ShardedTrainer:
         self.dist.all_to_all_single(out, inp, output_split_sizes=[int(x) for x in out_splits],
                                     input_split_sizes=[int(x) for x in in_splits], group=self.group)
 
+    def _empty(self, n, dtype):
+        return self.torch.empty(max(int(n), 1), dtype=dtype, device=self.device)[: int(n)]
+
     def step(self, b, t: int, step_size: float, reg_param: float, sync: bool = True) -> StepOut | None:
-        torch = self.torch
+        torch, R, W = self.torch, self.world, self.engine.width
         gm = self.global_rows(b)
         if gm == 0:  # SGD.scala:126-128: every rank skips together
             return StepOut(0.0, 0, 0, 0, executed=False)
-        W = self.engine.width
-        send = self.engine.plan(b)
-        send_t = torch.tensor(send, dtype=torch.int64, device=self.device)
-        recv_t = torch.empty_like(send_t)
-        self.dist.all_to_all_single(recv_t, send_t, group=self.group)
-        recv = recv_t.cpu().numpy()
-        U, n_recv = int(send.sum()), int(recv.sum())
-        req_send = torch.empty(max(U, 1), dtype=torch.int32, device=self.device)[:U]
-        self.engine.request_copy(req_send)
-        req_recv = torch.empty(max(n_recv, 1), dtype=torch.int32, device=self.device)[:n_recv]
-        self._a2a(req_recv, req_send, recv, send)
-        rows_out = torch.empty(max(n_recv, 1) * W, dtype=torch.float32, device=self.device)[: n_recv * W]
-        self.engine.serve(req_recv, n_recv, rows_out)
-        rows_in = torch.empty(max(U, 1) * W, dtype=torch.float32, device=self.device)[: U * W]
-        self._a2a(rows_in, rows_out, send * W, recv * W)
-        grads_out = torch.empty(max(U, 1) * W, dtype=torch.float32, device=self.device)[: U * W]
-        self.engine.local_grad(b, rows_in, grads_out)
-        grads_in = torch.empty(max(n_recv, 1) * W, dtype=torch.float32, device=self.device)[: n_recv * W]
-        self._a2a(grads_in, grads_out, recv * W, send * W)
-        self.engine.apply(req_recv, grads_in, n_recv, t, step_size, reg_param, gm)
+        send_slot, send_ent, counts = self.engine.route(b)
+        ent_out, pair_out = counts[:R], counts[R:]
+        cnt = torch.tensor(np.stack([ent_out, pair_out], axis=1).reshape(-1), dtype=torch.int64, device=self.device)
+        rcnt = torch.empty_like(cnt)
+        self.dist.all_to_all_single(rcnt, cnt, group=self.group)
+        rc = rcnt.cpu().numpy().reshape(R, 2)
+        ent_in, pair_in = rc[:, 0], rc[:, 1]
+        recv_slot = self._empty(ent_in.sum(), torch.int32)
+        self._a2a(recv_slot, send_slot, ent_in, ent_out)
+        recv_ent = self._empty(2 * ent_in.sum(), torch.int32)
+        self._a2a(recv_ent, send_ent, 2 * ent_in, 2 * ent_out)
+        partials = self.engine.owner_forward(recv_slot, recv_ent, ent_in, pair_in)
+        part_in = self._empty(pair_out.sum() * W, torch.float32)
+        self._a2a(part_in, partials, pair_out * W, pair_in * W)
+        s_send = self.engine.combine(b, part_in, int(pair_out.sum()))
+        s_recv = self._empty(pair_in.sum() * W, torch.float32)
+        self._a2a(s_recv, s_send, pair_in * W, pair_out * W)
+        self.engine.owner_update(s_recv, t, step_size, reg_param, gm)
         if not sync:
             return None
-        loss, nl = self.engine.last_loss()
+        loss, nl, U = self.engine.last_stats()
         tot = torch.tensor([loss, float(nl), float(U)], dtype=torch.float64, device=self.device)
         self.dist.all_reduce(tot, group=self.group)
-        return StepOut(float(tot[0]), gm, int(tot[1]), U)
+        return StepOut(float(tot[0]), gm, int(tot[1]), int(tot[2]))
+
+
+# ------------------------------------------------------------------------------ replicated
+class HipReplEngine:
+    """The whole table on every rank (small feature spaces, BASELINE config c2): the phase
+    functions fm_repl_grad / fm_repl_apply of include/fm_hip.h."""
+
+    def __init__(self, num_features: int, k: int, *, device: int = 0, seed: int = 0, init_sd: float = 0.01,
+                 w0: float = 0.0):
+        import torch
+
+        self.torch = torch
+        self.device = torch.device("cuda", device)
+        self.ctx = FMContext(num_features, k, device=device, seed=seed, init_sd=init_sd, w0=w0)
+        self.ctx.set_stream(torch.cuda.current_stream(self.device).cuda_stream)
+        self.kp = (k + 3) // 4 * 4
+        self.width = self.kp + 4
+        self.grad = torch.empty(num_features * self.width, dtype=torch.float32, device=self.device)
+        self._lib = N.load()
+
+    def batch(self, csr: N.CSRHost):
+        return self.ctx.batch(csr)
+
+    def grad_phase(self, b):
+        N.check(self._lib.fm_repl_grad(self.ctx.handle, b.handle, C.c_void_p(self.grad.data_ptr())), "fm_repl_grad")
+        return self.grad
+
+    def apply(self, grad, t: int, step_size: float, reg_param: float, global_rows: int) -> int:
+        return N.check(self._lib.fm_repl_apply(self.ctx.handle, C.c_void_p(grad.data_ptr()), int(t),
+                                               float(step_size), float(reg_param), int(global_rows)),
+                       "fm_repl_apply")
+
+    def last_stats(self):
+        loss, nl, nu = C.c_double(), C.c_int64(), C.c_int64()
+        N.check(self._lib.fm_last_stats(self.ctx.handle, C.byref(loss), C.byref(nl), C.byref(nu)), "fm_last_stats")
+        return loss.value, nl.value, nu.value
+
+    def init_random_range(self, begin: int, end: int):
+        self.ctx.init_random_range(begin, end)
+
+    def load_tables(self, ids, w, V):
+        self.ctx.load_tables(ids, w, V)
+
+    def export_tables(self):
+        return self.ctx.export_tables()
+
+
+class ReplicatedTrainer:
+    """Data-parallel step with the table replicated on every rank: local gradient sums into a
+    dense [F][kp + 4] fp32 buffer, one RCCL all-reduce (sum), the identical update everywhere.
+    For small tables (c2: 1M features x k = 8 -> 48 MB per all-reduce); larger feature spaces
+    use ShardedTrainer.  Equals the single-table step over the ranks' batches concatenated,
+    up to fp summation order."""
+
+    def __init__(self, num_features: int, k: int, *, rank: int, world: int, device: int = 0, seed: int = 0,
+                 init_sd: float = 0.01, w0: float = 0.0, group=None, engine=None):
+        import torch
+        import torch.distributed as dist
+
+        self.torch, self.dist = torch, dist
+        self.rank, self.world, self.group = rank, world, group
+        self.engine = engine if engine is not None else HipReplEngine(
+            num_features, k, device=device, seed=seed, init_sd=init_sd, w0=w0)
+        self.device = self.engine.device
+        self._global_rows = {}
+
+    @property
+    def ctx(self):
+        return getattr(self.engine, "ctx", None)
+
+    def batch(self, csr):
+        return self.engine.batch(csr)
+
+    def init_random_range(self, begin, end):
+        self.engine.init_random_range(begin, end)
+
+    def load_tables(self, ids, w, V):
+        self.engine.load_tables(ids, w, V)
+
+    def export_tables(self):
+        return self.engine.export_tables()
+
+    def global_rows(self, b) -> int:
+        key = id(b)
+        if key not in self._global_rows:
+            t = self.torch.tensor([int(b.n_rows)], dtype=self.torch.int64, device=self.device)
+            self.dist.all_reduce(t, group=self.group)
+            self._global_rows[key] = int(t.item())
+        return self._global_rows[key]
+
+    def step(self, b, t: int, step_size: float, reg_param: float, sync: bool = True) -> StepOut | None:
+        gm = self.global_rows(b)
+        if gm == 0:  # SGD.scala:126-128
+            return StepOut(0.0, 0, 0, 0, executed=False)
+        g = self.engine.grad_phase(b)
+        self.dist.all_reduce(g, group=self.group)
+        self.engine.apply(g, t, step_size, reg_param, gm)
+        if not sync:
+            return None
+        loss, nl, U = self.engine.last_stats()
+        tot = self.torch.tensor([loss, float(nl)], dtype=self.torch.float64, device=self.device)
+        self.dist.all_reduce(tot, group=self.group)
+        return StepOut(float(tot[0]), gm, int(tot[1]), int(U))

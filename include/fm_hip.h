@@ -190,32 +190,53 @@ int32_t fm_murmur3_bytes_hash(const uint8_t* data, int64_t len, int32_t seed);
 /* n successive nextDouble() of XORShiftRandom(seed). */
 int fm_xorshift_next_doubles(int64_t seed, int64_t n, double* out);
 
-/* ---- row-sharded multi-GPU step ---------------------------------------------------------
- * One context per rank (fm_config.shard_index / shard_count = rank / R); the caller exchanges
- * the device buffers between phases with all-to-all (RCCL over xGMI; see
- * fm_spark_amd/distributed.py).  Replaces the feature-keyed shuffles S1/S2/S5/S6 of the
- * reference plan (Model.scala:155-164, SGD.scala:148-166).  Wire rows and
- * gradients are fp32, kp + 4 floats per distinct id (kp = roundup(k, 4)):
- *   row  = [V(kp) | w | 0 0 0]        gradient = [sum gV (kp) | sum gw | 0 0 0]
- * Phase 1 (requester): sort the batch's entries by (owner, slot) and dedupe.  send_counts[R]
- * receives the number of distinct ids requested from each owner (their sum is U).
+/* ---- row-sharded multi-GPU step (owner-computes) -----------------------------------------
+ * One context per rank (fm_config.shard_index / shard_count = rank / R, R <= 64; the owner of
+ * feature id is id % R, its local slot id / R).  The caller exchanges the device buffers
+ * between phases with all-to-all (RCCL over xGMI; fm_spark_amd/distributed.py).  Replaces the
+ * feature-keyed shuffles S1/S2/S5/S6 and the per-sample window of the reference plan
+ * (Model.scala:155-164, :191, SGD.scala:148-166).
+ * A "pair" is (sample of a source rank, owner holding some of its entries).  Wire rows are fp32,
+ * kp + 4 floats per pair (kp = roundup(k, 4)):
+ *   partial = [sum v*x (kp) | sum v^2 x^2 | sum w*x | 0 0]     S = [vfxiSum (kp) | yhat | y | 0 0]
+ * Phase 1 (requester): partition the batch's entries by owner, CSR order kept, into
+ * send_slot (uint32 local slots, N) and send_ent ({sample, x bits}, N) -- device buffers of the
+ * batch's nnz.  counts[0..R) = entries to each owner, counts[R..2R) = pairs to each owner.
  * Synchronises the context's stream. */
-int fm_shard_plan(fm_ctx* ctx, const fm_batch* batch, int64_t* send_counts);
-/* Copy the plan's request list (U int32 local slots, owner-major) to a device buffer. */
-int fm_shard_request_copy(fm_ctx* ctx, void* dst_device);
-/* Phase 2 (owner): rows for n requested local slots, pending L1 applied. */
-int fm_shard_serve_device(fm_ctx* ctx, const void* req_slots, int64_t n, void* rows_out);
-/* Phase 3 (requester): forward from the U received rows (ordered as the request list) and the
- * per-distinct-id gradient sums of this rank's entries -> grads_out[U].  The rank's loss sum
- * is kept for fm_shard_last_loss / fm_loss_history. */
-int fm_shard_local_grad_device(fm_ctx* ctx, fm_batch* batch, const void* rows_in, void* grads_out);
-/* Phase 4 (owner): the n received (slot, gradient) pairs of all ranks, rank-major; sums per
- * slot in rank order and applies the update + L1 with global miniBatchSize global_rows
- * (the sum of every rank's rows).  Returns FM_NOTHING_TO_DO when global_rows == 0. */
-int fm_shard_apply_device(fm_ctx* ctx, const void* req_slots, const void* grads, int64_t n,
-                          int32_t t, double step_size, double reg_param, int64_t global_rows);
-/* This rank's (loss_sum, n_loss_rows) of the last step; the caller all-reduces. */
-int fm_shard_last_loss(fm_ctx* ctx, double* loss_sum, int64_t* n_loss_rows);
+int fm_shard_route(fm_ctx* ctx, fm_batch* batch, void* send_slot, void* send_ent, int64_t* counts);
+/* Phase 2 (owner): the n received entries (source-rank major: src_entries[r] from rank r, which
+ * sent src_pairs[r] pairs) -> partials_out[sum src_pairs] (source-major, sample order).  The
+ * received buffers must stay valid until fm_shard_owner_update. */
+int fm_shard_owner_forward(fm_ctx* ctx, const void* recv_slot, const void* recv_ent, int64_t n,
+                           const int64_t* src_entries, const int64_t* src_pairs, void* partials_out);
+/* Phase 3 (requester): the partials received from the owners (owner-major, counts[R + o] rows
+ * from owner o) -> per sample S, yhat and the loss; s_send gets the S rows in the same layout. */
+int fm_shard_combine(fm_ctx* ctx, fm_batch* batch, const void* partials_in, void* s_send);
+/* Phase 4 (owner): the S rows received for its pairs (same order as its partials) -> sort the
+ * received entries by slot (source rank, then CSR order within a slot), per-slot gradient sums,
+ * update + L1 with global miniBatchSize global_rows (the sum of every rank's rows).
+ * Returns FM_NOTHING_TO_DO when global_rows == 0 (every rank skips, SGD.scala:126-128). */
+int fm_shard_owner_update(fm_ctx* ctx, const void* s_recv, int32_t t, double step_size, double reg_param,
+                          int64_t global_rows);
+
+/* ---- replicated multi-GPU step (small tables) --------------------------------------------
+ * Every rank holds the whole table (shard_count = 1, same seed / same loaded tables) and steps
+ * its own rows of the global mini-batch.
+ * Phase 1: forward, sort and per-slot gradient sums of this rank's batch into the device
+ * buffer grad[num_features][kp + 4] fp32 = [sum g_V (kp) | sum g_w | touched | 0] (zeroed
+ * first; an empty batch contributes zeros and returns FM_NOTHING_TO_DO).
+ * The caller all-reduces grad (sum; RCCL over xGMI), then
+ * Phase 2: the update + L1 of SGD.scala:150-181 on every touched row with global miniBatchSize
+ * global_rows; identical on every rank, so the replicas stay identical.  Returns
+ * FM_NOTHING_TO_DO when global_rows == 0. */
+int fm_repl_grad(fm_ctx* ctx, fm_batch* batch, void* grad);
+int fm_repl_apply(fm_ctx* ctx, const void* grad, int32_t t, double step_size, double reg_param,
+                  int64_t global_rows);
+
+/* Statistics of the last step on this context: loss sum and loss rows of its samples, distinct
+ * ids (sharded: those this rank owns; replicated: touched rows of the whole step).  Multi-GPU
+ * callers all-reduce the first two (SGD.scala:134-139). */
+int fm_last_stats(fm_ctx* ctx, double* loss_sum, int64_t* n_loss_rows, int64_t* n_unique);
 
 #ifdef __cplusplus
 }

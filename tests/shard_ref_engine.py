@@ -1,6 +1,7 @@
-"""TEST INFRASTRUCTURE: a NumPy implementation of the sharded phase functions (plan / serve /
-local_grad / apply, include/fm_hip.h fm_shard_*) with the oracle's fp64 math, so the
-exchange protocol of fm_spark_amd.distributed.ShardedTrainer can run on CPU under gloo."""
+"""TEST INFRASTRUCTURE: a NumPy implementation of the sharded phase functions (route /
+owner_forward / combine / owner_update, include/fm_hip.h fm_shard_*) with the oracle's fp64
+math and the same fp32 wire formats, so the exchange protocol of
+fm_spark_amd.distributed.ShardedTrainer can run on CPU under gloo."""
 
 import math
 
@@ -13,7 +14,6 @@ class NpBatch:
         self.csr = csr
         self.n_rows = csr.n_rows
         self.nnz = csr.nnz
-        self.uidx = None
 
 
 class NumpyShardEngine:
@@ -23,12 +23,10 @@ class NumpyShardEngine:
         self.kp = (k + 3) // 4 * 4
         self.width = self.kp + 4
         self.rows = (num_features - rank + world - 1) // world
-        self.rpsh = (num_features + world - 1) // world
         self.w = np.zeros(self.rows)
         self.V = np.zeros((self.rows, k))
         self.present = np.zeros(self.rows, dtype=bool)
-        self.req = np.zeros(0, dtype=np.int32)
-        self.loss = (0.0, 0)
+        self.stats = (0.0, 0, 0)
 
     def batch(self, csr):
         return NpBatch(csr)
@@ -45,67 +43,88 @@ class NumpyShardEngine:
         slots = np.nonzero(self.present)[0]
         return (slots * self.R + self.rank).astype(np.int32), self.w[slots], self.V[slots]
 
-    def plan(self, b):
-        ids = b.csr.col.astype(np.int64)
-        ck = (ids % self.R) * self.rpsh + ids // self.R
-        uk, inv = np.unique(ck, return_inverse=True)
-        b.uidx = inv
-        self.req = (uk % self.rpsh).astype(np.int32)
-        return np.bincount(uk // self.rpsh, minlength=self.R).astype(np.int64)
-
-    def request_copy(self, dst):
-        dst.copy_(torch.from_numpy(self.req))
-
-    def serve(self, req, n, rows_out):
-        slots = req.numpy().astype(np.int64)
-        out = np.zeros((n, self.width), dtype=np.float32)
-        out[:, : self.k] = self.V[slots]
-        out[:, self.kp] = self.w[slots]
-        rows_out.copy_(torch.from_numpy(out.reshape(-1)))
-
-    def local_grad(self, b, rows_in, grads_out):
+    # requester -------------------------------------------------------------------
+    def route(self, b):
         csr = b.csr
-        U = len(self.req)
-        rows = rows_in.numpy().reshape(U, self.width).astype(np.float64)
-        m = csr.n_rows
-        srow = np.repeat(np.arange(m), np.diff(csr.row_ptr))
-        x = csr.val
-        V = rows[b.uidx, : self.k]
-        w = rows[b.uidx, self.kp]
-        vfxi = V * x[:, None]
-        S = np.zeros((m, self.k))
-        np.add.at(S, srow, vfxi)
-        wsum = np.zeros(m)
-        np.add.at(wsum, srow, w * x)
-        vv = np.zeros(m)
-        np.add.at(vv, srow, np.sum(V * V, axis=1) * x * x)
-        yhat = 0.5 * (np.sum(S * S, axis=1) - vv) + wsum + self.w0
+        ids = csr.col.astype(np.int64)
+        owner = ids % self.R
+        sample = np.repeat(np.arange(csr.n_rows), np.diff(csr.row_ptr))
+        order = np.argsort(owner, kind="stable")
+        send_slot = (ids[order] // self.R).astype(np.int32)
+        ent = np.stack([sample[order].astype(np.uint32), csr.val[order].astype(np.float32).view(np.uint32)], axis=1)
+        ents = np.bincount(owner, minlength=self.R)
+        has = np.zeros((csr.n_rows, self.R), dtype=bool)
+        has[sample, owner] = True
+        pairs = has.sum(axis=0)
+        self.pairidx = np.where(has, np.cumsum(has, axis=0) - 1, -1)  # [B][R]
+        self.pairs_out = pairs
+        counts = np.concatenate([ents, pairs]).astype(np.int64)
+        return torch.from_numpy(send_slot), torch.from_numpy(ent.view(np.int32).reshape(-1).copy()), counts
+
+    def combine(self, b, partials_in, n_pairs_out):
+        csr = b.csr
+        W, kp = self.width, self.kp
+        part = partials_in.numpy().reshape(-1, W).astype(np.float64)
+        poff = np.concatenate([[0], np.cumsum(self.pairs_out)])
+        B = csr.n_rows
+        S = np.zeros((B, kp))
+        vv = np.zeros(B)
+        wx = np.zeros(B)
+        for o in range(self.R):  # owner order
+            ix = self.pairidx[:, o]
+            m = ix >= 0
+            rows = part[poff[o] + ix[m]]
+            S[m] += rows[:, :kp]
+            vv[m] += rows[:, kp]
+            wx[m] += rows[:, kp + 1]
+        yhat = 0.5 * (np.sum(S * S, axis=1) - vv) + wx + self.w0
         has = np.diff(csr.row_ptr) > 0
         d = (yhat - csr.label)[has]
         self.loss = (float(np.sum(d * d)), int(has.sum()))
-        r = (yhat - csr.label)[srow]
-        gw = x * yhat[srow] - csr.label[srow]
-        gv = (S[srow] * x[:, None] - vfxi * x[:, None]) * r[:, None]
-        GW = np.zeros(U)
-        np.add.at(GW, b.uidx, gw)
-        GV = np.zeros((U, self.k))
-        np.add.at(GV, b.uidx, gv)
-        out = np.zeros((U, self.width), dtype=np.float32)
-        out[:, : self.k] = GV
-        out[:, self.kp] = GW
-        grads_out.copy_(torch.from_numpy(out.reshape(-1)))
+        out = np.zeros((int(n_pairs_out), W), dtype=np.float32)
+        for o in range(self.R):
+            ix = self.pairidx[:, o]
+            m = ix >= 0
+            out[poff[o] + ix[m], :kp] = S[m]
+            out[poff[o] + ix[m], kp] = yhat[m]
+            out[poff[o] + ix[m], kp + 1] = csr.label[m]
+        return torch.from_numpy(out.reshape(-1))
 
-    def apply(self, req, grads, n, t, step_size, reg_param, global_rows):
+    # owner -----------------------------------------------------------------------
+    def owner_forward(self, recv_slot, recv_ent, src_entries, src_pairs):
+        slots = recv_slot.numpy().astype(np.int64)
+        ent = recv_ent.numpy().view(np.uint32).reshape(-1, 2)
+        s, x = ent[:, 0].astype(np.int64), ent[:, 1].view(np.float32).astype(np.float64)
+        n = len(slots)
+        src = np.repeat(np.arange(self.R), src_entries)
+        head = np.ones(n, dtype=bool)
+        head[1:] = (s[1:] != s[:-1]) | (src[1:] != src[:-1])
+        pair = np.cumsum(head) - 1
+        P = int(head.sum())
+        assert P == int(np.sum(src_pairs))
+        V, w = self.V[slots], self.w[slots]
+        part = np.zeros((P, self.width))
+        np.add.at(part[:, : self.k], pair, V * x[:, None])
+        np.add.at(part[:, self.kp], pair, np.sum(V * V, axis=1) * x * x)
+        np.add.at(part[:, self.kp + 1], pair, w * x)
+        self.recv = (slots, x, pair)
+        return torch.from_numpy(part.astype(np.float32).reshape(-1))
+
+    def owner_update(self, s_recv, t, step_size, reg_param, global_rows):
         if global_rows == 0:
             return 1
+        slots, x, pair = self.recv
+        Srow = s_recv.numpy().reshape(-1, self.width).astype(np.float64)
+        S, yhat, y = Srow[pair, : self.k], Srow[pair, self.kp], Srow[pair, self.kp + 1]
         eta = step_size / math.sqrt(t)
         lam = eta * reg_param
-        slots = req.numpy().astype(np.int64)
-        G = grads.numpy().reshape(n, self.width).astype(np.float64)
+        V = self.V[slots]
+        gw = x * yhat - y  # SGD.scala:145
+        gv = (S * x[:, None] - V * x[:, None] * x[:, None]) * (yhat - y)[:, None]
         GW = np.zeros(self.rows)
         GV = np.zeros((self.rows, self.k))
-        np.add.at(GW, slots, G[:, self.kp])
-        np.add.at(GV, slots, G[:, : self.k])
+        np.add.at(GW, slots, gw)
+        np.add.at(GV, slots, gv)
         touched = np.unique(slots)
         w_new, V_new = self.w.copy(), self.V.copy()
         w_new[touched] = self.w[touched] - (GW[touched] / global_rows) * eta
@@ -115,7 +134,83 @@ class NumpyShardEngine:
         self.w[pres] = np.sign(w_new[pres]) * np.maximum(0.0, np.abs(w_new[pres]) - lam)
         self.V[pres] = np.sign(V_new[pres]) * np.maximum(0.0, np.abs(V_new[pres]) - lam)
         self.present = pres
+        self.stats = (self.loss[0], self.loss[1], len(touched))
         return 0
 
-    def last_loss(self):
-        return self.loss
+    def last_stats(self):
+        return self.stats
+
+
+class NumpyReplEngine:
+    """TEST INFRASTRUCTURE: the replicated phase functions (fm_repl_grad / fm_repl_apply) in
+    NumPy with the same fp32 gradient buffer layout [F][kp + 4]."""
+
+    def __init__(self, num_features, k, w0=0.0):
+        self.device = torch.device("cpu")
+        self.F, self.k, self.w0 = num_features, k, w0
+        self.kp = (k + 3) // 4 * 4
+        self.width = self.kp + 4
+        self.w = np.zeros(num_features)
+        self.V = np.zeros((num_features, k))
+        self.present = np.zeros(num_features, dtype=bool)
+        self.stats = (0.0, 0, 0)
+
+    def batch(self, csr):
+        return NpBatch(csr)
+
+    def load_tables(self, ids, w, V):
+        ids = np.asarray(ids, dtype=np.int64)
+        self.w[ids] = w
+        self.V[ids] = np.asarray(V).reshape(len(ids), self.k)
+        self.present[ids] = True
+
+    def export_tables(self):
+        ids = np.nonzero(self.present)[0]
+        return ids.astype(np.int32), self.w[ids], self.V[ids]
+
+    def grad_phase(self, b):
+        csr = b.csr
+        g = np.zeros((self.F, self.width))
+        self.loss = (0.0, 0)
+        if csr.n_rows:
+            ids = csr.col.astype(np.int64)
+            x = csr.val
+            srow = np.repeat(np.arange(csr.n_rows), np.diff(csr.row_ptr))
+            V, w = self.V[ids], self.w[ids]
+            S = np.zeros((csr.n_rows, self.k))
+            np.add.at(S, srow, V * x[:, None])
+            vv = np.zeros(csr.n_rows)
+            np.add.at(vv, srow, np.sum(V * V, axis=1) * x * x)
+            wx = np.zeros(csr.n_rows)
+            np.add.at(wx, srow, w * x)
+            yhat = 0.5 * (np.sum(S * S, axis=1) - vv) + wx + self.w0
+            has = np.diff(csr.row_ptr) > 0
+            d = (yhat - csr.label)[has]
+            self.loss = (float(np.sum(d * d)), int(has.sum()))
+            r = (yhat - csr.label)[srow]
+            np.add.at(g[:, : self.k], ids, (S[srow] * x[:, None] - V * x[:, None] * x[:, None]) * r[:, None])
+            np.add.at(g[:, self.kp], ids, x * yhat[srow] - csr.label[srow])
+            g[ids, self.kp + 1] = 1.0
+        self.grad = torch.from_numpy(g.astype(np.float32).reshape(-1))
+        return self.grad
+
+    def apply(self, grad, t, step_size, reg_param, global_rows):
+        if global_rows == 0:
+            return 1
+        G = grad.numpy().reshape(self.F, self.width).astype(np.float64)
+        touched = np.nonzero(G[:, self.kp + 1] > 0)[0]
+        eta = step_size / math.sqrt(t)
+        lam = eta * reg_param
+        w_new, V_new = self.w.copy(), self.V.copy()
+        w_new[touched] -= (G[touched, self.kp] / global_rows) * eta
+        V_new[touched] -= G[touched, : self.k] * (eta / global_rows)
+        pres = self.present.copy()
+        pres[touched] = True
+        self.w[pres] = np.sign(w_new[pres]) * np.maximum(0.0, np.abs(w_new[pres]) - lam)
+        self.V[pres] = np.sign(V_new[pres]) * np.maximum(0.0, np.abs(V_new[pres]) - lam)
+        self.present = pres
+        self.stats = (self.loss[0], self.loss[1], len(touched))
+        return 0
+
+    def last_stats(self):
+        return self.stats

@@ -23,7 +23,7 @@ def header_functions():
 def test_header_declares_the_boundary():
     names = header_functions()
     for required in ["fm_create", "fm_destroy", "fm_last_error", "fm_step", "fm_step_batch", "fm_predict",
-                     "fm_export_tables", "fm_load_tables", "fm_random_split", "fm_shard_plan", "fm_shard_apply_device"]:
+                     "fm_export_tables", "fm_load_tables", "fm_random_split", "fm_shard_route", "fm_shard_owner_update"]:
         assert required in names
 
 

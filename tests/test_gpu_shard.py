@@ -1,6 +1,7 @@
-"""GPU: the HIP sharded phase kernels (fm_shard_* of include/fm_hip.h).  R ranks are
-simulated in one process on one GPU (one fm_ctx per rank, all-to-all done by tensor
-slicing), compared with the single-table oracle step over the concatenated batches."""
+"""GPU: the HIP sharded phase kernels (fm_shard_* of include/fm_hip.h: route, owner_forward,
+combine, owner_update).  R ranks are simulated in one process on one GPU (one fm_ctx per
+rank, all-to-all done by tensor slicing), compared with the single-table oracle step over
+the concatenated batches."""
 
 import numpy as np
 import pytest
@@ -22,36 +23,32 @@ def _concat(parts):
 
 
 def _simulated_step(engines, batches, t, step_size, reg):
+    """One iteration of the ShardedTrainer protocol with the all-to-alls done by slicing."""
     import torch
 
     R = len(engines)
     W = engines[0].width
-    dev = engines[0].device
-    sends = [e.plan(b) for e, b in zip(engines, batches)]
-    reqs = []
-    for e, s in zip(engines, sends):
-        q = torch.empty(int(s.sum()), dtype=torch.int32, device=dev)
-        e.request_copy(q)
-        reqs.append(torch.split(q, s.tolist()))
-    recv_req = [torch.cat([reqs[r][o] for r in range(R)]) for o in range(R)]
-    rows_out = []
+    routed = [e.route(b) for e, b in zip(engines, batches)]
+    ent_cnt = [c[:R] for _, _, c in routed]   # [src][owner]
+    pair_cnt = [c[R:] for _, _, c in routed]
+    partials = []
     for o in range(R):
-        n = recv_req[o].numel()
-        out = torch.empty(n * W, dtype=torch.float32, device=dev)
-        engines[o].serve(recv_req[o], n, out)
-        rows_out.append(torch.split(out, [int(sends[r][o]) * W for r in range(R)]))
-    grads = []
+        slots = torch.cat([torch.split(routed[r][0], ent_cnt[r].tolist())[o] for r in range(R)])
+        ents = torch.cat([torch.split(routed[r][1], (2 * ent_cnt[r]).tolist())[o] for r in range(R)])
+        src_e = np.array([ent_cnt[r][o] for r in range(R)])
+        src_p = np.array([pair_cnt[r][o] for r in range(R)])
+        out = engines[o].owner_forward(slots, ents, src_e, src_p)
+        partials.append(torch.split(out, (src_p * W).tolist()))
+    s_rows = []
     for r in range(R):
-        rows_in = torch.cat([rows_out[o][r] for o in range(R)])
-        g = torch.empty(int(sends[r].sum()) * W, dtype=torch.float32, device=dev)
-        engines[r].local_grad(batches[r], rows_in, g)
-        grads.append(torch.split(g, [int(c) * W for c in sends[r]]))
+        pin = torch.cat([partials[o][r] for o in range(R)])
+        s = engines[r].combine(batches[r], pin, int(pair_cnt[r].sum()))
+        s_rows.append(torch.split(s, (pair_cnt[r] * W).tolist()))
     gm = sum(int(b.n_rows) for b in batches)
     for o in range(R):
-        gin = torch.cat([grads[r][o] for r in range(R)])
-        engines[o].apply(recv_req[o], gin, recv_req[o].numel(), t, step_size, reg, gm)
+        engines[o].owner_update(torch.cat([s_rows[r][o] for r in range(R)]), t, step_size, reg, gm)
     torch.cuda.synchronize()
-    return sum(e.last_loss()[0] for e in engines)
+    return sum(e.last_stats()[0] for e in engines), sum(e.last_stats()[2] for e in engines)
 
 
 @pytest.mark.parametrize("R,k", [(1, 8), (2, 16), (3, 5), (4, 32)])
@@ -69,9 +66,11 @@ def test_hip_shard_phases_match_single_table(gpu, R, k):
     for t in range(1, 4):
         parts = [make_problem(100 * t + r, 120 + 17 * r, F, k, 9, hot=11)[0] for r in range(R)]
         bs = [e.batch(CSRHost(p.row_ptr, p.col, p.val, p.label)) for e, p in zip(engines, parts)]
-        loss = _simulated_step(engines, bs, t, 0.3, 1e-4)
-        ref = R_.sgd_step_fast(model, _concat(parts), t, 0.3, 1e-4)
+        loss, nu = _simulated_step(engines, bs, t, 0.3, 1e-4)
+        cat = _concat(parts)
+        ref = R_.sgd_step_fast(model, cat, t, 0.3, 1e-4)
         assert loss == pytest.approx(ref.loss_sum, rel=1e-5)
+        assert nu == len(np.unique(cat.col))
     gi, gw, gV = zip(*[e.export_tables() for e in engines])
     gi = np.concatenate(gi)
     order = np.argsort(gi)
@@ -105,9 +104,85 @@ def test_sharded_trainer_world1_rccl(gpu):
             o = tr.step(tr.batch(CSRHost(p.row_ptr, p.col, p.val, p.label)), t, 0.2, 1e-5)
             ref = R_.sgd_step_fast(model, p, t, 0.2, 1e-5)
             assert o.loss_sum == pytest.approx(ref.loss_sum, rel=1e-5)
+            assert o.n_unique == len(np.unique(p.col))
         gi, gw, gV = tr.export_tables()
         np.testing.assert_array_equal(gi, np.nonzero(model.present)[0])
         np.testing.assert_allclose(gw, model.w[gi], rtol=1e-5, atol=1e-8)
         np.testing.assert_allclose(gV, model.V[gi], rtol=1e-5, atol=1e-8)
     finally:
         dist.destroy_process_group()
+
+
+def test_hip_shard_empty_rank_and_empty_rows(gpu):
+    """One rank steps an empty batch, the other one with empty rows; the global step still
+    equals the single-table step over the concatenation (m counts every row)."""
+    from fm_spark_amd._native import CSRHost
+    from fm_spark_amd.distributed import HipShardEngine
+
+    F, k, R = 97, 4, 2
+    _, ids, w, V = make_problem(8, 1, F, k, 1)
+    engines = [HipShardEngine(F, k, r, R) for r in range(R)]
+    for e in engines:
+        e.load_tables(ids, w, V)
+    model = R_.Model.empty(F, k)
+    model.load(ids, w, V)
+    empty = R_.CSR(np.zeros(1, np.int64), np.zeros(0, np.int32), np.zeros(0), np.zeros(0))
+    p = make_problem(9, 40, F, k, 5, hot=3)[0]
+    # make rows 3 and 7 empty
+    lens = np.diff(p.row_ptr)
+    keep = np.ones(p.nnz, bool)
+    for r_ in (3, 7):
+        keep[p.row_ptr[r_]:p.row_ptr[r_ + 1]] = False
+    lens[[3, 7]] = 0
+    q = R_.CSR(np.concatenate([[0], np.cumsum(lens)]).astype(np.int64), p.col[keep], p.val[keep], p.label)
+    parts = [empty, q]
+    bs = [e.batch(CSRHost(c.row_ptr, c.col, c.val, c.label)) for e, c in zip(engines, parts)]
+    loss, nu = _simulated_step(engines, bs, 1, 0.3, 1e-4)
+    ref = R_.sgd_step_fast(model, _concat(parts), 1, 0.3, 1e-4)
+    assert loss == pytest.approx(ref.loss_sum, rel=1e-5)
+    gi, gw, gV = zip(*[e.export_tables() for e in engines])
+    gi = np.concatenate(gi)
+    order = np.argsort(gi)
+    np.testing.assert_allclose(np.concatenate(gw)[order], model.w[gi[order]], rtol=1e-5, atol=1e-8)
+    np.testing.assert_allclose(np.concatenate(gV)[order], model.V[gi[order]], rtol=1e-5, atol=1e-8)
+
+
+@pytest.mark.parametrize("R,k", [(1, 8), (3, 16)])
+def test_hip_replicated_matches_single_table(gpu, R, k):
+    """fm_repl_grad / fm_repl_apply with R replicas in one process (the all-reduce is a tensor
+    sum), against the single-table oracle step over the concatenated batches; the replicas
+    stay bitwise identical."""
+    from fm_spark_amd._native import CSRHost
+    from fm_spark_amd.distributed import HipReplEngine
+
+    F = 401
+    _, ids, w, V = make_problem(12, 1, F, k, 1)
+    engines = [HipReplEngine(F, k) for _ in range(R)]
+    for e in engines:
+        e.load_tables(ids, w, V)
+    model = R_.Model.empty(F, k)
+    model.load(ids, w, V)
+    for t in range(1, 4):
+        parts = [make_problem(300 * t + r, 90 + 11 * r, F, k, 7, hot=5)[0] for r in range(R)]
+        bs = [e.batch(CSRHost(p.row_ptr, p.col, p.val, p.label)) for e, p in zip(engines, parts)]
+        grads = [e.grad_phase(b).clone() for e, b in zip(engines, bs)]
+        total = grads[0]
+        for g in grads[1:]:
+            total = total + g
+        gm = sum(p.n_rows for p in parts)
+        for e in engines:
+            e.apply(total, t, 0.3, 1e-4, gm)
+        cat = _concat(parts)
+        ref = R_.sgd_step_fast(model, cat, t, 0.3, 1e-4)
+        # each engine's loss covers its own rows
+        assert sum(engines[r].last_stats()[0] for r in range(R)) == pytest.approx(ref.loss_sum, rel=1e-5)
+        assert engines[0].last_stats()[2] == len(np.unique(cat.col))
+    exports = [e.export_tables() for e in engines]
+    gi, gw, gV = exports[0]
+    np.testing.assert_array_equal(gi, np.nonzero(model.present)[0])
+    np.testing.assert_allclose(gw, model.w[gi], rtol=1e-5, atol=1e-8)
+    np.testing.assert_allclose(gV, model.V[gi], rtol=1e-5, atol=1e-8)
+    for oi, ow, oV in exports[1:]:
+        np.testing.assert_array_equal(oi, gi)
+        np.testing.assert_array_equal(ow, gw)
+        np.testing.assert_array_equal(oV, gV)
