@@ -72,6 +72,31 @@ def algorithmic_bytes(F, k, B, z, U):
     return fwd, upd
 
 
+# HIP kernels behind each timed phase (the "update" phase is the segmented update + its combine)
+PHASE_KERNELS = {"forward": ["k_forward"], "update": ["k_segment_update", "k_segment_combine"],
+                 "owner_forward": ["k_forward"], "owner_update": ["k_segment_update", "k_segment_combine"]}
+
+
+def pmc_traffic(F, k, B, phase):
+    """HBM bytes per launch of `phase` from the committed rocprofv3 PMC passes of this workload
+    (profiles/pmc_*.json, made by tools/pmc.sh + tools/pmc_to_json.py with the calibrated
+    FETCH_SIZE/WRITE_SIZE corrections).  None when no pass of this exact workload is committed."""
+    import glob
+
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json"))):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if (d.get("num_features"), d.get("k"), d.get("batch_rows")) != (F, k, B):
+            continue
+        ks = d.get("kernels", {})
+        names = PHASE_KERNELS.get(phase, [])
+        if names and all("traffic_bytes" in ks.get(n, {}) for n in names):
+            return sum(ks[n]["traffic_bytes"] for n in names), os.path.relpath(f, ROOT) + " (" + d.get("build", "") + ")"
+    return None, None
+
+
 def cpu_baseline(cfg, batch, steps):
     """The fp64 C restatement (oracle/fm_oracle.c, OpenMP) timed on this host's cores on a
     bounded sample of the same workload: `steps` mini-batch steps over the full table."""
@@ -244,8 +269,10 @@ def main():
             # sort / plan / grad / serve bytes are implementation overhead, reported as times
             dom = max((n for n in kern if n in algo), key=lambda n: kern[n]["avg_ms"])
             ach = algo[dom] / (kern[dom]["avg_ms"] * 1e-3) / 1e9
+            traffic, tsrc = pmc_traffic(F, k, B, dom)
             line["roofline"] = {"bound": "hbm", "kernel": dom, "achieved": ach, "peak": HBM_PEAK_GBS,
-                                "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "traffic": None}
+                                "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "traffic": traffic,
+                                "algorithmic_bytes": algo[dom], "traffic_source": tsrc}
             step_bytes = fwd_b + upd_b
             line["step_roofline"] = {"bytes_per_step": step_bytes,
                                      "achieved_GBs": step_bytes / (ms_per_step * 1e-3) / 1e9,

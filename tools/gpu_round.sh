@@ -14,7 +14,7 @@ run() {  # name timeout cmd...
   tail -n 30 "gpurun_out/$name.log" >&2
   return $rc
 }
-run pytest_gpu 900 python -m pytest tests -m gpu -q -rf
+run pytest_gpu 900 python -u -m pytest tests -m gpu -q -rf --timeout 120 --timeout-method thread
 rc=$?; if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
 run bench 600 python bench.py --steps "$STEPS" --warmup 3 ${BENCH_ARGS:-} || exit $?
