@@ -95,9 +95,9 @@ void reserve_work(fm_ctx* ctx, int64_t B, int64_t N) {
   w.S.ensure(sizeof(float) * (size_t)std::max<int64_t>(B, 1) * ctx->kp);
   w.yl.ensure(sizeof(float) * 2 * (size_t)std::max<int64_t>(B, 1));
   w.sort.ensure(std::max<int64_t>(N, 1));
-  const int64_t nchunks = (N + 63) / 64;
-  w.part.ensure(sizeof(double) * (size_t)std::max<int64_t>(nchunks, 1) * 2 * (ctx->kp + 1));
-  w.ucnt.ensure(sizeof(uint32_t) * (size_t)std::max<int64_t>((nchunks + 3) / 4, 1));
+  const int64_t nranges = (N + 255) / 256;  // update waves (fm_kernels.hip, kWaveEnt)
+  w.part.ensure(sizeof(double) * (size_t)std::max<int64_t>(nranges, 1) * 2 * (ctx->kp + 2));
+  w.ucnt.ensure(sizeof(uint32_t) * (size_t)std::max<int64_t>((N + 1023) / 1024, 1));
   w.loss_part.ensure(sizeof(double) * 2 * 256 * 8);
 }
 

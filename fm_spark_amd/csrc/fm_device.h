@@ -21,6 +21,14 @@ __device__ __forceinline__ float4 shrink4(float4 v, double a) {
   return make_float4(shrink_f(v.x, a), shrink_f(v.y, a), shrink_f(v.z, a), shrink_f(v.w, a));
 }
 
+// fp32 soft-threshold, for the row catch-up and the update's final rounding: the operands are
+// fp32 values and fp32-rounded shrink amounts, the result differs from the fp64 form by at most
+// one rounding of the fp32 result.
+__device__ __forceinline__ float shrink1f(float z, float a) { return copysignf(fmaxf(fabsf(z) - a, 0.f), z); }
+__device__ __forceinline__ float4 shrink4f(float4 v, float a) {
+  return make_float4(shrink1f(v.x, a), shrink1f(v.y, a), shrink1f(v.z, a), shrink1f(v.w, a));
+}
+
 // Inclusive segmented scan over lanes [start_lane, lane] in a fixed tree order.  nsteps is the
 // wave-uniform depth the longest piece needs; the skipped steps would add nothing, so the
 // result is bitwise that of the full 6-step scan.

@@ -113,7 +113,7 @@ struct StepWork {
   DevBuf S;         // [B * kp] float: per-sample vfxiSum
   DevBuf yl;        // [B] float2 {yhat, y}
   DevBuf loss_part; // [n_fwd_blocks] double2 {loss, n_loss}
-  DevBuf part;      // [nchunks * 2 * (kp+1)] double partial gradients
+  DevBuf part;      // [ceil(N / 256) * 2 * (kp+2)] double partial gradients (one range per update wave)
   DevBuf ucnt;      // [n_update_blocks] uint32 distinct-id counts per block
   SortWork sort;
 };
@@ -133,12 +133,12 @@ struct StepParams {
 // partial_out != nullptr: the sharded owner's partial pass (rows [kp + 4] per pair, fm_shard.hip)
 void launch_forward(const TableView& T, const BatchDev& b, StepWork& w, const StepParams& p,
                     hipStream_t st, int64_t* n_fwd_blocks, float* partial_out = nullptr);
-// per-sample inputs of the segmented update: S rows of s_stride_q quads, {yhat, y} at yl[s * yl_stride]
+// per-sample inputs of the segmented update: S rows of s_stride floats, {yhat, y} at yl[s * yl_stride]
 struct SegSource {
   const float* S;
-  int s_stride_q;
+  int64_t s_stride;
   const float2* yl;
-  int yl_stride;
+  int64_t yl_stride;
 };
 // emit != nullptr (replicated mode): the per-slot gradient sums go to emit[rows][kp + 4] as
 // [sum g_V (kp) | sum g_w | 1 (touched) | 0] instead of being applied to the table

@@ -29,21 +29,28 @@
 
 #include "fm_device.h"
 
+
 namespace fmhip {
 
 namespace {
 
 constexpr int kBlock = 256;
-#ifndef FM_UPD_PF
-#define FM_UPD_PF 4
+constexpr int kWaveEnt = 256;  // sorted entries per update wave
+#ifndef FM_UPD_D
+#define FM_UPD_D 2
 #endif
-#ifndef FM_HDR_PAD
-#define FM_HDR_PAD 1
+constexpr int kUpdD = FM_UPD_D;  // entries whose rows a lane group loads ahead
+// experiment switches (tools/variants.sh; all 0 in the product build): drop the update's S-row
+// loads, row loads or row stores to measure what each costs
+#ifndef FM_ABL_NOS
+#define FM_ABL_NOS 0
 #endif
-#ifndef FM_UPD_CH
-#define FM_UPD_CH 4
+#ifndef FM_ABL_NOROW
+#define FM_ABL_NOROW 0
 #endif
-constexpr int kUpdateChunks = FM_UPD_CH;  // 64-entry chunks per update wave
+#ifndef FM_ABL_NOWR
+#define FM_ABL_NOWR 0
+#endif
 
 // The row header and one V quad brought current (absent rows read as zero).
 __device__ __forceinline__ void current_row(const RowHdr& h, float4& v, float& w, double cumE) {
@@ -187,239 +194,323 @@ struct SegArgs {
   const uint32_t* skeys;  // sorted feature slots
   const uint2* sents;     // their entries {sample, x bits}, same order
   int64_t N;
-  const float* S;   // per-sample rows of s_stride_q quads (vfxiSum first)
-  const float2* yl; // {yhat, y} of sample s at yl[s * yl_stride]
-  int s_stride_q;
-  int yl_stride;
-  double* part;     // [nranges][2][kp + 1]
-  int64_t nranges;  // ranges of L sorted entries, one wave each
-  int64_t L;        // entries per range (64 * CH)
+  const float* S;    // per-sample rows of s_stride floats (vfxiSum first)
+  const float2* yl;  // {yhat, y} of sample s at yl[s * yl_stride]
+  int64_t s_stride;
+  int64_t yl_stride;
+  double* part;      // [nranges][2][kp + 2] = [sum g_w | sum S*x*r (kp) | sum x*x*r]
+  int64_t nranges;   // ranges of L sorted entries (one update wave each)
+  int64_t L;         // entries per range (kWaveEnt)
   StepParams p;
   uint32_t* ucnt;  // [update blocks]
   float* emit;     // replicated mode: per-slot gradient sums [rows][kp + 4] instead of the update
 };
 
-// Per-entry scalars of the current chunk, staged in LDS for the G-lanes-per-entry phase.
-struct EntInfo {
-  uint32_t key;
-  int32_t s;
-  float x;
-  int32_t flags;  // valid | writes<<1 | complete<<2 | present<<3 | slot<<4 | start_lane<<8
-  double r;       // yhat - y
-  double ac;      // pending L1 of the row
+constexpr uint32_t kFValid = 1u, kFEnd = 2u, kFStart = 4u;
+
+// Lane-group geometry: Q lanes per entry, NF float4 column quads per lane (columns
+// 4 (q + Q n) .. + 3), NG = 64 / Q groups per wave, RL = 256 / NG entries per group.
+template <int Q, int NF>
+struct UpdGeom {
+  static constexpr int NG = 64 / Q;
+  static constexpr int RL = kWaveEnt / NG;
+  static constexpr int KP = 4 * Q * NF;   // widest kp served
+  static constexpr int PIECE = KP + 2;    // doubles per piece: [g_w | columns | b]
+  static constexpr int NGS = NG + 1;      // image row stride (entries): skewed against bank conflicts
+  static constexpr int IMG_N = RL * NGS;  // image slots
+  static constexpr int IMG = IMG_N * 36;  // {t, b} f64x2 | g_w f64 | {slot, flags} | sample
+  static constexpr int PIECES = 2 * NG * PIECE * 8;
+  static constexpr int BYTES = IMG > PIECES ? IMG : PIECES;
 };
 
-// One wave per range of CH consecutive chunks of 64 sorted entries (L = 64 * CH entries).
-//  Phase 1, one lane per entry: run structure (pieces of equal keys inside the chunk), the
-//    row header and the sample's (yhat, y); the linear gradient is scanned here.
-//  Phase 2, G lanes per entry (one float4 quad each), E = 64/G entries per round: S and V rows
-//    move as whole rows (16 rows per wave-instruction for k = 16); the loads of up to four
-//    rounds are in flight together, then the segmented scan (lane stride G, carries between
-//    rounds) and the write-back.
-//  Runs continue across the chunks of a range through register carries, so only runs crossing
-//    a range boundary leave fp64 partials (slot 0: the range's first piece when its run began
-//    before the range; slot 1: the last piece when its run continues past the range).  The
-//    next chunk's entries are loaded while the current chunk is processed.
-//  CH > 1 needs nq <= G (one quad-chunk), which the launcher guarantees.
-template <int G, int CH>
+// The interaction gradient of one entry (Model.scala:201-204, SGD.scala:146) is
+//   g_V[f] = (S[s][f] * x - (v[f] * x) * x) * r,   r = yhat - y,
+// so a feature's run sums to   A[f] - v[f] * b,   A[f] = sum_e S[s_e][f] * (x_e r_e),
+// b = sum_e x_e^2 r_e: neither sum needs the row, which is read once per run, with its header,
+// when the run closes.  g_w = x * yhat - y per entry (SGD.scala:145).
+//
+// One wave per 256 sorted entries.
+//  Phase 1, one lane per entry: run structure (ballots) and the entry's scalars
+//    t = x r, x^2 r and x yhat - y (fp64) from the sample's {yhat, y}, staged in the wave's LDS
+//    image (36 B per entry, step-major so that a step's entries are contiguous).
+//  Phase 2, NG lane groups of Q lanes (float4 column quads per lane): group g walks its RL
+//    consecutive entries in order, accumulating A, b and g_w in fp64 from the S rows of D
+//    entries loaded ahead (with the V row + header of those that close a run).  A run that
+//    begins and closes inside the group's entries is applied in place (update + L1,
+//    SGD.scala:150-181, or its gradient emitted in replicated mode).
+//  Phase 3: the pieces cut by group boundaries meet in LDS: the group holding a run's start
+//    extends its open piece through the following groups' head pieces and applies the run when
+//    it closes inside the wave; the wave's first piece (run begun in an earlier wave) and a run
+//    still open at the wave's end leave fp64 partials (slot 0 / slot 1), summed in wave order by
+//    k_segment_combine.  Every sum runs in a fixed order: the step is bitwise reproducible.
+template <int Q, int NF, int D0>
 __global__ __launch_bounds__(kBlock) void k_segment_update(SegArgs a) {
-  constexpr int E = 64 / G;           // entries per round
-  constexpr int PF = G < FM_UPD_PF ? G : FM_UPD_PF;  // rounds whose loads are issued together
-  __shared__ EntInfo info[kBlock / 64][64];
-  __shared__ float wnew_s[kBlock / 64][64];
+  using Geo = UpdGeom<Q, NF>;
+  constexpr int NG = Geo::NG, RL = Geo::RL, PIECE = Geo::PIECE, NP = kWaveEnt / 64, C = 4 * NF;
+  constexpr int D = D0 < RL ? D0 : RL;  // entries loaded ahead (divides RL)
+  __shared__ __align__(16) unsigned char smem_all[kBlock / 64][Geo::BYTES];
+  __shared__ int pflag_all[kBlock / 64][2 * NG];
   __shared__ uint32_t wcnt[kBlock / 64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  unsigned char* smem = smem_all[wave];
+  constexpr int NGS = Geo::NGS, IN = Geo::IMG_N;
+  double2* img_d = reinterpret_cast<double2*>(smem);            // {x r, x^2 r}
+  double* img_w = reinterpret_cast<double*>(smem + IN * 16);     // x yhat - y
+  uint2* img_k = reinterpret_cast<uint2*>(smem + IN * 24);       // {slot, flags}
+  int* img_s = reinterpret_cast<int*>(smem + IN * 32);           // sample
+  int* pflag = pflag_all[wave];
   const TableView& T = a.T;
-  const int kp = T.kp, nq = kp >> 2;
-#if FM_HDR_PAD
-  const int hq_end = (nq + 4) & ~3;  // end of the 64-B granule holding the header (in quads)
-#else
-  const int hq_end = nq + 1;
-#endif
-  const int64_t rg = (int64_t)blockIdx.x * (kBlock / 64) + wave;
-  const int64_t r0 = rg * a.L;
+  const int kp = T.kp;
+  const int64_t wid = (int64_t)blockIdx.x * (kBlock / 64) + wave;
+  const int64_t base = wid * kWaveEnt;
   const uint32_t kNone = 0xFFFFFFFFu;
-  const float4* __restrict__ S4 = reinterpret_cast<const float4*>(a.S);
-  EntInfo* inf = info[wave];
-  const int q_in = lane % G;  // this lane's quad inside a quad-chunk
-  const int j_in = lane / G;  // this lane's entry inside a round
-
   uint32_t ucount = 0;
-  double cw = 0.0;                                          // open piece's running w sum
-  double cv0 = 0.0, cv1 = 0.0, cv2 = 0.0, cv3 = 0.0;        // ... and V sums (this lane's quad)
-  bool open_started = false;  // the piece open at the previous chunk's end began in this range
-  uint32_t prev_last = (r0 > 0 && r0 < a.N) ? a.skeys[r0 - 1] : kNone;
-  int64_t pp = r0 + lane;
-  bool valid = r0 < a.N && pp < a.N;
-  uint32_t key = valid ? a.skeys[pp] : kNone;
-  uint2 en = valid ? a.sents[pp] : make_uint2(0u, 0u);
+  auto li = [](int e) { return (e % RL) * NGS + e / RL; };
 
-  for (int c = 0; c < CH; ++c) {
-    const int64_t p0 = r0 + (int64_t)c * 64;
-    if (p0 >= a.N) break;  // wave-uniform
-    // prefetch the next chunk of the range
-    const int64_t pn = p0 + 64 + lane;
-    const bool nvalid = (c + 1 < CH) && pn < a.N;
-    const uint32_t nkey = nvalid ? a.skeys[pn] : kNone;
-    const uint2 nen = nvalid ? a.sents[pn] : make_uint2(0u, 0u);
-
-    uint32_t prev_key = __shfl_up(key, 1);
-    uint32_t next_key = __shfl_down(key, 1);
-    if (lane == 0) prev_key = prev_last;
-    if (lane == 63) next_key = (p0 + 64 < a.N) ? a.skeys[p0 + 64] : kNone;
-    if (pp == a.N - 1) next_key = kNone;
-    const int s = (int)en.x;
-    const float xf = __uint_as_float(en.y);
-    const double x = (double)xf;
-    const RowHdr h = valid ? (*T.hdr(key)) : RowHdr{0.f, -1, 0.0};  // read before any write-back
-    const float2 yl = valid ? a.yl[(int64_t)s * a.yl_stride] : make_float2(0.f, 0.f);
-
-    const bool last_chunk = (c == CH - 1) || (p0 + 64 >= a.N);
-    const bool seg_start = valid && key != prev_key;  // a run of this key starts here
-    const bool seg_end = valid && key != next_key;     // ... ends here
-    const bool piece_head = valid && (lane == 0 || seg_start);
-    const bool writes = valid && (seg_end || (lane == 63 && last_chunk));
-    const uint64_t heads = __ballot(piece_head);
-    const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
-    const uint64_t hm = heads & upto;
-    const int start_lane = hm ? 63 - __clzll(hm) : 0;
-    const uint64_t starts = __ballot(seg_start);
-    ucount += (uint32_t)__popcll(starts);
-    // the lane-0 piece continues a piece of the previous chunk of this range
-    const bool cont = c > 0 && !(starts & 1ull);
-    const int dist = valid ? lane - start_lane : 0;
-    int nsteps = 0;
-    while (nsteps < 6 && __ballot(dist >= (1 << nsteps))) ++nsteps;
-    const bool head_is_start = ((starts >> start_lane) & 1ull) || (start_lane == 0 && cont && open_started);
-    const bool complete = head_is_start && seg_end;
-    const int slot = head_is_start ? 1 : 0;
-    const bool present = h.t >= 0;
-    const double ac = present ? a.p.cumE - h.cum : 0.0;  // pending L1 of this row
-    const double yhat = yl.x, y = yl.y;
-
-    // ---- linear term: g_w = deltaWi * pred - label (SGD.scala:145)
-    double gw = valid ? x * yhat - y : 0.0;
-    gw = seg_scan(gw, lane, start_lane, nsteps);
-    if (cont && start_lane == 0) gw += cw;
-    cw = __shfl(gw, 63);
-    if (writes) {
-      if (complete && a.emit) {  // [.. | sum g_w | touched]
-        *reinterpret_cast<float2*>(a.emit + (int64_t)key * (kp + 4) + kp) = make_float2((float)gw, 1.f);
-      } else if (complete) {  // the header is stored with the V row in phase 2
-        float w = present ? h.w : 0.f;
-        if (ac > 0.0) w = shrink_f(w, ac);
-        wnew_s[wave][lane] = upd_w(w, gw, a.p);  // SGD.scala:150, :171, :179
-      } else {
-        a.part[(rg * 2 + slot) * (int64_t)(kp + 1)] = gw;
-      }
+  if (base < a.N) {  // wave-uniform
+    // ---------------- phase 1: one lane per entry
+    uint32_t key[NP];
+    uint2 en[NP];
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+      const int64_t p = base + i * 64 + lane;
+      const bool v = p < a.N;
+      key[i] = v ? a.skeys[p] : kNone;
+      en[i] = v ? a.sents[p] : make_uint2(0u, 0u);
     }
-    open_started = __shfl((int)head_is_start, 63) != 0;
-    prev_last = __shfl(key, 63);
-
-    // ---- interaction term: g_V = (vfxiSum*x - (v*x)*x) * (pred - label) (Model.scala:201-204,
-    //      SGD.scala:146)
-    EntInfo me;
-    me.key = key;
-    me.s = s;
-    me.x = xf;
-    me.flags = (valid ? 1 : 0) | (writes ? 2 : 0) | (complete ? 4 : 0) | (present ? 8 : 0) | (slot << 4) |
-               (start_lane << 8);
-    me.r = yhat - y;
-    me.ac = ac;
+    const uint32_t before = base > 0 ? a.skeys[base - 1] : kNone;
+    const uint32_t after = base + kWaveEnt < a.N ? a.skeys[base + kWaveEnt] : kNone;
+    float2 yl[NP];
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+      const uint32_t up = __shfl_up(key[i], 1);
+      const uint32_t dn = __shfl_down(key[i], 1);
+      const uint32_t pl = i > 0 ? __shfl(key[i > 0 ? i - 1 : 0], 63) : before;
+      const uint32_t nf = i + 1 < NP ? __shfl(key[i + 1 < NP ? i + 1 : i], 0) : after;
+      const uint32_t prev = lane == 0 ? pl : up;
+      const uint32_t next = lane == 63 ? nf : dn;
+      const bool valid = key[i] != kNone;
+      const bool st = valid && key[i] != prev;
+      const bool end = valid && key[i] != next;
+      ucount += (uint32_t)__popcll(__ballot(st));
+      const int l = li(i * 64 + lane);
+      img_k[l] = make_uint2(key[i], (valid ? kFValid : 0u) | (end ? kFEnd : 0u) | (st ? kFStart : 0u));
+      img_s[l] = (int)en[i].x;
+      yl[i] = valid ? a.yl[(int64_t)en[i].x * a.yl_stride] : make_float2(0.f, 0.f);
+    }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    inf[lane] = me;
+    __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    for (int qc = 0; qc < nq; qc += G) {
-      const int q = qc + q_in;
-      const bool qok = q < nq;
-#pragma unroll 1
-      for (int rb = 0; rb < G; rb += PF) {
-        EntInfo ei[PF];
-        float4 sq[PF], v[PF];
+
+    // ---------------- phase 2: group g, lane q of the group
+    const int g = lane / Q, q = lane % Q;
+    float4 Sp[D][NF], Vp[D][NF], Hp[D];
+    auto prefetch = [&](int b0) {
 #pragma unroll
-        for (int u = 0; u < PF; ++u) ei[u] = inf[(rb + u) * E + j_in];
+      for (int u = 0; u < D; ++u) {
+        const int l = (b0 + u) * NGS + g;  // li(g * RL + b0 + u)
+        const uint2 kf = img_k[l];
+        const int s = img_s[l];
+        const bool valid = (kf.y & kFValid) != 0, end = (kf.y & kFEnd) != 0;
 #pragma unroll
-        for (int u = 0; u < PF; ++u) {
-          const bool vj = (ei[u].flags & 1) && qok;
-          sq[u] = vj ? S4[(int64_t)ei[u].s * a.s_stride_q + q] : make_float4(0.f, 0.f, 0.f, 0.f);
-          v[u] = (vj && (ei[u].flags & 8)) ? reinterpret_cast<const float4*>(T.v(ei[u].key))[q]
-                                           : make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int n = 0; n < NF; ++n) {
+          const int c = 4 * (q + Q * n);
+          const bool cv = valid && c < kp && !FM_ABL_NOS;
+          Sp[u][n] = cv ? *reinterpret_cast<const float4*>(a.S + (int64_t)s * a.s_stride + c)
+                        : make_float4(0.f, 0.f, 0.f, 0.f);
+          Vp[u][n] = (valid && c < kp && end && !FM_ABL_NOROW) ? *reinterpret_cast<const float4*>(T.v(kf.x) + c) : make_float4(0.f, 0.f, 0.f, 0.f);
         }
-#pragma unroll
-        for (int u = 0; u < PF; ++u) {
-          const int rd = rb + u;
-          const int j = rd * E + j_in;  // entry (lane of phase 1) this lane serves
-          const int fl = ei[u].flags;
-          const bool vj = (fl & 1) && qok;
-          const int sl = fl >> 8;
-          if (ei[u].ac > 0.0) v[u] = shrink4(v[u], ei[u].ac);
-          const double xd = ei[u].x, rj = ei[u].r;
-          double c0 = vj ? ((double)sq[u].x * xd - ((double)v[u].x * xd) * xd) * rj : 0.0;
-          double c1 = vj ? ((double)sq[u].y * xd - ((double)v[u].y * xd) * xd) * rj : 0.0;
-          double c2 = vj ? ((double)sq[u].z * xd - ((double)v[u].z * xd) * xd) * rj : 0.0;
-          double c3 = vj ? ((double)sq[u].w * xd - ((double)v[u].w * xd) * xd) * rj : 0.0;
-          // segmented scan over this round's entries (lane stride G), fixed tree order
-          const int lo = sl > rd * E ? sl : rd * E;  // first entry of the piece inside this round
-#pragma unroll
-          for (int o = 1; o < E; o <<= 1) {
-            if (o < (1 << nsteps)) {  // wave-uniform: skip steps no piece is long enough for
-              const double t0 = __shfl_up(c0, o * G), t1 = __shfl_up(c1, o * G);
-              const double t2 = __shfl_up(c2, o * G), t3 = __shfl_up(c3, o * G);
-              if (j - o >= lo) {
-                c0 += t0; c1 += t1; c2 += t2; c3 += t3;
-              }
-            }
-          }
-          // the piece started in an earlier round, or continues from the previous chunk
-          if (sl < rd * E || (rd == 0 && sl == 0 && cont)) {
-            c0 += cv0; c1 += cv1; c2 += cv2; c3 += cv3;
-          }
-          const int last = (E - 1) * G + q_in;  // the round's last entry, same quad
-          cv0 = __shfl(c0, last); cv1 = __shfl(c1, last);
-          cv2 = __shfl(c2, last); cv3 = __shfl(c3, last);
-          if ((fl & 1) && (fl & 2)) {
-            if ((fl & 4) && a.emit) {
-              if (qok)
-                reinterpret_cast<float4*>(a.emit + (int64_t)ei[u].key * (kp + 4))[q] =
-                    make_float4((float)c0, (float)c1, (float)c2, (float)c3);
-            } else if (fl & 4) {
-              float4* rec = reinterpret_cast<float4*>(T.v(ei[u].key));
-              if (qok)
-                rec[q] = make_float4(upd_v(v[u].x, c0, a.p), upd_v(v[u].y, c1, a.p), upd_v(v[u].z, c2, a.p),
-                                     upd_v(v[u].w, c3, a.p));
-              if (qc + G >= nq) {
-                // last quad-chunk: the header and the zero pad of its 64-B granule, stored by the
-                // same lanes so every granule of the record is written whole (see store_hdr)
-                for (int hq = nq + q_in; hq < hq_end; hq += G) {
-                  float4 hv = make_float4(0.f, 0.f, 0.f, 0.f);
-                  if (hq == nq) {
-                    RowHdr o;
-                    o.w = wnew_s[wave][j];
-                    o.t = a.p.epoch + 1;
-                    o.cum = a.p.cum_next;
-                    hv = *reinterpret_cast<const float4*>(&o);
-                  }
-                  rec[hq] = hv;
-                }
-              }
-            } else if (qok) {
-              double* prow = a.part + (((rg * 2 + ((fl >> 4) & 1)) * (int64_t)(kp + 1)) + 1 + 4 * q);
-              prow[0] = c0;
-              prow[1] = c1;
-              prow[2] = c2;
-              prow[3] = c3;
-            }
-          }
-        }
+        Hp[u] = (valid && end && !FM_ABL_NOROW) ? *reinterpret_cast<const float4*>(T.hdr(kf.x))
+                               : make_float4(0.f, __int_as_float(-1), 0.f, 0.f);
       }
+    };
+    prefetch(0);  // in flight together with phase 1's {yhat, y} reads
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+      const int l = li(i * 64 + lane);
+      const double xd = (double)__uint_as_float(en[i].y);
+      const double yh = (double)yl[i].x, yy = (double)yl[i].y;
+      const double rj = yh - yy;
+      img_d[l] = make_double2(xd * rj, (xd * xd) * rj);
+      img_w[l] = xd * yh - yy;  // g_w = deltaWi * pred - label (SGD.scala:145)
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    key = nkey;
-    en = nen;
-    pp += 64;
-    valid = nvalid;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+    // apply (or emit) a closed run: the row brought current (absent rows are all zero with
+    // cum = 0, so they need no case of their own), then SGD.scala:150-181
+    auto close_run = [&](uint32_t slot, const float4 (&vq)[NF], float4 hq, const double (&A)[C], double b, double gw) {
+      const RowHdr h = *reinterpret_cast<const RowHdr*>(&hq);
+      const float acf = (float)(a.p.cumE - h.cum);  // pending L1 of the row
+      const float lamf = (float)a.p.lam;
+      float* rec = T.v(slot);
+      if (FM_ABL_NOWR) return;
+#pragma unroll
+      for (int n = 0; n < NF; ++n) {
+        const int c = 4 * (q + Q * n);
+        if (c >= kp) continue;
+        const float4 v = shrink4f(vq[n], acf);
+        const double g0 = A[4 * n + 0] - (double)v.x * b, g1 = A[4 * n + 1] - (double)v.y * b;
+        const double g2 = A[4 * n + 2] - (double)v.z * b, g3 = A[4 * n + 3] - (double)v.w * b;
+        if (a.emit) {
+          *reinterpret_cast<float4*>(a.emit + (int64_t)slot * (kp + 4) + c) =
+              make_float4((float)g0, (float)g1, (float)g2, (float)g3);
+        } else {
+          // vec' = S_lambda(vec - sum * (eta / m))  (SGD.scala:153, :179)
+          const float4 u = make_float4((float)fma(g0, -a.p.scale_v, (double)v.x), (float)fma(g1, -a.p.scale_v, (double)v.y),
+                                       (float)fma(g2, -a.p.scale_v, (double)v.z), (float)fma(g3, -a.p.scale_v, (double)v.w));
+          *reinterpret_cast<float4*>(rec + c) = shrink4f(u, lamf);
+        }
+      }
+      if (a.emit) {
+        if (q == 0) *reinterpret_cast<float2*>(a.emit + (int64_t)slot * (kp + 4) + kp) = make_float2((float)gw, 1.f);
+        return;
+      }
+      // the header and the zero pad of its 64-B granule: the granule is written whole
+      const int span = 4 + ((16 - ((kp + 4) & 15)) & 15);
+      for (int i = 4 * q; i < span; i += 4 * Q) {
+        float4 hv = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (i == 0) {
+          RowHdr o;
+          o.w = upd_w(shrink1f(h.w, acf), gw, a.p);  // SGD.scala:150, :171
+          o.t = a.p.epoch + 1;
+          o.cum = a.p.cum_next;
+          hv = *reinterpret_cast<const float4*>(&o);
+        }
+        *reinterpret_cast<float4*>(rec + kp + i) = hv;
+      }
+    };
+
+    double acc[C], hacc[C];
+#pragma unroll
+    for (int j = 0; j < C; ++j) acc[j] = hacc[j] = 0.0;
+    double accb = 0.0, accw = 0.0, hb = 0.0, hw = 0.0;
+    int hst = 0;  // the group's head piece: 0 none, 1 open through the group's end, 2 closed
+    bool started = false, open = false;
+    uint32_t lastkey = kNone;
+#pragma unroll 1
+    for (int b0 = 0; b0 < RL; b0 += D) {
+      if (b0 > 0) prefetch(b0);
+#pragma unroll
+      for (int u = 0; u < D; ++u) {
+        const int l = (b0 + u) * NGS + g;
+        const uint2 kf = img_k[l];
+        if (!(kf.y & kFValid)) continue;
+        const double2 tb = img_d[l];
+        const double t = tb.x;
+        if (kf.y & kFStart) started = true;
+        open = true;
+        lastkey = kf.x;
+#pragma unroll
+        for (int n = 0; n < NF; ++n) {
+          acc[4 * n + 0] = fma((double)Sp[u][n].x, t, acc[4 * n + 0]);
+          acc[4 * n + 1] = fma((double)Sp[u][n].y, t, acc[4 * n + 1]);
+          acc[4 * n + 2] = fma((double)Sp[u][n].z, t, acc[4 * n + 2]);
+          acc[4 * n + 3] = fma((double)Sp[u][n].w, t, acc[4 * n + 3]);
+        }
+        accb += tb.y;
+        accw += img_w[l];
+        if (kf.y & kFEnd) {
+          if (started) {
+            close_run(kf.x, Vp[u], Hp[u], acc, accb, accw);
+          } else {  // the head piece closes
+#pragma unroll
+            for (int j = 0; j < C; ++j) hacc[j] = acc[j];
+            hb = accb;
+            hw = accw;
+            hst = 2;
+          }
+#pragma unroll
+          for (int j = 0; j < C; ++j) acc[j] = 0.0;
+          accb = 0.0;
+          accw = 0.0;
+          started = false;
+          open = false;
+        }
+      }
+    }
+    const bool tail = open && started;  // the open piece began in this group
+    if (open && !started) {             // the head piece runs through the group's end
+#pragma unroll
+      for (int j = 0; j < C; ++j) hacc[j] = acc[j];
+      hb = accb;
+      hw = accw;
+      hst = 1;
+    }
+
+    // ---------------- phase 3: pieces cut by group boundaries (the image is dead now)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    double* pc = reinterpret_cast<double*>(smem);
+    if (hst) {
+      double* ph = pc + (2 * g) * PIECE;
+#pragma unroll
+      for (int n = 0; n < NF; ++n)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) ph[1 + 4 * (q + Q * n) + j] = hacc[4 * n + j];
+      if (q == 0) {
+        ph[0] = hw;
+        ph[PIECE - 1] = hb;
+      }
+    }
+    if (q == 0) pflag[2 * g] = hst;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // extend a piece through the head pieces of groups g2 = from, from + 1, ...; true when it closes
+    auto extend = [&](double (&A)[C], double& b, double& gw, int from) -> bool {
+      for (int g2 = from; g2 < NG; ++g2) {
+        const int f2 = pflag[2 * g2];
+        if (f2 == 0) return false;  // unreachable: an open piece always continues into a head piece
+        const double* ph = pc + (2 * g2) * PIECE;
+#pragma unroll
+        for (int n = 0; n < NF; ++n)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) A[4 * n + j] += ph[1 + 4 * (q + Q * n) + j];
+        gw += ph[0];
+        b += ph[PIECE - 1];
+        if (f2 == 2) return true;
+      }
+      return false;
+    };
+    const int W = kp + 2;
+    auto write_part = [&](int slot, const double (&A)[C], double b, double gw) {
+      double* pr = a.part + (wid * 2 + slot) * (int64_t)W;
+#pragma unroll
+      for (int n = 0; n < NF; ++n) {
+        const int c = 4 * (q + Q * n);
+        if (c < kp) {
+          pr[1 + c + 0] = A[4 * n + 0];
+          pr[1 + c + 1] = A[4 * n + 1];
+          pr[1 + c + 2] = A[4 * n + 2];
+          pr[1 + c + 3] = A[4 * n + 3];
+        }
+      }
+      if (q == 0) {
+        pr[0] = gw;
+        pr[kp + 1] = b;
+      }
+    };
+    if (g == 0 && hst) {  // the wave's first piece: its run began in an earlier wave
+      if (hst == 1) extend(hacc, hb, hw, 1);
+      write_part(0, hacc, hb, hw);
+    }
+    if (tail) {
+      if (extend(acc, accb, accw, g + 1)) {
+        float4 vq[NF];
+#pragma unroll
+        for (int n = 0; n < NF; ++n) {
+          const int c = 4 * (q + Q * n);
+          vq[n] = c < kp ? *reinterpret_cast<const float4*>(T.v(lastkey) + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        const float4 hq = *reinterpret_cast<const float4*>(T.hdr(lastkey));
+        close_run(lastkey, vq, hq, acc, accb, accw);
+      } else {
+        write_part(1, acc, accb, accw);  // still open at the wave's end
+      }
+    }
   }
   if (lane == 0) wcnt[wave] = ucount;
   __syncthreads();
@@ -431,15 +522,59 @@ __global__ __launch_bounds__(kBlock) void k_segment_update(SegArgs a) {
   }
 }
 
-// Runs that cross range boundaries: the range holding the run's first entry owns it; one wave
-// per owner sums the following ranges' head partials in range order with lanes over the k+1
-// columns (a lane alone when the run ends in the next range).  Block 0 also closes the step with fixed-order reductions.
+// Runs that cross range boundaries: the range holding the run's first entry owns it and sums
+// the following ranges' head partials in range order (a lane alone when the run ends in the
+// next range, one wave per run with lanes over the factor columns otherwise), then applies the
+// same update as k_segment_update:  g_V[f] = sum S*x*r [f] - v[f] * sum x*x*r.  Block 0 also
+// closes the step with fixed-order reductions.
+// The row of `key` brought current, then columns [c_lo, c_hi) step c_step of the run's update
+// (sums[j] = sum S*x*r of column c_lo + j * c_step), then its header.
+struct RowCur {
+  bool present;
+  double ac;
+  float w;
+};
+__device__ __forceinline__ RowCur row_current(const SegArgs& a, uint32_t key) {
+  const RowHdr h = *a.T.hdr(key);
+  RowCur r;
+  r.present = h.t >= 0;
+  r.ac = r.present ? a.p.cumE - h.cum : 0.0;
+  r.w = r.present ? h.w : 0.f;
+  if (r.ac > 0.0) r.w = shrink_f(r.w, r.ac);
+  return r;
+}
+__device__ __forceinline__ void close_cols(const SegArgs& a, uint32_t key, const RowCur& rc, int c_lo, int c_hi,
+                                           int c_step, double b, const double* sums) {
+  const int kp = a.T.kp;
+  float* vrow = a.T.v(key);
+  float* gr = a.emit ? a.emit + (int64_t)key * (kp + 4) : nullptr;
+  for (int c = c_lo, j = 0; c < c_hi; c += c_step, ++j) {
+    float v = rc.present ? vrow[c] : 0.f;
+    if (rc.ac > 0.0) v = shrink_f(v, rc.ac);
+    const double gv = sums[j] - (double)v * b;
+    if (gr) gr[c] = (float)gv;
+    else vrow[c] = upd_v(v, gv, a.p);
+  }
+}
+__device__ __forceinline__ void close_hdr(const SegArgs& a, uint32_t key, const RowCur& rc, double gw) {
+  const int kp = a.T.kp;
+  if (a.emit) {
+    *reinterpret_cast<float2*>(a.emit + (int64_t)key * (kp + 4) + kp) = make_float2((float)gw, 1.f);
+  } else {
+    RowHdr o;
+    o.w = upd_w(rc.w, gw, a.p);
+    o.t = a.p.epoch + 1;
+    o.cum = a.p.cum_next;
+    store_hdr(a.T, key, o);
+  }
+}
+
 __global__ __launch_bounds__(kBlock) void k_segment_combine(SegArgs a, const double2* __restrict__ loss_part,
                                                             int64_t n_loss_blocks, int64_t n_ucnt,
                                                             double* __restrict__ stats_out) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int kp = a.T.kp;
-  const int64_t W = kp + 1;
+  const int64_t W = kp + 2;
   if (blockIdx.x == 0) {
     __shared__ double rl[kBlock], rc[kBlock], ru[kBlock];
     double l = 0.0, c = 0.0, u = 0.0;
@@ -466,7 +601,9 @@ __global__ __launch_bounds__(kBlock) void k_segment_combine(SegArgs a, const dou
       stats_out[2] = ru[0];
     }
   }
-  const int64_t chunk = (int64_t)blockIdx.x * kBlock + tid;  // range index
+  // 16 lanes per range (lane f: factor columns f, f + 16, ...)
+  const int64_t chunk = ((int64_t)blockIdx.x * kBlock + tid) / 16;  // range index
+  const int f = tid & 15;
   const int64_t L = a.L;
   bool owner = false;
   uint32_t key = 0;
@@ -475,56 +612,35 @@ __global__ __launch_bounds__(kBlock) void k_segment_combine(SegArgs a, const dou
     const int64_t p1 = p0 + L < a.N ? p0 + L : a.N;
     if (p1 < a.N) {
       key = a.skeys[p1 - 1];
-      // the chunk's last run continues into the next chunk and starts inside this chunk
+      // the range's last run continues into the next range and starts inside this range
       owner = a.skeys[p1] == key && !(a.skeys[p0] == key && p0 > 0 && a.skeys[p0 - 1] == key);
     }
   }
-  const TableView& T = a.T;
-  // common case: the run ends inside the next chunk -> this lane combines the two partials
+  // common case: the run ends inside the next range -> its two partials
   bool two = false;
   if (owner) {
     const int64_t c2 = chunk + 2;
     two = !(c2 < a.nranges && a.skeys[c2 * L] == key);
   }
-  if (owner && two && a.emit) {
+  if (owner && two) {
     const double* pt = a.part + (chunk * 2 + 1) * W;
     const double* ph = a.part + ((chunk + 1) * 2) * W;
-    float* gr = a.emit + (int64_t)key * (kp + 4);
-    for (int f = 0; f < kp; ++f) gr[f] = (float)(pt[1 + f] + ph[1 + f]);
-    *reinterpret_cast<float2*>(gr + kp) = make_float2((float)(pt[0] + ph[0]), 1.f);
-  } else if (owner && two) {
-    const double* pt = a.part + (chunk * 2 + 1) * W;
-    const double* ph = a.part + ((chunk + 1) * 2) * W;
-    const RowHdr h = *T.hdr(key);
-    const bool present = h.t >= 0;
-    const double ac = present ? a.p.cumE - h.cum : 0.0;
-    float w = present ? h.w : 0.f;
-    if (ac > 0.0) w = shrink_f(w, ac);
-    float* vrow = T.v(key);
-    for (int q = 0; q < (kp >> 2); ++q) {
-      float4 v = present ? reinterpret_cast<const float4*>(vrow)[q] : make_float4(0.f, 0.f, 0.f, 0.f);
-      if (ac > 0.0) v = shrink4(v, ac);
-      const double g0 = pt[1 + 4 * q + 0] + ph[1 + 4 * q + 0];
-      const double g1 = pt[1 + 4 * q + 1] + ph[1 + 4 * q + 1];
-      const double g2 = pt[1 + 4 * q + 2] + ph[1 + 4 * q + 2];
-      const double g3 = pt[1 + 4 * q + 3] + ph[1 + 4 * q + 3];
-      reinterpret_cast<float4*>(vrow)[q] =
-          make_float4(upd_v(v.x, g0, a.p), upd_v(v.y, g1, a.p), upd_v(v.z, g2, a.p), upd_v(v.w, g3, a.p));
+    const double b = pt[kp + 1] + ph[kp + 1];
+    const RowCur rc = row_current(a, key);
+    for (int c = f; c < kp; c += 16) {
+      const double sm = pt[1 + c] + ph[1 + c];
+      close_cols(a, key, rc, c, c + 1, 1, b, &sm);
     }
-    RowHdr o;
-    o.w = upd_w(w, pt[0] + ph[0], a.p);
-    o.t = a.p.epoch + 1;
-    o.cum = a.p.cum_next;
-    store_hdr(T, key, o);
+    if (f == 0) close_hdr(a, key, rc, pt[0] + ph[0]);
   }
-  // long runs (hot features): one wave per run, lanes over the k+1 columns, chunk order
-  uint64_t owners = __ballot(owner && !two);
+  // long runs (hot features): one wave per run, lanes over the factor columns, range order
+  uint64_t owners = __ballot(owner && !two && f == 0);
   while (owners) {
     const int l = __ffsll((unsigned long long)owners) - 1;
     owners &= owners - 1;
     const int64_t c0 = __shfl(chunk, l);
     const uint32_t k0 = __shfl(key, l);
-    // end of the run: first chunk after c0 whose first key differs
+    // end of the run: first range after c0 whose first key differs
     int64_t cend = c0 + 1;
     for (;;) {
       const int64_t c = cend + lane;
@@ -537,48 +653,33 @@ __global__ __launch_bounds__(kBlock) void k_segment_combine(SegArgs a, const dou
       cend += __ffsll((unsigned long long)~m) - 1;
       break;
     }
-    const RowHdr h = *T.hdr(k0);
-    const bool present = h.t >= 0;
-    const double ac = present ? a.p.cumE - h.cum : 0.0;
-    float wnew = 0.f;
-    for (int f0 = 0; f0 < W; f0 += 64) {
-      const int f = f0 + lane;
-      if (f < W) {
-        double g = a.part[(c0 * 2 + 1) * W + f];
-        int64_t c = c0 + 1;
-        for (; c + 4 <= cend; c += 4) {
-          const double g0 = a.part[((c + 0) * 2) * W + f];
-          const double g1 = a.part[((c + 1) * 2) * W + f];
-          const double g2 = a.part[((c + 2) * 2) * W + f];
-          const double g3 = a.part[((c + 3) * 2) * W + f];
-          g += g0;
-          g += g1;
-          g += g2;
-          g += g3;
-        }
-        for (; c < cend; ++c) g += a.part[(c * 2) * W + f];
-        if (a.emit) {
-          float* gr = a.emit + (int64_t)k0 * (kp + 4);
-          if (f == 0) *reinterpret_cast<float2*>(gr + kp) = make_float2((float)g, 1.f);
-          else gr[f - 1] = (float)g;
-        } else if (f == 0) {
-          float w = present ? h.w : 0.f;
-          if (ac > 0.0) w = shrink_f(w, ac);
-          wnew = upd_w(w, g, a.p);
-        } else {
-          float v = present ? T.v(k0)[f - 1] : 0.f;
-          if (ac > 0.0) v = shrink_f(v, ac);
-          T.v(k0)[f - 1] = upd_v(v, g, a.p);
-        }
+    // every lane sums the scalars (same addresses), lane j the columns j, j + 64, ...
+    double gw = a.part[(c0 * 2 + 1) * W], b = a.part[(c0 * 2 + 1) * W + kp + 1];
+    for (int64_t c = c0 + 1; c < cend; ++c) {
+      gw += a.part[(c * 2) * W];
+      b += a.part[(c * 2) * W + kp + 1];
+    }
+    double sums[4];  // kp <= 256
+    int j = 0;
+    for (int col = lane; col < kp; col += 64, ++j) {
+      double s = a.part[(c0 * 2 + 1) * W + 1 + col];
+      int64_t c = c0 + 1;
+      for (; c + 4 <= cend; c += 4) {
+        const double g0 = a.part[((c + 0) * 2) * W + 1 + col];
+        const double g1 = a.part[((c + 1) * 2) * W + 1 + col];
+        const double g2 = a.part[((c + 2) * 2) * W + 1 + col];
+        const double g3 = a.part[((c + 3) * 2) * W + 1 + col];
+        s += g0;
+        s += g1;
+        s += g2;
+        s += g3;
       }
+      for (; c < cend; ++c) s += a.part[(c * 2) * W + 1 + col];
+      sums[j] = s;
     }
-    if (lane == 0 && !a.emit) {
-      RowHdr o;
-      o.w = wnew;
-      o.t = a.p.epoch + 1;
-      o.cum = a.p.cum_next;
-      store_hdr(T, k0, o);
-    }
+    const RowCur rc = row_current(a, k0);
+    close_cols(a, k0, rc, lane, kp, 64, b, sums);
+    if (lane == 0) close_hdr(a, k0, rc, gw);
   }
 }
 
@@ -888,20 +989,18 @@ void launch_forward(const TableView& T, const BatchDev& b, StepWork& w, const St
 void launch_segment_update(const TableView& T, const BatchDev& b, StepWork& w, const StepParams& p,
                            const uint32_t* skeys, const uint2* sents, int64_t n_fwd_blocks,
                            double* stats_out, hipStream_t st, float* emit) {
-  SegSource src{w.S.as<float>(), T.kp / 4, w.yl.as<float2>(), 1};
+  SegSource src{w.S.as<float>(), T.kp, w.yl.as<float2>(), 1};
   launch_segment_update(T, b.nnz, src, w, p, skeys, sents, n_fwd_blocks, stats_out, st, emit);
 }
 
 void launch_segment_update(const TableView& T, int64_t N, const SegSource& src, StepWork& w, const StepParams& p,
                            const uint32_t* skeys, const uint2* sents, int64_t n_fwd_blocks, double* stats_out,
                            hipStream_t st, float* emit) {
-  const int nq = T.kp / 4;
-  const int G = nq <= 1 ? 1 : nq <= 2 ? 2 : nq <= 4 ? 4 : nq <= 8 ? 8 : 16;
-  const int CH = nq <= G ? kUpdateChunks : 1;  // carries across chunks need one quad-chunk
-  const int64_t L = 64 * (int64_t)CH;
+  const int64_t L = kWaveEnt;
   const int64_t nranges = (N + L - 1) / L;
-  w.part.ensure(sizeof(double) * (size_t)(nranges > 0 ? nranges : 1) * 2 * (T.kp + 1));
-  const int64_t ublocks = (nranges + (kBlock / 64) - 1) / (kBlock / 64);
+  w.part.ensure(sizeof(double) * (size_t)(nranges > 0 ? nranges : 1) * 2 * (T.kp + 2));
+  const int64_t per_block = (int64_t)kWaveEnt * (kBlock / 64);
+  const int64_t ublocks = (N + per_block - 1) / per_block;
   w.ucnt.ensure(sizeof(uint32_t) * (size_t)(ublocks > 0 ? ublocks : 1));
   SegArgs a;
   a.T = T;
@@ -910,7 +1009,7 @@ void launch_segment_update(const TableView& T, int64_t N, const SegSource& src, 
   a.N = N;
   a.S = src.S;
   a.yl = src.yl;
-  a.s_stride_q = src.s_stride_q;
+  a.s_stride = src.s_stride;
   a.yl_stride = src.yl_stride;
   a.part = w.part.as<double>();
   a.nranges = nranges;
@@ -918,27 +1017,22 @@ void launch_segment_update(const TableView& T, int64_t N, const SegSource& src, 
   a.p = p;
   a.ucnt = w.ucnt.as<uint32_t>();
   a.emit = emit;
-  if (nranges > 0) {
+  if (ublocks > 0) {
     const dim3 grid((unsigned)ublocks), blk(kBlock);
-    if (nq > G) {
-      hipLaunchKernelGGL((k_segment_update<16, 1>), grid, blk, 0, st, a);
-    } else if (G == 1) {
-      hipLaunchKernelGGL((k_segment_update<1, kUpdateChunks>), grid, blk, 0, st, a);
-    } else if (G == 2) {
-      hipLaunchKernelGGL((k_segment_update<2, kUpdateChunks>), grid, blk, 0, st, a);
-    } else if (G == 4) {
-      hipLaunchKernelGGL((k_segment_update<4, kUpdateChunks>), grid, blk, 0, st, a);
-    } else if (G == 8) {
-      hipLaunchKernelGGL((k_segment_update<8, kUpdateChunks>), grid, blk, 0, st, a);
-    } else {
-      hipLaunchKernelGGL((k_segment_update<16, kUpdateChunks>), grid, blk, 0, st, a);
-    }
+    const int nq = T.kp / 4;  // column quads
+    if (nq <= 1) hipLaunchKernelGGL((k_segment_update<1, 1, kUpdD>), grid, blk, 0, st, a);
+    else if (nq <= 2) hipLaunchKernelGGL((k_segment_update<2, 1, kUpdD>), grid, blk, 0, st, a);
+    else if (nq <= 4) hipLaunchKernelGGL((k_segment_update<4, 1, kUpdD>), grid, blk, 0, st, a);
+    else if (nq <= 8) hipLaunchKernelGGL((k_segment_update<8, 1, kUpdD>), grid, blk, 0, st, a);
+    else if (nq <= 16) hipLaunchKernelGGL((k_segment_update<16, 1, kUpdD>), grid, blk, 0, st, a);
+    else if (nq <= 32) hipLaunchKernelGGL((k_segment_update<16, 2, 2>), grid, blk, 0, st, a);
+    else hipLaunchKernelGGL((k_segment_update<16, 4, 1>), grid, blk, 0, st, a);
     FM_HIP_CHECK(hipGetLastError());
   }
-  int64_t cblocks = (nranges + kBlock - 1) / kBlock;
+  int64_t cblocks = (nranges * 16 + kBlock - 1) / kBlock;
   if (cblocks < 1) cblocks = 1;
   hipLaunchKernelGGL(k_segment_combine, dim3((unsigned)cblocks), dim3(kBlock), 0, st, a,
-                     w.loss_part.as<double2>(), n_fwd_blocks, nranges > 0 ? ublocks : (int64_t)0, stats_out);
+                     w.loss_part.as<double2>(), n_fwd_blocks, ublocks, stats_out);
   FM_HIP_CHECK(hipGetLastError());
 }
 

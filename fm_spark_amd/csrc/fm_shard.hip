@@ -538,7 +538,7 @@ int fm_shard_owner_update(fm_ctx* ctx, const void* s_recv, int32_t t, double ste
     e0 = ctx->prof_begin(st);
     const float* S = reinterpret_cast<const float*>(s_recv);
     const int W = ctx->kp + 4;
-    SegSource src{S, W / 4, reinterpret_cast<const float2*>(S + ctx->kp), W / 2};
+    SegSource src{S, W, reinterpret_cast<const float2*>(S + ctx->kp), W / 2};
     launch_segment_update(ctx->view(), n, src, ctx->work, p, skeys, sents, ctx->sh_loss_blocks, stats, st);
     ctx->prof_end("owner_update", e0, st);
     ctx->epoch += 1;

@@ -117,7 +117,7 @@ def test_loss_grad_matches_oracle(gpu):
     np.testing.assert_allclose(gdv, rdv, rtol=1e-5, atol=1e-9)
 
 
-@pytest.mark.parametrize("k", [1, 3, 4, 8, 10, 16, 32])
+@pytest.mark.parametrize("k", [1, 3, 4, 8, 10, 16, 32, 48, 72, 136])
 def test_step_parity_k(gpu, k):
     F = 97
     batches = []
@@ -142,7 +142,7 @@ def test_step_parity_l1(gpu, reg):
 
 
 def test_step_parity_hot_row(gpu):
-    """One id in ~90% of 5000 rows: its run crosses many 64-entry chunks (combine path)."""
+    """One id in ~90% of 5000 rows: its run crosses many 256-entry update waves (combine path)."""
     F, k = 2000, 16
     csr, ids, w, V = make_problem(11, 5000, F, k, 10, hot=17)
     model, g, losses = run_both([csr], F, k, ids, w, V, step_size=0.1, reg_param=1e-6)
