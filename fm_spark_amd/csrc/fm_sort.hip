@@ -27,7 +27,10 @@ namespace {
 
 constexpr int kBlock = 256;
 constexpr int kWaves = kBlock / 64;
-constexpr int kRounds = 16;
+#ifndef FM_SORT_ROUNDS
+#define FM_SORT_ROUNDS 16
+#endif
+constexpr int kRounds = FM_SORT_ROUNDS;  // keys per thread per tile
 constexpr int kTile = kBlock * kRounds;  // 4096 keys per tile
 constexpr int kMaxRadix = 1 << 10;
 

@@ -13,6 +13,11 @@
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s line %d\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)
 
+__global__ void k_gather_payload(const uint32_t* __restrict__ idx, const uint2* __restrict__ ent, uint2* __restrict__ out,
+                                 int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) out[i] = ent[idx[i]];
+}
+
 int main(int argc, char** argv) {
   const int64_t n = argc > 1 ? atoll(argv[1]) : 10223616;
   const int bits = argc > 2 ? atoi(argv[2]) : 27;
@@ -70,5 +75,63 @@ int main(int argc, char** argv) {
   int64_t bad = 0;
   for (int64_t i = 0; i < n; ++i) bad += (k1[i] != k2[i]) || (v1[i].x != v2[i].x) || (v1[i].y != v2[i].y);
   printf("mismatches vs rocprim (both stable): %lld\n", (long long)bad);
+  // rocPRIM keys-only sort of packed 64-bit words (key << 24 | entry index): one stream per pass
+  {
+    std::vector<uint64_t> pk(n);
+    for (int64_t i = 0; i < n; ++i) pk[i] = ((uint64_t)keys[i] << 24) | (uint64_t)i;
+    uint64_t *dp, *dp2;
+    CK(hipMalloc(&dp, 8 * n)); CK(hipMalloc(&dp2, 8 * n));
+    CK(hipMemcpy(dp, pk.data(), 8 * n, hipMemcpyHostToDevice));
+    size_t tmp2 = 0;
+    CK(rocprim::radix_sort_keys(nullptr, tmp2, dp, dp2, (size_t)n, 24, 24 + bits, st));
+    void* dtmp2;
+    CK(hipMalloc(&dtmp2, tmp2));
+    for (int w = 0; w < 3; ++w) CK(rocprim::radix_sort_keys(dtmp2, tmp2, dp, dp2, (size_t)n, 24, 24 + bits, st));
+    CK(hipEventRecord(a, st));
+    for (int r = 0; r < R; ++r) CK(rocprim::radix_sort_keys(dtmp2, tmp2, dp, dp2, (size_t)n, 24, 24 + bits, st));
+    CK(hipEventRecord(b, st));
+    CK(hipEventSynchronize(b));
+    CK(hipEventElapsedTime(&ms, a, b));
+    printf("rocprim radix_sort_keys uint64 (key<<24|index) bits 24..%d: %.3f ms\n", 24 + bits, ms / R);
+    // 16-byte pairs: 4-B key + 16-B payload would be one more stream; here 4-B keys only
+    CK(hipEventRecord(a, st));
+    size_t tmp3 = 0;
+    uint32_t* dk3;
+    CK(hipMalloc(&dk3, 4 * n));
+    CK(rocprim::radix_sort_keys(nullptr, tmp3, dk, dk3, (size_t)n, 0, bits, st));
+    void* dtmp3;
+    CK(hipMalloc(&dtmp3, tmp3));
+    for (int w = 0; w < 3; ++w) CK(rocprim::radix_sort_keys(dtmp3, tmp3, dk, dk3, (size_t)n, 0, bits, st));
+    CK(hipEventRecord(a, st));
+    for (int r = 0; r < R; ++r) CK(rocprim::radix_sort_keys(dtmp3, tmp3, dk, dk3, (size_t)n, 0, bits, st));
+    CK(hipEventRecord(b, st));
+    CK(hipEventSynchronize(b));
+    CK(hipEventElapsedTime(&ms, a, b));
+    printf("rocprim radix_sort_keys uint32 bits 0..%d: %.3f ms\n", bits, ms / R);
+  }
+  // (key, index) sort + payload gather
+  {
+    fmhip::SortWork sw2;
+    const uint32_t* ok2;
+    const uint32_t* oi2;
+    uint2* dg;
+    CK(hipMalloc(&dg, 8 * n));
+    auto run = [&] {
+      fmhip::radix_sort_pairs(sw2, dk, nullptr, n, bits, st, &ok2, &oi2);
+      hipLaunchKernelGGL(k_gather_payload, dim3(4096), dim3(256), 0, st, oi2, dv, dg, n);
+    };
+    for (int w = 0; w < 3; ++w) run();
+    CK(hipEventRecord(a, st));
+    for (int r = 0; r < R; ++r) run();
+    CK(hipEventRecord(b, st));
+    CK(hipEventSynchronize(b));
+    CK(hipEventElapsedTime(&ms, a, b));
+    printf("fm_hip radix_sort_pairs(key, index) + payload gather n=%lld: %.3f ms\n", (long long)n, ms / R);
+    std::vector<uint2> v3(n);
+    CK(hipMemcpy(v3.data(), dg, 8 * n, hipMemcpyDeviceToHost));
+    int64_t bad3 = 0;
+    for (int64_t i = 0; i < n; ++i) bad3 += (v1[i].x != v3[i].x) || (v1[i].y != v3[i].y);
+    printf("mismatches (index sort + gather vs rocprim): %lld\n", (long long)bad3);
+  }
   return 0;
 }
