@@ -96,10 +96,12 @@ SIGNATURES = {
     "fm_xorshift_hash_seed": (C.c_int64, [C.c_int64]),
     "fm_murmur3_bytes_hash": (C.c_int32, [C.POINTER(C.c_uint8), C.c_int64, C.c_int32]),
     "fm_xorshift_next_doubles": (C.c_int, [C.c_int64, C.c_int64, _DP]),
+    "fm_set_side_stream": (C.c_int, [_P, _P]),
     "fm_shard_route": (C.c_int, [_P, _P, _P, _P, _I64P]),
-    "fm_shard_owner_forward": (C.c_int, [_P, _P, _P, C.c_int64, _I64P, _I64P, _P]),
+    "fm_shard_owner_prepare": (C.c_int, [_P, _P, _P, _P, C.c_int64, _I64P, _I64P]),
+    "fm_shard_owner_forward": (C.c_int, [_P, _P, _P]),
     "fm_shard_combine": (C.c_int, [_P, _P, _P, _P]),
-    "fm_shard_owner_update": (C.c_int, [_P, _P, C.c_int32, C.c_double, C.c_double, C.c_int64]),
+    "fm_shard_owner_update": (C.c_int, [_P, _P, _P, C.c_int32, C.c_double, C.c_double, C.c_int64]),
     "fm_repl_grad": (C.c_int, [_P, _P, _P]),
     "fm_repl_apply": (C.c_int, [_P, _P, C.c_int32, C.c_double, C.c_double, C.c_int64]),
     "fm_last_stats": (C.c_int, [_P, _DP, _I64P, _I64P]),

@@ -205,7 +205,8 @@ int fm_create(const fm_config* cfg, fm_ctx** out) {
     c->rows = (cfg->num_features - cfg->shard_index + cfg->shard_count - 1) / cfg->shard_count;
     FM_HIP_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     c->own_stream = true;
-    FM_HIP_CHECK(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+    FM_HIP_CHECK(hipStreamCreateWithFlags(&c->side_own, hipStreamNonBlocking));
+    c->side = c->side_own;
     FM_HIP_CHECK(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
     FM_HIP_CHECK(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
     FM_HIP_CHECK(hipEventCreateWithFlags(&c->ev_upd_done, hipEventDisableTiming));
@@ -235,6 +236,14 @@ int fm_set_stream(fm_ctx* ctx, void* s) {
     // NULL selects the device's default (null) stream, which is what torch's default stream is
     ctx->stream = reinterpret_cast<hipStream_t>(s);
     ctx->own_stream = false;
+    return FM_OK;
+  });
+}
+
+int fm_set_side_stream(fm_ctx* ctx, void* s) {
+  return guarded(ctx, [&]() -> int {
+    FM_HIP_CHECK(hipStreamSynchronize(ctx->side));
+    ctx->side = s ? reinterpret_cast<hipStream_t>(s) : ctx->side_own;
     return FM_OK;
   });
 }

@@ -31,6 +31,41 @@ struct ProfEntry {
   int64_t n = 0;
 };
 
+// Per-batch state of the row-sharded step (fm_shard.hip).  Everything a sharded iteration
+// derives from the batch alone (the owner routing, the received entries' pair table and their
+// slot order) is produced ahead of the iteration on the side stream and kept here, so the next
+// batch's preparation overlaps the current iteration.
+struct ShardBatchState {
+  // requester: fm_shard_route -> fm_shard_combine
+  DevBuf pairidx;                  // [B][R] int32 pair index of (sample, owner), -1 if none
+  std::vector<int64_t> pairs_out;  // pairs sent to each owner
+  int64_t route_nnz = -1;
+  DevBuf poff;                     // [R+1] int64 owner blocks of the partial / S rows
+  int64_t loss_blocks = 0;
+  bool combined = false;
+  // owner: fm_shard_owner_prepare -> fm_shard_owner_forward -> fm_shard_owner_update
+  bool prepared = false;
+  const uint32_t* recv_slot = nullptr;  // caller's buffers, valid until owner_forward completes
+  const uint2* recv_ent = nullptr;
+  int64_t n = 0, P = 0;
+  Pinned pin_off;
+  DevBuf src_off;            // [R+1] int64 source offsets of the received entries
+  DevBuf pair_ptr;           // [P+1] int64 entry offsets of the pairs
+  DevBuf skeys, sents;       // received entries sorted by slot: slots / {pair, x bits}
+  hipEvent_t ready_fwd = nullptr;  // side stream: pair table done
+  hipEvent_t ready_upd = nullptr;  // side stream: slot sort done
+  hipEvent_t last_use = nullptr;   // main stream: the iteration's update has read everything
+  void release(int device) {
+    (void)hipSetDevice(device);
+    for (hipEvent_t e : {ready_fwd, ready_upd, last_use})
+      if (e) (void)hipEventSynchronize(e);
+    for (hipEvent_t e : {ready_fwd, ready_upd, last_use})
+      if (e) (void)hipEventDestroy(e);
+    ready_fwd = ready_upd = last_use = nullptr;
+    for (DevBuf* b : {&pairidx, &poff, &src_off, &pair_ptr, &skeys, &sents}) b->release();
+  }
+};
+
 }  // namespace fmhip
 
 using namespace fmhip;
@@ -45,8 +80,10 @@ struct fm_batch {
   hipEvent_t ready = nullptr;     // recorded on the side stream after the prepared sort
   hipEvent_t last_use = nullptr;  // recorded on the main stream after a step read skeys/sents
   bool prepared = false;
+  std::unique_ptr<ShardBatchState> sh;  // sharded contexts only
   ~fm_batch() {
     (void)hipSetDevice(device);
+    if (sh) sh->release(device);
     if (ready) (void)hipEventSynchronize(ready);
     if (last_use) (void)hipEventSynchronize(last_use);
     if (ready) (void)hipEventDestroy(ready);
@@ -68,6 +105,7 @@ struct fm_ctx {
   hipStream_t stream = nullptr;
   bool own_stream = false;
   hipStream_t side = nullptr;  // the entry sort runs here, overlapped with the forward
+  hipStream_t side_own = nullptr;  // the context's own side stream (fm_set_side_stream may replace side)
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   hipEvent_t ev_upd_done = nullptr;  // last main-stream read of the shared sort workspace
   DevBuf rec;  // [rows * stride] float records (V row + header)
@@ -78,34 +116,22 @@ struct fm_ctx {
   int64_t hist_cap = 0;
   StepWork work;
   Pinned pinned;
-  Pinned sh_pin_off, sh_pin_poff;  // host staging of the sharded phases' small H2D copies
   // profiling
   bool prof = false;
   std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> pending;
   std::vector<hipEvent_t> free_events;
   std::map<std::string, ProfEntry> prof_acc;
   std::vector<std::string> prof_order;
-  // sharded step state (fm_shard.hip)
-  //  requester (route / combine)
+  // sharded step scratch (fm_shard.hip): used only on the side stream by fm_shard_route and
+  // fm_shard_owner_prepare (the per-batch results live in fm_batch::sh)
   DevBuf sh_okey;      // [N] owner of each entry (partition sort keys)
   DevBuf sh_mask;      // [B] uint64 owners present in each sample
   DevBuf sh_tcnt;      // [R][tiles] pair counts -> exclusive offsets
   DevBuf sh_tot;       // [R] pairs per owner, then [R] entries per owner (uint64)
-  DevBuf sh_pairidx;   // [B][R] int32 pair index of (sample, owner), -1 if none
-  const fm_batch* sh_route_batch = nullptr;
-  int64_t sh_route_nnz = -1;
-  std::vector<int64_t> sh_pairs_out;  // pairs sent to each owner
-  int64_t sh_loss_blocks = 0;
-  bool sh_combined = false;
-  //  owner (owner_forward / owner_update)
-  const uint32_t* sh_recv_slot = nullptr;  // caller's buffer, valid until owner_update
-  int64_t sh_recv_n = -1;
-  int64_t sh_P = 0;                        // pairs received
-  DevBuf sh_src_off;   // [R+1] int64 source offsets of the received entries
   DevBuf sh_bsum;      // pair-head scan block sums (+ total)
-  DevBuf sh_pair_ptr;  // [P+1] int64 entry offsets of the pairs
-  DevBuf sh_ent2;      // [n] uint2 {pair, x bits}
-  DevBuf sh_skeys, sh_sents;  // sorted slots / {pair, x}
+  DevBuf sh_ent2;      // [n] uint2 {pair, x bits}: the slot sort's payload
+  SortWork side_sort;  // radix sort workspace of the side stream
+  Pinned side_pinned;  // route counts (device -> host)
   // replicated step state (fm_repl_*)
   DevBuf repl_cnt;            // touched-row counter (uint64)
   bool repl_pending = false;  // fm_repl_grad ran, fm_repl_apply not yet
@@ -195,14 +221,15 @@ struct fm_ctx {
     if (ev_fork) (void)hipEventDestroy(ev_fork);
     if (ev_join) (void)hipEventDestroy(ev_join);
     if (ev_upd_done) (void)hipEventDestroy(ev_upd_done);
-    if (side) (void)hipStreamDestroy(side);
+    if (side_own) (void)hipStreamSynchronize(side_own);
+    if (side_own) (void)hipStreamDestroy(side_own);
     rec.release();
     loss_hist.release();
     DevBuf* bufs[] = {&work.S, &work.yl, &work.loss_part, &work.part, &work.ucnt,
                       &work.sort.keys_a, &work.sort.keys_b, &work.sort.vals_a, &work.sort.vals_b,
-                      &work.sort.counts, &work.sort.digit_tot, &sh_okey, &sh_mask, &sh_tcnt, &sh_tot,
-                      &sh_pairidx, &sh_src_off, &sh_bsum, &sh_pair_ptr, &sh_ent2, &sh_skeys, &sh_sents,
-                      &repl_cnt};
+                      &work.sort.counts, &work.sort.digit_tot, &side_sort.keys_a, &side_sort.keys_b,
+                      &side_sort.vals_a, &side_sort.vals_b, &side_sort.counts, &side_sort.digit_tot,
+                      &sh_okey, &sh_mask, &sh_tcnt, &sh_tot, &sh_bsum, &sh_ent2, &repl_cnt};
     for (auto* b : bufs) b->release();
     if (own_stream && stream) (void)hipStreamDestroy(stream);
   }

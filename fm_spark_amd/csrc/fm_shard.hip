@@ -1,29 +1,32 @@
 // Row-sharded FM SGD step, owner-computes (one context per rank; the owner of feature id is
 // id % R, its local slot id / R).  Every rank holds 1/R of the table and steps its own
-// mini-batch; one iteration is four phases of the C-ABI joined by three all-to-alls:
+// mini-batch.  One iteration is five phases of the C-ABI joined by three all-to-alls; the
+// first two depend on the batch alone and run one iteration ahead on the side stream:
 //
 //   fm_shard_route          requester: the batch's entries partitioned by owner (CSR order kept)
 //                           as {slot} and {sample, x}; per sample the owners it touches and the
-//                           pair index of every (sample, owner) pair
+//                           pair index of every (sample, owner) pair                 [side]
 //   -- all-to-all entries -->
-//   fm_shard_owner_forward  owner: per received (source, sample) pair, the partial forward sums
-//                           over the entries it owns: [sum v*x | sum v^2 x^2 | sum w*x], lazy L1
-//                           caught up on read (FactorizationMachinesModel.scala:173-221)
+//   fm_shard_owner_prepare  owner: the received entries' pair table (pair = (source, sample))
+//                           and their stable order by slot (source rank, then CSR order) [side]
+//   fm_shard_owner_forward  owner: per received pair, the partial forward sums over the entries
+//                           it owns: [sum v*x | sum v^2 x^2 | sum w*x], lazy L1 caught up on read
+//                           (FactorizationMachinesModel.scala:173-221)                [main]
 //   -- all-to-all partials <--
 //   fm_shard_combine        requester: per sample, the owners' partials summed in owner order
 //                           (fp64) -> vfxiSum S, yhat, loss; S | yhat | y sent back per pair
 //   -- all-to-all S -->
-//   fm_shard_owner_update   owner: the received entries sorted by slot (stable: source rank
-//                           order, then CSR order) and the fused segmented gradient + update + L1
-//                           of fm_kernels.hip (SGD.scala:143-181) on its own rows
+//   fm_shard_owner_update   owner: the fused segmented gradient + update + L1 of fm_kernels.hip
+//                           (SGD.scala:143-181) over the slot-sorted entries, on its own rows
 //
 // Semantics equal the single-table step over the ranks' batches concatenated in rank order
 // (global miniBatchSize m = sum of the ranks' rows), up to fp summation order: the forward
 // sums are split per owner (fp32 on the wire), the per-feature gradient sums run over the
 // same entries in the same order.  Deterministic for a given R.
-// Traffic per rank and step (k = 16, z = 39, R = 8): entries 12 B each, partials and S rows
-// (kp + 4) * 4 B per (sample, owner) pair -- about 400 MB, against about 1 GB when rows and
-// gradients of every distinct id travel instead.
+// Traffic per rank and step (k = 16, z = 39, R = 8): entries 12 B each (off the critical path:
+// exchanged during the previous iteration), partials and S rows (kp + 4) * 4 B per
+// (sample, owner) pair -- about 400 MB, against about 1 GB when rows and gradients of every
+// distinct id travel instead.
 // Wire rows are kp + 4 floats: partial [sum vx (kp) | vv | wx | 0 0], S [S (kp) | yhat | y | 0 0].
 #include <algorithm>
 #include <cmath>
@@ -318,6 +321,18 @@ inline int team_for(int nq) {
   return G;
 }
 
+// owner blocks of the partial / S rows: poff[o] = pairs sent to owners before o
+__global__ void k_owner_offsets(const unsigned long long* __restrict__ pairs, int R, int64_t* __restrict__ poff) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    int64_t acc = 0;
+    for (int o = 0; o < R; ++o) {
+      poff[o] = acc;
+      acc += (int64_t)pairs[o];
+    }
+    poff[R] = acc;
+  }
+}
+
 }  // namespace
 
 }  // namespace fmhip
@@ -341,25 +356,46 @@ StepParams shard_params(fm_ctx* ctx, int32_t t, double step_size, double reg_par
   return p;
 }
 
+// The batch's sharded state, created on first use with its events already "done".
+ShardBatchState& shard_state(fm_ctx* ctx, fm_batch* b) {
+  FM_REQUIRE(b != nullptr && b->owner == ctx, "batch belongs to another context");
+  FM_REQUIRE(ctx->cfg.shard_count >= 1, "bad context");
+  if (!b->sh) {
+    std::unique_ptr<ShardBatchState> s(new ShardBatchState());
+    FM_HIP_CHECK(hipEventCreateWithFlags(&s->ready_fwd, hipEventDisableTiming));
+    FM_HIP_CHECK(hipEventCreateWithFlags(&s->ready_upd, hipEventDisableTiming));
+    FM_HIP_CHECK(hipEventCreateWithFlags(&s->last_use, hipEventDisableTiming));
+    FM_HIP_CHECK(hipEventRecord(s->ready_fwd, ctx->side));
+    FM_HIP_CHECK(hipEventRecord(s->ready_upd, ctx->side));
+    FM_HIP_CHECK(hipEventRecord(s->last_use, ctx->stream));
+    b->sh = std::move(s);
+  }
+  return *b->sh;
+}
+
 }  // namespace
 
 extern "C" {
 
 int fm_shard_route(fm_ctx* ctx, fm_batch* b, void* send_slot, void* send_ent, int64_t* counts) {
   return guarded(ctx, [&]() -> int {
-    FM_REQUIRE(b != nullptr && b->owner == ctx && counts != nullptr, "bad arguments");
+    FM_REQUIRE(counts != nullptr, "bad arguments");
+    ShardBatchState& S = shard_state(ctx, b);
     const int R = ctx->cfg.shard_count;
     FM_REQUIRE(R <= kMaxR, "the owner-computes sharded step supports at most 64 ranks");
     const int64_t B = b->dev.n_rows, N = b->dev.nnz;
     FM_REQUIRE(N == 0 || (send_slot && send_ent), "null send buffer");
-    hipStream_t st = ctx->stream;
+    hipStream_t st = ctx->side;
+    // the batch's previous iteration may still read its requester state on the main stream
+    FM_HIP_CHECK(hipStreamWaitEvent(st, S.last_use, 0));
     hipEvent_t e0 = ctx->prof_begin(st);
     const int64_t ntiles = std::max<int64_t>((B + kBlock - 1) / kBlock, 1);
     ctx->sh_okey.ensure(sizeof(uint32_t) * std::max<int64_t>(N, 4) + 16);
     ctx->sh_mask.ensure(sizeof(uint64_t) * std::max<int64_t>(B, 1));
     ctx->sh_tcnt.ensure(sizeof(uint32_t) * R * ntiles);
     ctx->sh_tot.ensure(sizeof(unsigned long long) * 2 * R);
-    ctx->sh_pairidx.ensure(sizeof(int32_t) * std::max<int64_t>(B, 1) * R);
+    S.pairidx.ensure(sizeof(int32_t) * std::max<int64_t>(B, 1) * R);
+    S.poff.ensure(sizeof(int64_t) * (R + 1));
     unsigned long long* tot = ctx->sh_tot.as<unsigned long long>();  // [R] pairs, [R] entries
     FM_HIP_CHECK(hipMemsetAsync(tot, 0, sizeof(unsigned long long) * 2 * R, st));
     if (B > 0) {
@@ -370,124 +406,153 @@ int fm_shard_route(fm_ctx* ctx, fm_batch* b, void* send_slot, void* send_ent, in
       hipLaunchKernelGGL(k_rows_scan, dim3((unsigned)R), dim3(kBlock), 0, st, ctx->sh_tcnt.as<uint32_t>(), ntiles,
                          tot);
       hipLaunchKernelGGL(k_pair_index, dim3((unsigned)ntiles), dim3(kBlock), 0, st, ctx->sh_mask.as<uint64_t>(), B,
-                         R, ntiles, ctx->sh_tcnt.as<uint32_t>(), ctx->sh_pairidx.as<int32_t>());
+                         R, ntiles, ctx->sh_tcnt.as<uint32_t>(), S.pairidx.as<int32_t>());
     }
+    hipLaunchKernelGGL(k_owner_offsets, dim3(1), dim3(64), 0, st, tot, R, S.poff.as<int64_t>());
     if (N > 0) {
       hipLaunchKernelGGL(k_owner_keys, dim3(blocks_for(N)), dim3(kBlock), 0, st, b->dev.col.as<uint32_t>(), N,
                          (uint32_t)R, ctx->sh_okey.as<uint32_t>());
       const uint32_t *sk = nullptr, *si = nullptr;
-      radix_sort_pairs(ctx->work.sort, ctx->sh_okey.as<uint32_t>(), nullptr, N, bits_for(R - 1), st, &sk, &si);
+      radix_sort_pairs(ctx->side_sort, ctx->sh_okey.as<uint32_t>(), nullptr, N, bits_for(R - 1), st, &sk, &si);
       hipLaunchKernelGGL(k_route_pack, dim3(blocks_for(N)), dim3(kBlock), 0, st, si, N, b->dev.col.as<uint32_t>(),
                          b->dev.ent.as<uint2>(), (uint32_t)R, reinterpret_cast<uint32_t*>(send_slot),
                          reinterpret_cast<uint2*>(send_ent));
     }
     FM_HIP_CHECK(hipGetLastError());
     ctx->prof_end("route", e0, st);
-    ctx->pinned.ensure(sizeof(unsigned long long) * 2 * R);
-    FM_HIP_CHECK(hipMemcpyAsync(ctx->pinned.p, tot, sizeof(unsigned long long) * 2 * R, hipMemcpyDeviceToHost, st));
-    FM_HIP_CHECK(hipStreamSynchronize(st));
-    const unsigned long long* hc = reinterpret_cast<const unsigned long long*>(ctx->pinned.p);
-    ctx->sh_pairs_out.assign(R, 0);
+    ctx->side_pinned.ensure(sizeof(unsigned long long) * 2 * R);
+    FM_HIP_CHECK(hipMemcpyAsync(ctx->side_pinned.p, tot, sizeof(unsigned long long) * 2 * R, hipMemcpyDeviceToHost, st));
+    FM_HIP_CHECK(hipStreamSynchronize(st));  // the side stream only: the main stream keeps running
+    const unsigned long long* hc = reinterpret_cast<const unsigned long long*>(ctx->side_pinned.p);
+    S.pairs_out.assign(R, 0);
     int64_t ne = 0;
     for (int o = 0; o < R; ++o) {
       counts[o] = (int64_t)hc[R + o];      // entries to owner o
       counts[R + o] = (int64_t)hc[o];      // (sample, owner) pairs to owner o
-      ctx->sh_pairs_out[o] = (int64_t)hc[o];
+      S.pairs_out[o] = (int64_t)hc[o];
       ne += (int64_t)hc[R + o];
     }
     FM_REQUIRE(ne == N, "route: inconsistent entry count");
-    ctx->sh_route_batch = b;
-    ctx->sh_route_nnz = N;
-    ctx->sh_combined = false;
+    S.route_nnz = N;
+    S.combined = false;
     return FM_OK;
   });
 }
 
-int fm_shard_owner_forward(fm_ctx* ctx, const void* recv_slot, const void* recv_ent, int64_t n,
-                           const int64_t* src_entries, const int64_t* src_pairs, void* partials_out) {
+int fm_shard_owner_prepare(fm_ctx* ctx, fm_batch* b, const void* recv_slot, const void* recv_ent, int64_t n,
+                           const int64_t* src_entries, const int64_t* src_pairs) {
   return guarded(ctx, [&]() -> int {
+    ShardBatchState& S = shard_state(ctx, b);
     const int R = ctx->cfg.shard_count;
     FM_REQUIRE(n >= 0 && src_entries && src_pairs, "bad arguments");
     std::vector<int64_t> off(R + 1, 0);
     int64_t P = 0;
     for (int r = 0; r < R; ++r) {
       FM_REQUIRE(src_entries[r] >= 0 && src_pairs[r] >= 0 && src_pairs[r] <= src_entries[r], "bad source counts");
+      FM_REQUIRE(src_entries[r] == 0 || src_pairs[r] >= 1, "bad source counts");
       off[r + 1] = off[r] + src_entries[r];
       P += src_pairs[r];
     }
     FM_REQUIRE(off[R] == n, "source entry counts do not add up to n");
-    FM_REQUIRE(n == 0 || (recv_slot && recv_ent && partials_out), "null buffer");
-    hipStream_t st = ctx->stream;
+    FM_REQUIRE(n < (int64_t(1) << 32) - 1 && P < (int64_t(1) << 32) - 1, "too many received entries");
+    FM_REQUIRE(n == 0 || (recv_slot && recv_ent), "null buffer");
+    hipStream_t st = ctx->side;
+    FM_HIP_CHECK(hipStreamWaitEvent(st, S.last_use, 0));
+    // the staging of this batch's previous preparation has been consumed once its pair table was
+    FM_HIP_CHECK(hipEventSynchronize(S.ready_fwd));
     hipEvent_t e0 = ctx->prof_begin(st);
     const int64_t nb = std::max<int64_t>((n + kTileS - 1) / kTileS, 1);
-    ctx->sh_src_off.ensure(sizeof(int64_t) * (2 * R + 2));  // [R+1] source offsets, [R+1] owner offsets
-    ctx->sh_bsum.ensure(sizeof(uint32_t) * nb + sizeof(unsigned long long));
-    ctx->sh_pair_ptr.ensure(sizeof(int64_t) * (P + 1));
-    ctx->sh_ent2.ensure(sizeof(uint2) * std::max<int64_t>(n, 1));
-    // staging stays untouched until the next route synchronises the stream
-    ctx->sh_pin_off.ensure(sizeof(int64_t) * (R + 1));
-    std::memcpy(ctx->sh_pin_off.p, off.data(), sizeof(int64_t) * (R + 1));
-    FM_HIP_CHECK(hipMemcpyAsync(ctx->sh_src_off.p, ctx->sh_pin_off.p, sizeof(int64_t) * (R + 1), hipMemcpyHostToDevice, st));
-    int64_t* pair_ptr = ctx->sh_pair_ptr.as<int64_t>();
+    S.src_off.ensure(sizeof(int64_t) * (R + 1));
+    S.pair_ptr.ensure(sizeof(int64_t) * (P + 1));
+    S.pin_off.ensure(sizeof(int64_t) * (R + 1));
+    std::memcpy(S.pin_off.p, off.data(), sizeof(int64_t) * (R + 1));
+    FM_HIP_CHECK(hipMemcpyAsync(S.src_off.p, S.pin_off.p, sizeof(int64_t) * (R + 1), hipMemcpyHostToDevice, st));
+    int64_t* pair_ptr = S.pair_ptr.as<int64_t>();
     // the pair table closes with n (pair_ptr[P])
-    FM_HIP_CHECK(hipMemcpyAsync(pair_ptr + P, ctx->sh_src_off.as<int64_t>() + R, sizeof(int64_t),
-                                hipMemcpyDeviceToDevice, st));
+    FM_HIP_CHECK(hipMemcpyAsync(pair_ptr + P, S.src_off.as<int64_t>() + R, sizeof(int64_t), hipMemcpyDeviceToDevice, st));
     if (n > 0) {
+      ctx->sh_bsum.ensure(sizeof(uint32_t) * nb + sizeof(unsigned long long));
+      ctx->sh_ent2.ensure(sizeof(uint2) * n);
       const uint2* ent = reinterpret_cast<const uint2*>(recv_ent);
       uint32_t* bsum = ctx->sh_bsum.as<uint32_t>();
       auto* total = reinterpret_cast<unsigned long long*>(bsum + nb);
-      hipLaunchKernelGGL(k_heads_count, dim3((unsigned)nb), dim3(kBlock), 0, st, ent, n,
-                         ctx->sh_src_off.as<int64_t>(), R, bsum);
+      hipLaunchKernelGGL(k_heads_count, dim3((unsigned)nb), dim3(kBlock), 0, st, ent, n, S.src_off.as<int64_t>(), R,
+                         bsum);
       hipLaunchKernelGGL(k_rows_scan, dim3(1), dim3(kBlock), 0, st, bsum, nb, total);
-      hipLaunchKernelGGL(k_heads_apply, dim3((unsigned)nb), dim3(kBlock), 0, st, ent, n,
-                         ctx->sh_src_off.as<int64_t>(), R, bsum, pair_ptr, ctx->sh_ent2.as<uint2>());
+      hipLaunchKernelGGL(k_heads_apply, dim3((unsigned)nb), dim3(kBlock), 0, st, ent, n, S.src_off.as<int64_t>(), R,
+                         bsum, pair_ptr, ctx->sh_ent2.as<uint2>());
+      FM_HIP_CHECK(hipGetLastError());
+    }
+    FM_HIP_CHECK(hipEventRecord(S.ready_fwd, st));
+    if (n > 0) {
+      // the update's grouping: received entries sorted by slot (stable: source rank, then CSR order)
+      S.skeys.ensure(sizeof(uint32_t) * n);
+      S.sents.ensure(sizeof(uint2) * n);
+      const uint32_t* sk = nullptr;
+      const uint2* sv = nullptr;
+      radix_sort_pairs64(ctx->side_sort, reinterpret_cast<const uint32_t*>(recv_slot), ctx->sh_ent2.as<uint2>(), n,
+                         bits_for(std::max<int64_t>(ctx->rows - 1, 1)), st, &sk, &sv, S.skeys.as<uint32_t>(),
+                         S.sents.as<uint2>());
+    }
+    FM_HIP_CHECK(hipEventRecord(S.ready_upd, st));
+    ctx->prof_end("owner_prepare", e0, st);
+    S.recv_slot = reinterpret_cast<const uint32_t*>(recv_slot);
+    S.recv_ent = reinterpret_cast<const uint2*>(recv_ent);
+    S.n = n;
+    S.P = P;
+    S.prepared = true;
+    return FM_OK;
+  });
+}
+
+int fm_shard_owner_forward(fm_ctx* ctx, fm_batch* b, void* partials_out) {
+  return guarded(ctx, [&]() -> int {
+    ShardBatchState& S = shard_state(ctx, b);
+    FM_REQUIRE(S.prepared, "fm_shard_owner_prepare must run on this batch first");
+    FM_REQUIRE(S.P == 0 || partials_out, "null buffer");
+    hipStream_t st = ctx->stream;
+    FM_HIP_CHECK(hipStreamWaitEvent(st, S.ready_fwd, 0));
+    hipEvent_t e0 = ctx->prof_begin(st);
+    if (S.P > 0) {
       // partial forward over the pairs, rows of the local table (lazy L1 caught up on read)
       BatchDev view;
-      view.n_rows = P;
-      view.nnz = n;
-      view.row_ptr.p = pair_ptr;
-      view.col.p = const_cast<void*>(recv_slot);
-      view.ent.p = const_cast<void*>(recv_ent);
+      view.n_rows = S.P;
+      view.nnz = S.n;
+      view.row_ptr.p = S.pair_ptr.p;
+      view.col.p = const_cast<uint32_t*>(S.recv_slot);
+      view.ent.p = const_cast<uint2*>(S.recv_ent);
       StepParams p{};
       p.cumE = ctx->cum_host.back();
       int64_t nblk = 0;
-      if (P > 0) launch_forward(ctx->view(), view, ctx->work, p, st, &nblk, reinterpret_cast<float*>(partials_out));
+      launch_forward(ctx->view(), view, ctx->work, p, st, &nblk, reinterpret_cast<float*>(partials_out));
+      view.row_ptr.p = view.col.p = view.ent.p = nullptr;  // borrowed
       FM_HIP_CHECK(hipGetLastError());
     }
     ctx->prof_end("owner_forward", e0, st);
-    ctx->sh_recv_slot = reinterpret_cast<const uint32_t*>(recv_slot);
-    ctx->sh_recv_n = n;
-    ctx->sh_P = P;
     return FM_OK;
   });
 }
 
 int fm_shard_combine(fm_ctx* ctx, fm_batch* b, const void* partials_in, void* s_send) {
   return guarded(ctx, [&]() -> int {
-    FM_REQUIRE(b != nullptr && ctx->sh_route_batch == b && ctx->sh_route_nnz == b->dev.nnz,
+    ShardBatchState& S = shard_state(ctx, b);
+    FM_REQUIRE(S.route_nnz == b->dev.nnz && (int)S.pairs_out.size() == ctx->cfg.shard_count,
                "fm_shard_route must run on this batch first");
     const int R = ctx->cfg.shard_count;
     const int64_t B = b->dev.n_rows;
     int64_t Ps = 0;
-    for (int o = 0; o < R; ++o) Ps += ctx->sh_pairs_out[o];
+    for (int o = 0; o < R; ++o) Ps += S.pairs_out[o];
     FM_REQUIRE(Ps == 0 || (partials_in && s_send), "null buffer");
     hipStream_t st = ctx->stream;
     hipEvent_t e0 = ctx->prof_begin(st);
-    // owner blocks of the partial / S buffers
-    ctx->sh_src_off.ensure(sizeof(int64_t) * (2 * R + 2));
-    int64_t* poff_dev = ctx->sh_src_off.as<int64_t>() + (R + 1);
-    ctx->sh_pin_poff.ensure(sizeof(int64_t) * (R + 1));
-    int64_t* hp = reinterpret_cast<int64_t*>(ctx->sh_pin_poff.p);
-    hp[0] = 0;
-    for (int o = 0; o < R; ++o) hp[o + 1] = hp[o] + ctx->sh_pairs_out[o];
-    FM_HIP_CHECK(hipMemcpyAsync(poff_dev, hp, sizeof(int64_t) * (R + 1), hipMemcpyHostToDevice, st));
     const int nq = ctx->kp / 4;
     const int GS = team_for(nq);
     const int64_t tpb = kBlock / GS;
     int64_t blocks = std::max<int64_t>((B + tpb - 1) / tpb, 1);
     if (blocks > 256 * 8) blocks = 256 * 8;
     ctx->work.loss_part.ensure(sizeof(double) * 2 * 256 * 8);  // reserve_work's size: no reallocation later
-    const int32_t* pi = ctx->sh_pairidx.as<int32_t>();
+    const int32_t* pi = S.pairidx.as<int32_t>();
+    const int64_t* poff = S.poff.as<int64_t>();
     const float* pin = reinterpret_cast<const float*>(partials_in);
     float* so = reinterpret_cast<float*>(s_send);
     const float* lab = b->dev.label.as<float>();
@@ -496,57 +561,50 @@ int fm_shard_combine(fm_ctx* ctx, fm_batch* b, const void* partials_in, void* s_
     const int kp = ctx->kp;
     const dim3 grid((unsigned)blocks), blk(kBlock);
     switch (GS) {
-      case 1: hipLaunchKernelGGL(k_shard_combine<1>, grid, blk, 0, st, pi, poff_dev, R, B, pin, lab, kp, w0, so, lp); break;
-      case 2: hipLaunchKernelGGL(k_shard_combine<2>, grid, blk, 0, st, pi, poff_dev, R, B, pin, lab, kp, w0, so, lp); break;
-      case 4: hipLaunchKernelGGL(k_shard_combine<4>, grid, blk, 0, st, pi, poff_dev, R, B, pin, lab, kp, w0, so, lp); break;
-      case 8: hipLaunchKernelGGL(k_shard_combine<8>, grid, blk, 0, st, pi, poff_dev, R, B, pin, lab, kp, w0, so, lp); break;
-      default: hipLaunchKernelGGL(k_shard_combine<16>, grid, blk, 0, st, pi, poff_dev, R, B, pin, lab, kp, w0, so, lp); break;
+      case 1: hipLaunchKernelGGL(k_shard_combine<1>, grid, blk, 0, st, pi, poff, R, B, pin, lab, kp, w0, so, lp); break;
+      case 2: hipLaunchKernelGGL(k_shard_combine<2>, grid, blk, 0, st, pi, poff, R, B, pin, lab, kp, w0, so, lp); break;
+      case 4: hipLaunchKernelGGL(k_shard_combine<4>, grid, blk, 0, st, pi, poff, R, B, pin, lab, kp, w0, so, lp); break;
+      case 8: hipLaunchKernelGGL(k_shard_combine<8>, grid, blk, 0, st, pi, poff, R, B, pin, lab, kp, w0, so, lp); break;
+      default: hipLaunchKernelGGL(k_shard_combine<16>, grid, blk, 0, st, pi, poff, R, B, pin, lab, kp, w0, so, lp); break;
     }
     FM_HIP_CHECK(hipGetLastError());
     ctx->prof_end("combine", e0, st);
-    ctx->sh_loss_blocks = blocks;
-    ctx->sh_combined = true;
+    S.loss_blocks = blocks;
+    S.combined = true;
     return FM_OK;
   });
 }
 
-int fm_shard_owner_update(fm_ctx* ctx, const void* s_recv, int32_t t, double step_size, double reg_param,
-                          int64_t global_rows) {
+int fm_shard_owner_update(fm_ctx* ctx, fm_batch* b, const void* s_recv, int32_t t, double step_size,
+                          double reg_param, int64_t global_rows) {
   return guarded(ctx, [&]() -> int {
+    ShardBatchState& S = shard_state(ctx, b);
     FM_REQUIRE(global_rows >= 0, "negative global_rows");
     if (global_rows == 0) return FM_NOTHING_TO_DO;  // SGD.scala:126-128 (every rank skips)
     FM_REQUIRE(t >= 1, "iteration index t must be >= 1");
-    FM_REQUIRE(ctx->sh_recv_n >= 0 && ctx->sh_combined, "owner_forward and combine must run first");
-    const int64_t n = ctx->sh_recv_n;
-    FM_REQUIRE(n == 0 || s_recv != nullptr, "null buffer");
+    FM_REQUIRE(std::isfinite(step_size) && std::isfinite(reg_param), "non-finite step size / regParam");
+    FM_REQUIRE(S.prepared && S.combined, "owner_prepare, owner_forward and combine must run on this batch first");
+    const int64_t n = S.n;
+    FM_REQUIRE(S.P == 0 || s_recv != nullptr, "null buffer");
     hipStream_t st = ctx->stream;
     StepParams p = shard_params(ctx, t, step_size, reg_param, global_rows);
     ctx->ensure_hist(ctx->epoch + 1);
     double* stats = ctx->loss_hist.as<double>() + 3 * (int64_t)ctx->epoch;
+    FM_HIP_CHECK(hipStreamWaitEvent(st, S.ready_upd, 0));
     hipEvent_t e0 = ctx->prof_begin(st);
-    const uint32_t* skeys = nullptr;
-    const uint2* sents = nullptr;
-    if (n > 0) {
-      reserve_work(ctx, 1, n);
-      ctx->sh_skeys.ensure(sizeof(uint32_t) * n);
-      ctx->sh_sents.ensure(sizeof(uint2) * n);
-      radix_sort_pairs64(ctx->work.sort, ctx->sh_recv_slot, ctx->sh_ent2.as<uint2>(), n,
-                         bits_for(std::max<int64_t>(ctx->rows - 1, 1)), st, &skeys, &sents,
-                         ctx->sh_skeys.as<uint32_t>(), ctx->sh_sents.as<uint2>());
-    }
-    ctx->prof_end("owner_sort", e0, st);
-    e0 = ctx->prof_begin(st);
-    const float* S = reinterpret_cast<const float*>(s_recv);
+    const float* Srow = reinterpret_cast<const float*>(s_recv);
     const int W = ctx->kp + 4;
-    SegSource src{S, W, reinterpret_cast<const float2*>(S + ctx->kp), W / 2};
-    launch_segment_update(ctx->view(), n, src, ctx->work, p, skeys, sents, ctx->sh_loss_blocks, stats, st);
+    SegSource src{Srow, W, reinterpret_cast<const float2*>(Srow ? Srow + ctx->kp : nullptr), W / 2};
+    launch_segment_update(ctx->view(), n, src, ctx->work, p, S.skeys.as<uint32_t>(), S.sents.as<uint2>(),
+                          S.loss_blocks, stats, st);
     ctx->prof_end("owner_update", e0, st);
+    FM_HIP_CHECK(hipEventRecord(S.last_use, st));
     ctx->epoch += 1;
     ctx->cum_host.push_back(p.cum_next);
-    ctx->sh_recv_n = -1;
-    ctx->sh_recv_slot = nullptr;
-    ctx->sh_combined = false;
-    ctx->sh_route_batch = nullptr;
+    S.prepared = false;
+    S.combined = false;
+    S.recv_slot = nullptr;
+    S.recv_ent = nullptr;
     return FM_OK;
   });
 }

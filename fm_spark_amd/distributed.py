@@ -5,12 +5,17 @@ The reference shards its model implicitly: every join / groupBy on featureId shu
 exploded entries and the model Datasets by feature hash (SURVEY §2b, S1/S2/S5/S6:
 FactorizationMachinesModel.scala:155-164, FactorizationMachinesSGD.scala:148-166).  Here the
 table is row-sharded by ``owner = id % R`` (slot ``id // R``) across R ranks and the work
-moves to the rows instead of the rows to the work.  One SGD iteration is four phases of the
+moves to the rows instead of the rows to the work.  One SGD iteration is five phases of the
 C-ABI (include/fm_hip.h, fm_shard_*) joined by three all-to-alls:
 
-    route (requester: entries by owner) -> a2a entries -> owner_forward (partial sums per
-    (sample, owner) pair) -> a2a partials back -> combine (requester: S, yhat, loss) ->
-    a2a S to the owners -> owner_update (sort by slot, per-slot gradient sums, update + L1)
+    route (requester: entries by owner) -> a2a entries -> owner_prepare (pair table, slot
+    sort)  ||  owner_forward (partial sums per (sample, owner) pair) -> a2a partials back ->
+    combine (requester: S, yhat, loss) -> a2a S to the owners -> owner_update (per-slot
+    gradient sums, update + L1)
+
+The first two phases depend on the batch alone: ``ShardedTrainer.step(b, ..., prefetch=next)``
+issues them for the next batch right after the current iteration's update, on the side stream,
+so the next routing, entry exchange and slot sort overlap the current update.
 
 Every rank steps its own mini-batch; the iteration's miniBatchSize is the sum over ranks
 (weak scaling: the global batch grows with R).  The result equals one single-table step over
@@ -21,6 +26,7 @@ given R).  Only entries (12 B) and two kp + 4 float rows per (sample, owner) pai
 
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
 
 import numpy as np
@@ -41,12 +47,16 @@ class HipShardEngine:
         self.R = world
         self.ctx = FMContext(num_features, k, device=device, seed=seed, init_sd=init_sd, w0=w0, shard_index=rank,
                              shard_count=world)
-        # launch on torch's stream so the C-ABI kernels and the collectives are stream-ordered
-        self.ctx.set_stream(torch.cuda.current_stream(self.device).cuda_stream)
+        # launch on torch's streams so the C-ABI kernels and the collectives are stream-ordered:
+        # the iteration on the current stream, batch-only preparation on a side stream
+        self.main_stream = torch.cuda.current_stream(self.device)
+        self.side_stream = torch.cuda.Stream(self.device)
+        self.ctx.set_stream(self.main_stream.cuda_stream)
+        self._lib = N.load()
+        N.check(self._lib.fm_set_side_stream(self.ctx.handle, C.c_void_p(self.side_stream.cuda_stream)),
+                "fm_set_side_stream")
         self.kp = (k + 3) // 4 * 4
         self.width = self.kp + 4
-        self._lib = N.load()
-        self._keep = None
 
     def _empty(self, n, dtype):
         return self.torch.empty(max(int(n), 1), dtype=dtype, device=self.device)[: int(n)]
@@ -54,6 +64,10 @@ class HipShardEngine:
     @staticmethod
     def _ptr(t):
         return C.c_void_p(t.data_ptr() if t.numel() else 0)
+
+    def side(self):
+        """Context for the batch-only phases and their exchange (torch's current stream = side)."""
+        return self.torch.cuda.stream(self.side_stream)
 
     def batch(self, csr: N.CSRHost):
         return self.ctx.batch(csr)
@@ -68,14 +82,16 @@ class HipShardEngine:
                                          N.ptr(counts, C.c_int64)), "fm_shard_route")
         return send_slot, send_ent, counts
 
-    def owner_forward(self, recv_slot, recv_ent, src_entries, src_pairs):
+    def owner_prepare(self, b, recv_slot, recv_ent, src_entries, src_pairs):
         se = np.ascontiguousarray(src_entries, dtype=np.int64)
         sp = np.ascontiguousarray(src_pairs, dtype=np.int64)
-        out = self._empty(int(sp.sum()) * self.width, self.torch.float32)
-        self._keep = (recv_slot, recv_ent)  # read again by owner_update
-        N.check(self._lib.fm_shard_owner_forward(self.ctx.handle, self._ptr(recv_slot), self._ptr(recv_ent),
-                                                 int(recv_slot.numel()), N.ptr(se, C.c_int64),
-                                                 N.ptr(sp, C.c_int64), self._ptr(out)), "fm_shard_owner_forward")
+        N.check(self._lib.fm_shard_owner_prepare(self.ctx.handle, b.handle, self._ptr(recv_slot), self._ptr(recv_ent),
+                                                 int(recv_slot.numel()), N.ptr(se, C.c_int64), N.ptr(sp, C.c_int64)),
+                "fm_shard_owner_prepare")
+
+    def owner_forward(self, b, n_pairs_in: int):
+        out = self._empty(int(n_pairs_in) * self.width, self.torch.float32)
+        N.check(self._lib.fm_shard_owner_forward(self.ctx.handle, b.handle, self._ptr(out)), "fm_shard_owner_forward")
         return out
 
     def combine(self, b, partials_in, n_pairs_out: int):
@@ -84,11 +100,17 @@ class HipShardEngine:
                 "fm_shard_combine")
         return s_send
 
-    def owner_update(self, s_recv, t: int, step_size: float, reg_param: float, global_rows: int) -> int:
-        rc = N.check(self._lib.fm_shard_owner_update(self.ctx.handle, self._ptr(s_recv), int(t), float(step_size),
-                                                     float(reg_param), int(global_rows)), "fm_shard_owner_update")
-        self._keep = None
-        return rc
+    def owner_update(self, b, s_recv, t: int, step_size: float, reg_param: float, global_rows: int) -> int:
+        return N.check(self._lib.fm_shard_owner_update(self.ctx.handle, b.handle, self._ptr(s_recv), int(t),
+                                                       float(step_size), float(reg_param), int(global_rows)),
+                       "fm_shard_owner_update")
+
+    def retire(self, tensors):
+        """Tensors allocated on the side stream and read by the main stream: keep their memory
+        from being reused before the main stream's reads are done."""
+        for t in tensors:
+            if t.numel():
+                t.record_stream(self.main_stream)
 
     def last_stats(self):
         """(loss_sum, n_loss_rows) of this rank's samples, distinct ids this rank owns."""
@@ -104,6 +126,16 @@ class HipShardEngine:
 
     def export_tables(self):
         return self.ctx.export_tables()
+
+
+class _Plan:
+    """One batch's exchange plan: what the batch-only phases produced (counts per peer and the
+    received entries, which the owner phases read until the iteration's forward is done)."""
+
+    __slots__ = ("ent_in", "ent_out", "pair_in", "pair_out", "keep")
+
+    def __init__(self, ent_in, ent_out, pair_in, pair_out, keep):
+        self.ent_in, self.ent_out, self.pair_in, self.pair_out, self.keep = ent_in, ent_out, pair_in, pair_out, keep
 
 
 class ShardedTrainer:
@@ -123,6 +155,7 @@ class ShardedTrainer:
             num_features, k, rank, world, device=device, seed=seed, init_sd=init_sd, w0=w0)
         self.device = self.engine.device
         self._global_rows = {}
+        self._plans = {}
 
     # convenience passthroughs -------------------------------------------------------
     @property
@@ -158,35 +191,74 @@ class ShardedTrainer:
     def _empty(self, n, dtype):
         return self.torch.empty(max(int(n), 1), dtype=dtype, device=self.device)[: int(n)]
 
-    def step(self, b, t: int, step_size: float, reg_param: float, sync: bool = True) -> StepOut | None:
-        torch, R, W = self.torch, self.world, self.engine.width
+    def _side(self):
+        side = getattr(self.engine, "side", None)
+        return side() if side is not None else contextlib.nullcontext()
+
+    def prefetch(self, b) -> None:
+        """The batch-only phases of b's iteration (route, entry exchange, owner pair table and slot
+        sort), enqueued on the side stream.  Every rank must prefetch the same iterations in the
+        same order (the exchange is collective).  Idempotent until b's step consumes it."""
+        key = id(b)
+        if key in self._plans:
+            return
+        torch, R = self.torch, self.world
+        with self._side():
+            send_slot, send_ent, counts = self.engine.route(b)
+            ent_out, pair_out = counts[:R], counts[R:]
+            cnt = torch.tensor(np.stack([ent_out, pair_out], axis=1).reshape(-1), dtype=torch.int64,
+                               device=self.device)
+            rcnt = torch.empty_like(cnt)
+            self.dist.all_to_all_single(rcnt, cnt, group=self.group)
+            rc = rcnt.cpu().numpy().reshape(R, 2)
+            ent_in, pair_in = rc[:, 0], rc[:, 1]
+            recv_slot = self._empty(ent_in.sum(), torch.int32)
+            self._a2a(recv_slot, send_slot, ent_in, ent_out)
+            recv_ent = self._empty(2 * ent_in.sum(), torch.int32)
+            self._a2a(recv_ent, send_ent, 2 * ent_in, 2 * ent_out)
+            self.engine.owner_prepare(b, recv_slot, recv_ent, ent_in, pair_in)
+        self._plans[key] = _Plan(ent_in, ent_out, pair_in, pair_out, (recv_slot, recv_ent))
+
+    def step(self, b, t: int, step_size: float, reg_param: float, sync: bool = True, prefetch=None) -> StepOut | None:
+        """One iteration on this rank's batch b.  ``prefetch``: the batch of the next iteration,
+        whose batch-only phases are then enqueued behind this iteration's update (collective:
+        pass the same schedule on every rank)."""
+        W = self.engine.width
         gm = self.global_rows(b)
         if gm == 0:  # SGD.scala:126-128: every rank skips together
+            self._drop_plan(b)
+            if prefetch is not None:
+                self.prefetch(prefetch)
             return StepOut(0.0, 0, 0, 0, executed=False)
-        send_slot, send_ent, counts = self.engine.route(b)
-        ent_out, pair_out = counts[:R], counts[R:]
-        cnt = torch.tensor(np.stack([ent_out, pair_out], axis=1).reshape(-1), dtype=torch.int64, device=self.device)
-        rcnt = torch.empty_like(cnt)
-        self.dist.all_to_all_single(rcnt, cnt, group=self.group)
-        rc = rcnt.cpu().numpy().reshape(R, 2)
-        ent_in, pair_in = rc[:, 0], rc[:, 1]
-        recv_slot = self._empty(ent_in.sum(), torch.int32)
-        self._a2a(recv_slot, send_slot, ent_in, ent_out)
-        recv_ent = self._empty(2 * ent_in.sum(), torch.int32)
-        self._a2a(recv_ent, send_ent, 2 * ent_in, 2 * ent_out)
-        partials = self.engine.owner_forward(recv_slot, recv_ent, ent_in, pair_in)
-        part_in = self._empty(pair_out.sum() * W, torch.float32)
-        self._a2a(part_in, partials, pair_out * W, pair_in * W)
-        s_send = self.engine.combine(b, part_in, int(pair_out.sum()))
-        s_recv = self._empty(pair_in.sum() * W, torch.float32)
-        self._a2a(s_recv, s_send, pair_in * W, pair_out * W)
-        self.engine.owner_update(s_recv, t, step_size, reg_param, gm)
+        self.prefetch(b)  # no-op when an earlier step already did
+        plan = self._plans.pop(id(b))
+        partials = self.engine.owner_forward(b, int(plan.pair_in.sum()))
+        part_in = self._empty(plan.pair_out.sum() * W, self.torch.float32)
+        self._a2a(part_in, partials, plan.pair_out * W, plan.pair_in * W)
+        s_send = self.engine.combine(b, part_in, int(plan.pair_out.sum()))
+        s_recv = self._empty(plan.pair_in.sum() * W, self.torch.float32)
+        self._a2a(s_recv, s_send, plan.pair_in * W, plan.pair_out * W)
+        self.engine.owner_update(b, s_recv, t, step_size, reg_param, gm)
+        self._retire(plan)
+        if prefetch is not None:
+            self.prefetch(prefetch)
         if not sync:
             return None
         loss, nl, U = self.engine.last_stats()
-        tot = torch.tensor([loss, float(nl), float(U)], dtype=torch.float64, device=self.device)
+        tot = self.torch.tensor([loss, float(nl), float(U)], dtype=self.torch.float64, device=self.device)
         self.dist.all_reduce(tot, group=self.group)
         return StepOut(float(tot[0]), gm, int(tot[1]), int(tot[2]))
+
+    def _retire(self, plan):
+        retire = getattr(self.engine, "retire", None)
+        if retire is not None:
+            retire(plan.keep)
+        plan.keep = None
+
+    def _drop_plan(self, b):
+        plan = self._plans.pop(id(b), None)
+        if plan is not None:
+            self._retire(plan)
 
 
 # ------------------------------------------------------------------------------ replicated

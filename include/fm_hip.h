@@ -88,6 +88,10 @@ const char* fm_last_error(void);
 /* Launch on an externally owned HIP stream (hipStream_t passed as void*); NULL = the device's
  * default (null) stream.  A new context launches on a non-blocking stream of its own. */
 int fm_set_stream(fm_ctx* ctx, void* hip_stream);
+/* The context's side stream (hipStream_t as void*), on which batch-only work runs ahead of its
+ * step: fm_batch_prepare, fm_shard_route, fm_shard_owner_prepare.  NULL = the context's own
+ * non-blocking side stream (the default). */
+int fm_set_side_stream(fm_ctx* ctx, void* hip_stream);
 int fm_sync(fm_ctx* ctx);
 /* Pre-size the per-step workspace so no step allocates. */
 int fm_reserve(fm_ctx* ctx, int64_t max_rows, int64_t max_nnz);
@@ -199,25 +203,33 @@ int fm_xorshift_next_doubles(int64_t seed, int64_t n, double* out);
  * A "pair" is (sample of a source rank, owner holding some of its entries).  Wire rows are fp32,
  * kp + 4 floats per pair (kp = roundup(k, 4)):
  *   partial = [sum v*x (kp) | sum v^2 x^2 | sum w*x | 0 0]     S = [vfxiSum (kp) | yhat | y | 0 0]
+ * Every phase is keyed by `batch`, this rank's mini-batch of the iteration; its state lives with
+ * the batch.  Phases 1 and 1b depend on the batch alone and run on the side stream
+ * (fm_set_side_stream), so the next iteration's routing, entry exchange and slot sort overlap the
+ * current iteration; phases 2-4 run on the main stream and wait for them through events.
  * Phase 1 (requester): partition the batch's entries by owner, CSR order kept, into
  * send_slot (uint32 local slots, N) and send_ent ({sample, x bits}, N) -- device buffers of the
  * batch's nnz.  counts[0..R) = entries to each owner, counts[R..2R) = pairs to each owner.
- * Synchronises the context's stream. */
+ * Synchronises the side stream (not the main stream). */
 int fm_shard_route(fm_ctx* ctx, fm_batch* batch, void* send_slot, void* send_ent, int64_t* counts);
-/* Phase 2 (owner): the n received entries (source-rank major: src_entries[r] from rank r, which
- * sent src_pairs[r] pairs) -> partials_out[sum src_pairs] (source-major, sample order).  The
- * received buffers must stay valid until fm_shard_owner_update. */
-int fm_shard_owner_forward(fm_ctx* ctx, const void* recv_slot, const void* recv_ent, int64_t n,
-                           const int64_t* src_entries, const int64_t* src_pairs, void* partials_out);
+/* Phase 1b (owner): the n received entries (source-rank major: src_entries[r] from rank r, which
+ * sent src_pairs[r] pairs) -> their pair table and their order by slot (stable: source rank,
+ * then CSR order), kept with `batch`.  No host synchronisation.  recv_slot / recv_ent must stay
+ * valid until the main stream has run fm_shard_owner_forward of this batch. */
+int fm_shard_owner_prepare(fm_ctx* ctx, fm_batch* batch, const void* recv_slot, const void* recv_ent,
+                           int64_t n, const int64_t* src_entries, const int64_t* src_pairs);
+/* Phase 2 (owner): partials_out[sum src_pairs] (source-major, sample order): per received pair
+ * the partial forward sums over the entries this rank owns, lazy L1 caught up on read. */
+int fm_shard_owner_forward(fm_ctx* ctx, fm_batch* batch, void* partials_out);
 /* Phase 3 (requester): the partials received from the owners (owner-major, counts[R + o] rows
  * from owner o) -> per sample S, yhat and the loss; s_send gets the S rows in the same layout. */
 int fm_shard_combine(fm_ctx* ctx, fm_batch* batch, const void* partials_in, void* s_send);
-/* Phase 4 (owner): the S rows received for its pairs (same order as its partials) -> sort the
- * received entries by slot (source rank, then CSR order within a slot), per-slot gradient sums,
- * update + L1 with global miniBatchSize global_rows (the sum of every rank's rows).
- * Returns FM_NOTHING_TO_DO when global_rows == 0 (every rank skips, SGD.scala:126-128). */
-int fm_shard_owner_update(fm_ctx* ctx, const void* s_recv, int32_t t, double step_size, double reg_param,
-                          int64_t global_rows);
+/* Phase 4 (owner): the S rows received for its pairs (same order as its partials) -> per-slot
+ * gradient sums over the slot-sorted entries, update + L1 with global miniBatchSize global_rows
+ * (the sum of every rank's rows).  Returns FM_NOTHING_TO_DO when global_rows == 0 (every rank
+ * skips, SGD.scala:126-128). */
+int fm_shard_owner_update(fm_ctx* ctx, fm_batch* batch, const void* s_recv, int32_t t, double step_size,
+                          double reg_param, int64_t global_rows);
 
 /* ---- replicated multi-GPU step (small tables) --------------------------------------------
  * Every rank holds the whole table (shard_count = 1, same seed / same loaded tables) and steps

@@ -56,8 +56,8 @@ class NumpyShardEngine:
         has = np.zeros((csr.n_rows, self.R), dtype=bool)
         has[sample, owner] = True
         pairs = has.sum(axis=0)
-        self.pairidx = np.where(has, np.cumsum(has, axis=0) - 1, -1)  # [B][R]
-        self.pairs_out = pairs
+        b.pairidx = np.where(has, np.cumsum(has, axis=0) - 1, -1)  # [B][R]
+        b.pairs_out = pairs
         counts = np.concatenate([ents, pairs]).astype(np.int64)
         return torch.from_numpy(send_slot), torch.from_numpy(ent.view(np.int32).reshape(-1).copy()), counts
 
@@ -65,13 +65,13 @@ class NumpyShardEngine:
         csr = b.csr
         W, kp = self.width, self.kp
         part = partials_in.numpy().reshape(-1, W).astype(np.float64)
-        poff = np.concatenate([[0], np.cumsum(self.pairs_out)])
+        poff = np.concatenate([[0], np.cumsum(b.pairs_out)])
         B = csr.n_rows
         S = np.zeros((B, kp))
         vv = np.zeros(B)
         wx = np.zeros(B)
         for o in range(self.R):  # owner order
-            ix = self.pairidx[:, o]
+            ix = b.pairidx[:, o]
             m = ix >= 0
             rows = part[poff[o] + ix[m]]
             S[m] += rows[:, :kp]
@@ -80,10 +80,10 @@ class NumpyShardEngine:
         yhat = 0.5 * (np.sum(S * S, axis=1) - vv) + wx + self.w0
         has = np.diff(csr.row_ptr) > 0
         d = (yhat - csr.label)[has]
-        self.loss = (float(np.sum(d * d)), int(has.sum()))
+        b.loss = (float(np.sum(d * d)), int(has.sum()))
         out = np.zeros((int(n_pairs_out), W), dtype=np.float32)
         for o in range(self.R):
-            ix = self.pairidx[:, o]
+            ix = b.pairidx[:, o]
             m = ix >= 0
             out[poff[o] + ix[m], :kp] = S[m]
             out[poff[o] + ix[m], kp] = yhat[m]
@@ -91,7 +91,11 @@ class NumpyShardEngine:
         return torch.from_numpy(out.reshape(-1))
 
     # owner -----------------------------------------------------------------------
-    def owner_forward(self, recv_slot, recv_ent, src_entries, src_pairs):
+    def owner_prepare(self, b, recv_slot, recv_ent, src_entries, src_pairs):
+        b.recv_in = (recv_slot.clone(), recv_ent.clone(), np.asarray(src_entries), np.asarray(src_pairs))
+
+    def owner_forward(self, b, n_pairs_in):
+        recv_slot, recv_ent, src_entries, src_pairs = b.recv_in
         slots = recv_slot.numpy().astype(np.int64)
         ent = recv_ent.numpy().view(np.uint32).reshape(-1, 2)
         s, x = ent[:, 0].astype(np.int64), ent[:, 1].view(np.float32).astype(np.float64)
@@ -101,19 +105,19 @@ class NumpyShardEngine:
         head[1:] = (s[1:] != s[:-1]) | (src[1:] != src[:-1])
         pair = np.cumsum(head) - 1
         P = int(head.sum())
-        assert P == int(np.sum(src_pairs))
+        assert P == int(np.sum(src_pairs)) == n_pairs_in
         V, w = self.V[slots], self.w[slots]
         part = np.zeros((P, self.width))
         np.add.at(part[:, : self.k], pair, V * x[:, None])
         np.add.at(part[:, self.kp], pair, np.sum(V * V, axis=1) * x * x)
         np.add.at(part[:, self.kp + 1], pair, w * x)
-        self.recv = (slots, x, pair)
+        b.recv = (slots, x, pair)
         return torch.from_numpy(part.astype(np.float32).reshape(-1))
 
-    def owner_update(self, s_recv, t, step_size, reg_param, global_rows):
+    def owner_update(self, b, s_recv, t, step_size, reg_param, global_rows):
         if global_rows == 0:
             return 1
-        slots, x, pair = self.recv
+        slots, x, pair = b.recv
         Srow = s_recv.numpy().reshape(-1, self.width).astype(np.float64)
         S, yhat, y = Srow[pair, : self.k], Srow[pair, self.kp], Srow[pair, self.kp + 1]
         eta = step_size / math.sqrt(t)
@@ -134,7 +138,7 @@ class NumpyShardEngine:
         self.w[pres] = np.sign(w_new[pres]) * np.maximum(0.0, np.abs(w_new[pres]) - lam)
         self.V[pres] = np.sign(V_new[pres]) * np.maximum(0.0, np.abs(V_new[pres]) - lam)
         self.present = pres
-        self.stats = (self.loss[0], self.loss[1], len(touched))
+        self.stats = (b.loss[0], b.loss[1], len(touched))
         return 0
 
     def last_stats(self):

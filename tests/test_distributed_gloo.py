@@ -49,9 +49,12 @@ def _worker(rank, world, port, outdir, mode="sharded"):
             tr = ReplicatedTrainer(F, K, rank=rank, world=world, engine=NumpyReplEngine(F, K))
         tr.load_tables(ids, w, V)
         losses = []
+        bs = [tr.batch(_problem_for(rank, t)) for t in range(1, STEPS + 1)]
         for t in range(1, STEPS + 1):
-            b = tr.batch(_problem_for(rank, t))
-            o = tr.step(b, t, 0.4, 1e-3)
+            # sharded: from step 2 on, the next batch's route / entry exchange / owner preparation
+            # is prefetched behind the current update (the bench's schedule)
+            kw = {"prefetch": bs[t]} if mode == "sharded" and 2 <= t < STEPS else {}
+            o = tr.step(bs[t - 1], t, 0.4, 1e-3, **kw)
             losses.append(o.loss_sum)
         gi, gw, gV = tr.export_tables()
         np.savez(os.path.join(outdir, f"r{rank}.npz"), ids=gi, w=gw, V=gV, losses=np.array(losses))

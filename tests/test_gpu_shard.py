@@ -31,14 +31,20 @@ def _simulated_step(engines, batches, t, step_size, reg):
     routed = [e.route(b) for e, b in zip(engines, batches)]
     ent_cnt = [c[:R] for _, _, c in routed]   # [src][owner]
     pair_cnt = [c[R:] for _, _, c in routed]
-    partials = []
+    keep = []
+    torch.cuda.synchronize()  # the slicing below runs on the main stream, owner_prepare on the side streams
     for o in range(R):
         slots = torch.cat([torch.split(routed[r][0], ent_cnt[r].tolist())[o] for r in range(R)])
         ents = torch.cat([torch.split(routed[r][1], (2 * ent_cnt[r]).tolist())[o] for r in range(R)])
         src_e = np.array([ent_cnt[r][o] for r in range(R)])
         src_p = np.array([pair_cnt[r][o] for r in range(R)])
-        out = engines[o].owner_forward(slots, ents, src_e, src_p)
-        partials.append(torch.split(out, (src_p * W).tolist()))
+        engines[o].owner_prepare(batches[o], slots, ents, src_e, src_p)
+        keep.append((slots, ents, src_p))
+    torch.cuda.synchronize()  # route / prepare ran on the engines' side streams
+    partials = []
+    for o in range(R):
+        out = engines[o].owner_forward(batches[o], int(keep[o][2].sum()))
+        partials.append(torch.split(out, (keep[o][2] * W).tolist()))
     s_rows = []
     for r in range(R):
         pin = torch.cat([partials[o][r] for o in range(R)])
@@ -46,7 +52,7 @@ def _simulated_step(engines, batches, t, step_size, reg):
         s_rows.append(torch.split(s, (pair_cnt[r] * W).tolist()))
     gm = sum(int(b.n_rows) for b in batches)
     for o in range(R):
-        engines[o].owner_update(torch.cat([s_rows[r][o] for r in range(R)]), t, step_size, reg, gm)
+        engines[o].owner_update(batches[o], torch.cat([s_rows[r][o] for r in range(R)]), t, step_size, reg, gm)
     torch.cuda.synchronize()
     return sum(e.last_stats()[0] for e in engines), sum(e.last_stats()[2] for e in engines)
 
@@ -99,12 +105,15 @@ def test_sharded_trainer_world1_rccl(gpu):
         tr.load_tables(ids, w, V)
         model = R_.Model.empty(F, k)
         model.load(ids, w, V)
-        for t in range(1, 4):
-            p = make_problem(50 + t, 200, F, k, 8, hot=2)[0]
-            o = tr.step(tr.batch(CSRHost(p.row_ptr, p.col, p.val, p.label)), t, 0.2, 1e-5)
-            ref = R_.sgd_step_fast(model, p, t, 0.2, 1e-5)
+        probs = [make_problem(50 + t, 200, F, k, 8, hot=2)[0] for t in range(1, 6)]
+        bs = [tr.batch(CSRHost(p.row_ptr, p.col, p.val, p.label)) for p in probs]
+        # steps 1-2 plain, steps 3-5 with the next batch prefetched behind each update
+        for t in range(1, 6):
+            nxt = bs[t] if 3 <= t < 5 else None
+            o = tr.step(bs[t - 1], t, 0.2, 1e-5, prefetch=nxt)
+            ref = R_.sgd_step_fast(model, probs[t - 1], t, 0.2, 1e-5)
             assert o.loss_sum == pytest.approx(ref.loss_sum, rel=1e-5)
-            assert o.n_unique == len(np.unique(p.col))
+            assert o.n_unique == len(np.unique(probs[t - 1].col))
         gi, gw, gV = tr.export_tables()
         np.testing.assert_array_equal(gi, np.nonzero(model.present)[0])
         np.testing.assert_allclose(gw, model.w[gi], rtol=1e-5, atol=1e-8)
