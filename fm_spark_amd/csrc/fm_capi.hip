@@ -462,11 +462,47 @@ int fm_predict(fm_ctx* ctx, const fm_csr* csr, double lo, double hi, double* pre
     upload_batch(ctx, csr, b.get(), false);
     DevBuf dp;
     dp.ensure(sizeof(double) * csr->n_rows);
-    launch_predict(ctx->view(), b->dev, ctx->cum_host.back(), ctx->cfg.num_features, ctx->cfg.w0, lo, hi, dp.as<double>(),
-                   ctx->stream);
+    launch_predict(ctx->view(), b->dev, ctx->cum_host.back(), ctx->cfg.w0, lo, hi, dp.as<double>(), ctx->stream);
     FM_HIP_CHECK(hipMemcpyAsync(pred, dp.p, sizeof(double) * csr->n_rows, hipMemcpyDeviceToHost, ctx->stream));
     FM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
     dp.release();
+    return FM_OK;
+  });
+}
+
+int fm_predict_batch(fm_ctx* ctx, fm_batch* b, double lo, double hi, double* pred) {
+  return guarded(ctx, [&]() -> int {
+    FM_REQUIRE(b != nullptr && b->owner == ctx, "batch belongs to another context");
+    const int64_t B = b->dev.n_rows;
+    FM_REQUIRE(B == 0 || pred, "null argument");
+    if (B == 0) return FM_OK;
+    DevBuf dp;
+    dp.ensure(sizeof(double) * B);
+    hipEvent_t e0 = ctx->prof_begin(ctx->stream);
+    launch_predict(ctx->view(), b->dev, ctx->cum_host.back(), ctx->cfg.w0, lo, hi, dp.as<double>(), ctx->stream);
+    ctx->prof_end("predict", e0, ctx->stream);
+    FM_HIP_CHECK(hipMemcpyAsync(pred, dp.p, sizeof(double) * B, hipMemcpyDeviceToHost, ctx->stream));
+    FM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    dp.release();
+    return FM_OK;
+  });
+}
+
+int fm_init_from_batch(fm_ctx* ctx, fm_batch* b, int64_t* n_present) {
+  return guarded(ctx, [&]() -> int {
+    FM_REQUIRE(b != nullptr && b->owner == ctx, "batch belongs to another context");
+    launch_init_entries(ctx->view(), b->dev.col.as<uint32_t>(), b->dev.nnz, ctx->cfg.seed, ctx->cfg.init_sd, ctx->epoch,
+                        ctx->cum_host.back(), ctx->stream);
+    if (n_present) {
+      DevBuf d;
+      d.ensure(sizeof(int64_t));
+      launch_count_present(ctx->view(), d.as<int64_t>(), ctx->stream);
+      FM_HIP_CHECK(hipMemcpyAsync(n_present, d.p, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+      FM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+      d.release();
+    } else {
+      FM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    }
     return FM_OK;
   });
 }

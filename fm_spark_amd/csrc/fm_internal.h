@@ -130,9 +130,16 @@ struct StepParams {
   double w0;
 };
 
-// partial_out != nullptr: the sharded owner's partial pass (rows [kp + 4] per pair, fm_shard.hip)
+// predict mode of the forward: clamp bounds and the fp64 output per sample
+struct PredictOut {
+  double lo, hi;
+  double* pred;
+};
+// partial_out != nullptr: the sharded owner's partial pass (rows [kp + 4] per pair, fm_shard.hip);
+// pred != nullptr: FactorizationMachinesModel.predict (p.w0, p.cumE used)
 void launch_forward(const TableView& T, const BatchDev& b, StepWork& w, const StepParams& p,
-                    hipStream_t st, int64_t* n_fwd_blocks, float* partial_out = nullptr);
+                    hipStream_t st, int64_t* n_fwd_blocks, float* partial_out = nullptr,
+                    const PredictOut* pred = nullptr);
 // per-sample inputs of the segmented update: S rows of s_stride floats, {yhat, y} at yl[s * yl_stride]
 struct SegSource {
   const float* S;
@@ -159,8 +166,10 @@ void launch_load_rows(const TableView& T, const int32_t* ids, int64_t n, const d
                       const double* V, int32_t epoch, double cumE, hipStream_t st);
 void launch_flush(const TableView& T, int32_t epoch, double cumE, hipStream_t st);
 void launch_table_reset(const TableView& T, hipStream_t st);
-void launch_predict(const TableView& T, const BatchDev& b, double cumE, int64_t num_features,
-                    double w0, double lo, double hi, double* pred, hipStream_t st);
+void launch_predict(const TableView& T, const BatchDev& b, double cumE, double w0, double lo, double hi,
+                    double* pred, hipStream_t st);
+void launch_init_entries(const TableView& T, const uint32_t* col, int64_t n, uint64_t seed, double sd,
+                         int32_t epoch, double cumE, hipStream_t st);
 void launch_loss_grad(const TableView& T, const BatchDev& b, double cumE, double w0, double* pred,
                       double* loss, double* dw, double* dv, int32_t* absent_flag, hipStream_t st);
 void launch_segment_sum(const uint32_t* skeys, const uint32_t* svals, int64_t n, const double* vecs,

@@ -68,16 +68,24 @@ __device__ __forceinline__ void current_row(const RowHdr& h, float4& v, float& w
 }
 
 // ------------------------------------------------------------------------ forward
-// PARTIAL: the sharded owner's pass (fm_shard.hip).  "Samples" are (source rank, sample)
+// MODE kTrain: the step's forward (S, {yhat, y}, loss partials).
+// MODE kPartial: the sharded owner's pass (fm_shard.hip).  "Samples" are (source rank, sample)
 // pairs of the entries this owner received; the output per pair is the partial row
 // [sum v*x (kp) | sum v^2 x^2 | sum w*x | 0 0] (fp32) instead of S / yhat / loss.
-template <int GS, int TEAM, bool PARTIAL>
+// MODE kPredict: FactorizationMachinesModel.predict (Model.scala:90-133): ids outside the table
+// or absent from the model are dropped (the inner joins, :103-112), a row left without a learned
+// feature scores globalBias unclamped (na.fill, :86), every other row
+// least(greatest(yhat, minLabel), maxLabel) (:129-132), fp64 into pred_out.
+constexpr int kTrain = 0, kPartial = 1, kPredict = 2;
+template <int GS, int TEAM, int MODE>
 __global__ __launch_bounds__(kBlock) void k_forward(TableView T, const int64_t* __restrict__ row_ptr,
                                                     const uint32_t* __restrict__ col,
                                                     const uint2* __restrict__ ent,
                                                     const float* __restrict__ label, int64_t B,
                                                     double w0, double cumE, float* __restrict__ S_out,
-                                                    float2* __restrict__ yl_out, double2* __restrict__ loss_part) {
+                                                    float2* __restrict__ yl_out, double2* __restrict__ loss_part,
+                                                    double lo, double hi, double* __restrict__ pred_out) {
+  constexpr bool PARTIAL = MODE == kPartial;
   constexpr int RPP = TEAM / GS;  // entries per pass
   constexpr int TPB = kBlock / TEAM;
   constexpr int U = 4;            // passes in flight
@@ -92,6 +100,7 @@ __global__ __launch_bounds__(kBlock) void k_forward(TableView T, const int64_t* 
   for (int64_t s = (int64_t)blockIdx.x * TPB + tid / TEAM; s < B; s += (int64_t)gridDim.x * TPB) {
     const int64_t e0 = row_ptr[s], e1 = row_ptr[s + 1];
     double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0, vv = 0.0, wx = 0.0;
+    uint32_t npres = 0;  // kPredict: learned entries of the sample (this lane's share)
     for (int64_t eb = e0 + rs; eb < e1; eb += U * RPP) {
       uint32_t id[U];
       float x[U];
@@ -101,6 +110,7 @@ __global__ __launch_bounds__(kBlock) void k_forward(TableView T, const int64_t* 
         const int64_t e = eb + j * RPP;
         ok[j] = e < e1;
         id[j] = ok[j] ? col[e] : 0u;
+        if (MODE == kPredict) ok[j] = ok[j] && id[j] < (uint64_t)T.rows;
         x[j] = ok[j] ? __uint_as_float(ent[e].y) : 0.f;
       }
       RowHdr h[U];
@@ -118,6 +128,7 @@ __global__ __launch_bounds__(kBlock) void k_forward(TableView T, const int64_t* 
 #pragma unroll
       for (int j = 0; j < U; ++j) {
         float w;
+        if (MODE == kPredict && g == 0 && h[j].t >= 0) ++npres;
         current_row(h[j], v[j], w, cumE);
         const double xd = x[j];
         // vfxi = v * x (Model.scala:179), VectorSum over the sample (:191)
@@ -140,6 +151,7 @@ __global__ __launch_bounds__(kBlock) void k_forward(TableView T, const int64_t* 
     for (int o = 1; o < TEAM; o <<= 1) {
       vv += __shfl_xor(vv, o);
       wx += __shfl_xor(wx, o);
+      if (MODE == kPredict) npres += __shfl_xor(npres, o);
     }
     if (PARTIAL) {
       const int W = kp + 4;
@@ -153,6 +165,10 @@ __global__ __launch_bounds__(kBlock) void k_forward(TableView T, const int64_t* 
     for (int o = 1; o < GS; o <<= 1) ss += __shfl_xor(ss, o);
     // sumVx + wixiSum + w0 (Model.scala:221, :260-262)
     const double yhat = 0.5 * (ss - vv) + wx + w0;
+    if (MODE == kPredict) {
+      if (tl == 0) pred_out[s] = npres == 0 ? w0 : fmin(fmax(yhat, lo), hi);
+      continue;
+    }
     if (rs == 0 && qok)
       *reinterpret_cast<float4*>(S_out + s * kp + g * 4) = make_float4((float)a0, (float)a1, (float)a2, (float)a3);
     if (tl == 0) {
@@ -165,7 +181,7 @@ __global__ __launch_bounds__(kBlock) void k_forward(TableView T, const int64_t* 
       }
     }
   }
-  if (PARTIAL) return;
+  if (MODE != kTrain) return;
   // deterministic block reduction of the loss partials
   __shared__ double red[2][kBlock / 64];
 #pragma unroll
@@ -760,6 +776,26 @@ __global__ void k_init_random(TableView T, const int32_t* __restrict__ ids, int6
   }
 }
 
+// createInitialModel (SGD.scala:218-252) from the data itself: every id of the batch's entries
+// that this context owns and that is absent gets the seeded draw of k_init_random.  The draw is a
+// function of (seed, id, factor) only, so no distinct pass is needed: entries of one id that race
+// write identical bytes, and rows already present are kept.
+__global__ void k_init_entries(TableView T, const uint32_t* __restrict__ col, int64_t n, uint64_t seed, double sd,
+                               int32_t epoch, double cumE) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t id = (int64_t)col[i];
+    if (id % T.shard_count != T.shard_index) continue;
+    const int64_t slot = id / T.shard_count;
+    if (slot >= T.rows || T.hdr(slot)->t >= 0) continue;
+    for (int f = 0; f < T.kp; ++f) T.v(slot)[f] = f < T.k ? gauss_draw(seed, id, f, sd) : 0.f;
+    RowHdr o;
+    o.w = gauss_draw(seed, id, -1, sd);
+    o.t = epoch;
+    o.cum = cumE;
+    store_hdr(T, slot, o);
+  }
+}
+
 __global__ void k_load_rows(TableView T, const int32_t* __restrict__ ids, int64_t n, const double* __restrict__ w,
                             const double* __restrict__ V, int32_t epoch, double cumE) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
@@ -803,46 +839,6 @@ __global__ void k_count_present(TableView T, unsigned long long* out) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
   if ((threadIdx.x & 63) == 0 && c) atomicAdd(out, c);
-}
-
-// FactorizationMachinesModel.predict/transform (Model.scala:69-133), one thread per sample.
-// Global ids arrive in b.col; ids >= num_features or absent from the model are dropped.
-__global__ void k_predict(TableView T, const int64_t* __restrict__ row_ptr, const uint32_t* __restrict__ col,
-                          const uint2* __restrict__ ent, int64_t B, int64_t num_features, double cumE,
-                          double w0, double lo, double hi, double* __restrict__ pred) {
-  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < B; s += (int64_t)gridDim.x * blockDim.x) {
-    double acc[64];
-    for (int f = 0; f < 64; ++f) acc[f] = 0.0;
-    double wx = 0.0, vv = 0.0;
-    int n = 0;
-    for (int64_t e = row_ptr[s]; e < row_ptr[s + 1]; ++e) {
-      const int64_t id = col[e];
-      if (id >= num_features) continue;
-      const RowHdr h = (*T.hdr(id));
-      if (h.t < 0) continue;
-      const double a = cumE - h.cum;
-      const double x = (double)__uint_as_float(ent[e].y);
-      const float w = a > 0.0 ? shrink_f(h.w, a) : h.w;
-      wx += (double)w * x;
-      double v2 = 0.0;
-      for (int f = 0; f < T.k; ++f) {
-        float v = T.v(id)[f];
-        if (a > 0.0) v = shrink_f(v, a);
-        acc[f & 63] += (double)v * x;  // k <= 64 on this path (checked on the host)
-        v2 += (double)v * v;
-      }
-      vv += v2 * x * x;
-      ++n;
-    }
-    if (n == 0) {
-      pred[s] = w0;  // na.fill(globalBias), Model.scala:86 (unclamped)
-    } else {
-      double ss = 0.0;
-      for (int f = 0; f < T.k; ++f) ss += acc[f] * acc[f];
-      const double yhat = 0.5 * (ss - vv) + wx + w0;
-      pred[s] = fmin(fmax(yhat, lo), hi);  // least(greatest(pred, min), max), :131
-    }
-  }
 }
 
 // calcLossGrad per-entry outputs (Model.scala:135-234), one thread per sample.
@@ -953,35 +949,43 @@ inline unsigned grid_for(int64_t n, int block, int64_t cap = 256 * 16) {
 
 template <int GS, int TEAM>
 void launch_fwd_t(const TableView& T, const BatchDev& b, StepWork& w, const StepParams& p, hipStream_t st,
-                  int64_t* nblk, float* partial_out) {
+                  int64_t* nblk, float* partial_out, const PredictOut* pred) {
   constexpr int TPB = kBlock / TEAM;
   int64_t blocks = (b.n_rows + TPB - 1) / TPB;
   if (blocks > 256 * 8) blocks = 256 * 8;
   if (blocks < 1) blocks = 1;
   *nblk = blocks;
+  const dim3 grid((unsigned)blocks), blk(kBlock);
+  if (pred) {
+    hipLaunchKernelGGL((k_forward<GS, TEAM, kPredict>), grid, blk, 0, st, T, b.row_ptr.as<int64_t>(),
+                       b.col.as<uint32_t>(), b.ent.as<uint2>(), nullptr, b.n_rows, p.w0, p.cumE, nullptr, nullptr,
+                       nullptr, pred->lo, pred->hi, pred->pred);
+    return;
+  }
+  if (partial_out) {
+    hipLaunchKernelGGL((k_forward<GS, TEAM, kPartial>), grid, blk, 0, st, T, b.row_ptr.as<int64_t>(),
+                       b.col.as<uint32_t>(), b.ent.as<uint2>(), nullptr, b.n_rows, p.w0, p.cumE, partial_out, nullptr,
+                       nullptr, 0.0, 0.0, nullptr);
+    return;
+  }
   w.loss_part.ensure(sizeof(double2) * blocks);
-  if (partial_out)
-    hipLaunchKernelGGL((k_forward<GS, TEAM, true>), dim3((unsigned)blocks), dim3(kBlock), 0, st, T,
-                       b.row_ptr.as<int64_t>(), b.col.as<uint32_t>(), b.ent.as<uint2>(), nullptr, b.n_rows, p.w0,
-                       p.cumE, partial_out, nullptr, nullptr);
-  else
-    hipLaunchKernelGGL((k_forward<GS, TEAM, false>), dim3((unsigned)blocks), dim3(kBlock), 0, st, T,
-                       b.row_ptr.as<int64_t>(), b.col.as<uint32_t>(), b.ent.as<uint2>(), b.label.as<float>(),
-                       b.n_rows, p.w0, p.cumE, w.S.as<float>(), w.yl.as<float2>(), w.loss_part.as<double2>());
+  hipLaunchKernelGGL((k_forward<GS, TEAM, kTrain>), grid, blk, 0, st, T, b.row_ptr.as<int64_t>(),
+                     b.col.as<uint32_t>(), b.ent.as<uint2>(), b.label.as<float>(), b.n_rows, p.w0, p.cumE,
+                     w.S.as<float>(), w.yl.as<float2>(), w.loss_part.as<double2>(), 0.0, 0.0, nullptr);
 }
 
 }  // namespace
 
 void launch_forward(const TableView& T, const BatchDev& b, StepWork& w, const StepParams& p, hipStream_t st,
-                    int64_t* n_fwd_blocks, float* partial_out) {
+                    int64_t* nblk, float* partial_out, const PredictOut* pred) {
   const int nq = T.kp / 4;
-  if (nq <= 1) launch_fwd_t<1, 16>(T, b, w, p, st, n_fwd_blocks, partial_out);
-  else if (nq <= 2) launch_fwd_t<2, 16>(T, b, w, p, st, n_fwd_blocks, partial_out);
-  else if (nq <= 4) launch_fwd_t<4, 16>(T, b, w, p, st, n_fwd_blocks, partial_out);
-  else if (nq <= 8) launch_fwd_t<8, 16>(T, b, w, p, st, n_fwd_blocks, partial_out);
-  else if (nq <= 16) launch_fwd_t<16, 16>(T, b, w, p, st, n_fwd_blocks, partial_out);
-  else if (nq <= 32) launch_fwd_t<32, 32>(T, b, w, p, st, n_fwd_blocks, partial_out);
-  else if (nq <= 64) launch_fwd_t<64, 64>(T, b, w, p, st, n_fwd_blocks, partial_out);
+  if (nq <= 1) launch_fwd_t<1, 16>(T, b, w, p, st, nblk, partial_out, pred);
+  else if (nq <= 2) launch_fwd_t<2, 16>(T, b, w, p, st, nblk, partial_out, pred);
+  else if (nq <= 4) launch_fwd_t<4, 16>(T, b, w, p, st, nblk, partial_out, pred);
+  else if (nq <= 8) launch_fwd_t<8, 16>(T, b, w, p, st, nblk, partial_out, pred);
+  else if (nq <= 16) launch_fwd_t<16, 16>(T, b, w, p, st, nblk, partial_out, pred);
+  else if (nq <= 32) launch_fwd_t<32, 32>(T, b, w, p, st, nblk, partial_out, pred);
+  else if (nq <= 64) launch_fwd_t<64, 64>(T, b, w, p, st, nblk, partial_out, pred);
   else FM_REQUIRE(false, "dimFactorization > 256 is not supported");
   FM_HIP_CHECK(hipGetLastError());
 }
@@ -1044,6 +1048,14 @@ void launch_init_random(const TableView& T, const int32_t* ids, int64_t n, int64
   FM_HIP_CHECK(hipGetLastError());
 }
 
+void launch_init_entries(const TableView& T, const uint32_t* col, int64_t n, uint64_t seed, double sd, int32_t epoch,
+                         double cumE, hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_init_entries, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, st, T, col, n, seed, sd, epoch,
+                     cumE);
+  FM_HIP_CHECK(hipGetLastError());
+}
+
 void launch_load_rows(const TableView& T, const int32_t* ids, int64_t n, const double* w, const double* V,
                       int32_t epoch, double cumE, hipStream_t st) {
   if (n <= 0) return;
@@ -1089,14 +1101,17 @@ void launch_count_present(const TableView& T, int64_t* out, hipStream_t st) {
   FM_HIP_CHECK(hipGetLastError());
 }
 
-void launch_predict(const TableView& T, const BatchDev& b, double cumE, int64_t num_features, double w0,
-                    double lo, double hi, double* pred, hipStream_t st) {
-  FM_REQUIRE(T.k <= 64, "fm_predict supports dimFactorization <= 64");
+void launch_predict(const TableView& T, const BatchDev& b, double cumE, double w0, double lo, double hi,
+                    double* pred, hipStream_t st) {
   FM_REQUIRE(T.shard_count == 1, "fm_predict needs the whole table (shard_count == 1)");
   if (b.n_rows <= 0) return;
-  hipLaunchKernelGGL(k_predict, dim3(grid_for(b.n_rows, kBlock)), dim3(kBlock), 0, st, T, b.row_ptr.as<int64_t>(),
-                     b.col.as<uint32_t>(), b.ent.as<uint2>(), b.n_rows, num_features, cumE, w0, lo, hi, pred);
-  FM_HIP_CHECK(hipGetLastError());
+  StepParams p{};
+  p.cumE = cumE;
+  p.w0 = w0;
+  PredictOut po{lo, hi, pred};
+  StepWork unused;
+  int64_t nblk = 0;
+  launch_forward(T, b, unused, p, st, &nblk, nullptr, &po);
 }
 
 void launch_loss_grad(const TableView& T, const BatchDev& b, double cumE, double w0, double* pred, double* loss,

@@ -104,6 +104,13 @@ class FMContext:
     def init_random_range(self, begin: int, end: int):
         N.check(self._lib.fm_init_random_range(self.handle, int(begin), int(end)), "fm_init_random_range")
 
+    def init_from_batch(self, b: "DeviceBatch") -> int:
+        """createInitialModel over a device-resident dataset (SGD.scala:224-241): the seeded draw for
+        every absent id of b's entries, on the device; returns the number of present rows."""
+        n = C.c_int64()
+        N.check(self._lib.fm_init_from_batch(self.handle, b.handle, C.byref(n)), "fm_init_from_batch")
+        return n.value
+
     def export_tables(self):
         n = C.c_int64()
         N.check(self._lib.fm_export_tables(self.handle, None, None, None, 0, C.byref(n)), "fm_export_tables")
@@ -162,6 +169,12 @@ class FMContext:
         N.check(self._lib.fm_predict(self.handle, C.byref(csr.c), float(min_label), float(max_label),
                                      N.ptr(out, C.c_double)), "fm_predict")
         return out[: csr.n_rows]
+
+    def predict_batch(self, b: DeviceBatch, min_label: float, max_label: float) -> np.ndarray:
+        out = np.zeros(max(b.n_rows, 1))
+        N.check(self._lib.fm_predict_batch(self.handle, b.handle, float(min_label), float(max_label),
+                                           N.ptr(out, C.c_double)), "fm_predict_batch")
+        return out[: b.n_rows]
 
     def loss_grad(self, csr: N.CSRHost):
         n = max(csr.nnz, 1)

@@ -322,13 +322,14 @@ class FactorizationMachinesSGD:
         vectors = dataset[p["featuresCol"]]
         labels = np.asarray(dataset[p["labelCol"]], dtype=np.float64)
         rp, col, val = _explode(vectors)
-        distinct = np.unique(col)  # createInitialModel: distinct active feature ids (:224-232)
-        F = p["numFeatures"] or (int(distinct.max()) + 1 if len(distinct) else 1)
+        F = p["numFeatures"] or (int(col.max()) + 1 if len(col) else 1)
         ctx = FMContext(F, k, device=p["device"], seed=p["seed"], init_sd=p["initialSd"], w0=0.0)
         if initial_tables is not None:
             ctx.load_tables(*initial_tables)
-        elif len(distinct):
-            ctx.init_random(distinct.astype(np.int32))
+        elif len(col):
+            # createInitialModel (:224-241): the draw for every distinct active feature id, on the
+            # device over the whole dataset's entries
+            ctx.init_from_batch(ctx.batch(N.CSRHost(rp, col, val, labels)))
         # randomSplit(Array.fill(maxIter)(miniBatchFraction), 1234L) (:111-112)
         order_cols = []
         extra = None

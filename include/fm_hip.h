@@ -104,6 +104,12 @@ int fm_load_tables(fm_ctx* ctx, const int32_t* ids, int64_t n, const double* w, 
 int fm_init_random(fm_ctx* ctx, const int32_t* ids, int64_t n);
 /* Same for every id in [id_begin, id_end) (ids this shard does not own are skipped). */
 int fm_init_random_range(fm_ctx* ctx, int64_t id_begin, int64_t id_end);
+/* createInitialModel over a device-resident dataset (SGD.scala:224-241: the distinct active ids of
+ * the data, then the random draw): every id of the batch's entries that this context owns and
+ * that is absent gets the same draw as fm_init_random; present rows are kept.  Runs on the device
+ * over the entries (the draw depends on (seed, id, factor) only, so no distinct pass is needed).
+ * *n_present (may be NULL) receives the number of present rows afterwards. */
+int fm_init_from_batch(fm_ctx* ctx, fm_batch* data, int64_t* n_present);
 /* Export every present row owned by this context, ascending id, after applying the
  * pending L1 shrink.  cap = capacity in rows; *n receives the number of present rows
  * (call with cap 0 to size).  V is row-major [n][k]. */
@@ -150,6 +156,9 @@ int fm_loss_history(fm_ctx* ctx, double* loss, int64_t cap, int64_t* n);
  * feature gets w0 unclamped (na.fill, :86); otherwise clamp(yhat, min_label, max_label)
  * (:129-132).  Pass -inf/+inf for the unclamped score. */
 int fm_predict(fm_ctx* ctx, const fm_csr* csr, double min_label, double max_label, double* pred);
+/* The same on a device-resident batch (fm_batch_create): transform over a cached DataFrame
+ * without re-uploading it.  pred is a host buffer of fm_batch_rows(batch) doubles. */
+int fm_predict_batch(fm_ctx* ctx, fm_batch* batch, double min_label, double max_label, double* pred);
 /* calcLossGrad (Model.scala:135-234), per active entry e in CSR order:
  * pred[e] = yhat of its row (unclamped), loss[e] = (yhat - y)^2, delta_w[e] = x,
  * delta_v[e*k + f] = vfxiSum_f * x - (v_f * x) * x.  Any output may be NULL.

@@ -246,3 +246,58 @@ def test_prepared_batches_bitwise_equal(gpu):
     for x, y in zip(a, b):
         assert np.array_equal(x, y)
     assert np.array_equal(la, lb)
+
+
+@pytest.mark.parametrize("k", [3, 16, 80])
+def test_predict_matches_oracle(gpu, k):
+    """transform/predict (Model.scala:69-133) on the team forward kernel: ids the model does not
+    hold (absent rows, ids >= num_features) are dropped, rows left empty score w0 unclamped, the
+    rest are clamped; host CSR (fm_predict) and device batch (fm_predict_batch) agree bitwise.
+    k = 80 exercises the wide-row path (the old thread-per-sample kernel stopped at 64)."""
+    from fm_spark_amd.engine import FMContext
+
+    F = 700
+    csr, ids, w, V = make_problem(71 + k, 400, F + 50, k, 9, hot=4)  # ids up to F + 49
+    keep = ids[(ids % 3 != 0) & (ids < F)]  # every third id absent from the model
+    ctx = FMContext(F, k, w0=0.25)
+    ctx.load_tables(keep, w[keep], V[keep])
+    model = R.Model.empty(F, k)
+    model.load(keep, w[keep], V[keep])
+    model.w0 = 0.25
+    ref = R.predict(model, csr, -0.5, 1.5, num_features=F)
+    got = ctx.predict(to_host(csr), -0.5, 1.5)
+    np.testing.assert_allclose(got, ref, rtol=RTOL, atol=ATOL)
+    inrange = csr.col < F
+    sub = R.CSR(np.concatenate([[0], np.cumsum([inrange[a:b].sum() for a, b in zip(csr.row_ptr[:-1], csr.row_ptr[1:])])]).astype(np.int64),
+                csr.col[inrange], csr.val[inrange], csr.label)
+    db = ctx.batch(to_host(sub))  # device batches only hold ids < num_features
+    got_b = ctx.predict_batch(db, -0.5, 1.5)
+    np.testing.assert_array_equal(got_b, ctx.predict(to_host(sub), -0.5, 1.5))
+    np.testing.assert_allclose(got_b, ref, rtol=RTOL, atol=ATOL)
+
+
+@pytest.mark.parametrize("shards", [1, 3])
+def test_init_from_batch_equals_distinct_init(gpu, shards):
+    """createInitialModel on the device over the data's entries (fm_init_from_batch) equals
+    fm_init_random over np.unique of the ids, bitwise, per shard; present rows are kept."""
+    from fm_spark_amd.engine import FMContext
+
+    F, k = 5000, 12
+    csr = make_problem(91, 800, F, k, 15, hot=17)[0]
+    for r in range(shards):
+        a = FMContext(F, k, seed=77, init_sd=0.02, shard_index=r, shard_count=shards)
+        b = FMContext(F, k, seed=77, init_sd=0.02, shard_index=r, shard_count=shards)
+        n = a.init_from_batch(a.batch(to_host(csr)))
+        u = np.unique(csr.col)
+        mine = u[u % shards == r]
+        b.init_random(mine)
+        assert n == len(mine)
+        for x, y in zip(a.export_tables(), b.export_tables()):
+            assert np.array_equal(x, y)
+        # a second pass over other data keeps the rows already present
+        before = a.export_tables()
+        csr2 = make_problem(92, 300, F, k, 15)[0]
+        a.init_from_batch(a.batch(to_host(csr2)))
+        gi, gw, gV = a.export_tables()
+        pos = np.searchsorted(gi, before[0])
+        assert np.array_equal(gw[pos], before[1]) and np.array_equal(gV[pos], before[2])
