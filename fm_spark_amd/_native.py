@@ -90,6 +90,7 @@ SIGNATURES = {
     "fm_profile_enable": (C.c_int, [_P, C.c_int32]),
     "fm_profile_read": (C.c_int, [_P, C.c_char_p, C.c_int64, _DP, _I64P, C.c_int64, _I64P]),
     "fm_profile_reset": (C.c_int, [_P]),
+    "fm_read_libsvm": (C.c_int, [C.c_char_p, C.c_int64, C.c_int64, _DP, _I64P, _I32P, _DP, _I64P, _I64P, _I64P]),
     "fm_random_split": (
         C.c_int,
         [C.c_int32, _I64P, C.c_char_p, _DP, C.POINTER(C.c_int8), _I32P, _I64P, _I32P, _DP, _I64P,

@@ -15,6 +15,8 @@ from __future__ import annotations
 
 from dataclasses import dataclass
 
+import os
+
 import numpy as np
 
 N_NUMERIC = 13
@@ -95,27 +97,89 @@ def synthetic_batch(n_rows: int, num_features: int, *, seed: int = DEFAULT_SEED,
     return Batch(row_ptr=row_ptr, col=ids.reshape(-1).astype(np.int32), val=vals.reshape(-1), label=y)
 
 
+def read_libsvm_csr(path: str):
+    """Spark 2.1 ``libsvm`` data source for one file (MLUtils.parseLibSVMFile), parsed natively
+    (fm_read_libsvm in libfm_hip.so).  Returns (labels, row_ptr, col, val, num_features)."""
+    import ctypes as C
+
+    from . import _native as N
+
+    lib = N.load()
+    b, nnz, nf = C.c_int64(), C.c_int64(), C.c_int64()
+    bp = os.fsencode(path)
+    N.check(lib.fm_read_libsvm(bp, 0, 0, None, None, None, None, C.byref(b), C.byref(nnz), C.byref(nf)),
+            "fm_read_libsvm")
+    labels = np.zeros(max(b.value, 1))
+    row_ptr = np.zeros(b.value + 1, dtype=np.int64)
+    col = np.zeros(max(nnz.value, 1), dtype=np.int32)
+    val = np.zeros(max(nnz.value, 1))
+    N.check(lib.fm_read_libsvm(bp, max(b.value, 1), max(nnz.value, 1), N.ptr(labels, C.c_double),
+                               N.ptr(row_ptr, C.c_int64), N.ptr(col, C.c_int32), N.ptr(val, C.c_double),
+                               C.byref(b), C.byref(nnz), C.byref(nf)), "fm_read_libsvm")
+    return labels[: b.value], row_ptr, col[: nnz.value], val[: nnz.value], nf.value
+
+
 def read_libsvm(path: str):
-    """Spark 2.1 ``libsvm`` source semantics for one file (labels, 0-based sparse rows).
-    Returns (labels, rows, num_features) with rows as lists of (index, value) pairs."""
-    labels, rows = [], []
-    max_idx = -1
+    """The same as (labels, rows, num_features) with rows as lists of (index, value) pairs."""
+    labels, row_ptr, col, val, nf = read_libsvm_csr(path)
+    rows = [list(zip(col[a:b].tolist(), val[a:b].tolist())) for a, b in zip(row_ptr[:-1], row_ptr[1:])]
+    return labels, rows, nf
+
+
+# ------------------------------------------------------------------ MovieLens features (demo)
+MAX_USER_ID = 671       # FactorizationMachinesSample.scala:13
+MAX_MOVIE_ID = 164979   # FactorizationMachinesSample.scala:14
+
+
+def read_ratings_csv(path: str):
+    """ratings.csv of ml-latest-small (header userId,movieId,rating,timestamp), the input of
+    FactorizationMachinesSample.scala:97-102.  Returns (user_id, movie_id, rating) arrays."""
+    users, movies, ratings = [], [], []
     with open(path) as fh:
+        header = fh.readline().strip().split(",")
+        iu, im, ir = header.index("userId"), header.index("movieId"), header.index("rating")
         for line in fh:
-            line = line.split("#", 1)[0].strip()
-            if not line:
+            if not line.strip():
                 continue
-            items = line.split()
-            labels.append(float(items[0]))
-            pairs = []
-            prev = -1
-            for it in items[1:]:
-                i, v = it.split(":")
-                idx = int(i) - 1
-                if idx < 0 or idx <= prev:
-                    raise ValueError(f"indices must be one-based and ascending: {line!r}")
-                prev = idx
-                pairs.append((idx, float(v)))
-                max_idx = max(max_idx, idx)
-            rows.append(pairs)
-    return np.asarray(labels), rows, max_idx + 1
+            f = line.rstrip("\n").split(",")
+            users.append(int(f[iu]))
+            movies.append(int(f[im]))
+            ratings.append(float(f[ir]))
+    return np.asarray(users, np.int64), np.asarray(movies, np.int64), np.asarray(ratings, np.float64)
+
+
+def movielens_features(user_id, movie_id, rating):
+    """createRatingDataFrame (FactorizationMachinesSample.scala:75-128) as CSR rows.
+
+    Per user, the set of distinct "movieId:rating" strings (collect_set); one row per element
+    (explode) with label = rating and the sparse features of udfCrateFeatureVec (:76-95):
+    userId -> 1.0, MaxUserId + movieId -> 1.0, and, when the user's set has at least two
+    elements, every OTHER movie m of the set at MaxUserId + MaxMovieId + m with weight
+    1 / (|set| - 1).  Vector size MaxUserId + 2 * MaxMovieId.  Spark leaves the row order of the
+    groupBy unspecified; here users ascend and each user's rows follow (movieId, rating).
+    Returns (labels, row_ptr, col, val, num_features)."""
+    size = MAX_USER_ID + MAX_MOVIE_ID + MAX_MOVIE_ID
+    by_user = {}
+    for u, m, r in zip(np.asarray(user_id).tolist(), np.asarray(movie_id).tolist(), np.asarray(rating).tolist()):
+        by_user.setdefault(int(u), set()).add((int(m), float(r)))  # collect_set of "movieId:rating"
+    labels, row_ptr, cols, vals = [], [0], [], []
+    for u in sorted(by_user):
+        mr = sorted(by_user[u])
+        for cur_m, cur_r in mr:  # explode(movieRatings)
+            feat = {}
+            if len(mr) >= 2:
+                wgt = 1.0 / (len(mr) - 1.0)
+                for m, _ in mr:
+                    if m != cur_m:
+                        feat[MAX_USER_ID + MAX_MOVIE_ID + m] = wgt
+            feat[u] = 1.0
+            feat[MAX_USER_ID + cur_m] = 1.0
+            for i in sorted(feat):  # Vectors.sparse sorts by index
+                if not 0 <= i < size:
+                    raise ValueError(f"feature index {i} outside the vector size {size}")
+                cols.append(i)
+                vals.append(feat[i])
+            labels.append(cur_r)
+            row_ptr.append(len(cols))
+    return (np.asarray(labels, np.float64), np.asarray(row_ptr, np.int64), np.asarray(cols, np.int32),
+            np.asarray(vals, np.float64), size)

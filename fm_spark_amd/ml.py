@@ -32,6 +32,15 @@ from .linalg import DenseVector, Vector, Vectors, active_map
 log = logging.getLogger("org.apache.spark.ml.fm")
 
 
+@dataclass(frozen=True)
+class Param:
+    """A named parameter of an estimator (org.apache.spark.ml.param.Param): ``fm.regParam``;
+    param maps (ParamGridBuilder, ``copy(extra)``) are keyed by its name."""
+
+    parent: str
+    name: str
+
+
 # ------------------------------------------------------------------------ DataFrame
 class DataFrame:
     """Columns by name + partition sizes (rows laid out partition after partition)."""
@@ -303,10 +312,11 @@ class FactorizationMachinesSGD:
     def getInitialSd(self): return self._params["initialSd"]
 
     def copy(self, extra: dict | None = None) -> "FactorizationMachinesSGD":
-        """defaultCopy (SGD.scala:254): same uid, params overridden by extra."""
+        """defaultCopy (SGD.scala:254): same uid, params overridden by extra (keyed by name or Param)."""
         c = FactorizationMachinesSGD(self.uid)
         c._params = dict(self._params)
-        c._params.update(extra or {})
+        for key, value in (extra or {}).items():
+            c._params[key.name if isinstance(key, Param) else key] = value
         return c
 
     def transformSchema(self, schema):
@@ -370,3 +380,10 @@ class FactorizationMachinesSGD:
         model.setMinLabel(p["minLabel"]).setMaxLabel(p["maxLabel"])
         model.parent = self
         return model
+
+
+# fm.regParam, fm.dimFactorization, ...: the Param handles spark.ml tuning keys grids by
+for _name in ("dimFactorization", "featuresCol", "labelCol", "predictionCol", "maxIter", "miniBatchFraction",
+              "regParam", "stepSize", "minLabel", "maxLabel", "initialSd", "seed"):
+    setattr(FactorizationMachinesSGD, _name, property(lambda self, _n=_name: Param(self.uid, _n)))
+del _name

@@ -181,6 +181,15 @@ int fm_profile_read(fm_ctx* ctx, char* names, int64_t names_cap, double* total_m
                     int64_t* launches, int64_t cap, int64_t* n);
 int fm_profile_reset(fm_ctx* ctx);
 
+/* ---- input format: Spark 2.1 `libsvm` data source (data/sample.txt, config c1) ------------ */
+/* MLUtils.parseLibSVMFile semantics: trimmed lines, '#'-lines and empty lines skipped, one-based
+ * strictly ascending indices (stored 0-based), numFeatures = max last index + 1 (an empty row
+ * counts as index 0).  Call with cap_rows = cap_nnz = 0 to size: *n_rows, *nnz, *num_features
+ * are always filled; then again with buffers label[n_rows], row_ptr[n_rows + 1], col[nnz],
+ * val[nnz].  A malformed line is an FM_ERR_ARG with the line in fm_last_error(). */
+int fm_read_libsvm(const char* path, int64_t cap_rows, int64_t cap_nnz, double* label, int64_t* row_ptr,
+                   int32_t* col, double* val, int64_t* n_rows, int64_t* nnz, int64_t* num_features);
+
 /* ---- mini-batch sampler: Dataset.randomSplit replay (SGD.scala:111-112) --------------- */
 /* Host-side replay of Spark 2.1.0 randomSplit(weights, seed) on a cached DataFrame whose
  * rows are given partition by partition (part_ptr[n_parts+1]).  Each partition is sorted
