@@ -39,7 +39,8 @@ constexpr int kWaveEnt = 256;  // sorted entries per update wave
 #ifndef FM_UPD_D
 #define FM_UPD_D 2
 #endif
-constexpr int kUpdD = FM_UPD_D;  // entries whose rows a lane group loads ahead
+constexpr int kUpdD = FM_UPD_D;  // entries whose rows a lane group loads per step
+
 // experiment switches (tools/variants.sh; all 0 in the product build): drop the update's S-row
 // loads, row loads or row stores to measure what each costs
 #ifndef FM_ABL_NOS
@@ -320,8 +321,9 @@ __global__ __launch_bounds__(kBlock) void k_segment_update(SegArgs a) {
 
     // ---------------- phase 2: group g, lane q of the group
     const int g = lane / Q, q = lane % Q;
-    float4 Sp[D][NF], Vp[D][NF], Hp[D];
-    auto prefetch = [&](int b0) {
+    // two buffers of D entries: the rows of the next step are in flight while a step is consumed
+    float4 Sp0[D][NF], Vp0[D][NF], Hp0[D], Sp1[D][NF], Vp1[D][NF], Hp1[D];
+    auto prefetch = [&](int b0, float4 (&Sp)[D][NF], float4 (&Vp)[D][NF], float4 (&Hp)[D]) {
 #pragma unroll
       for (int u = 0; u < D; ++u) {
         const int l = (b0 + u) * NGS + g;  // li(g * RL + b0 + u)
@@ -340,7 +342,7 @@ __global__ __launch_bounds__(kBlock) void k_segment_update(SegArgs a) {
                                : make_float4(0.f, __int_as_float(-1), 0.f, 0.f);
       }
     };
-    prefetch(0);  // in flight together with phase 1's {yhat, y} reads
+    prefetch(0, Sp0, Vp0, Hp0);  // in flight together with phase 1's {yhat, y} reads
 #pragma unroll
     for (int i = 0; i < NP; ++i) {
       const int l = li(i * 64 + lane);
@@ -405,9 +407,7 @@ __global__ __launch_bounds__(kBlock) void k_segment_update(SegArgs a) {
     int hst = 0;  // the group's head piece: 0 none, 1 open through the group's end, 2 closed
     bool started = false, open = false;
     uint32_t lastkey = kNone;
-#pragma unroll 1
-    for (int b0 = 0; b0 < RL; b0 += D) {
-      if (b0 > 0) prefetch(b0);
+    auto consume = [&](int b0, const float4 (&Sp)[D][NF], const float4 (&Vp)[D][NF], const float4 (&Hp)[D]) {
 #pragma unroll
       for (int u = 0; u < D; ++u) {
         const int l = (b0 + u) * NGS + g;
@@ -444,6 +444,15 @@ __global__ __launch_bounds__(kBlock) void k_segment_update(SegArgs a) {
           started = false;
           open = false;
         }
+      }
+    };
+#pragma unroll 1
+    for (int b0 = 0; b0 < RL; b0 += 2 * D) {
+      if (b0 + D < RL) prefetch(b0 + D, Sp1, Vp1, Hp1);
+      consume(b0, Sp0, Vp0, Hp0);
+      if (b0 + D < RL) {
+        if (b0 + 2 * D < RL) prefetch(b0 + 2 * D, Sp0, Vp0, Hp0);
+        consume(b0 + D, Sp1, Vp1, Hp1);
       }
     }
     const bool tail = open && started;  // the open piece began in this group
