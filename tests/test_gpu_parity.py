@@ -301,3 +301,34 @@ def test_init_from_batch_equals_distinct_init(gpu, shards):
         gi, gw, gV = a.export_tables()
         pos = np.searchsorted(gi, before[0])
         assert np.array_equal(gw[pos], before[1]) and np.array_equal(gV[pos], before[2])
+
+
+def test_int_max_feature_ids(gpu):
+    """Config c4's id range: numFeatures = Int.MaxValue, so slot * stride exceeds
+    2^31 floats and the sort keys are 31 bits wide.  One table of 2^31 - 1 rows at k = 4 (64-B
+    records, 137 GB of HBM).  The step is invariant under relabelling ids, so the device run on
+    ids spread up to Int.MaxValue - 1 is compared with the oracle on the compact labels 0..n-1."""
+    from fm_spark_amd.engine import FMContext
+
+    F, k, n = 2**31 - 1, 4, 300
+    big = np.unique(np.concatenate([[0, 1, 2**30, 2**31 - 2, 2**31 - 3], 
+                                    np.random.default_rng(5).integers(2**31 - 10**6, 2**31 - 1, n)]))[:n]
+    n = len(big)
+    csrs = [make_problem(500 + i, 300, n, k, 9, hot=3)[0] for i in range(2)]
+    _, ids, w, V = make_problem(501, 1, n, k, 1)
+    model = R.Model.empty(n, k)
+    model.load(ids, w, V)
+    ctx = FMContext(F, k)
+    ctx.load_tables(big[ids], w, V)
+    losses = []
+    for t, c in enumerate(csrs, start=1):
+        ref = R.sgd_step_fast(model, c, t, 0.3, 1e-4)
+        bc = R.CSR(c.row_ptr, big[c.col].astype(np.int32), c.val, c.label)
+        out = ctx.step(to_host(bc), t, 0.3, 1e-4)
+        assert out.loss_sum == pytest.approx(ref.loss_sum, rel=RTOL)
+        assert out.n_unique == len(np.unique(c.col))
+    gi, gw, gV = ctx.export_tables()
+    ctx.close()
+    np.testing.assert_array_equal(gi, big[np.nonzero(model.present)[0]])
+    np.testing.assert_allclose(gw, model.w[model.present], rtol=RTOL, atol=ATOL)
+    np.testing.assert_allclose(gV, model.V[model.present], rtol=RTOL, atol=ATOL)
