@@ -135,7 +135,8 @@ struct PredictOut {
   double lo, hi;
   double* pred;
 };
-// partial_out != nullptr: the sharded owner's partial pass (rows [kp + 4] per pair, fm_shard.hip);
+// partial_out != nullptr: the sharded owner's partial pass (fm_shard.hip): [pairs][kp] vectors
+// followed by [pairs] float2 scalars;
 // pred != nullptr: FactorizationMachinesModel.predict (p.w0, p.cumE used)
 void launch_forward(const TableView& T, const BatchDev& b, StepWork& w, const StepParams& p,
                     hipStream_t st, int64_t* n_fwd_blocks, float* partial_out = nullptr,

@@ -71,8 +71,8 @@ __device__ __forceinline__ void current_row(const RowHdr& h, float4& v, float& w
 // ------------------------------------------------------------------------ forward
 // MODE kTrain: the step's forward (S, {yhat, y}, loss partials).
 // MODE kPartial: the sharded owner's pass (fm_shard.hip).  "Samples" are (source rank, sample)
-// pairs of the entries this owner received; the output per pair is the partial row
-// [sum v*x (kp) | sum v^2 x^2 | sum w*x | 0 0] (fp32) instead of S / yhat / loss.
+// pairs of the entries this owner received; the output per pair is the partial vector
+// sum v*x (kp fp32, S_out) and the scalars {sum v^2 x^2, sum w*x} (yl_out) instead of S / yhat / loss.
 // MODE kPredict: FactorizationMachinesModel.predict (Model.scala:90-133): ids outside the table
 // or absent from the model are dropped (the inner joins, :103-112), a row left without a learned
 // feature scores globalBias unclamped (na.fill, :86), every other row
@@ -154,11 +154,10 @@ __global__ __launch_bounds__(kBlock) void k_forward(TableView T, const int64_t* 
       wx += __shfl_xor(wx, o);
       if (MODE == kPredict) npres += __shfl_xor(npres, o);
     }
-    if (PARTIAL) {
-      const int W = kp + 4;
+    if (PARTIAL) {  // vectors [pair][kp] in S_out, scalars {sum v^2 x^2, sum w x} in yl_out
       if (rs == 0 && qok)
-        *reinterpret_cast<float4*>(S_out + s * W + g * 4) = make_float4((float)a0, (float)a1, (float)a2, (float)a3);
-      if (tl == 0) *reinterpret_cast<float4*>(S_out + s * W + kp) = make_float4((float)vv, (float)wx, 0.f, 0.f);
+        *reinterpret_cast<float4*>(S_out + s * kp + g * 4) = make_float4((float)a0, (float)a1, (float)a2, (float)a3);
+      if (tl == 0) yl_out[s] = make_float2((float)vv, (float)wx);
       continue;
     }
     double ss = qok ? a0 * a0 + a1 * a1 + a2 * a2 + a3 * a3 : 0.0;
@@ -971,10 +970,10 @@ void launch_fwd_t(const TableView& T, const BatchDev& b, StepWork& w, const Step
                        nullptr, pred->lo, pred->hi, pred->pred);
     return;
   }
-  if (partial_out) {
+  if (partial_out) {  // [n_rows][kp] vectors, then [n_rows] float2 scalars
     hipLaunchKernelGGL((k_forward<GS, TEAM, kPartial>), grid, blk, 0, st, T, b.row_ptr.as<int64_t>(),
-                       b.col.as<uint32_t>(), b.ent.as<uint2>(), nullptr, b.n_rows, p.w0, p.cumE, partial_out, nullptr,
-                       nullptr, 0.0, 0.0, nullptr);
+                       b.col.as<uint32_t>(), b.ent.as<uint2>(), nullptr, b.n_rows, p.w0, p.cumE, partial_out,
+                       reinterpret_cast<float2*>(partial_out + b.n_rows * T.kp), nullptr, 0.0, 0.0, nullptr);
     return;
   }
   w.loss_part.ensure(sizeof(double2) * blocks);
@@ -985,9 +984,32 @@ void launch_fwd_t(const TableView& T, const BatchDev& b, StepWork& w, const Step
 
 }  // namespace
 
+// The sharded owner's partial pass sees short segments (about z / R entries per pair): its team
+// is sized so one round of U = 4 passes covers a segment, instead of 16 lanes per segment.
+template <int GS>
+void launch_partial_t(const TableView& T, const BatchDev& b, StepWork& w, const StepParams& p, hipStream_t st,
+                      int64_t* nblk, float* partial_out) {
+  const double avg = b.n_rows > 0 ? (double)b.nnz / (double)b.n_rows : 0.0;
+  if (GS <= 16 && avg <= 4.0) launch_fwd_t<GS, GS>(T, b, w, p, st, nblk, partial_out, nullptr);
+  else if (GS <= 16 && avg <= 8.0) launch_fwd_t<GS, (2 * GS > 16 ? 16 : 2 * GS)>(T, b, w, p, st, nblk, partial_out, nullptr);
+  else launch_fwd_t<GS, (GS > 16 ? GS : 16)>(T, b, w, p, st, nblk, partial_out, nullptr);
+}
+
 void launch_forward(const TableView& T, const BatchDev& b, StepWork& w, const StepParams& p, hipStream_t st,
                     int64_t* nblk, float* partial_out, const PredictOut* pred) {
   const int nq = T.kp / 4;
+  if (partial_out && !pred) {
+    if (nq <= 1) launch_partial_t<1>(T, b, w, p, st, nblk, partial_out);
+    else if (nq <= 2) launch_partial_t<2>(T, b, w, p, st, nblk, partial_out);
+    else if (nq <= 4) launch_partial_t<4>(T, b, w, p, st, nblk, partial_out);
+    else if (nq <= 8) launch_partial_t<8>(T, b, w, p, st, nblk, partial_out);
+    else if (nq <= 16) launch_partial_t<16>(T, b, w, p, st, nblk, partial_out);
+    else if (nq <= 32) launch_fwd_t<32, 32>(T, b, w, p, st, nblk, partial_out, pred);
+    else if (nq <= 64) launch_fwd_t<64, 64>(T, b, w, p, st, nblk, partial_out, pred);
+    else FM_REQUIRE(false, "dimFactorization > 256 is not supported");
+    FM_HIP_CHECK(hipGetLastError());
+    return;
+  }
   if (nq <= 1) launch_fwd_t<1, 16>(T, b, w, p, st, nblk, partial_out, pred);
   else if (nq <= 2) launch_fwd_t<2, 16>(T, b, w, p, st, nblk, partial_out, pred);
   else if (nq <= 4) launch_fwd_t<4, 16>(T, b, w, p, st, nblk, partial_out, pred);

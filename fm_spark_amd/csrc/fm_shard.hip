@@ -24,10 +24,12 @@
 // sums are split per owner (fp32 on the wire), the per-feature gradient sums run over the
 // same entries in the same order.  Deterministic for a given R.
 // Traffic per rank and step (k = 16, z = 39, R = 8): entries 12 B each (off the critical path:
-// exchanged during the previous iteration), partials and S rows (kp + 4) * 4 B per
-// (sample, owner) pair -- about 400 MB, against about 1 GB when rows and gradients of every
-// distinct id travel instead.
-// Wire rows are kp + 4 floats: partial [sum vx (kp) | vv | wx | 0 0], S [S (kp) | yhat | y | 0 0].
+// exchanged during the previous iteration), partials and S (kp + 2) * 4 B per (sample, owner)
+// pair -- about 2 x 150 MB, against about 1 GB when rows and gradients of every distinct id
+// travel instead.
+// Wire buffers are structures of arrays over the pairs, so every k-vector is 16-B aligned and a
+// 64-B row at k = 16: partials [P][kp] sum v*x then [P] {sum v^2 x^2, sum w x}; S [P][kp] vfxiSum
+// then [P] {yhat, y}.
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
@@ -226,17 +228,19 @@ __global__ __launch_bounds__(kBlock) void k_heads_apply(const uint2* __restrict_
 // Team of GS lanes per sample (one quad each): the owners' partials summed in owner order
 // in fp64 -> S = vfxiSum, yhat = 0.5 (|S|^2 - sum v^2 x^2) + sum w x + w0
 // (FactorizationMachinesModel.scala:221, :260-262), the loss partial (:230), and the S rows
-// sent back to every owner holding entries of the sample.
+// sent back to every owner holding entries of the sample.  Wire layout (structure of arrays):
+// part_vec / s_vec [pair][kp], part_sc / s_sc [pair] float2 ({sum v^2 x^2, sum w x} / {yhat, y}).
 template <int GS>
 __global__ __launch_bounds__(kBlock) void k_shard_combine(const int32_t* __restrict__ pairidx,
                                                           const int64_t* __restrict__ poff, int R, int64_t B,
-                                                          const float* __restrict__ part_in,
+                                                          const float* __restrict__ part_vec,
+                                                          const float2* __restrict__ part_sc,
                                                           const float* __restrict__ label, int kp, double w0,
-                                                          float* __restrict__ s_send,
+                                                          float* __restrict__ s_vec, float2* __restrict__ s_sc,
                                                           double2* __restrict__ loss_part) {
   constexpr int TPB = kBlock / GS;
   const int tid = threadIdx.x, g = tid % GS;
-  const int nq = kp >> 2, W = kp + 4;
+  const int nq = kp >> 2;
   double loss_acc = 0.0, nloss = 0.0;
   for (int64_t s = (int64_t)blockIdx.x * TPB + tid / GS; s < B; s += (int64_t)gridDim.x * TPB) {
     const int32_t* pi = pairidx + s * R;
@@ -245,7 +249,7 @@ __global__ __launch_bounds__(kBlock) void k_shard_combine(const int32_t* __restr
     for (int o = 0; o < R; ++o) {
       const int32_t ix = pi[o];
       if (ix >= 0) {
-        const float2 t = *reinterpret_cast<const float2*>(part_in + (poff[o] + ix) * W + kp);
+        const float2 t = part_sc[poff[o] + ix];
         vv += (double)t.x;
         wx += (double)t.y;
         any = true;
@@ -258,7 +262,7 @@ __global__ __launch_bounds__(kBlock) void k_shard_combine(const int32_t* __restr
         for (int o = 0; o < R; ++o) {
           const int32_t ix = pi[o];
           if (ix >= 0) {
-            const float4 t = reinterpret_cast<const float4*>(part_in + (poff[o] + ix) * W)[q];
+            const float4 t = reinterpret_cast<const float4*>(part_vec + (poff[o] + ix) * kp)[q];
             a0 += (double)t.x; a1 += (double)t.y; a2 += (double)t.z; a3 += (double)t.w;
           }
         }
@@ -266,7 +270,7 @@ __global__ __launch_bounds__(kBlock) void k_shard_combine(const int32_t* __restr
         const float4 sq = make_float4((float)a0, (float)a1, (float)a2, (float)a3);
         for (int o = 0; o < R; ++o) {
           const int32_t ix = pi[o];
-          if (ix >= 0) reinterpret_cast<float4*>(s_send + (poff[o] + ix) * W)[q] = sq;
+          if (ix >= 0) reinterpret_cast<float4*>(s_vec + (poff[o] + ix) * kp)[q] = sq;
         }
       }
     }
@@ -277,8 +281,7 @@ __global__ __launch_bounds__(kBlock) void k_shard_combine(const int32_t* __restr
       const float y = label[s];
       for (int o = 0; o < R; ++o) {
         const int32_t ix = pi[o];
-        if (ix >= 0)
-          *reinterpret_cast<float4*>(s_send + (poff[o] + ix) * W + kp) = make_float4((float)yhat, y, 0.f, 0.f);
+        if (ix >= 0) s_sc[poff[o] + ix] = make_float2((float)yhat, y);
       }
       if (any) {
         const double d = yhat - (double)y;
@@ -553,19 +556,21 @@ int fm_shard_combine(fm_ctx* ctx, fm_batch* b, const void* partials_in, void* s_
     ctx->work.loss_part.ensure(sizeof(double) * 2 * 256 * 8);  // reserve_work's size: no reallocation later
     const int32_t* pi = S.pairidx.as<int32_t>();
     const int64_t* poff = S.poff.as<int64_t>();
+    const int kp = ctx->kp;
     const float* pin = reinterpret_cast<const float*>(partials_in);
+    const float2* psc = reinterpret_cast<const float2*>(pin ? pin + Ps * kp : nullptr);
     float* so = reinterpret_cast<float*>(s_send);
+    float2* ssc = reinterpret_cast<float2*>(so ? so + Ps * kp : nullptr);
     const float* lab = b->dev.label.as<float>();
     double2* lp = ctx->work.loss_part.as<double2>();
     const double w0 = ctx->cfg.w0;
-    const int kp = ctx->kp;
     const dim3 grid((unsigned)blocks), blk(kBlock);
     switch (GS) {
-      case 1: hipLaunchKernelGGL(k_shard_combine<1>, grid, blk, 0, st, pi, poff, R, B, pin, lab, kp, w0, so, lp); break;
-      case 2: hipLaunchKernelGGL(k_shard_combine<2>, grid, blk, 0, st, pi, poff, R, B, pin, lab, kp, w0, so, lp); break;
-      case 4: hipLaunchKernelGGL(k_shard_combine<4>, grid, blk, 0, st, pi, poff, R, B, pin, lab, kp, w0, so, lp); break;
-      case 8: hipLaunchKernelGGL(k_shard_combine<8>, grid, blk, 0, st, pi, poff, R, B, pin, lab, kp, w0, so, lp); break;
-      default: hipLaunchKernelGGL(k_shard_combine<16>, grid, blk, 0, st, pi, poff, R, B, pin, lab, kp, w0, so, lp); break;
+      case 1: hipLaunchKernelGGL(k_shard_combine<1>, grid, blk, 0, st, pi, poff, R, B, pin, psc, lab, kp, w0, so, ssc, lp); break;
+      case 2: hipLaunchKernelGGL(k_shard_combine<2>, grid, blk, 0, st, pi, poff, R, B, pin, psc, lab, kp, w0, so, ssc, lp); break;
+      case 4: hipLaunchKernelGGL(k_shard_combine<4>, grid, blk, 0, st, pi, poff, R, B, pin, psc, lab, kp, w0, so, ssc, lp); break;
+      case 8: hipLaunchKernelGGL(k_shard_combine<8>, grid, blk, 0, st, pi, poff, R, B, pin, psc, lab, kp, w0, so, ssc, lp); break;
+      default: hipLaunchKernelGGL(k_shard_combine<16>, grid, blk, 0, st, pi, poff, R, B, pin, psc, lab, kp, w0, so, ssc, lp); break;
     }
     FM_HIP_CHECK(hipGetLastError());
     ctx->prof_end("combine", e0, st);
@@ -592,9 +597,8 @@ int fm_shard_owner_update(fm_ctx* ctx, fm_batch* b, const void* s_recv, int32_t 
     double* stats = ctx->loss_hist.as<double>() + 3 * (int64_t)ctx->epoch;
     FM_HIP_CHECK(hipStreamWaitEvent(st, S.ready_upd, 0));
     hipEvent_t e0 = ctx->prof_begin(st);
-    const float* Srow = reinterpret_cast<const float*>(s_recv);
-    const int W = ctx->kp + 4;
-    SegSource src{Srow, W, reinterpret_cast<const float2*>(Srow ? Srow + ctx->kp : nullptr), W / 2};
+    const float* Srow = reinterpret_cast<const float*>(s_recv);  // [P][kp] S, then [P] {yhat, y}
+    SegSource src{Srow, ctx->kp, reinterpret_cast<const float2*>(Srow ? Srow + S.P * ctx->kp : nullptr), 1};
     launch_segment_update(ctx->view(), n, src, ctx->work, p, S.skeys.as<uint32_t>(), S.sents.as<uint2>(),
                           S.loss_blocks, stats, st);
     ctx->prof_end("owner_update", e0, st);

@@ -20,7 +20,7 @@ so the next routing, entry exchange and slot sort overlap the current update.
 Every rank steps its own mini-batch; the iteration's miniBatchSize is the sum over ranks
 (weak scaling: the global batch grows with R).  The result equals one single-table step over
 the ranks' batches concatenated in rank order, up to fp summation order (deterministic for a
-given R).  Only entries (12 B) and two kp + 4 float rows per (sample, owner) pair cross xGMI
+given R).  Only entries (12 B) and twice kp + 2 floats per (sample, owner) pair cross xGMI
 -- no table row or per-id gradient does.
 """
 
@@ -56,7 +56,7 @@ class HipShardEngine:
         N.check(self._lib.fm_set_side_stream(self.ctx.handle, C.c_void_p(self.side_stream.cuda_stream)),
                 "fm_set_side_stream")
         self.kp = (k + 3) // 4 * 4
-        self.width = self.kp + 4
+        self.width = self.kp + 2  # floats per pair on the wire: [P][kp] vectors, then [P][2] scalars
 
     def _empty(self, n, dtype):
         return self.torch.empty(max(int(n), 1), dtype=dtype, device=self.device)[: int(n)]
@@ -191,6 +191,14 @@ class ShardedTrainer:
     def _empty(self, n, dtype):
         return self.torch.empty(max(int(n), 1), dtype=dtype, device=self.device)[: int(n)]
 
+    def _a2a_pairs(self, out, inp, out_pairs, in_pairs):
+        """All-to-all of a pair buffer in the wire layout (include/fm_hip.h): the [P][kp] vector
+        section, then the [P][2] scalar section, each exchanged with its own splits."""
+        kp = self.engine.kp
+        po, pi = int(np.sum(out_pairs)), int(np.sum(in_pairs))
+        self._a2a(out[: po * kp], inp[: pi * kp], out_pairs * kp, in_pairs * kp)
+        self._a2a(out[po * kp:], inp[pi * kp:], out_pairs * 2, in_pairs * 2)
+
     def _side(self):
         side = getattr(self.engine, "side", None)
         return side() if side is not None else contextlib.nullcontext()
@@ -234,10 +242,10 @@ class ShardedTrainer:
         plan = self._plans.pop(id(b))
         partials = self.engine.owner_forward(b, int(plan.pair_in.sum()))
         part_in = self._empty(plan.pair_out.sum() * W, self.torch.float32)
-        self._a2a(part_in, partials, plan.pair_out * W, plan.pair_in * W)
+        self._a2a_pairs(part_in, partials, plan.pair_out, plan.pair_in)
         s_send = self.engine.combine(b, part_in, int(plan.pair_out.sum()))
         s_recv = self._empty(plan.pair_in.sum() * W, self.torch.float32)
-        self._a2a(s_recv, s_send, plan.pair_in * W, plan.pair_out * W)
+        self._a2a_pairs(s_recv, s_send, plan.pair_in, plan.pair_out)
         self.engine.owner_update(b, s_recv, t, step_size, reg_param, gm)
         self._retire(plan)
         if prefetch is not None:

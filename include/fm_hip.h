@@ -218,9 +218,11 @@ int fm_xorshift_next_doubles(int64_t seed, int64_t n, double* out);
  * between phases with all-to-all (RCCL over xGMI; fm_spark_amd/distributed.py).  Replaces the
  * feature-keyed shuffles S1/S2/S5/S6 and the per-sample window of the reference plan
  * (Model.scala:155-164, :191, SGD.scala:148-166).
- * A "pair" is (sample of a source rank, owner holding some of its entries).  Wire rows are fp32,
- * kp + 4 floats per pair (kp = roundup(k, 4)):
- *   partial = [sum v*x (kp) | sum v^2 x^2 | sum w*x | 0 0]     S = [vfxiSum (kp) | yhat | y | 0 0]
+ * A "pair" is (sample of a source rank, owner holding some of its entries).  Wire buffers are fp32
+ * structures of arrays over P pairs, kp + 2 floats per pair (kp = roundup(k, 4)):
+ *   partials = [P][kp] sum v*x, then [P][2] {sum v^2 x^2, sum w*x}
+ *   S        = [P][kp] vfxiSum, then [P][2] {yhat, y}
+ * so the exchange is two all-to-alls per direction (the vector section, the scalar section).
  * Every phase is keyed by `batch`, this rank's mini-batch of the iteration; its state lives with
  * the batch.  Phases 1 and 1b depend on the batch alone and run on the side stream
  * (fm_set_side_stream), so the next iteration's routing, entry exchange and slot sort overlap the

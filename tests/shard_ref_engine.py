@@ -9,6 +9,16 @@ import numpy as np
 import torch
 
 
+def rows_to_soa(rows, kp):
+    """[P][kp + 2] rows -> the wire layout: [P][kp] vectors, then [P][2] scalars (flat)."""
+    return np.ascontiguousarray(np.concatenate([rows[:, :kp].reshape(-1), rows[:, kp:kp + 2].reshape(-1)]))
+
+
+def soa_to_rows(flat, kp):
+    P = len(flat) // (kp + 2)
+    return np.concatenate([flat[: P * kp].reshape(P, kp), flat[P * kp:].reshape(P, 2)], axis=1)
+
+
 class NpBatch:
     def __init__(self, csr):
         self.csr = csr
@@ -21,7 +31,7 @@ class NumpyShardEngine:
         self.device = torch.device("cpu")
         self.F, self.k, self.R, self.rank, self.w0 = num_features, k, world, rank, w0
         self.kp = (k + 3) // 4 * 4
-        self.width = self.kp + 4
+        self.width = self.kp + 2  # wire: [P][kp] vectors, then [P][2] scalars
         self.rows = (num_features - rank + world - 1) // world
         self.w = np.zeros(self.rows)
         self.V = np.zeros((self.rows, k))
@@ -63,8 +73,8 @@ class NumpyShardEngine:
 
     def combine(self, b, partials_in, n_pairs_out):
         csr = b.csr
-        W, kp = self.width, self.kp
-        part = partials_in.numpy().reshape(-1, W).astype(np.float64)
+        kp = self.kp
+        part = soa_to_rows(partials_in.numpy(), kp).astype(np.float64)
         poff = np.concatenate([[0], np.cumsum(b.pairs_out)])
         B = csr.n_rows
         S = np.zeros((B, kp))
@@ -81,14 +91,14 @@ class NumpyShardEngine:
         has = np.diff(csr.row_ptr) > 0
         d = (yhat - csr.label)[has]
         b.loss = (float(np.sum(d * d)), int(has.sum()))
-        out = np.zeros((int(n_pairs_out), W), dtype=np.float32)
+        out = np.zeros((int(n_pairs_out), kp + 2), dtype=np.float32)
         for o in range(self.R):
             ix = b.pairidx[:, o]
             m = ix >= 0
             out[poff[o] + ix[m], :kp] = S[m]
             out[poff[o] + ix[m], kp] = yhat[m]
             out[poff[o] + ix[m], kp + 1] = csr.label[m]
-        return torch.from_numpy(out.reshape(-1))
+        return torch.from_numpy(rows_to_soa(out, kp))
 
     # owner -----------------------------------------------------------------------
     def owner_prepare(self, b, recv_slot, recv_ent, src_entries, src_pairs):
@@ -107,18 +117,18 @@ class NumpyShardEngine:
         P = int(head.sum())
         assert P == int(np.sum(src_pairs)) == n_pairs_in
         V, w = self.V[slots], self.w[slots]
-        part = np.zeros((P, self.width))
+        part = np.zeros((P, self.kp + 2))
         np.add.at(part[:, : self.k], pair, V * x[:, None])
         np.add.at(part[:, self.kp], pair, np.sum(V * V, axis=1) * x * x)
         np.add.at(part[:, self.kp + 1], pair, w * x)
         b.recv = (slots, x, pair)
-        return torch.from_numpy(part.astype(np.float32).reshape(-1))
+        return torch.from_numpy(rows_to_soa(part.astype(np.float32), self.kp))
 
     def owner_update(self, b, s_recv, t, step_size, reg_param, global_rows):
         if global_rows == 0:
             return 1
         slots, x, pair = b.recv
-        Srow = s_recv.numpy().reshape(-1, self.width).astype(np.float64)
+        Srow = soa_to_rows(s_recv.numpy(), self.kp).astype(np.float64)
         S, yhat, y = Srow[pair, : self.k], Srow[pair, self.kp], Srow[pair, self.kp + 1]
         eta = step_size / math.sqrt(t)
         lam = eta * reg_param

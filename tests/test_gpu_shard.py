@@ -22,12 +22,31 @@ def _concat(parts):
                   np.concatenate([p.val for p in parts]), np.concatenate([p.label for p in parts]))
 
 
+def split_pairs(buf, counts, kp):
+    """A pair buffer in the wire layout ([P][kp] vectors, then [P][2] scalars) cut per peer."""
+    import torch
+
+    counts = [int(c) for c in counts]
+    P = sum(counts)
+    vec = torch.split(buf[: P * kp], [c * kp for c in counts])
+    sc = torch.split(buf[P * kp:], [c * 2 for c in counts])
+    return list(zip(vec, sc))
+
+
+def cat_pairs(parts):
+    """Concatenate per-peer pieces back into the wire layout (what an all-to-all delivers)."""
+    import torch
+
+    return torch.cat([v for v, _ in parts] + [s for _, s in parts])
+
+
 def _simulated_step(engines, batches, t, step_size, reg):
     """One iteration of the ShardedTrainer protocol with the all-to-alls done by slicing."""
     import torch
 
     R = len(engines)
     W = engines[0].width
+    kp = engines[0].kp
     routed = [e.route(b) for e, b in zip(engines, batches)]
     ent_cnt = [c[:R] for _, _, c in routed]   # [src][owner]
     pair_cnt = [c[R:] for _, _, c in routed]
@@ -44,15 +63,15 @@ def _simulated_step(engines, batches, t, step_size, reg):
     partials = []
     for o in range(R):
         out = engines[o].owner_forward(batches[o], int(keep[o][2].sum()))
-        partials.append(torch.split(out, (keep[o][2] * W).tolist()))
+        partials.append(split_pairs(out, keep[o][2], kp))
     s_rows = []
     for r in range(R):
-        pin = torch.cat([partials[o][r] for o in range(R)])
+        pin = cat_pairs([partials[o][r] for o in range(R)])
         s = engines[r].combine(batches[r], pin, int(pair_cnt[r].sum()))
-        s_rows.append(torch.split(s, (pair_cnt[r] * W).tolist()))
+        s_rows.append(split_pairs(s, pair_cnt[r], kp))
     gm = sum(int(b.n_rows) for b in batches)
     for o in range(R):
-        engines[o].owner_update(batches[o], torch.cat([s_rows[r][o] for r in range(R)]), t, step_size, reg, gm)
+        engines[o].owner_update(batches[o], cat_pairs([s_rows[r][o] for r in range(R)]), t, step_size, reg, gm)
     torch.cuda.synchronize()
     return sum(e.last_stats()[0] for e in engines), sum(e.last_stats()[2] for e in engines)
 
