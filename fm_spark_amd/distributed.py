@@ -140,15 +140,16 @@ class _Plan:
 
 class ShardedTrainer:
     """Drives one rank of the sharded step.  ``engine`` supplies the phase functions (HIP on a
-    GPU); ``group`` is the torch.distributed process group (nccl = RCCL on ROCm)."""
+    GPU); ``group`` is the torch.distributed process group (nccl = RCCL on ROCm); ``comm`` the
+    module the collectives go through (torch.distributed unless a test stages them)."""
 
     def __init__(self, num_features: int, k: int, *, rank: int, world: int, device: int = 0, seed: int = 0,
-                 init_sd: float = 0.01, w0: float = 0.0, group=None, engine=None):
+                 init_sd: float = 0.01, w0: float = 0.0, group=None, engine=None, comm=None):
         import torch
         import torch.distributed as dist
 
         self.torch = torch
-        self.dist = dist
+        self.dist = comm if comm is not None else dist
         self.rank, self.world = rank, world
         self.group = group
         self.engine = engine if engine is not None else HipShardEngine(
@@ -322,11 +323,11 @@ class ReplicatedTrainer:
     up to fp summation order."""
 
     def __init__(self, num_features: int, k: int, *, rank: int, world: int, device: int = 0, seed: int = 0,
-                 init_sd: float = 0.01, w0: float = 0.0, group=None, engine=None):
+                 init_sd: float = 0.01, w0: float = 0.0, group=None, engine=None, comm=None):
         import torch
         import torch.distributed as dist
 
-        self.torch, self.dist = torch, dist
+        self.torch, self.dist = torch, comm if comm is not None else dist
         self.rank, self.world, self.group = rank, world, group
         self.engine = engine if engine is not None else HipReplEngine(
             num_features, k, device=device, seed=seed, init_sd=init_sd, w0=w0)
