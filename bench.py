@@ -54,10 +54,16 @@ def parse():
     p.add_argument("--features", type=int, default=0, help="override num_features (experiments)")
     p.add_argument("--k", type=int, default=0, help="override k (experiments)")
     p.add_argument("--rows", type=int, default=0, help="override rows per batch (experiments)")
+    p.add_argument("--zipf", type=float, default=0.0, help="override the Zipf exponent (c5's hot rows: 1.2)")
     p.add_argument("--force-sharded", action="store_true",
                    help="run the row-sharded RCCL path even with one rank (tests the N > 1 code path)")
     p.add_argument("--no-prefetch", action="store_true",
                    help="sort each batch inside its own step instead of during the previous step")
+    p.add_argument("--host-path", action="store_true",
+                   help="single table: time fm_step with the host CSR each call (PCIe-inclusive, as a JNI "
+                        "caller sees it) instead of device-resident batches; reported, never the headline")
+    p.add_argument("--prefetch-depth", type=int, default=1,
+                   help="single table: how many steps ahead a batch is sorted on the side stream")
     return p.parse_args()
 
 
@@ -153,9 +159,9 @@ def main():
 
     cfg = CONFIGS[args.config]
     F, k, B, zipf_s, desc = cfg
-    if args.features or args.k or args.rows:
-        F, k, B = args.features or F, args.k or k, args.rows or B
-        desc = f"override F={F} k={k} B={B} ({desc})"
+    if args.features or args.k or args.rows or args.zipf:
+        F, k, B, zipf_s = args.features or F, args.k or k, args.rows or B, args.zipf or zipf_s
+        desc = f"override F={F} k={k} B={B} zipf={zipf_s} ({desc})"
         cfg = (F, k, B, zipf_s, desc)
     t0 = time.perf_counter()
     host_batches = [synthetic_batch(B, F, batch_index=rank * 1000 + i, zipf_s=zipf_s) for i in range(args.batches)]
@@ -183,13 +189,23 @@ def main():
             ctx.profile_reset()
             ctx.profile_enable(True)
         prefetch = not args.no_prefetch
-        t_start = time.perf_counter()
-        if prefetch:
-            dbatches[0].prepare()  # every batch's sort runs inside the timed region
-        for i in range(args.steps):
+        depth = max(1, min(args.prefetch_depth, len(dbatches) - 1))
+        if args.host_path:
+            hosts = [CSRHost(b.row_ptr, b.col, b.val, b.label) for b in host_batches]
+            prefetch = False
+            t_start = time.perf_counter()
+            for i in range(args.steps):
+                t += 1
+                ctx.step(hosts[i % len(hosts)], t, STEP_SIZE, REG_PARAM)
+        else:
+            t_start = time.perf_counter()
+        if prefetch and not args.host_path:
+            for j in range(min(depth, args.steps)):
+                dbatches[j % len(dbatches)].prepare()  # every batch's sort runs inside the timed region
+        for i in range(0 if args.host_path else args.steps):
             t += 1
-            if prefetch and i + 1 < args.steps:
-                dbatches[(i + 1) % len(dbatches)].prepare()  # sorted on the side stream during step i
+            if prefetch and i + depth < args.steps:
+                dbatches[(i + depth) % len(dbatches)].prepare()  # sorted on the side stream during step i
             ctx.step_batch(dbatches[i % len(dbatches)], t, STEP_SIZE, REG_PARAM, sync=False)
         ctx.sync()
         torch.cuda.synchronize()
@@ -199,7 +215,10 @@ def main():
         losses = ctx.loss_history()
         assert os.environ.get("FM_ABLATE") or np.all(np.isfinite(losses)), "non-finite loss"
         U_mean = float(np.mean([uniques[i % len(dbatches)] for i in range(args.steps)]))
-        parallelism = "single table" + (", next batch sorted during the current step" if prefetch else "")
+        parallelism = "single table" + ((", next batch sorted during the current step" if depth == 1 else
+                                         f", batches sorted {depth} steps ahead on the side stream") if prefetch else "")
+        if args.host_path:
+            parallelism += ", host CSR uploaded by fm_step every step (PCIe-inclusive)"
     else:
         from fm_spark_amd.distributed import ShardedTrainer
 

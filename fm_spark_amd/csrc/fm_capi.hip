@@ -5,8 +5,10 @@
 #include <cstdlib>
 #include <cmath>
 #include <cstring>
+#include <atomic>
 #include <map>
 #include <memory>
+#include <thread>
 #include <utility>
 
 #include "fm_context.h"
@@ -30,9 +32,27 @@ void DevBuf::release() {
   bytes = 0;
 }
 
-// Validates and uploads a host CSR.  check_range: ids must be owned by this context's
-// table (training); otherwise any non-negative int32 id is accepted (predict drops
-// unknown ids).
+// f(lo, hi) over [0, n) in contiguous chunks on up to 16 host threads (the GPU box's CPU share per
+// GPU); small ranges run inline.
+template <class F>
+static void parallel_chunks(int64_t n, int64_t min_per_thread, F&& f) {
+  const int64_t hw = std::max<int64_t>(1, (int64_t)std::thread::hardware_concurrency());
+  const int64_t T = std::max<int64_t>(1, std::min<int64_t>({16, hw, n / std::max<int64_t>(min_per_thread, 1)}));
+  if (T <= 1) {
+    f(int64_t(0), n);
+    return;
+  }
+  std::vector<std::thread> th;
+  th.reserve(T);
+  for (int64_t t = 0; t < T; ++t) th.emplace_back([&, t] { f(n * t / T, n * (t + 1) / T); });
+  for (auto& x : th) x.join();
+}
+
+// Validates and uploads a host CSR into b's device buffers (grown, never shrunk).  The exploded
+// entries {sample, x fp32} are built by host threads straight into the context's pinned staging
+// and copied asynchronously on the context's stream; the call returns after the copies (the
+// staging is reused by the next upload).  check_range: ids must be owned by this context's
+// table (training); otherwise any non-negative int32 id is accepted (predict drops unknown ids).
 void upload_batch(fm_ctx* ctx, const fm_csr* c, fm_batch* b, bool check_range) {
   FM_REQUIRE(c != nullptr, "null fm_csr");
   FM_REQUIRE(c->n_rows >= 0 && c->nnz >= 0, "negative n_rows / nnz");
@@ -48,46 +68,72 @@ void upload_batch(fm_ctx* ctx, const fm_csr* c, fm_batch* b, bool check_range) {
   } else {
     FM_REQUIRE(N == 0, "nnz > 0 with n_rows == 0");
   }
-  std::vector<uint32_t> col(N);
-  std::vector<uint32_t> ent(2 * N);  // exploded entries {sample, x bits}
-  std::vector<float> lab(B);
-  int64_t mx = -1;
+  // pinned staging: [row_ptr int64 B+1][label f32 B][col u32 N][ent u32x2 N]
+  const size_t o_lab = sizeof(int64_t) * (B + 1);
+  const size_t o_col = (o_lab + sizeof(float) * B + 15) / 16 * 16;
+  const size_t o_ent = (o_col + sizeof(uint32_t) * N + 15) / 16 * 16;
+  const size_t bytes = o_ent + sizeof(uint32_t) * 2 * N + 16;
+  FM_HIP_CHECK(hipStreamSynchronize(ctx->stream));  // the staging may still feed a queued copy
+  ctx->up_pin.ensure(bytes);
+  char* base = reinterpret_cast<char*>(ctx->up_pin.p);
+  int64_t* rp = reinterpret_cast<int64_t*>(base);
+  float* lab = reinterpret_cast<float*>(base + o_lab);
+  uint32_t* col = reinterpret_cast<uint32_t*>(base + o_col);
+  uint32_t* ent = reinterpret_cast<uint32_t*>(base + o_ent);
+  if (B > 0) std::memcpy(rp, c->row_ptr, sizeof(int64_t) * (B + 1));
+  else rp[0] = 0;
   const int64_t F = ctx->cfg.num_features;
-  for (int64_t e = 0; e < N; ++e) {
-    const int32_t id = c->col[e];
-    FM_REQUIRE(id >= 0, "negative feature id");
-    if (check_range) {
-      FM_REQUIRE(id < F, "feature id >= num_features");
+  std::atomic<int> bad{0};  // 1 negative id, 2 id >= num_features
+  std::atomic<int64_t> mx{-1};
+  parallel_chunks(B, 4096, [&](int64_t r0, int64_t r1) {
+    int64_t lmx = -1;
+    int lbad = 0;
+    for (int64_t i = r0; i < r1; ++i) {
+      lab[i] = (float)c->label[i];
+      for (int64_t e = c->row_ptr[i]; e < c->row_ptr[i + 1]; ++e) {
+        const int32_t id = c->col[e];
+        if (id < 0) lbad |= 1;
+        else if (check_range && id >= F) lbad |= 2;
+        col[e] = (uint32_t)id;
+        lmx = std::max<int64_t>(lmx, id);
+        const float xf = (float)c->val[e];
+        uint32_t xb;
+        std::memcpy(&xb, &xf, 4);
+        ent[2 * e] = (uint32_t)i;
+        ent[2 * e + 1] = xb;
+      }
     }
-    col[e] = (uint32_t)id;
-    mx = std::max<int64_t>(mx, id);
-    const float xf = (float)c->val[e];
-    uint32_t xb;
-    std::memcpy(&xb, &xf, 4);
-    ent[2 * e + 1] = xb;
-  }
-  for (int64_t i = 0; i < B; ++i)
-    for (int64_t e = c->row_ptr[i]; e < c->row_ptr[i + 1]; ++e) ent[2 * e] = (uint32_t)i;
-  for (int64_t i = 0; i < B; ++i) lab[i] = (float)c->label[i];
+    if (lbad) bad.fetch_or(lbad);
+    int64_t cur = mx.load();
+    while (lmx > cur && !mx.compare_exchange_weak(cur, lmx)) {
+    }
+  });
+  FM_REQUIRE(!(bad.load() & 1), "negative feature id");
+  FM_REQUIRE(!(bad.load() & 2), "feature id >= num_features");
   b->owner = ctx;
   b->device = ctx->cfg.device;
-  b->max_id = mx;
+  b->max_id = mx.load();
   b->dev.n_rows = B;
   b->dev.nnz = N;
   b->dev.row_ptr.ensure(sizeof(int64_t) * (B + 1));
   b->dev.col.ensure(sizeof(uint32_t) * std::max<int64_t>(N, 4) + 16);
   b->dev.ent.ensure(sizeof(uint32_t) * 2 * std::max<int64_t>(N, 4) + 16);
   b->dev.label.ensure(sizeof(float) * std::max<int64_t>(B, 4) + 16);
-  if (B > 0) FM_HIP_CHECK(hipMemcpy(b->dev.row_ptr.p, c->row_ptr, sizeof(int64_t) * (B + 1), hipMemcpyHostToDevice));
-  else {
-    const int64_t z = 0;
-    FM_HIP_CHECK(hipMemcpy(b->dev.row_ptr.p, &z, sizeof(int64_t), hipMemcpyHostToDevice));
-  }
+  hipStream_t st = ctx->stream;
+  FM_HIP_CHECK(hipMemcpyAsync(b->dev.row_ptr.p, rp, sizeof(int64_t) * (B + 1), hipMemcpyHostToDevice, st));
   if (N > 0) {
-    FM_HIP_CHECK(hipMemcpy(b->dev.col.p, col.data(), sizeof(uint32_t) * N, hipMemcpyHostToDevice));
-    FM_HIP_CHECK(hipMemcpy(b->dev.ent.p, ent.data(), sizeof(uint32_t) * 2 * N, hipMemcpyHostToDevice));
+    FM_HIP_CHECK(hipMemcpyAsync(b->dev.col.p, col, sizeof(uint32_t) * N, hipMemcpyHostToDevice, st));
+    FM_HIP_CHECK(hipMemcpyAsync(b->dev.ent.p, ent, sizeof(uint32_t) * 2 * N, hipMemcpyHostToDevice, st));
   }
-  if (B > 0) FM_HIP_CHECK(hipMemcpy(b->dev.label.p, lab.data(), sizeof(float) * B, hipMemcpyHostToDevice));
+  if (B > 0) FM_HIP_CHECK(hipMemcpyAsync(b->dev.label.p, lab, sizeof(float) * B, hipMemcpyHostToDevice, st));
+  FM_HIP_CHECK(hipStreamSynchronize(st));
+}
+
+// The context's reusable batch for the host-buffer entry points (fm_step, fm_predict,
+// fm_loss_grad): its device buffers persist across calls.
+fm_batch* host_batch(fm_ctx* ctx) {
+  if (!ctx->host_batch) ctx->host_batch.reset(new fm_batch());
+  return ctx->host_batch.get();
 }
 
 void reserve_work(fm_ctx* ctx, int64_t B, int64_t N) {
@@ -431,11 +477,10 @@ int fm_step(fm_ctx* ctx, const fm_csr* csr, int32_t t, double step_size, double 
       }
       return FM_NOTHING_TO_DO;
     }
-    std::unique_ptr<fm_batch> b(new fm_batch());
-    upload_batch(ctx, csr, b.get(), true);
+    fm_batch* b = host_batch(ctx);
+    upload_batch(ctx, csr, b, true);
     fm_step_out tmp;
-    const int rc = step_impl(ctx, b.get(), t, step_size, reg_param, out ? out : &tmp);
-    return rc;
+    return step_impl(ctx, b, t, step_size, reg_param, out ? out : &tmp);
   });
 }
 
@@ -458,8 +503,8 @@ int fm_predict(fm_ctx* ctx, const fm_csr* csr, double lo, double hi, double* pre
   return guarded(ctx, [&]() -> int {
     FM_REQUIRE(csr != nullptr && (csr->n_rows == 0 || pred), "null argument");
     if (csr->n_rows == 0) return FM_OK;
-    std::unique_ptr<fm_batch> b(new fm_batch());
-    upload_batch(ctx, csr, b.get(), false);
+    fm_batch* b = host_batch(ctx);
+    upload_batch(ctx, csr, b, false);
     DevBuf dp;
     dp.ensure(sizeof(double) * csr->n_rows);
     launch_predict(ctx->view(), b->dev, ctx->cum_host.back(), ctx->cfg.w0, lo, hi, dp.as<double>(), ctx->stream);
@@ -511,8 +556,8 @@ int fm_loss_grad(fm_ctx* ctx, const fm_csr* csr, double* pred, double* loss, dou
   return guarded(ctx, [&]() -> int {
     FM_REQUIRE(csr != nullptr, "null argument");
     if (csr->n_rows == 0 || csr->nnz == 0) return FM_OK;
-    std::unique_ptr<fm_batch> b(new fm_batch());
-    upload_batch(ctx, csr, b.get(), true);
+    fm_batch* b = host_batch(ctx);
+    upload_batch(ctx, csr, b, true);
     const int64_t N = csr->nnz;
     const int k = ctx->cfg.k;
     DevBuf dpred, dloss, ddw, ddv, dabs;

@@ -116,6 +116,8 @@ struct fm_ctx {
   int64_t hist_cap = 0;
   StepWork work;
   Pinned pinned;
+  Pinned up_pin;                         // host CSR upload staging (upload_batch)
+  std::unique_ptr<fm_batch> host_batch;  // reused by fm_step / fm_predict / fm_loss_grad
   // profiling
   bool prof = false;
   std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> pending;
