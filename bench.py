@@ -303,7 +303,7 @@ def main():
             line["step_roofline"] = {"bytes_per_step": step_bytes,
                                      "achieved_GBs": step_bytes / (ms_per_step * 1e-3) / 1e9,
                                      "frac": step_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS}
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and world == 1:  # the CPU baseline belongs to the N = 1 line
             try:
                 line["cpu_baseline"] = cpu_baseline(cfg, host_batches[0], args.cpu_steps)
             except Exception as e:  # reported, never silently replaced
