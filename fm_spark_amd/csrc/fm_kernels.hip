@@ -78,8 +78,14 @@ __device__ __forceinline__ void current_row(const RowHdr& h, float4& v, float& w
 // feature scores globalBias unclamped (na.fill, :86), every other row
 // least(greatest(yhat, minLabel), maxLabel) (:129-132), fp64 into pred_out.
 constexpr int kTrain = 0, kPartial = 1, kPredict = 2;
+#ifndef FM_FWD_U
+#define FM_FWD_U 4  // passes (entries per lane) whose rows are in flight together
+#endif
+#ifndef FM_FWD_MINW
+#define FM_FWD_MINW 1  // waves per SIMD the register allocation must allow
+#endif
 template <int GS, int TEAM, int MODE>
-__global__ __launch_bounds__(kBlock) void k_forward(TableView T, const int64_t* __restrict__ row_ptr,
+__global__ __launch_bounds__(kBlock, FM_FWD_MINW) void k_forward(TableView T, const int64_t* __restrict__ row_ptr,
                                                     const uint32_t* __restrict__ col,
                                                     const uint2* __restrict__ ent,
                                                     const float* __restrict__ label, int64_t B,
@@ -89,7 +95,7 @@ __global__ __launch_bounds__(kBlock) void k_forward(TableView T, const int64_t* 
   constexpr bool PARTIAL = MODE == kPartial;
   constexpr int RPP = TEAM / GS;  // entries per pass
   constexpr int TPB = kBlock / TEAM;
-  constexpr int U = 4;            // passes in flight
+  constexpr int U = FM_FWD_U;     // passes in flight
   const int tid = threadIdx.x;
   const int tl = tid % TEAM;
   const int g = tl % GS;
