@@ -1,0 +1,27 @@
+"""CPU: the library's host-only C++ (libsvm reader, randomSplit replay, MurmurHash3 / XORShift)
+built from the product sources with g++ -fsanitize=address,undefined and exercised by
+tests/native/host_sanitize.cpp (malformed inputs, too-small buffers, the SMHasher value)."""
+
+import os
+import shutil
+import subprocess
+
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="g++ not available")
+def test_host_code_under_asan_ubsan(tmp_path):
+    exe = tmp_path / "host_sanitize"
+    srcs = [os.path.join(HERE, "native", "host_sanitize.cpp"),
+            os.path.join(ROOT, "fm_spark_amd", "csrc", "fm_sampler.cpp"),
+            os.path.join(ROOT, "fm_spark_amd", "csrc", "fm_libsvm.cpp")]
+    subprocess.run(["g++", "-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined",
+                    "-fno-sanitize-recover=all", *srcs, "-o", str(exe)], check=True)
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0", UBSAN_OPTIONS="print_stacktrace=1")
+    env.pop("LD_PRELOAD", None)
+    r = subprocess.run([str(exe), str(tmp_path)], capture_output=True, text=True, env=env, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "0 failure(s)" in r.stdout
