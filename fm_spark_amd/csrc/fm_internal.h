@@ -130,17 +130,24 @@ struct StepParams {
   double w0;
 };
 
-// predict mode of the forward: clamp bounds and the fp64 output per sample
-struct PredictOut {
-  double lo, hi;
-  double* pred;
+// the forward's inference modes (fm_kernels.hip): 2 = predict (clamp bounds, fp64 score per
+// sample into pred), 3 = calcLossGrad (fp64 pred / loss / dw per entry, dv [entries][k], the
+// absent-id flag)
+struct FwdOut {
+  int mode = 0;
+  double lo = 0.0, hi = 0.0;
+  double* pred = nullptr;
+  double* loss = nullptr;
+  double* dw = nullptr;
+  double* dv = nullptr;
+  int32_t* absent = nullptr;
 };
 // partial_out != nullptr: the sharded owner's partial pass (fm_shard.hip): [pairs][kp] vectors
 // followed by [pairs] float2 scalars;
 // pred != nullptr: FactorizationMachinesModel.predict (p.w0, p.cumE used)
 void launch_forward(const TableView& T, const BatchDev& b, StepWork& w, const StepParams& p,
                     hipStream_t st, int64_t* n_fwd_blocks, float* partial_out = nullptr,
-                    const PredictOut* pred = nullptr);
+                    const FwdOut* pred = nullptr);
 // per-sample inputs of the segmented update: S rows of s_stride floats, {yhat, y} at yl[s * yl_stride]
 struct SegSource {
   const float* S;

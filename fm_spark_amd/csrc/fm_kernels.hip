@@ -77,7 +77,10 @@ __device__ __forceinline__ void current_row(const RowHdr& h, float4& v, float& w
 // or absent from the model are dropped (the inner joins, :103-112), a row left without a learned
 // feature scores globalBias unclamped (na.fill, :86), every other row
 // least(greatest(yhat, minLabel), maxLabel) (:129-132), fp64 into pred_out.
-constexpr int kTrain = 0, kPartial = 1, kPredict = 2;
+// MODE kLossGrad: calcLossGrad's per-entry columns (Model.scala:225-233): the sample's yhat, its
+// squared error, deltaWi = x and deltaVi = vfxiSum * x - (v * x) * x, fp64 from the team's fp64
+// sums (a second walk over the sample's entries re-reads their rows); absent ids set the flag.
+constexpr int kTrain = 0, kPartial = 1, kPredict = 2, kLossGrad = 3;
 #ifndef FM_FWD_U
 #define FM_FWD_U 4  // passes (entries per lane) whose rows are in flight together
 #endif
@@ -91,7 +94,7 @@ __global__ __launch_bounds__(kBlock, FM_FWD_MINW) void k_forward(TableView T, co
                                                     const float* __restrict__ label, int64_t B,
                                                     double w0, double cumE, float* __restrict__ S_out,
                                                     float2* __restrict__ yl_out, double2* __restrict__ loss_part,
-                                                    double lo, double hi, double* __restrict__ pred_out) {
+                                                    FwdOut xo) {
   constexpr bool PARTIAL = MODE == kPartial;
   constexpr int RPP = TEAM / GS;  // entries per pass
   constexpr int TPB = kBlock / TEAM;
@@ -172,7 +175,32 @@ __global__ __launch_bounds__(kBlock, FM_FWD_MINW) void k_forward(TableView T, co
     // sumVx + wixiSum + w0 (Model.scala:221, :260-262)
     const double yhat = 0.5 * (ss - vv) + wx + w0;
     if (MODE == kPredict) {
-      if (tl == 0) pred_out[s] = npres == 0 ? w0 : fmin(fmax(yhat, lo), hi);
+      if (tl == 0) xo.pred[s] = npres == 0 ? w0 : fmin(fmax(yhat, xo.lo), xo.hi);
+      continue;
+    }
+    if (MODE == kLossGrad) {
+      const double d = yhat - (double)label[s];
+      const int k = T.k;
+      for (int64_t e = e0 + rs; e < e1; e += RPP) {
+        const uint32_t id = col[e];
+        const double xd = (double)__uint_as_float(ent[e].y);
+        const RowHdr h = *T.hdr(id);
+        float4 v = qok ? reinterpret_cast<const float4*>(T.v(id))[g] : make_float4(0.f, 0.f, 0.f, 0.f);
+        float w;
+        current_row(h, v, w, cumE);
+        if (g == 0) {
+          if (h.t < 0) *xo.absent = 1;
+          xo.pred[e] = yhat;    // prediction (Model.scala:221)
+          xo.loss[e] = d * d;   // pow(pred - label, 2.0) (:230)
+          xo.dw[e] = xd;        // deltaWi (:200)
+        }
+        double* out = xo.dv + e * k;  // deltaVi (:201-204), columns 4g .. 4g + 3 of k
+        const int c = 4 * g;
+        if (c + 0 < k) out[c + 0] = a0 * xd - ((double)v.x * xd) * xd;
+        if (c + 1 < k) out[c + 1] = a1 * xd - ((double)v.y * xd) * xd;
+        if (c + 2 < k) out[c + 2] = a2 * xd - ((double)v.z * xd) * xd;
+        if (c + 3 < k) out[c + 3] = a3 * xd - ((double)v.w * xd) * xd;
+      }
       continue;
     }
     if (rs == 0 && qok)
@@ -855,59 +883,6 @@ __global__ void k_count_present(TableView T, unsigned long long* out) {
   if ((threadIdx.x & 63) == 0 && c) atomicAdd(out, c);
 }
 
-// calcLossGrad per-entry outputs (Model.scala:135-234), one thread per sample.
-__global__ void k_loss_grad(TableView T, const int64_t* __restrict__ row_ptr, const uint32_t* __restrict__ col,
-                            const uint2* __restrict__ ent, const float* __restrict__ label, int64_t B,
-                            double cumE, double w0, double* pred, double* loss, double* dw, double* dv,
-                            int32_t* absent) {
-  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < B; s += (int64_t)gridDim.x * blockDim.x) {
-    double acc[64];
-    for (int f = 0; f < 64; ++f) acc[f] = 0.0;
-    double wx = 0.0, vv = 0.0;
-    const int64_t e0 = row_ptr[s], e1 = row_ptr[s + 1];
-    for (int64_t e = e0; e < e1; ++e) {
-      const int64_t id = col[e];
-      const RowHdr h = (*T.hdr(id));
-      if (h.t < 0) {
-        *absent = 1;
-        continue;
-      }
-      const double a = cumE - h.cum;
-      const double x = (double)__uint_as_float(ent[e].y);
-      const float w = a > 0.0 ? shrink_f(h.w, a) : h.w;
-      wx += (double)w * x;
-      double v2 = 0.0;
-      for (int f = 0; f < T.k; ++f) {
-        float v = T.v(id)[f];
-        if (a > 0.0) v = shrink_f(v, a);
-        acc[f & 63] += (double)v * x;
-        v2 += (double)v * v;
-      }
-      vv += v2 * x * x;
-    }
-    double ss = 0.0;
-    for (int f = 0; f < T.k; ++f) ss += acc[f] * acc[f];
-    const double yhat = 0.5 * (ss - vv) + wx + w0;
-    const double d = yhat - (double)label[s];
-    for (int64_t e = e0; e < e1; ++e) {
-      const int64_t id = col[e];
-      const RowHdr h = (*T.hdr(id));
-      const double x = (double)__uint_as_float(ent[e].y);
-      if (pred) pred[e] = yhat;
-      if (loss) loss[e] = d * d;
-      if (dw) dw[e] = x;
-      if (dv) {
-        const double a = h.t >= 0 ? cumE - h.cum : 0.0;
-        for (int f = 0; f < T.k; ++f) {
-          float v = h.t >= 0 ? T.v(id)[f] : 0.f;
-          if (a > 0.0) v = shrink_f(v, a);
-          dv[e * T.k + f] = acc[f & 63] * x - ((double)v * x) * x;
-        }
-      }
-    }
-  }
-}
-
 // groupBy(key).agg(VectorSum(vec)) on sorted keys: each run summed sequentially in input
 // order (the stable sort keeps it), FactorizationMachines.scala:56-67.
 __global__ void k_segment_sum(const uint32_t* __restrict__ skeys, const uint32_t* __restrict__ svals, int64_t n,
@@ -963,29 +938,36 @@ inline unsigned grid_for(int64_t n, int block, int64_t cap = 256 * 16) {
 
 template <int GS, int TEAM>
 void launch_fwd_t(const TableView& T, const BatchDev& b, StepWork& w, const StepParams& p, hipStream_t st,
-                  int64_t* nblk, float* partial_out, const PredictOut* pred) {
+                  int64_t* nblk, float* partial_out, const FwdOut* xo) {
   constexpr int TPB = kBlock / TEAM;
   int64_t blocks = (b.n_rows + TPB - 1) / TPB;
   if (blocks > 256 * 8) blocks = 256 * 8;
   if (blocks < 1) blocks = 1;
   *nblk = blocks;
   const dim3 grid((unsigned)blocks), blk(kBlock);
-  if (pred) {
+  const FwdOut none{};
+  if (xo && xo->mode == kPredict) {
     hipLaunchKernelGGL((k_forward<GS, TEAM, kPredict>), grid, blk, 0, st, T, b.row_ptr.as<int64_t>(),
                        b.col.as<uint32_t>(), b.ent.as<uint2>(), nullptr, b.n_rows, p.w0, p.cumE, nullptr, nullptr,
-                       nullptr, pred->lo, pred->hi, pred->pred);
+                       nullptr, *xo);
+    return;
+  }
+  if (xo && xo->mode == kLossGrad) {
+    hipLaunchKernelGGL((k_forward<GS, TEAM, kLossGrad>), grid, blk, 0, st, T, b.row_ptr.as<int64_t>(),
+                       b.col.as<uint32_t>(), b.ent.as<uint2>(), b.label.as<float>(), b.n_rows, p.w0, p.cumE, nullptr,
+                       nullptr, nullptr, *xo);
     return;
   }
   if (partial_out) {  // [n_rows][kp] vectors, then [n_rows] float2 scalars
     hipLaunchKernelGGL((k_forward<GS, TEAM, kPartial>), grid, blk, 0, st, T, b.row_ptr.as<int64_t>(),
                        b.col.as<uint32_t>(), b.ent.as<uint2>(), nullptr, b.n_rows, p.w0, p.cumE, partial_out,
-                       reinterpret_cast<float2*>(partial_out + b.n_rows * T.kp), nullptr, 0.0, 0.0, nullptr);
+                       reinterpret_cast<float2*>(partial_out + b.n_rows * T.kp), nullptr, none);
     return;
   }
   w.loss_part.ensure(sizeof(double2) * blocks);
   hipLaunchKernelGGL((k_forward<GS, TEAM, kTrain>), grid, blk, 0, st, T, b.row_ptr.as<int64_t>(),
                      b.col.as<uint32_t>(), b.ent.as<uint2>(), b.label.as<float>(), b.n_rows, p.w0, p.cumE,
-                     w.S.as<float>(), w.yl.as<float2>(), w.loss_part.as<double2>(), 0.0, 0.0, nullptr);
+                     w.S.as<float>(), w.yl.as<float2>(), w.loss_part.as<double2>(), none);
 }
 
 }  // namespace
@@ -1002,7 +984,7 @@ void launch_partial_t(const TableView& T, const BatchDev& b, StepWork& w, const 
 }
 
 void launch_forward(const TableView& T, const BatchDev& b, StepWork& w, const StepParams& p, hipStream_t st,
-                    int64_t* nblk, float* partial_out, const PredictOut* pred) {
+                    int64_t* nblk, float* partial_out, const FwdOut* pred) {
   const int nq = T.kp / 4;
   if (partial_out && !pred) {
     if (nq <= 1) launch_partial_t<1>(T, b, w, p, st, nblk, partial_out);
@@ -1145,21 +1127,33 @@ void launch_predict(const TableView& T, const BatchDev& b, double cumE, double w
   StepParams p{};
   p.cumE = cumE;
   p.w0 = w0;
-  PredictOut po{lo, hi, pred};
+  FwdOut xo{};
+  xo.mode = kPredict;
+  xo.lo = lo;
+  xo.hi = hi;
+  xo.pred = pred;
   StepWork unused;
   int64_t nblk = 0;
-  launch_forward(T, b, unused, p, st, &nblk, nullptr, &po);
+  launch_forward(T, b, unused, p, st, &nblk, nullptr, &xo);
 }
 
 void launch_loss_grad(const TableView& T, const BatchDev& b, double cumE, double w0, double* pred, double* loss,
                       double* dw, double* dv, int32_t* absent_flag, hipStream_t st) {
-  FM_REQUIRE(T.k <= 64, "fm_loss_grad supports dimFactorization <= 64");
   FM_REQUIRE(T.shard_count == 1, "fm_loss_grad needs the whole table (shard_count == 1)");
   if (b.n_rows <= 0) return;
-  hipLaunchKernelGGL(k_loss_grad, dim3(grid_for(b.n_rows, kBlock)), dim3(kBlock), 0, st, T,
-                     b.row_ptr.as<int64_t>(), b.col.as<uint32_t>(), b.ent.as<uint2>(), b.label.as<float>(),
-                     b.n_rows, cumE, w0, pred, loss, dw, dv, absent_flag);
-  FM_HIP_CHECK(hipGetLastError());
+  StepParams p{};
+  p.cumE = cumE;
+  p.w0 = w0;
+  FwdOut xo{};
+  xo.mode = kLossGrad;
+  xo.pred = pred;
+  xo.loss = loss;
+  xo.dw = dw;
+  xo.dv = dv;
+  xo.absent = absent_flag;
+  StepWork unused;
+  int64_t nblk = 0;
+  launch_forward(T, b, unused, p, st, &nblk, nullptr, &xo);
 }
 
 void launch_segment_sum(const uint32_t* skeys, const uint32_t* svals, int64_t n, const double* vecs, int32_t k,

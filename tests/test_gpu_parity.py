@@ -101,13 +101,15 @@ def test_vector_sum_by_key_many(gpu):
     assert np.array_equal(gs, rs)  # same sequential order -> bitwise
 
 
-def test_loss_grad_matches_oracle(gpu):
+@pytest.mark.parametrize("k", [5, 16, 80])
+def test_loss_grad_matches_oracle(gpu, k):
+    """calcLossGrad on the team forward kernel (loss-grad mode; k = 80 beyond the old kernel's 64)."""
     from fm_spark_amd.engine import FMContext
 
-    csr, ids, w, V = make_problem(5, 300, 60, 5, 6)
-    model = R.Model.empty(60, 5)
+    csr, ids, w, V = make_problem(5, 300, 60, k, 6)
+    model = R.Model.empty(60, k)
     model.load(ids, w, V)
-    ctx = FMContext(60, 5)
+    ctx = FMContext(60, k)
     ctx.load_tables(ids, w, V)
     gp, gl, gdw, gdv = ctx.loss_grad(to_host(csr))
     rp, rl, rdw, rdv = R.loss_grad(model, csr)
