@@ -119,7 +119,7 @@ def test_loss_grad_matches_oracle(gpu, k):
     np.testing.assert_allclose(gdv, rdv, rtol=1e-5, atol=1e-9)
 
 
-@pytest.mark.parametrize("k", [1, 3, 4, 8, 10, 16, 32, 48, 72, 136])
+@pytest.mark.parametrize("k", [1, 2, 3, 4, 8, 10, 16, 32, 48, 72, 136, 256])
 def test_step_parity_k(gpu, k):
     F = 97
     batches = []
