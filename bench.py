@@ -196,7 +196,7 @@ def main():
             t_start = time.perf_counter()
             for i in range(args.steps):
                 t += 1
-                ctx.step(hosts[i % len(hosts)], t, STEP_SIZE, REG_PARAM)
+                ctx.step(hosts[i % len(hosts)], t, STEP_SIZE, REG_PARAM, sync=False)
         else:
             t_start = time.perf_counter()
         if prefetch and not args.host_path:

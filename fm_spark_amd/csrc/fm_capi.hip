@@ -20,6 +20,9 @@ void set_error(const std::string& msg) { g_last_error = msg; }
 
 void DevBuf::ensure(size_t n) {
   if (n <= bytes && p) return;
+  // growing: work already queued on any stream may still read the old buffer (asynchronous
+  // steps), so the device drains before it is freed
+  if (p) FM_HIP_CHECK(hipDeviceSynchronize());
   release();
   if (n == 0) n = 16;
   FM_HIP_CHECK(hipMalloc(&p, n));
@@ -48,19 +51,26 @@ static void parallel_chunks(int64_t n, int64_t min_per_thread, F&& f) {
   for (auto& x : th) x.join();
 }
 
-// Validates and uploads a host CSR into b's device buffers (grown, never shrunk).  The exploded
-// entries {sample, x fp32} are built by host threads straight into the context's pinned staging
-// and copied asynchronously on the context's stream; the call returns after the copies (the
-// staging is reused by the next upload).  check_range: ids must be owned by this context's
-// table (training); otherwise any non-negative int32 id is accepted (predict drops unknown ids).
-void upload_batch(fm_ctx* ctx, const fm_csr* c, fm_batch* b, bool check_range) {
+// Host CSR -> the device batch layout in pinned staging: [row_ptr int64 B+1][label f32 B]
+// [col u32 N][ent u32x2 N] (ent = the exploded {sample, x fp32}).  Validated on the way; host
+// threads write the staging directly.  check_range: ids must be owned by this context's table
+// (training); otherwise any non-negative int32 id is accepted (predict drops unknown ids).
+struct Staged {
+  int64_t B = 0, N = 0, max_id = -1;
+  size_t o_lab = 0, o_col = 0, o_ent = 0;
+};
+
+static Staged stage_csr(fm_ctx* ctx, const fm_csr* c, bool check_range, Pinned& pin) {
   FM_REQUIRE(c != nullptr, "null fm_csr");
   FM_REQUIRE(c->n_rows >= 0 && c->nnz >= 0, "negative n_rows / nnz");
   FM_REQUIRE(c->n_rows < (int64_t(1) << 31), "n_rows must be < 2^31");
   FM_REQUIRE(c->nnz < (int64_t(1) << 31), "nnz must be < 2^31 per batch");
   FM_REQUIRE(c->n_rows == 0 || (c->row_ptr && c->label), "null row_ptr / label");
   FM_REQUIRE(c->nnz == 0 || (c->col && c->val), "null col / val");
+  Staged g;
   const int64_t B = c->n_rows, N = c->nnz;
+  g.B = B;
+  g.N = N;
   if (B > 0) {
     FM_REQUIRE(c->row_ptr[0] == 0, "row_ptr[0] must be 0");
     FM_REQUIRE(c->row_ptr[B] == N, "row_ptr[n_rows] must equal nnz");
@@ -68,18 +78,15 @@ void upload_batch(fm_ctx* ctx, const fm_csr* c, fm_batch* b, bool check_range) {
   } else {
     FM_REQUIRE(N == 0, "nnz > 0 with n_rows == 0");
   }
-  // pinned staging: [row_ptr int64 B+1][label f32 B][col u32 N][ent u32x2 N]
-  const size_t o_lab = sizeof(int64_t) * (B + 1);
-  const size_t o_col = (o_lab + sizeof(float) * B + 15) / 16 * 16;
-  const size_t o_ent = (o_col + sizeof(uint32_t) * N + 15) / 16 * 16;
-  const size_t bytes = o_ent + sizeof(uint32_t) * 2 * N + 16;
-  FM_HIP_CHECK(hipStreamSynchronize(ctx->stream));  // the staging may still feed a queued copy
-  ctx->up_pin.ensure(bytes);
-  char* base = reinterpret_cast<char*>(ctx->up_pin.p);
+  g.o_lab = sizeof(int64_t) * (B + 1);
+  g.o_col = (g.o_lab + sizeof(float) * B + 15) / 16 * 16;
+  g.o_ent = (g.o_col + sizeof(uint32_t) * N + 15) / 16 * 16;
+  pin.ensure(g.o_ent + sizeof(uint32_t) * 2 * N + 16);
+  char* base = reinterpret_cast<char*>(pin.p);
   int64_t* rp = reinterpret_cast<int64_t*>(base);
-  float* lab = reinterpret_cast<float*>(base + o_lab);
-  uint32_t* col = reinterpret_cast<uint32_t*>(base + o_col);
-  uint32_t* ent = reinterpret_cast<uint32_t*>(base + o_ent);
+  float* lab = reinterpret_cast<float*>(base + g.o_lab);
+  uint32_t* col = reinterpret_cast<uint32_t*>(base + g.o_col);
+  uint32_t* ent = reinterpret_cast<uint32_t*>(base + g.o_ent);
   if (B > 0) std::memcpy(rp, c->row_ptr, sizeof(int64_t) * (B + 1));
   else rp[0] = 0;
   const int64_t F = ctx->cfg.num_features;
@@ -110,26 +117,48 @@ void upload_batch(fm_ctx* ctx, const fm_csr* c, fm_batch* b, bool check_range) {
   });
   FM_REQUIRE(!(bad.load() & 1), "negative feature id");
   FM_REQUIRE(!(bad.load() & 2), "feature id >= num_features");
+  g.max_id = mx.load();
+  return g;
+}
+
+static bool batch_fits(const fm_batch* b, const Staged& g) {
+  return b->dev.row_ptr.bytes >= sizeof(int64_t) * (g.B + 1) &&
+         b->dev.col.bytes >= sizeof(uint32_t) * std::max<int64_t>(g.N, 4) + 16 &&
+         b->dev.ent.bytes >= sizeof(uint32_t) * 2 * std::max<int64_t>(g.N, 4) + 16 &&
+         b->dev.label.bytes >= sizeof(float) * std::max<int64_t>(g.B, 4) + 16;
+}
+
+// b's device buffers (grown, never shrunk) filled from the staging by async copies on st.
+static void copy_staged(fm_ctx* ctx, const Staged& g, const Pinned& pin, fm_batch* b, hipStream_t st) {
+  const int64_t B = g.B, N = g.N;
   b->owner = ctx;
   b->device = ctx->cfg.device;
-  b->max_id = mx.load();
+  b->max_id = g.max_id;
   b->dev.n_rows = B;
   b->dev.nnz = N;
   b->dev.row_ptr.ensure(sizeof(int64_t) * (B + 1));
   b->dev.col.ensure(sizeof(uint32_t) * std::max<int64_t>(N, 4) + 16);
   b->dev.ent.ensure(sizeof(uint32_t) * 2 * std::max<int64_t>(N, 4) + 16);
   b->dev.label.ensure(sizeof(float) * std::max<int64_t>(B, 4) + 16);
-  hipStream_t st = ctx->stream;
-  FM_HIP_CHECK(hipMemcpyAsync(b->dev.row_ptr.p, rp, sizeof(int64_t) * (B + 1), hipMemcpyHostToDevice, st));
+  const char* base = reinterpret_cast<const char*>(pin.p);
+  FM_HIP_CHECK(hipMemcpyAsync(b->dev.row_ptr.p, base, sizeof(int64_t) * (B + 1), hipMemcpyHostToDevice, st));
   if (N > 0) {
-    FM_HIP_CHECK(hipMemcpyAsync(b->dev.col.p, col, sizeof(uint32_t) * N, hipMemcpyHostToDevice, st));
-    FM_HIP_CHECK(hipMemcpyAsync(b->dev.ent.p, ent, sizeof(uint32_t) * 2 * N, hipMemcpyHostToDevice, st));
+    FM_HIP_CHECK(hipMemcpyAsync(b->dev.col.p, base + g.o_col, sizeof(uint32_t) * N, hipMemcpyHostToDevice, st));
+    FM_HIP_CHECK(hipMemcpyAsync(b->dev.ent.p, base + g.o_ent, sizeof(uint32_t) * 2 * N, hipMemcpyHostToDevice, st));
   }
-  if (B > 0) FM_HIP_CHECK(hipMemcpyAsync(b->dev.label.p, lab, sizeof(float) * B, hipMemcpyHostToDevice, st));
-  FM_HIP_CHECK(hipStreamSynchronize(st));
+  if (B > 0) FM_HIP_CHECK(hipMemcpyAsync(b->dev.label.p, base + g.o_lab, sizeof(float) * B, hipMemcpyHostToDevice, st));
 }
 
-// The context's reusable batch for the host-buffer entry points (fm_step, fm_predict,
+// Synchronous upload (fm_batch_create, fm_predict, fm_loss_grad): staged in the context's
+// pinned buffer, copied on the context's stream, returns after the copies.
+void upload_batch(fm_ctx* ctx, const fm_csr* c, fm_batch* b, bool check_range) {
+  FM_HIP_CHECK(hipStreamSynchronize(ctx->stream));  // the staging / b may still feed queued work
+  const Staged g = stage_csr(ctx, c, check_range, ctx->up_pin);
+  copy_staged(ctx, g, ctx->up_pin, b, ctx->stream);
+  FM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+}
+
+// The context's reusable batch for the synchronous host-buffer entry points (fm_predict,
 // fm_loss_grad): its device buffers persist across calls.
 fm_batch* host_batch(fm_ctx* ctx) {
   if (!ctx->host_batch) ctx->host_batch.reset(new fm_batch());
@@ -477,10 +506,28 @@ int fm_step(fm_ctx* ctx, const fm_csr* csr, int32_t t, double step_size, double 
       }
       return FM_NOTHING_TO_DO;
     }
-    fm_batch* b = host_batch(ctx);
-    upload_batch(ctx, csr, b, true);
-    fm_step_out tmp;
-    return step_impl(ctx, b, t, step_size, reg_param, out ? out : &tmp);
+    // two upload slots used in turn: while the device runs step i from one slot, the host explodes
+    // batch i + 1 into the other slot's pinned staging and its copies queue on the copy stream
+    HostSlot& h = ctx->hslot[ctx->hnext];
+    ctx->hnext ^= 1;
+    if (!h.batch) {
+      h.batch.reset(new fm_batch());
+      FM_HIP_CHECK(hipEventCreateWithFlags(&h.copied, hipEventDisableTiming));
+      FM_HIP_CHECK(hipEventCreateWithFlags(&h.consumed, hipEventDisableTiming));
+      FM_HIP_CHECK(hipEventRecord(h.copied, ctx->stream));
+      FM_HIP_CHECK(hipEventRecord(h.consumed, ctx->stream));
+    }
+    if (!ctx->copy_stream) FM_HIP_CHECK(hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking));
+    FM_HIP_CHECK(hipEventSynchronize(h.copied));  // the slot's staging has been copied out
+    const Staged g = stage_csr(ctx, csr, true, h.pin);
+    if (!batch_fits(h.batch.get(), g)) FM_HIP_CHECK(hipEventSynchronize(h.consumed));  // before reallocating
+    FM_HIP_CHECK(hipStreamWaitEvent(ctx->copy_stream, h.consumed, 0));  // the slot's last step read it
+    copy_staged(ctx, g, h.pin, h.batch.get(), ctx->copy_stream);
+    FM_HIP_CHECK(hipEventRecord(h.copied, ctx->copy_stream));
+    FM_HIP_CHECK(hipStreamWaitEvent(ctx->stream, h.copied, 0));
+    const int rc = step_impl(ctx, h.batch.get(), t, step_size, reg_param, out);  // out == NULL: no host sync
+    FM_HIP_CHECK(hipEventRecord(h.consumed, ctx->stream));
+    return rc;
   });
 }
 

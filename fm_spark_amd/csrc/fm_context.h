@@ -26,6 +26,15 @@ struct Pinned {
   }
 };
 
+// One upload slot of fm_step's host-buffer path: pinned staging + device batch, with the events
+// that say when the staging may be rewritten and when the batch may be refilled.
+struct HostSlot {
+  std::unique_ptr<fm_batch> batch;
+  Pinned pin;
+  hipEvent_t copied = nullptr;    // copy stream: the staging's copies are done
+  hipEvent_t consumed = nullptr;  // main stream: the step that read the batch is done
+};
+
 struct ProfEntry {
   double ms = 0.0;
   int64_t n = 0;
@@ -117,7 +126,10 @@ struct fm_ctx {
   StepWork work;
   Pinned pinned;
   Pinned up_pin;                         // host CSR upload staging (upload_batch)
-  std::unique_ptr<fm_batch> host_batch;  // reused by fm_step / fm_predict / fm_loss_grad
+  std::unique_ptr<fm_batch> host_batch;  // reused by fm_predict / fm_loss_grad
+  HostSlot hslot[2];                     // fm_step's double-buffered uploads
+  int hnext = 0;
+  hipStream_t copy_stream = nullptr;     // their host -> device copies
   // profiling
   bool prof = false;
   std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> pending;
@@ -214,6 +226,12 @@ struct fm_ctx {
   ~fm_ctx() {
     (void)hipSetDevice(cfg.device);
     if (stream) (void)hipStreamSynchronize(stream);
+    if (copy_stream) (void)hipStreamSynchronize(copy_stream);
+    for (auto& h : hslot) {
+      if (h.copied) (void)hipEventDestroy(h.copied);
+      if (h.consumed) (void)hipEventDestroy(h.consumed);
+    }
+    if (copy_stream) (void)hipStreamDestroy(copy_stream);
     for (auto& pe : pending) {
       (void)hipEventDestroy(pe.second.first);
       (void)hipEventDestroy(pe.second.second);

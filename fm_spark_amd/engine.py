@@ -134,7 +134,13 @@ class FMContext:
     def batch(self, csr: N.CSRHost) -> DeviceBatch:
         return DeviceBatch(self, csr)
 
-    def step(self, csr: N.CSRHost, t: int, step_size: float, reg_param: float) -> StepOut:
+    def step(self, csr: N.CSRHost, t: int, step_size: float, reg_param: float, sync: bool = True):
+        """One iteration from a host CSR.  sync=False only enqueues (the host buffers are free on
+        return; losses via loss_history), so consecutive calls overlap upload and compute."""
+        if not sync:
+            N.check(self._lib.fm_step(self.handle, C.byref(csr.c), int(t), float(step_size), float(reg_param), None),
+                    "fm_step")
+            return None
         out = N.fm_step_out()
         rc = N.check(self._lib.fm_step(self.handle, C.byref(csr.c), int(t), float(step_size), float(reg_param),
                                        C.byref(out)), "fm_step")

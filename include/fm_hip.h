@@ -140,9 +140,11 @@ int64_t fm_batch_nnz(const fm_batch* b);
  *   soft-threshold S_lambda on EVERY present row              (SGD.scala:177-181)
  * t is the 1-based iteration index (tuple._2 + 1, SGD.scala:119).  Returns
  * FM_NOTHING_TO_DO for n_rows == 0 without touching the model (SGD.scala:126-128).
- * fm_step copies the host batch first; fm_step_batch uses a device-resident batch and,
- * when out == NULL, only enqueues (no host synchronisation; losses are kept on the device,
- * see fm_loss_history). */
+ * fm_step takes the host batch (borrowed for the call only: it is exploded into pinned staging
+ * by host threads, then copied asynchronously); fm_step_batch uses a device-resident batch.
+ * With out == NULL both only enqueue (no host synchronisation; losses are kept on the device,
+ * see fm_loss_history): consecutive fm_step calls then overlap the next batch's host work and
+ * copies with the current step (two upload slots used in turn). */
 int fm_step(fm_ctx* ctx, const fm_csr* batch, int32_t t, double step_size, double reg_param,
             fm_step_out* out);
 int fm_step_batch(fm_ctx* ctx, fm_batch* batch, int32_t t, double step_size,

@@ -334,3 +334,30 @@ def test_int_max_feature_ids(gpu):
     np.testing.assert_array_equal(gi, big[np.nonzero(model.present)[0]])
     np.testing.assert_allclose(gw, model.w[model.present], rtol=RTOL, atol=ATOL)
     np.testing.assert_allclose(gV, model.V[model.present], rtol=RTOL, atol=ATOL)
+
+
+def test_host_step_async_matches_sync(gpu):
+    """fm_step from host CSRs without host synchronisation (two upload slots in turn) gives the
+    same tables and losses, bit for bit, as synchronous calls; the host buffers are free on
+    return (overwritten right after each call here)."""
+    from fm_spark_amd.engine import FMContext
+
+    F, k = 2000, 16
+    csrs = [make_problem(610 + i, 700 + 50 * i, F, k, 12, hot=5)[0] for i in range(5)]
+    _, ids, w, V = make_problem(611, 1, F, k, 1)
+    outs = []
+    for sync in (True, False):
+        ctx = FMContext(F, k)
+        ctx.load_tables(ids, w, V)
+        for t, c in enumerate(csrs, start=1):
+            h = to_host(R.CSR(c.row_ptr.copy(), c.col.copy(), c.val.copy(), c.label.copy()))
+            ctx.step(h, t, 0.2, 1e-5, sync=sync)
+            h.col[:] = 0  # the call borrowed the buffers only for its duration
+            h.val[:] = 1e9
+        ctx.sync()
+        outs.append((ctx.export_tables(), ctx.loss_history()))
+        ctx.close()
+    (a, la), (b, lb) = outs
+    for x, y in zip(a, b):
+        assert np.array_equal(x, y)
+    assert np.array_equal(la, lb) and len(la) == len(csrs)
