@@ -630,9 +630,10 @@ __device__ __forceinline__ void close_hdr(const SegArgs& a, uint32_t key, const 
 __global__ __launch_bounds__(kBlock) void k_segment_combine(SegArgs a, const double2* __restrict__ loss_part,
                                                             int64_t n_loss_blocks, int64_t n_ucnt,
                                                             double* __restrict__ stats_out) {
-  const int tid = threadIdx.x, lane = tid & 63;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int kp = a.T.kp;
   const int64_t W = kp + 2;
+  __shared__ double run_sum[kBlock / 64][258];  // one long run's summed piece per wave (kp <= 256)
   if (blockIdx.x == 0) {
     __shared__ double rl[kBlock], rc[kBlock], ru[kBlock];
     double l = 0.0, c = 0.0, u = 0.0;
@@ -711,33 +712,43 @@ __global__ __launch_bounds__(kBlock) void k_segment_combine(SegArgs a, const dou
       cend += __ffsll((unsigned long long)~m) - 1;
       break;
     }
-    // every lane sums the scalars (same addresses), lane j the columns j, j + 64, ...
-    double gw = a.part[(c0 * 2 + 1) * W], b = a.part[(c0 * 2 + 1) * W + kp + 1];
-    for (int64_t c = c0 + 1; c < cend; ++c) {
-      gw += a.part[(c * 2) * W];
-      b += a.part[(c * 2) * W + kp + 1];
-    }
-    double sums[4];  // kp <= 256
-    int j = 0;
-    for (int col = lane; col < kp; col += 64, ++j) {
-      double s = a.part[(c0 * 2 + 1) * W + 1 + col];
-      int64_t c = c0 + 1;
-      for (; c + 4 <= cend; c += 4) {
-        const double g0 = a.part[((c + 0) * 2) * W + 1 + col];
-        const double g1 = a.part[((c + 1) * 2) * W + 1 + col];
-        const double g2 = a.part[((c + 2) * 2) * W + 1 + col];
-        const double g3 = a.part[((c + 3) * 2) * W + 1 + col];
-        s += g0;
-        s += g1;
-        s += g2;
-        s += g3;
+    // the run's pieces = the owner range's tail + the head pieces of ranges c0+1 .. cend-1, each a
+    // row of W = kp + 2 doubles [g_w | sum S*x*r (kp) | sum x*x*r].  The wave sums them as 8 column
+    // lanes x 8 range groups (range group rg takes ranges c0+1+rg, +8, ...), then combines the 8
+    // groups by a fixed xor tree and adds the tail: a fixed order, so the step stays bitwise
+    // reproducible, with every lane loading (hot runs at R = 8 span hundreds of ranges).
+    const int cl = lane & 7, rg = lane >> 3;
+    for (int col0 = 0; col0 < (int)W; col0 += 8) {
+      const int col = col0 + cl;
+      double s = 0.0;
+      if (col < (int)W) {
+        int64_t c = c0 + 1 + rg;
+        for (; c + 8 < cend; c += 16) {  // two loads in flight per lane
+          const double g0 = a.part[(c * 2) * W + col];
+          const double g1 = a.part[((c + 8) * 2) * W + col];
+          s += g0;
+          s += g1;
+        }
+        for (; c < cend; c += 8) s += a.part[(c * 2) * W + col];
       }
-      for (; c < cend; ++c) s += a.part[(c * 2) * W + 1 + col];
-      sums[j] = s;
+      s += __shfl_xor(s, 8);
+      s += __shfl_xor(s, 16);
+      s += __shfl_xor(s, 32);
+      if (col < (int)W && rg == 0) run_sum[wave][col] = a.part[(c0 * 2 + 1) * W + col] + s;
     }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const double gw = run_sum[wave][0], b = run_sum[wave][kp + 1];
+    double sums[4];  // kp <= 256: columns lane, lane + 64, ...
+    int j = 0;
+    for (int col = lane; col < kp; col += 64, ++j) sums[j] = run_sum[wave][1 + col];
     const RowCur rc = row_current(a, k0);
     close_cols(a, k0, rc, lane, kp, 64, b, sums);
     if (lane == 0) close_hdr(a, k0, rc, gw);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();  // run_sum is rewritten by the wave's next long run
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
 }
 
