@@ -58,7 +58,7 @@ struct ShardBatchState {
   const uint2* recv_ent = nullptr;
   int64_t n = 0, P = 0;
   Pinned pin_off;
-  DevBuf src_off;            // [R+1] int64 source offsets of the received entries
+  DevBuf src_off;            // [R+1] int64 source offsets of the received entries, then [R+1] pair offsets
   DevBuf pair_ptr;           // [P+1] int64 entry offsets of the pairs
   DevBuf skeys, sents;       // received entries sorted by slot: slots / {pair, x bits}
   hipEvent_t ready_fwd = nullptr;  // side stream: pair table done
@@ -142,7 +142,8 @@ struct fm_ctx {
   DevBuf sh_mask;      // [B] uint64 owners present in each sample
   DevBuf sh_tcnt;      // [R][tiles] pair counts -> exclusive offsets
   DevBuf sh_tot;       // [R] pairs per owner, then [R] entries per owner (uint64)
-  DevBuf sh_bsum;      // pair-head scan block sums (+ total)
+  DevBuf sh_pay;       // [N] uint2 route payload {pair index within the owner's block, x bits}
+  DevBuf sh_skey;      // [N] owner-partitioned route keys
   DevBuf sh_ent2;      // [n] uint2 {pair, x bits}: the slot sort's payload
   SortWork side_sort;  // radix sort workspace of the side stream
   Pinned side_pinned;  // route counts (device -> host)
@@ -249,7 +250,7 @@ struct fm_ctx {
                       &work.sort.keys_a, &work.sort.keys_b, &work.sort.vals_a, &work.sort.vals_b,
                       &work.sort.counts, &work.sort.digit_tot, &side_sort.keys_a, &side_sort.keys_b,
                       &side_sort.vals_a, &side_sort.vals_b, &side_sort.counts, &side_sort.digit_tot,
-                      &sh_okey, &sh_mask, &sh_tcnt, &sh_tot, &sh_bsum, &sh_ent2, &repl_cnt};
+                      &sh_okey, &sh_mask, &sh_tcnt, &sh_tot, &sh_pay, &sh_skey, &sh_ent2, &repl_cnt};
     for (auto* b : bufs) b->release();
     if (own_stream && stream) (void)hipStreamDestroy(stream);
   }

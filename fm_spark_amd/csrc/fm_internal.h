@@ -100,6 +100,10 @@ void radix_sort_pairs64(SortWork& w, const uint32_t* keys_in, const uint2* vals_
                         int key_bits, hipStream_t st, const uint32_t** keys_out,
                         const uint2** vals_out, uint32_t* final_keys = nullptr,
                         uint2* final_vals = nullptr);
+// Stable sort by key bits [lo_bit, hi_bit) only (the bits below ride along), output written to
+// final_keys / final_vals.
+void radix_sort_pairs64_bits(SortWork& w, const uint32_t* keys_in, const uint2* vals_in, int64_t n, int lo_bit,
+                             int hi_bit, hipStream_t st, uint32_t* final_keys, uint2* final_vals);
 
 // ---------------------------------------------------------------- step kernels
 // A device-resident mini-batch: the exploded (sampleId, featureId, featureValue) rows of

@@ -3,12 +3,14 @@
 // mini-batch.  One iteration is five phases of the C-ABI joined by three all-to-alls; the
 // first two depend on the batch alone and run one iteration ahead on the side stream:
 //
-//   fm_shard_route          requester: the batch's entries partitioned by owner (CSR order kept)
-//                           as {slot} and {sample, x}; per sample the owners it touches and the
-//                           pair index of every (sample, owner) pair                 [side]
+//   fm_shard_route          requester: per sample the owners it touches and the pair index of
+//                           every (sample, owner) pair; the entries partitioned by owner (CSR
+//                           order kept) as {slot} and {pair index within the owner's block, x}
+//                           by one stable radix pass over owner bits above the slot   [side]
 //   -- all-to-all entries -->
-//   fm_shard_owner_prepare  owner: the received entries' pair table (pair = (source, sample))
-//                           and their stable order by slot (source rank, then CSR order) [side]
+//   fm_shard_owner_prepare  owner: the received entries' pair table (pair = source offset + the
+//                           carried local index; one pass) and their stable order by slot
+//                           (source rank, then CSR order)                               [side]
 //   fm_shard_owner_forward  owner: per received pair, the partial forward sums over the entries
 //                           it owns: [sum v*x | sum v^2 x^2 | sum w*x], lazy L1 caught up on read
 //                           (FactorizationMachinesModel.scala:173-221)                [main]
@@ -43,7 +45,6 @@ namespace fmhip {
 namespace {
 
 constexpr int kBlock = 256;
-constexpr int kTileS = 4096;  // entries per block in the pair-head scan
 constexpr int kMaxR = 64;     // owner masks are uint64
 
 __device__ __forceinline__ uint32_t incl_scan_u32(uint32_t v, int lane) {
@@ -56,30 +57,70 @@ __device__ __forceinline__ uint32_t incl_scan_u32(uint32_t v, int lane) {
 }
 
 // ------------------------------------------------------------------ requester: route
-__global__ void k_owner_keys(const uint32_t* __restrict__ col, int64_t n, uint32_t R, uint32_t* __restrict__ okey) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    okey[i] = col[i] % R;
+constexpr int kTeamR = 16;  // lanes per sample in the route kernels (coalesced entry reads)
+
+__device__ __forceinline__ uint64_t team_or64(uint64_t m) {
+  uint32_t lo = (uint32_t)m, hi = (uint32_t)(m >> 32);
+#pragma unroll
+  for (int o = 1; o < kTeamR; o <<= 1) {
+    lo |= __shfl_xor(lo, o);
+    hi |= __shfl_xor(hi, o);
+  }
+  return ((uint64_t)hi << 32) | lo;
 }
 
-// per sample: the owners it touches (bit mask); per owner: entry counts
+// per sample (a team of lanes over its entries): the owners it touches (bit mask); per owner:
+// entry counts
 __global__ __launch_bounds__(kBlock) void k_sample_mask(const int64_t* __restrict__ row_ptr,
                                                         const uint32_t* __restrict__ col, int64_t B, uint32_t R,
                                                         uint64_t* __restrict__ mask,
                                                         unsigned long long* __restrict__ ecount) {
+  constexpr int TPB = kBlock / kTeamR;
   __shared__ uint32_t cnt[kMaxR];
   if (threadIdx.x < kMaxR) cnt[threadIdx.x] = 0;
   __syncthreads();
-  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < B; s += (int64_t)gridDim.x * blockDim.x) {
+  const int tl = threadIdx.x % kTeamR;
+  for (int64_t s0 = (int64_t)blockIdx.x * TPB; s0 < B; s0 += (int64_t)gridDim.x * TPB) {  // block-uniform
+    const int64_t s = s0 + threadIdx.x / kTeamR;
     uint64_t m = 0;
-    for (int64_t e = row_ptr[s]; e < row_ptr[s + 1]; ++e) {
-      const uint32_t o = col[e] % R;
-      m |= 1ull << o;
-      atomicAdd(&cnt[o], 1u);
+    if (s < B) {
+      for (int64_t e = row_ptr[s] + tl; e < row_ptr[s + 1]; e += kTeamR) {
+        const uint32_t o = col[e] % R;
+        m |= 1ull << o;
+        atomicAdd(&cnt[o], 1u);
+      }
     }
-    mask[s] = m;
+    m = team_or64(m);
+    if (s < B && tl == 0) mask[s] = m;
   }
   __syncthreads();
   if (threadIdx.x < R && cnt[threadIdx.x]) atomicAdd(&ecount[threadIdx.x], (unsigned long long)cnt[threadIdx.x]);
+}
+
+// per entry, in CSR order: key = owner << sb | slot and the wire payload {pair index of (sample,
+// owner) within the owner's block, x bits}, so one stable pass over the owner bits lays out the
+// send buffers
+__global__ __launch_bounds__(kBlock) void k_route_keys(const int64_t* __restrict__ row_ptr,
+                                                       const uint32_t* __restrict__ col,
+                                                       const uint2* __restrict__ ent, int64_t B, uint32_t R, int sb,
+                                                       const int32_t* __restrict__ pairidx,
+                                                       uint32_t* __restrict__ key, uint2* __restrict__ pay) {
+  constexpr int TPB = kBlock / kTeamR;
+  const int tl = threadIdx.x % kTeamR;
+  for (int64_t s = (int64_t)blockIdx.x * TPB + threadIdx.x / kTeamR; s < B; s += (int64_t)gridDim.x * TPB) {
+    for (int64_t e = row_ptr[s] + tl; e < row_ptr[s + 1]; e += kTeamR) {
+      const uint32_t id = col[e];
+      const uint32_t o = id % R;
+      key[e] = (o << sb) | (id / R);
+      pay[e] = make_uint2((uint32_t)pairidx[s * R + o], ent[e].y);
+    }
+  }
+}
+
+__global__ void k_key_slots(const uint32_t* __restrict__ key, int64_t n, uint32_t slot_mask,
+                            uint32_t* __restrict__ slot) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    slot[i] = key[i] & slot_mask;
 }
 
 // pairs per (owner, tile of kBlock samples) -> tcnt[o][tile]
@@ -150,77 +191,20 @@ __global__ __launch_bounds__(kBlock) void k_pair_index(const uint64_t* __restric
   }
 }
 
-// entries in owner-partitioned order (sidx: stable partition of entry indices) -> wire
-__global__ void k_route_pack(const uint32_t* __restrict__ sidx, int64_t n, const uint32_t* __restrict__ col,
-                             const uint2* __restrict__ ent, uint32_t R, uint32_t* __restrict__ send_slot,
-                             uint2* __restrict__ send_ent) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const uint32_t e = sidx[i];
-    send_slot[i] = col[e] / R;
-    send_ent[i] = ent[e];
-  }
-}
-
 // ------------------------------------------------------------------ owner: pairs
-// i starts a (source, sample) pair: first entry of a source's segment, or a new sample
-__device__ __forceinline__ bool pair_head(const uint2* __restrict__ ent, int64_t i, const int64_t* __restrict__ src_off,
-                                          int R) {
-  if (i == 0) return true;
-  for (int r = 1; r < R; ++r)
-    if (src_off[r] == i) return true;
-  return ent[i].x != ent[i - 1].x;
-}
-
-__global__ __launch_bounds__(kBlock) void k_heads_count(const uint2* __restrict__ ent, int64_t n,
-                                                        const int64_t* __restrict__ src_off, int R,
-                                                        uint32_t* __restrict__ bsum) {
-  __shared__ uint32_t ws[kBlock / 64];
-  const int64_t base = (int64_t)blockIdx.x * kTileS;
-  uint32_t c = 0;
-  for (int i = threadIdx.x; i < kTileS; i += kBlock) {
-    const int64_t p = base + i;
-    c += (p < n && pair_head(ent, p, src_off, R)) ? 1u : 0u;
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
-  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = c;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t t = 0;
-    for (int w = 0; w < kBlock / 64; ++w) t += ws[w];
-    bsum[blockIdx.x] = t;
-  }
-}
-
-// pair_ptr[pair] = its first entry; ent2[i] = {pair of i, x bits}
-__global__ __launch_bounds__(kBlock) void k_heads_apply(const uint2* __restrict__ ent, int64_t n,
-                                                        const int64_t* __restrict__ src_off, int R,
-                                                        const uint32_t* __restrict__ boff,
-                                                        int64_t* __restrict__ pair_ptr, uint2* __restrict__ ent2) {
-  __shared__ uint32_t ws[kBlock / 64];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t base = (int64_t)blockIdx.x * kTileS;
-  uint32_t carry = boff[blockIdx.x];
-  for (int r = 0; r < kTileS / kBlock; ++r) {
-    const int64_t p = base + (int64_t)r * kBlock + threadIdx.x;
-    const bool valid = p < n;
-    const uint32_t f = (valid && pair_head(ent, p, src_off, R)) ? 1u : 0u;
-    const uint32_t inc = incl_scan_u32(f, lane);
-    if (lane == 63) ws[wave] = inc;
-    __syncthreads();
-    uint32_t pre = 0, tot = 0;
-#pragma unroll
-    for (int w = 0; w < kBlock / 64; ++w) {
-      pre += w < wave ? ws[w] : 0u;
-      tot += ws[w];
-    }
-    if (valid) {
-      const uint32_t u = carry + pre + inc - 1u;
-      if (f) pair_ptr[u] = p;
-      ent2[p] = make_uint2(u, ent[p].y);
-    }
-    carry += tot;
-    __syncthreads();
+// The received entries are source-major, each source's in its CSR order, carrying their pair's
+// index within that source's block: ent2 = {pair = pbase[source] + local, x}, and the first
+// entry of every pair opens it in pair_ptr (one pass, no scan).
+__global__ void k_pair_table(const uint2* __restrict__ ent, int64_t n, const int64_t* __restrict__ src_off,
+                             const int64_t* __restrict__ pbase, int R, int64_t* __restrict__ pair_ptr,
+                             uint2* __restrict__ ent2) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    int r = 0;
+    while (r + 1 < R && src_off[r + 1] <= i) ++r;
+    const uint2 e = ent[i];
+    const uint32_t pair = (uint32_t)pbase[r] + e.x;
+    ent2[i] = make_uint2(pair, e.y);
+    if (i == src_off[r] || ent[i - 1].x != e.x) pair_ptr[pair] = i;
   }
 }
 
@@ -402,7 +386,7 @@ int fm_shard_route(fm_ctx* ctx, fm_batch* b, void* send_slot, void* send_ent, in
     unsigned long long* tot = ctx->sh_tot.as<unsigned long long>();  // [R] pairs, [R] entries
     FM_HIP_CHECK(hipMemsetAsync(tot, 0, sizeof(unsigned long long) * 2 * R, st));
     if (B > 0) {
-      hipLaunchKernelGGL(k_sample_mask, dim3(blocks_for(B)), dim3(kBlock), 0, st, b->dev.row_ptr.as<int64_t>(),
+      hipLaunchKernelGGL(k_sample_mask, dim3(blocks_for(B * kTeamR)), dim3(kBlock), 0, st, b->dev.row_ptr.as<int64_t>(),
                          b->dev.col.as<uint32_t>(), B, (uint32_t)R, ctx->sh_mask.as<uint64_t>(), tot + R);
       hipLaunchKernelGGL(k_pair_count, dim3((unsigned)ntiles), dim3(kBlock), 0, st, ctx->sh_mask.as<uint64_t>(), B,
                          R, ntiles, ctx->sh_tcnt.as<uint32_t>());
@@ -413,13 +397,21 @@ int fm_shard_route(fm_ctx* ctx, fm_batch* b, void* send_slot, void* send_ent, in
     }
     hipLaunchKernelGGL(k_owner_offsets, dim3(1), dim3(64), 0, st, tot, R, S.poff.as<int64_t>());
     if (N > 0) {
-      hipLaunchKernelGGL(k_owner_keys, dim3(blocks_for(N)), dim3(kBlock), 0, st, b->dev.col.as<uint32_t>(), N,
-                         (uint32_t)R, ctx->sh_okey.as<uint32_t>());
-      const uint32_t *sk = nullptr, *si = nullptr;
-      radix_sort_pairs(ctx->side_sort, ctx->sh_okey.as<uint32_t>(), nullptr, N, bits_for(R - 1), st, &sk, &si);
-      hipLaunchKernelGGL(k_route_pack, dim3(blocks_for(N)), dim3(kBlock), 0, st, si, N, b->dev.col.as<uint32_t>(),
-                         b->dev.ent.as<uint2>(), (uint32_t)R, reinterpret_cast<uint32_t*>(send_slot),
-                         reinterpret_cast<uint2*>(send_ent));
+      // wire keys owner << sb | slot with payload {pair index within the owner's block, x}; one
+      // stable pass over the owner bits partitions them (CSR order kept inside each owner)
+      const int sb = bits_for(std::max<int64_t>(ctx->rows - 1, 1));
+      const int ob = bits_for(R - 1);
+      FM_REQUIRE(sb + ob <= 32, "route key does not fit 32 bits");
+      ctx->sh_pay.ensure(sizeof(uint2) * std::max<int64_t>(N, 4) + 16);
+      ctx->sh_skey.ensure(sizeof(uint32_t) * std::max<int64_t>(N, 4) + 16);
+      hipLaunchKernelGGL(k_route_keys, dim3(blocks_for(B * kTeamR)), dim3(kBlock), 0, st,
+                         b->dev.row_ptr.as<int64_t>(), b->dev.col.as<uint32_t>(), b->dev.ent.as<uint2>(), B,
+                         (uint32_t)R, sb, S.pairidx.as<int32_t>(), ctx->sh_okey.as<uint32_t>(),
+                         ctx->sh_pay.as<uint2>());
+      radix_sort_pairs64_bits(ctx->side_sort, ctx->sh_okey.as<uint32_t>(), ctx->sh_pay.as<uint2>(), N, sb, sb + ob, st,
+                              ctx->sh_skey.as<uint32_t>(), reinterpret_cast<uint2*>(send_ent));
+      hipLaunchKernelGGL(k_key_slots, dim3(blocks_for(N)), dim3(kBlock), 0, st, ctx->sh_skey.as<uint32_t>(), N,
+                         (uint32_t)((sb >= 32) ? 0xFFFFFFFFu : ((1u << sb) - 1u)), reinterpret_cast<uint32_t*>(send_slot));
     }
     FM_HIP_CHECK(hipGetLastError());
     ctx->prof_end("route", e0, st);
@@ -448,12 +440,13 @@ int fm_shard_owner_prepare(fm_ctx* ctx, fm_batch* b, const void* recv_slot, cons
     ShardBatchState& S = shard_state(ctx, b);
     const int R = ctx->cfg.shard_count;
     FM_REQUIRE(n >= 0 && src_entries && src_pairs, "bad arguments");
-    std::vector<int64_t> off(R + 1, 0);
+    std::vector<int64_t> off(2 * (R + 1), 0);  // [R+1] source entry offsets, [R+1] source pair offsets
     int64_t P = 0;
     for (int r = 0; r < R; ++r) {
       FM_REQUIRE(src_entries[r] >= 0 && src_pairs[r] >= 0 && src_pairs[r] <= src_entries[r], "bad source counts");
       FM_REQUIRE(src_entries[r] == 0 || src_pairs[r] >= 1, "bad source counts");
       off[r + 1] = off[r] + src_entries[r];
+      off[R + 1 + r + 1] = off[R + 1 + r] + src_pairs[r];
       P += src_pairs[r];
     }
     FM_REQUIRE(off[R] == n, "source entry counts do not add up to n");
@@ -464,26 +457,19 @@ int fm_shard_owner_prepare(fm_ctx* ctx, fm_batch* b, const void* recv_slot, cons
     // the staging of this batch's previous preparation has been consumed once its pair table was
     FM_HIP_CHECK(hipEventSynchronize(S.ready_fwd));
     hipEvent_t e0 = ctx->prof_begin(st);
-    const int64_t nb = std::max<int64_t>((n + kTileS - 1) / kTileS, 1);
-    S.src_off.ensure(sizeof(int64_t) * (R + 1));
+    S.src_off.ensure(sizeof(int64_t) * 2 * (R + 1));
     S.pair_ptr.ensure(sizeof(int64_t) * (P + 1));
-    S.pin_off.ensure(sizeof(int64_t) * (R + 1));
-    std::memcpy(S.pin_off.p, off.data(), sizeof(int64_t) * (R + 1));
-    FM_HIP_CHECK(hipMemcpyAsync(S.src_off.p, S.pin_off.p, sizeof(int64_t) * (R + 1), hipMemcpyHostToDevice, st));
+    S.pin_off.ensure(sizeof(int64_t) * 2 * (R + 1));
+    std::memcpy(S.pin_off.p, off.data(), sizeof(int64_t) * 2 * (R + 1));
+    FM_HIP_CHECK(hipMemcpyAsync(S.src_off.p, S.pin_off.p, sizeof(int64_t) * 2 * (R + 1), hipMemcpyHostToDevice, st));
     int64_t* pair_ptr = S.pair_ptr.as<int64_t>();
     // the pair table closes with n (pair_ptr[P])
     FM_HIP_CHECK(hipMemcpyAsync(pair_ptr + P, S.src_off.as<int64_t>() + R, sizeof(int64_t), hipMemcpyDeviceToDevice, st));
     if (n > 0) {
-      ctx->sh_bsum.ensure(sizeof(uint32_t) * nb + sizeof(unsigned long long));
       ctx->sh_ent2.ensure(sizeof(uint2) * n);
-      const uint2* ent = reinterpret_cast<const uint2*>(recv_ent);
-      uint32_t* bsum = ctx->sh_bsum.as<uint32_t>();
-      auto* total = reinterpret_cast<unsigned long long*>(bsum + nb);
-      hipLaunchKernelGGL(k_heads_count, dim3((unsigned)nb), dim3(kBlock), 0, st, ent, n, S.src_off.as<int64_t>(), R,
-                         bsum);
-      hipLaunchKernelGGL(k_rows_scan, dim3(1), dim3(kBlock), 0, st, bsum, nb, total);
-      hipLaunchKernelGGL(k_heads_apply, dim3((unsigned)nb), dim3(kBlock), 0, st, ent, n, S.src_off.as<int64_t>(), R,
-                         bsum, pair_ptr, ctx->sh_ent2.as<uint2>());
+      hipLaunchKernelGGL(k_pair_table, dim3(blocks_for(n)), dim3(kBlock), 0, st, reinterpret_cast<const uint2*>(recv_ent),
+                         n, S.src_off.as<int64_t>(), S.src_off.as<int64_t>() + (R + 1), R, pair_ptr,
+                         ctx->sh_ent2.as<uint2>());
       FM_HIP_CHECK(hipGetLastError());
     }
     FM_HIP_CHECK(hipEventRecord(S.ready_fwd, st));

@@ -308,7 +308,7 @@ inline int digit_bits(int key_bits, int* passes) {
 template <class P>
 static void radix_sort_impl(SortWork& w, const uint32_t* keys_in, const P* vals_in, int64_t n, int key_bits,
                             hipStream_t st, const uint32_t** keys_out, const P** vals_out,
-                            uint32_t* final_keys = nullptr, P* final_vals = nullptr) {
+                            uint32_t* final_keys = nullptr, P* final_vals = nullptr, int lo_bit = 0) {
   FM_REQUIRE(n >= 0 && n < (int64_t(1) << 32) - 1, "sort size out of range");
   w.ensure(n > 0 ? n : 1);
   if (n == 0) {
@@ -328,7 +328,7 @@ static void radix_sort_impl(SortWork& w, const uint32_t* keys_in, const P* vals_
   // the count kernel reads keys as uint4 when the tile is full: needs 16-byte alignment
   const bool aligned = (reinterpret_cast<uintptr_t>(keys_in) & 15u) == 0;
   for (int p = 0; p < passes; ++p) {
-    const int shift = rb * p;
+    const int shift = lo_bit + rb * p;
     if (p == 0 && !aligned) {
       FM_HIP_CHECK(hipMemcpyAsync(kbuf[1], keys_in, sizeof(uint32_t) * n, hipMemcpyDeviceToDevice, st));
       kin = kbuf[1];
@@ -352,6 +352,14 @@ static void radix_sort_impl(SortWork& w, const uint32_t* keys_in, const P* vals_
 void radix_sort_pairs(SortWork& w, const uint32_t* keys_in, const uint32_t* vals_in, int64_t n, int key_bits,
                       hipStream_t st, const uint32_t** keys_out, const uint32_t** vals_out) {
   radix_sort_impl<uint32_t>(w, keys_in, vals_in, n, key_bits, st, keys_out, vals_out);
+}
+
+void radix_sort_pairs64_bits(SortWork& w, const uint32_t* keys_in, const uint2* vals_in, int64_t n, int lo_bit,
+                             int hi_bit, hipStream_t st, uint32_t* final_keys, uint2* final_vals) {
+  FM_REQUIRE(lo_bit >= 0 && hi_bit > lo_bit && hi_bit <= 32, "bad sort bit range");
+  const uint32_t* ko = nullptr;
+  const uint2* vo = nullptr;
+  radix_sort_impl<uint2>(w, keys_in, vals_in, n, hi_bit - lo_bit, st, &ko, &vo, final_keys, final_vals, lo_bit);
 }
 
 void radix_sort_pairs64(SortWork& w, const uint32_t* keys_in, const uint2* vals_in, int64_t n, int key_bits,

@@ -230,8 +230,9 @@ int fm_xorshift_next_doubles(int64_t seed, int64_t n, double* out);
  * (fm_set_side_stream), so the next iteration's routing, entry exchange and slot sort overlap the
  * current iteration; phases 2-4 run on the main stream and wait for them through events.
  * Phase 1 (requester): partition the batch's entries by owner, CSR order kept, into
- * send_slot (uint32 local slots, N) and send_ent ({sample, x bits}, N) -- device buffers of the
- * batch's nnz.  counts[0..R) = entries to each owner, counts[R..2R) = pairs to each owner.
+ * send_slot (uint32 local slots, N) and send_ent ({index of the entry's (sample, owner) pair
+ * among this rank's pairs to that owner, x bits}, N) -- device buffers of the batch's nnz.
+ * counts[0..R) = entries to each owner, counts[R..2R) = pairs to each owner.
  * Synchronises the side stream (not the main stream). */
 int fm_shard_route(fm_ctx* ctx, fm_batch* batch, void* send_slot, void* send_ent, int64_t* counts);
 /* Phase 1b (owner): the n received entries (source-rank major: src_entries[r] from rank r, which

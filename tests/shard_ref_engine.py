@@ -61,13 +61,15 @@ class NumpyShardEngine:
         sample = np.repeat(np.arange(csr.n_rows), np.diff(csr.row_ptr))
         order = np.argsort(owner, kind="stable")
         send_slot = (ids[order] // self.R).astype(np.int32)
-        ent = np.stack([sample[order].astype(np.uint32), csr.val[order].astype(np.float32).view(np.uint32)], axis=1)
         ents = np.bincount(owner, minlength=self.R)
         has = np.zeros((csr.n_rows, self.R), dtype=bool)
         has[sample, owner] = True
         pairs = has.sum(axis=0)
         b.pairidx = np.where(has, np.cumsum(has, axis=0) - 1, -1)  # [B][R]
         b.pairs_out = pairs
+        # wire entry = {index of its (sample, owner) pair within this rank's pairs to the owner, x}
+        local = b.pairidx[sample[order], owner[order]].astype(np.uint32)
+        ent = np.stack([local, csr.val[order].astype(np.float32).view(np.uint32)], axis=1)
         counts = np.concatenate([ents, pairs]).astype(np.int64)
         return torch.from_numpy(send_slot), torch.from_numpy(ent.view(np.int32).reshape(-1).copy()), counts
 
