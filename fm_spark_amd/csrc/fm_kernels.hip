@@ -87,6 +87,9 @@ constexpr int kTrain = 0, kPartial = 1, kPredict = 2, kLossGrad = 3;
 #ifndef FM_FWD_MINW
 #define FM_FWD_MINW 1  // waves per SIMD the register allocation must allow
 #endif
+#ifndef FM_FWD_GRID
+#define FM_FWD_GRID 2048  // forward blocks at most (grid-stride over samples beyond)
+#endif
 template <int GS, int TEAM, int MODE>
 __global__ __launch_bounds__(kBlock, FM_FWD_MINW) void k_forward(TableView T, const int64_t* __restrict__ row_ptr,
                                                     const uint32_t* __restrict__ col,
@@ -952,7 +955,7 @@ void launch_fwd_t(const TableView& T, const BatchDev& b, StepWork& w, const Step
                   int64_t* nblk, float* partial_out, const FwdOut* xo) {
   constexpr int TPB = kBlock / TEAM;
   int64_t blocks = (b.n_rows + TPB - 1) / TPB;
-  if (blocks > 256 * 8) blocks = 256 * 8;
+  if (blocks > FM_FWD_GRID) blocks = FM_FWD_GRID;
   if (blocks < 1) blocks = 1;
   *nblk = blocks;
   const dim3 grid((unsigned)blocks), blk(kBlock);
