@@ -104,6 +104,42 @@ def test_hip_shard_phases_match_single_table(gpu, R, k):
     np.testing.assert_allclose(np.concatenate(gV)[order], model.V[gi[order]], rtol=1e-5, atol=1e-8)
 
 
+def test_hip_shard_c3_r8_matches_single_table(gpu):
+    """Config c3's table at R = 8 (100M hashed features, k = 16, owner = id % 8), eight ranks of
+    32K synthetic rows each (the bench's generator), two iterations of the sharded phases
+    against one single-table HIP step over the concatenated batches: losses, distinct counts
+    and every touched row (the two paths differ only in fp summation order)."""
+    from fm_spark_amd._native import CSRHost
+    from fm_spark_amd.data import synthetic_batch
+    from fm_spark_amd.distributed import HipShardEngine
+    from fm_spark_amd.engine import FMContext
+
+    F, k, R, B = 100_000_000, 16, 8, 32768
+    ref = FMContext(F, k, seed=5, init_sd=0.01)
+    engines = [HipShardEngine(F, k, r, R) for r in range(R)]
+    for t in (1, 2):
+        parts = [synthetic_batch(B, F, batch_index=100 * t + r) for r in range(R)]
+        cat = _concat([R_.CSR(p.row_ptr, p.col, p.val, p.label) for p in parts])
+        cb = ref.batch(CSRHost(cat.row_ptr, cat.col, cat.val, cat.label))
+        before = np.zeros(0, np.int32) if t == 1 else ids
+        ref.init_from_batch(cb)  # createInitialModel's rows for the new ids, loaded on every owner
+        ids, w, V = ref.export_tables()
+        new = ~np.isin(ids, before)
+        for e in engines:
+            e.load_tables(ids[new], w[new], V[new])
+        o = ref.step_batch(cb, t, 0.1, 1e-6, sync=True)
+        bs = [e.batch(CSRHost(p.row_ptr, p.col, p.val, p.label)) for e, p in zip(engines, parts)]
+        loss, nu = _simulated_step(engines, bs, t, 0.1, 1e-6)
+        assert nu == o.n_unique == len(np.unique(cat.col))
+        assert loss == pytest.approx(o.loss_sum, rel=1e-9)
+    gi, gw, gV = ref.export_tables()
+    si, sw, sV = (np.concatenate(x) for x in zip(*[e.export_tables() for e in engines]))
+    order = np.argsort(si)
+    np.testing.assert_array_equal(si[order], gi)
+    np.testing.assert_allclose(sw[order], gw, rtol=1e-5, atol=1e-8)
+    np.testing.assert_allclose(sV[order], gV, rtol=1e-5, atol=1e-8)
+
+
 def test_sharded_trainer_world1_rccl(gpu):
     """The full ShardedTrainer over torch.distributed (nccl = RCCL) with one rank."""
     import os
