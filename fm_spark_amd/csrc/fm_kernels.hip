@@ -82,15 +82,24 @@ __device__ __forceinline__ void current_row(const RowHdr& h, float4& v, float& w
 // sums (a second walk over the sample's entries re-reads their rows); absent ids set the flag.
 constexpr int kTrain = 0, kPartial = 1, kPredict = 2, kLossGrad = 3;
 #ifndef FM_FWD_U
-#define FM_FWD_U 4  // passes (entries per lane) whose rows are in flight together
+#define FM_FWD_U 4  // sharded partial pass: passes (entries per lane) whose rows are in flight together
 #endif
 #ifndef FM_FWD_MINW
 #define FM_FWD_MINW 1  // waves per SIMD the register allocation must allow
 #endif
+// The step's forward (and predict / loss-grad): 32 lanes per sample, 2 passes in flight -- the
+// same 16 rows in flight per sample at k = 16 as 16 lanes x 4 passes, with fewer registers per
+// lane (measured 1.196 against 1.213 ms per c3 step, 5 runs each on two boxes)
+#ifndef FM_FWD_TEAM
+#define FM_FWD_TEAM 32
+#endif
+#ifndef FM_FWD_TU
+#define FM_FWD_TU 2
+#endif
 #ifndef FM_FWD_GRID
 #define FM_FWD_GRID 2048  // forward blocks at most (grid-stride over samples beyond)
 #endif
-template <int GS, int TEAM, int MODE>
+template <int GS, int TEAM, int MODE, int U>
 __global__ __launch_bounds__(kBlock, FM_FWD_MINW) void k_forward(TableView T, const int64_t* __restrict__ row_ptr,
                                                     const uint32_t* __restrict__ col,
                                                     const uint2* __restrict__ ent,
@@ -101,7 +110,6 @@ __global__ __launch_bounds__(kBlock, FM_FWD_MINW) void k_forward(TableView T, co
   constexpr bool PARTIAL = MODE == kPartial;
   constexpr int RPP = TEAM / GS;  // entries per pass
   constexpr int TPB = kBlock / TEAM;
-  constexpr int U = FM_FWD_U;     // passes in flight
   const int tid = threadIdx.x;
   const int tl = tid % TEAM;
   const int g = tl % GS;
@@ -950,7 +958,7 @@ inline unsigned grid_for(int64_t n, int block, int64_t cap = 256 * 16) {
   return (unsigned)g;
 }
 
-template <int GS, int TEAM>
+template <int GS, int TEAM, int U>
 void launch_fwd_t(const TableView& T, const BatchDev& b, StepWork& w, const StepParams& p, hipStream_t st,
                   int64_t* nblk, float* partial_out, const FwdOut* xo) {
   constexpr int TPB = kBlock / TEAM;
@@ -961,25 +969,25 @@ void launch_fwd_t(const TableView& T, const BatchDev& b, StepWork& w, const Step
   const dim3 grid((unsigned)blocks), blk(kBlock);
   const FwdOut none{};
   if (xo && xo->mode == kPredict) {
-    hipLaunchKernelGGL((k_forward<GS, TEAM, kPredict>), grid, blk, 0, st, T, b.row_ptr.as<int64_t>(),
+    hipLaunchKernelGGL((k_forward<GS, TEAM, kPredict, U>), grid, blk, 0, st, T, b.row_ptr.as<int64_t>(),
                        b.col.as<uint32_t>(), b.ent.as<uint2>(), nullptr, b.n_rows, p.w0, p.cumE, nullptr, nullptr,
                        nullptr, *xo);
     return;
   }
   if (xo && xo->mode == kLossGrad) {
-    hipLaunchKernelGGL((k_forward<GS, TEAM, kLossGrad>), grid, blk, 0, st, T, b.row_ptr.as<int64_t>(),
+    hipLaunchKernelGGL((k_forward<GS, TEAM, kLossGrad, U>), grid, blk, 0, st, T, b.row_ptr.as<int64_t>(),
                        b.col.as<uint32_t>(), b.ent.as<uint2>(), b.label.as<float>(), b.n_rows, p.w0, p.cumE, nullptr,
                        nullptr, nullptr, *xo);
     return;
   }
   if (partial_out) {  // [n_rows][kp] vectors, then [n_rows] float2 scalars
-    hipLaunchKernelGGL((k_forward<GS, TEAM, kPartial>), grid, blk, 0, st, T, b.row_ptr.as<int64_t>(),
+    hipLaunchKernelGGL((k_forward<GS, TEAM, kPartial, U>), grid, blk, 0, st, T, b.row_ptr.as<int64_t>(),
                        b.col.as<uint32_t>(), b.ent.as<uint2>(), nullptr, b.n_rows, p.w0, p.cumE, partial_out,
                        reinterpret_cast<float2*>(partial_out + b.n_rows * T.kp), nullptr, none);
     return;
   }
   w.loss_part.ensure(sizeof(double2) * blocks);
-  hipLaunchKernelGGL((k_forward<GS, TEAM, kTrain>), grid, blk, 0, st, T, b.row_ptr.as<int64_t>(),
+  hipLaunchKernelGGL((k_forward<GS, TEAM, kTrain, U>), grid, blk, 0, st, T, b.row_ptr.as<int64_t>(),
                      b.col.as<uint32_t>(), b.ent.as<uint2>(), b.label.as<float>(), b.n_rows, p.w0, p.cumE,
                      w.S.as<float>(), w.yl.as<float2>(), w.loss_part.as<double2>(), none);
 }
@@ -992,9 +1000,9 @@ template <int GS>
 void launch_partial_t(const TableView& T, const BatchDev& b, StepWork& w, const StepParams& p, hipStream_t st,
                       int64_t* nblk, float* partial_out) {
   const double avg = b.n_rows > 0 ? (double)b.nnz / (double)b.n_rows : 0.0;
-  if (GS <= 16 && avg <= 4.0) launch_fwd_t<GS, GS>(T, b, w, p, st, nblk, partial_out, nullptr);
-  else if (GS <= 16 && avg <= 8.0) launch_fwd_t<GS, (2 * GS > 16 ? 16 : 2 * GS)>(T, b, w, p, st, nblk, partial_out, nullptr);
-  else launch_fwd_t<GS, (GS > 16 ? GS : 16)>(T, b, w, p, st, nblk, partial_out, nullptr);
+  if (GS <= 16 && avg <= 4.0) launch_fwd_t<GS, GS, FM_FWD_U>(T, b, w, p, st, nblk, partial_out, nullptr);
+  else if (GS <= 16 && avg <= 8.0) launch_fwd_t<GS, (2 * GS > 16 ? 16 : 2 * GS), FM_FWD_U>(T, b, w, p, st, nblk, partial_out, nullptr);
+  else launch_fwd_t<GS, (GS > 16 ? GS : 16), FM_FWD_U>(T, b, w, p, st, nblk, partial_out, nullptr);
 }
 
 void launch_forward(const TableView& T, const BatchDev& b, StepWork& w, const StepParams& p, hipStream_t st,
@@ -1006,19 +1014,20 @@ void launch_forward(const TableView& T, const BatchDev& b, StepWork& w, const St
     else if (nq <= 4) launch_partial_t<4>(T, b, w, p, st, nblk, partial_out);
     else if (nq <= 8) launch_partial_t<8>(T, b, w, p, st, nblk, partial_out);
     else if (nq <= 16) launch_partial_t<16>(T, b, w, p, st, nblk, partial_out);
-    else if (nq <= 32) launch_fwd_t<32, 32>(T, b, w, p, st, nblk, partial_out, pred);
-    else if (nq <= 64) launch_fwd_t<64, 64>(T, b, w, p, st, nblk, partial_out, pred);
+    else if (nq <= 32) launch_fwd_t<32, 32, FM_FWD_U>(T, b, w, p, st, nblk, partial_out, pred);
+    else if (nq <= 64) launch_fwd_t<64, 64, FM_FWD_U>(T, b, w, p, st, nblk, partial_out, pred);
     else FM_REQUIRE(false, "dimFactorization > 256 is not supported");
     FM_HIP_CHECK(hipGetLastError());
     return;
   }
-  if (nq <= 1) launch_fwd_t<1, 16>(T, b, w, p, st, nblk, partial_out, pred);
-  else if (nq <= 2) launch_fwd_t<2, 16>(T, b, w, p, st, nblk, partial_out, pred);
-  else if (nq <= 4) launch_fwd_t<4, 16>(T, b, w, p, st, nblk, partial_out, pred);
-  else if (nq <= 8) launch_fwd_t<8, 16>(T, b, w, p, st, nblk, partial_out, pred);
-  else if (nq <= 16) launch_fwd_t<16, 16>(T, b, w, p, st, nblk, partial_out, pred);
-  else if (nq <= 32) launch_fwd_t<32, 32>(T, b, w, p, st, nblk, partial_out, pred);
-  else if (nq <= 64) launch_fwd_t<64, 64>(T, b, w, p, st, nblk, partial_out, pred);
+  constexpr int TM = FM_FWD_TEAM, TU = FM_FWD_TU;
+  if (nq <= 1) launch_fwd_t<1, TM, TU>(T, b, w, p, st, nblk, partial_out, pred);
+  else if (nq <= 2) launch_fwd_t<2, TM, TU>(T, b, w, p, st, nblk, partial_out, pred);
+  else if (nq <= 4) launch_fwd_t<4, (TM < 4 ? 4 : TM), TU>(T, b, w, p, st, nblk, partial_out, pred);
+  else if (nq <= 8) launch_fwd_t<8, (TM < 8 ? 8 : TM), TU>(T, b, w, p, st, nblk, partial_out, pred);
+  else if (nq <= 16) launch_fwd_t<16, (TM < 16 ? 16 : TM), TU>(T, b, w, p, st, nblk, partial_out, pred);
+  else if (nq <= 32) launch_fwd_t<32, 32, FM_FWD_U>(T, b, w, p, st, nblk, partial_out, pred);
+  else if (nq <= 64) launch_fwd_t<64, 64, FM_FWD_U>(T, b, w, p, st, nblk, partial_out, pred);
   else FM_REQUIRE(false, "dimFactorization > 256 is not supported");
   FM_HIP_CHECK(hipGetLastError());
 }

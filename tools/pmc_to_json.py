@@ -8,7 +8,10 @@ requests x 64 B: a 128-B line request (the row gathers: V + header of one 128-B 
 coalesced streams) is tallied at half its bytes (rd80 and stream: exactly 1/2), a 64-B request
 in full (rd64: 1.03x).  The step kernels' reads are line requests except the update's S-row
 gathers (64 B), so  traffic = 2 * FETCH + WRITE  is exact for k_forward and an upper bound
-for k_segment_update (its S gathers are double counted)."""
+for k_segment_update (its S gathers are double counted).  With a 4th argument (a directory of
+the update's ablation passes, tools/abl_pmc.sh: base-FETCH_SIZE.csv and nos-FETCH_SIZE.csv, the
+build with and without the S-row loads) the S gathers' FETCH share is measured and counted once:
+traffic = 2 * (FETCH - S) + S + WRITE for k_segment_update."""
 import csv
 import glob
 import json
@@ -33,6 +36,19 @@ for k, d in acc.items():
         e["write_bytes"] = m["WRITE_SIZE"] * 1024
         e["traffic_bytes"] = 2 * m["FETCH_SIZE"] * 1024 + m["WRITE_SIZE"] * 1024
     res["kernels"][k] = e
+abl = sys.argv[4] if len(sys.argv) > 4 else None
+if abl and "k_segment_update" in res["kernels"]:
+
+    def mean_fetch(path):
+        v = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
+             if r["Kernel_Name"].startswith("k_segment_update") and r["Counter_Name"] == "FETCH_SIZE"]
+        return sum(v) / len(v)
+
+    s_kib = mean_fetch(os.path.join(abl, "base-FETCH_SIZE.csv")) - mean_fetch(os.path.join(abl, "nos-FETCH_SIZE.csv"))
+    e = res["kernels"]["k_segment_update"]
+    e["s_gather_fetch_bytes"] = s_kib * 1024
+    e["traffic_bytes"] = 2 * (e["fetch_bytes_counted"] - s_kib * 1024) + s_kib * 1024 + e["write_bytes"]
+    res["update_s_correction"] = abl
 txt = json.dumps(res, indent=1, sort_keys=True)
 if out:
     open(out, "w").write(txt + "\n")
