@@ -25,8 +25,13 @@ namespace {
 #define FM_SORT_XCD 1
 #endif
 
-constexpr int kBlock = 256;
+#ifndef FM_SORT_BLOCK
+#define FM_SORT_BLOCK 256
+#endif
+constexpr int kBlock = FM_SORT_BLOCK;  // 256 (4 waves) or 512 (8 waves: twice the tile, longer digit runs)
+static_assert(kBlock == 256 || kBlock == 512, "sort block must be 256 or 512 threads");
 constexpr int kWaves = kBlock / 64;
+constexpr int kMinRB = kBlock == 512 ? 9 : 8;  // the block scans hold R / kBlock >= 1 digits per thread
 #ifndef FM_SORT_ROUNDS
 #define FM_SORT_ROUNDS 16
 #endif
@@ -282,7 +287,7 @@ void SortWork::ensure(int64_t n) {
 }
 
 template <class P, int RB>
-static void radix_pass(const uint32_t* kin, const P* vin, uint32_t* ko, P* vo, int64_t n, int shift,
+static void radix_pass_impl(const uint32_t* kin, const P* vin, uint32_t* ko, P* vo, int64_t n, int shift,
                        SortWork& w, int64_t ntiles, hipStream_t st) {
   hipLaunchKernelGGL(k_radix_count<RB>, dim3((unsigned)ntiles), dim3(kBlock), 0, st, kin, n, shift,
                      w.counts.as<uint32_t>(), ntiles);
@@ -293,13 +298,23 @@ static void radix_pass(const uint32_t* kin, const P* vin, uint32_t* ko, P* vo, i
   FM_HIP_CHECK(hipGetLastError());
 }
 
+template <class P, int RB>
+static void radix_pass(const uint32_t* kin, const P* vin, uint32_t* ko, P* vo, int64_t n, int shift,
+                       SortWork& w, int64_t ntiles, hipStream_t st) {
+  if constexpr ((1 << RB) >= kBlock) {
+    radix_pass_impl<P, RB>(kin, vin, ko, vo, n, shift, w, ntiles, st);
+  } else {
+    FM_REQUIRE(false, "sort digit narrower than the block");
+  }
+}
+
 // Digit width: the fewest passes of at most FM_SORT_MAXRB bits, spread evenly (27-bit feature
-// slots: 3 passes of 9 bits), never narrower than 8 bits.
+// slots: 3 passes of 9 bits), never narrower than kMinRB bits.
 inline int digit_bits(int key_bits, int* passes) {
   const int kb = key_bits < 1 ? 1 : key_bits;
   int p = (kb + FM_SORT_MAXRB - 1) / FM_SORT_MAXRB;
   int rb = (kb + p - 1) / p;
-  if (rb < 8) rb = 8;
+  if (rb < kMinRB) rb = kMinRB;
   p = (kb + rb - 1) / rb;
   *passes = p;
   return rb;
