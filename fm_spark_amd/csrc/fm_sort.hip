@@ -5,10 +5,10 @@
 // up contiguous and in their original (CSR) order, so every per-feature sum downstream runs
 // in a fixed order and the step is bitwise reproducible.
 //
-// Per pass (RB-bit digit, 8..10 bits: 27-bit feature slots take 3 passes of 9 bits):
-//   count   : one 256-thread block per 4096-key tile, LDS histogram  -> counts[digit][tile]
+// Per pass (RB-bit digit, 9..10 bits: 27-bit feature slots take 3 passes of 9 bits):
+//   count   : one 512-thread block per 4096-key tile, LDS histogram  -> counts[digit][tile]
 //   scan    : one block per digit, exclusive scan along tiles        -> counts, digit totals
-//   scatter : each wave ranks its 1024 keys with RB ballots per round (wave64 match), the
+//   scatter : each wave ranks its 512 keys with RB ballots per round (wave64 match), the
 //             block stages the tile in LDS in digit order, then writes runs coalesced; tiles
 //             are mapped to XCDs in contiguous groups.
 // HBM traffic per pass: 4 B (count) + (4 + P) B read + (4 + P) B write per pair.
@@ -26,14 +26,14 @@ namespace {
 #endif
 
 #ifndef FM_SORT_BLOCK
-#define FM_SORT_BLOCK 256
+#define FM_SORT_BLOCK 512
 #endif
-constexpr int kBlock = FM_SORT_BLOCK;  // 256 (4 waves) or 512 (8 waves: twice the tile, longer digit runs)
+constexpr int kBlock = FM_SORT_BLOCK;  // 512: 8 waves x 8 keys per lane; two blocks (16 waves) per CU
 static_assert(kBlock == 256 || kBlock == 512, "sort block must be 256 or 512 threads");
 constexpr int kWaves = kBlock / 64;
 constexpr int kMinRB = kBlock == 512 ? 9 : 8;  // the block scans hold R / kBlock >= 1 digits per thread
 #ifndef FM_SORT_ROUNDS
-#define FM_SORT_ROUNDS 16
+#define FM_SORT_ROUNDS 8
 #endif
 constexpr int kRounds = FM_SORT_ROUNDS;  // keys per thread per tile
 constexpr int kTile = kBlock * kRounds;  // 4096 keys per tile
