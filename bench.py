@@ -64,7 +64,42 @@ def parse():
                         "caller sees it) instead of device-resident batches; reported, never the headline")
     p.add_argument("--prefetch-depth", type=int, default=1,
                    help="single table: how many steps ahead a batch is sorted on the side stream")
+    p.add_argument("--host-path-steps", type=int, default=12,
+                   help="N = 1: after the timed region, time this many fm_step calls with the host CSR "
+                        "(PCIe-inclusive, what a JNI caller gets) for host_path_ms_per_step; 0 = skip")
     return p.parse_args()
+
+
+def median_step_ms(events):
+    """Median of the per-step device times between consecutive step-start events (BASELINE.md:
+    median over >= 20 steps); the events sit on the stream the steps are launched on."""
+    d = [events[i].elapsed_time(events[i + 1]) for i in range(len(events) - 1)]
+    return float(np.median(d)) if d else None
+
+
+def host_path_leg(ctx, host_batches, t, steps, torch):
+    """fm_step with a host CSR every call (staged, copied over PCIe, exploded on the device, then
+    the step): the rate a JNI caller sees.  Two warm-up calls, then `steps` timed calls, each
+    bracketed by events on the context's stream; returns (median ms, mean ms, next t)."""
+    from fm_spark_amd._native import CSRHost
+
+    hosts = [CSRHost(b.row_ptr, b.col, b.val, b.label) for b in host_batches]
+    st = torch.cuda.current_stream()
+    for i in range(2):
+        t += 1
+        ctx.step(hosts[i % len(hosts)], t, STEP_SIZE, REG_PARAM, sync=False)
+    ctx.sync()
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
+    t0 = time.perf_counter()
+    for i in range(steps):
+        evs[i].record(st)
+        t += 1
+        ctx.step(hosts[i % len(hosts)], t, STEP_SIZE, REG_PARAM, sync=False)
+    evs[steps].record(st)
+    ctx.sync()
+    torch.cuda.synchronize()
+    mean = 1000.0 * (time.perf_counter() - t0) / steps
+    return median_step_ms(evs), mean, t
 
 
 def log(msg):
@@ -168,8 +203,14 @@ def main():
     log(f"[rank {rank}] generated {args.batches} batches in {time.perf_counter() - t0:.1f}s")
     z = host_batches[0].nnz / B
 
+    median_ms = None
+    host_path = None
     if not sharded:
         ctx = FMContext(F, k, device=local_rank, seed=20261015, init_sd=INIT_SD)
+        # launch on a torch stream of our own so torch events can bracket every step on it
+        main_stream = torch.cuda.Stream()
+        torch.cuda.set_stream(main_stream)
+        ctx.set_stream(main_stream.cuda_stream)
         ctx.init_random_range(0, F)
         dbatches = [ctx.batch(CSRHost(b.row_ptr, b.col, b.val, b.label)) for b in host_batches]
         ctx.reserve(B, max(b.nnz for b in host_batches))
@@ -202,18 +243,29 @@ def main():
         if prefetch and not args.host_path:
             for j in range(min(depth, args.steps)):
                 dbatches[j % len(dbatches)].prepare()  # every batch's sort runs inside the timed region
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
         for i in range(0 if args.host_path else args.steps):
             t += 1
+            evs[i].record(main_stream)
             if prefetch and i + depth < args.steps:
                 dbatches[(i + depth) % len(dbatches)].prepare()  # sorted on the side stream during step i
             ctx.step_batch(dbatches[i % len(dbatches)], t, STEP_SIZE, REG_PARAM, sync=False)
+        evs[args.steps].record(main_stream)
         ctx.sync()
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t_start
+        if not args.host_path:
+            median_ms = median_step_ms(evs)
         prof = ctx.profile_read() if args.profile_kernels else {}
         ctx.profile_enable(False)
         losses = ctx.loss_history()
         assert os.environ.get("FM_ABLATE") or np.all(np.isfinite(losses)), "non-finite loss"
+        if args.host_path_steps > 0 and not args.host_path and rank == 0:
+            hmed, hmean, t = host_path_leg(ctx, host_batches, t, args.host_path_steps, torch)
+            host_path = {"median_ms_per_step": hmed, "mean_ms_per_step": hmean, "steps": args.host_path_steps,
+                         "samples_per_s": B / (hmed * 1e-3) if hmed else None,
+                         "what": "fm_step with the host CSR each call: 8 B/entry + row_ptr + fp64 labels over PCIe, "
+                                 "device-side explode, then the step (two upload slots, copies overlap the previous step)"}
         U_mean = float(np.mean([uniques[i % len(dbatches)] for i in range(args.steps)]))
         parallelism = "single table" + ((", next batch sorted during the current step" if depth == 1 else
                                          f", batches sorted {depth} steps ahead on the side stream") if prefetch else "")
@@ -242,13 +294,17 @@ def main():
         t_start = time.perf_counter()
         # every timed batch's route / entry exchange / owner preparation runs inside the timed
         # region: batch i + 1's is enqueued behind step i's update (side stream)
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
         for i in range(args.steps):
             t += 1
             nxt = dbatches[(i + 1) % nb] if prefetch and i + 1 < args.steps else None
+            evs[i].record(tr.engine.main_stream)
             tr.step(dbatches[i % nb], t, STEP_SIZE, REG_PARAM, sync=False, prefetch=nxt)
+        evs[args.steps].record(tr.engine.main_stream)
         tr.ctx.sync()
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t_start
+        median_ms = median_step_ms(evs)
         prof = tr.ctx.profile_read() if args.profile_kernels else {}
         losses = tr.ctx.loss_history()
         assert os.environ.get("FM_ABLATE") or np.all(np.isfinite(losses)), "non-finite loss"
@@ -275,6 +331,7 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": ms_per_step,
+            "median_ms_per_step": median_ms,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -303,6 +360,9 @@ def main():
             line["step_roofline"] = {"bytes_per_step": step_bytes,
                                      "achieved_GBs": step_bytes / (ms_per_step * 1e-3) / 1e9,
                                      "frac": step_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS}
+        if host_path:
+            line["host_path_ms_per_step"] = host_path["median_ms_per_step"]
+            line["host_path"] = host_path
         if not args.no_cpu_baseline and world == 1:  # the CPU baseline belongs to the N = 1 line
             try:
                 line["cpu_baseline"] = cpu_baseline(cfg, host_batches[0], args.cpu_steps)

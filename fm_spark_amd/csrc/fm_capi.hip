@@ -51,13 +51,14 @@ static void parallel_chunks(int64_t n, int64_t min_per_thread, F&& f) {
   for (auto& x : th) x.join();
 }
 
-// Host CSR -> the device batch layout in pinned staging: [row_ptr int64 B+1][label f32 B]
-// [col u32 N][ent u32x2 N] (ent = the exploded {sample, x fp32}).  Validated on the way; host
-// threads write the staging directly.  check_range: ids must be owned by this context's table
+// Host CSR -> pinned staging [row_ptr int64 B+1][label f64 B][col u32 N][x f32 N]: 8 B per
+// entry cross PCIe; the device rebuilds each entry's sample index from row_ptr (k_explode) into
+// the exploded {sample, x} entries of Model.scala:148-153.  Validated on the way; host threads
+// write the staging directly.  check_range: ids must be owned by this context's table
 // (training); otherwise any non-negative int32 id is accepted (predict drops unknown ids).
 struct Staged {
   int64_t B = 0, N = 0, max_id = -1;
-  size_t o_lab = 0, o_col = 0, o_ent = 0;
+  size_t o_lab = 0, o_col = 0, o_x = 0, bytes = 0;
 };
 
 static Staged stage_csr(fm_ctx* ctx, const fm_csr* c, bool check_range, Pinned& pin) {
@@ -79,14 +80,15 @@ static Staged stage_csr(fm_ctx* ctx, const fm_csr* c, bool check_range, Pinned& 
     FM_REQUIRE(N == 0, "nnz > 0 with n_rows == 0");
   }
   g.o_lab = sizeof(int64_t) * (B + 1);
-  g.o_col = (g.o_lab + sizeof(float) * B + 15) / 16 * 16;
-  g.o_ent = (g.o_col + sizeof(uint32_t) * N + 15) / 16 * 16;
-  pin.ensure(g.o_ent + sizeof(uint32_t) * 2 * N + 16);
+  g.o_col = (g.o_lab + sizeof(double) * B + 15) / 16 * 16;
+  g.o_x = (g.o_col + sizeof(uint32_t) * N + 15) / 16 * 16;
+  g.bytes = g.o_x + sizeof(float) * N;
+  pin.ensure(g.bytes + 16);
   char* base = reinterpret_cast<char*>(pin.p);
   int64_t* rp = reinterpret_cast<int64_t*>(base);
-  float* lab = reinterpret_cast<float*>(base + g.o_lab);
+  double* lab = reinterpret_cast<double*>(base + g.o_lab);
   uint32_t* col = reinterpret_cast<uint32_t*>(base + g.o_col);
-  uint32_t* ent = reinterpret_cast<uint32_t*>(base + g.o_ent);
+  float* xs = reinterpret_cast<float*>(base + g.o_x);
   if (B > 0) std::memcpy(rp, c->row_ptr, sizeof(int64_t) * (B + 1));
   else rp[0] = 0;
   const int64_t F = ctx->cfg.num_features;
@@ -96,18 +98,14 @@ static Staged stage_csr(fm_ctx* ctx, const fm_csr* c, bool check_range, Pinned& 
     int64_t lmx = -1;
     int lbad = 0;
     for (int64_t i = r0; i < r1; ++i) {
-      lab[i] = (float)c->label[i];
+      lab[i] = c->label[i];  // Double, as the reference's label column (SGD.scala:145-146)
       for (int64_t e = c->row_ptr[i]; e < c->row_ptr[i + 1]; ++e) {
         const int32_t id = c->col[e];
         if (id < 0) lbad |= 1;
         else if (check_range && id >= F) lbad |= 2;
         col[e] = (uint32_t)id;
         lmx = std::max<int64_t>(lmx, id);
-        const float xf = (float)c->val[e];
-        uint32_t xb;
-        std::memcpy(&xb, &xf, 4);
-        ent[2 * e] = (uint32_t)i;
-        ent[2 * e + 1] = xb;
+        xs[e] = (float)c->val[e];
       }
     }
     if (lbad) bad.fetch_or(lbad);
@@ -125,10 +123,13 @@ static bool batch_fits(const fm_batch* b, const Staged& g) {
   return b->dev.row_ptr.bytes >= sizeof(int64_t) * (g.B + 1) &&
          b->dev.col.bytes >= sizeof(uint32_t) * std::max<int64_t>(g.N, 4) + 16 &&
          b->dev.ent.bytes >= sizeof(uint32_t) * 2 * std::max<int64_t>(g.N, 4) + 16 &&
-         b->dev.label.bytes >= sizeof(float) * std::max<int64_t>(g.B, 4) + 16;
+         b->dev.label.bytes >= sizeof(double) * std::max<int64_t>(g.B, 4) + 16 &&
+         b->up.bytes >= g.bytes + 16;
 }
 
-// b's device buffers (grown, never shrunk) filled from the staging by async copies on st.
+// b's device buffers (grown, never shrunk) filled from the staging by one async copy on st (into
+// b->up, the staging's device image), then col / label / row_ptr and the exploded entries are
+// laid out from it by one kernel pass on st.
 static void copy_staged(fm_ctx* ctx, const Staged& g, const Pinned& pin, fm_batch* b, hipStream_t st) {
   const int64_t B = g.B, N = g.N;
   b->owner = ctx;
@@ -139,14 +140,14 @@ static void copy_staged(fm_ctx* ctx, const Staged& g, const Pinned& pin, fm_batc
   b->dev.row_ptr.ensure(sizeof(int64_t) * (B + 1));
   b->dev.col.ensure(sizeof(uint32_t) * std::max<int64_t>(N, 4) + 16);
   b->dev.ent.ensure(sizeof(uint32_t) * 2 * std::max<int64_t>(N, 4) + 16);
-  b->dev.label.ensure(sizeof(float) * std::max<int64_t>(B, 4) + 16);
-  const char* base = reinterpret_cast<const char*>(pin.p);
-  FM_HIP_CHECK(hipMemcpyAsync(b->dev.row_ptr.p, base, sizeof(int64_t) * (B + 1), hipMemcpyHostToDevice, st));
-  if (N > 0) {
-    FM_HIP_CHECK(hipMemcpyAsync(b->dev.col.p, base + g.o_col, sizeof(uint32_t) * N, hipMemcpyHostToDevice, st));
-    FM_HIP_CHECK(hipMemcpyAsync(b->dev.ent.p, base + g.o_ent, sizeof(uint32_t) * 2 * N, hipMemcpyHostToDevice, st));
-  }
-  if (B > 0) FM_HIP_CHECK(hipMemcpyAsync(b->dev.label.p, base + g.o_lab, sizeof(float) * B, hipMemcpyHostToDevice, st));
+  b->dev.label.ensure(sizeof(double) * std::max<int64_t>(B, 4) + 16);
+  b->up.ensure(g.bytes + 16);
+  FM_HIP_CHECK(hipMemcpyAsync(b->up.p, pin.p, g.bytes, hipMemcpyHostToDevice, st));
+  const char* up = b->up.as<char>();
+  launch_explode(reinterpret_cast<const int64_t*>(up), reinterpret_cast<const double*>(up + g.o_lab),
+                 reinterpret_cast<const uint32_t*>(up + g.o_col), reinterpret_cast<const float*>(up + g.o_x), B, N,
+                 b->dev.row_ptr.as<int64_t>(), b->dev.label.as<double>(), b->dev.col.as<uint32_t>(),
+                 b->dev.ent.as<uint2>(), st);
 }
 
 // Synchronous upload (fm_batch_create, fm_predict, fm_loss_grad): staged in the context's
@@ -168,7 +169,7 @@ fm_batch* host_batch(fm_ctx* ctx) {
 void reserve_work(fm_ctx* ctx, int64_t B, int64_t N) {
   StepWork& w = ctx->work;
   w.S.ensure(sizeof(float) * (size_t)std::max<int64_t>(B, 1) * ctx->kp);
-  w.yl.ensure(sizeof(float) * 2 * (size_t)std::max<int64_t>(B, 1));
+  w.yl.ensure(sizeof(double2) * (size_t)std::max<int64_t>(B, 1));
   w.sort.ensure(std::max<int64_t>(N, 1));
   const int64_t nranges = (N + 255) / 256;  // update waves (fm_kernels.hip, kWaveEnt)
   w.part.ensure(sizeof(double) * (size_t)std::max<int64_t>(nranges, 1) * 2 * (ctx->kp + 2));

@@ -84,6 +84,7 @@ struct fm_batch {
   int device = 0;
   BatchDev dev;
   int64_t max_id = -1;
+  DevBuf up;  // device image of the host staging (fm_capi.hip copy_staged)
   // feature-major view produced by fm_batch_prepare (consumed once by the next step)
   DevBuf skeys, sents;
   hipEvent_t ready = nullptr;     // recorded on the side stream after the prepared sort
@@ -99,6 +100,7 @@ struct fm_batch {
     if (last_use) (void)hipEventDestroy(last_use);
     skeys.release();
     sents.release();
+    up.release();
     dev.row_ptr.release();
     dev.col.release();
     dev.ent.release();
@@ -265,6 +267,15 @@ int guarded(fm_ctx* ctx, F&& f) {
     return FM_ERR_ARG;
   }
   std::lock_guard<std::mutex> lk(ctx->mu);
+  // the caller's current device is restored on the way out (torch and other contexts keep theirs)
+  int prev_dev = -1;
+  if (hipGetDevice(&prev_dev) != hipSuccess) prev_dev = -1;
+  struct Restore {
+    int d;
+    ~Restore() {
+      if (d >= 0) (void)hipSetDevice(d);
+    }
+  } restore{prev_dev};
   try {
     FM_HIP_CHECK(hipSetDevice(ctx->cfg.device));
     return f();

@@ -110,12 +110,12 @@ void radix_sort_pairs64_bits(SortWork& w, const uint32_t* keys_in, const uint2* 
 // Model.scala:148-153 kept both as CSR (row_ptr) and as COO entries ent[e] = {sample, x bits}.
 struct BatchDev {
   int64_t n_rows = 0, nnz = 0;
-  DevBuf row_ptr, col, ent, label;  // int64 [B+1], uint32 [N] feature slot, uint2 [N], float [B]
+  DevBuf row_ptr, col, ent, label;  // int64 [B+1], uint32 [N] feature slot, uint2 [N], double [B]
 };
 
 struct StepWork {
   DevBuf S;         // [B * kp] float: per-sample vfxiSum
-  DevBuf yl;        // [B] float2 {yhat, y}
+  DevBuf yl;        // [B] double2 {yhat, y} (fp64: r = yhat - y enters every gradient)
   DevBuf loss_part; // [n_fwd_blocks] double2 {loss, n_loss}
   DevBuf part;      // [ceil(N / 256) * 2 * (kp+2)] double partial gradients (one range per update wave)
   DevBuf ucnt;      // [n_update_blocks] uint32 distinct-id counts per block
@@ -156,7 +156,7 @@ void launch_forward(const TableView& T, const BatchDev& b, StepWork& w, const St
 struct SegSource {
   const float* S;
   int64_t s_stride;
-  const float2* yl;
+  const double2* yl;
   int64_t yl_stride;
 };
 // emit != nullptr (replicated mode): the per-slot gradient sums go to emit[rows][kp + 4] as
@@ -188,5 +188,10 @@ void launch_segment_sum(const uint32_t* skeys, const uint32_t* svals, int64_t n,
                         int32_t k, uint32_t* run_index, int32_t* out_keys, double* out_sums,
                         int64_t* n_out_dev, hipStream_t st);
 void launch_count_present(const TableView& T, int64_t* out, hipStream_t st);
+// the uploaded CSR image (row_ptr, label, col, x) -> the device batch: row_ptr / label / col copied,
+// ent[e] = {sample of e, x bits} rebuilt from row_ptr (the explode of Model.scala:148-153)
+void launch_explode(const int64_t* row_ptr_in, const double* label_in, const uint32_t* col_in, const float* x_in,
+                    int64_t B, int64_t N, int64_t* row_ptr, double* label, uint32_t* col, uint2* ent,
+                    hipStream_t st);
 
 }  // namespace fmhip

@@ -25,6 +25,7 @@
 // SGD.scala:157-181).  S_b(S_a(z)) = S_{a+b}(z) for a, b >= 0, so each row header keeps the
 // cumulative shrink `cum` it has received; a row read when the running total is cumE is first
 // brought current by S_{cumE - cum}.  Export flushes every row.
+#include <algorithm>
 #include <cstdlib>
 
 #include "fm_device.h"
@@ -103,9 +104,9 @@ template <int GS, int TEAM, int MODE, int U>
 __global__ __launch_bounds__(kBlock, FM_FWD_MINW) void k_forward(TableView T, const int64_t* __restrict__ row_ptr,
                                                     const uint32_t* __restrict__ col,
                                                     const uint2* __restrict__ ent,
-                                                    const float* __restrict__ label, int64_t B,
+                                                    const double* __restrict__ label, int64_t B,
                                                     double w0, double cumE, float* __restrict__ S_out,
-                                                    float2* __restrict__ yl_out, double2* __restrict__ loss_part,
+                                                    double2* __restrict__ yl_out, double2* __restrict__ loss_part,
                                                     FwdOut xo) {
   constexpr bool PARTIAL = MODE == kPartial;
   constexpr int RPP = TEAM / GS;  // entries per pass
@@ -177,7 +178,7 @@ __global__ __launch_bounds__(kBlock, FM_FWD_MINW) void k_forward(TableView T, co
     if (PARTIAL) {  // vectors [pair][kp] in S_out, scalars {sum v^2 x^2, sum w x} in yl_out
       if (rs == 0 && qok)
         *reinterpret_cast<float4*>(S_out + s * kp + g * 4) = make_float4((float)a0, (float)a1, (float)a2, (float)a3);
-      if (tl == 0) yl_out[s] = make_float2((float)vv, (float)wx);
+      if (tl == 0) yl_out[s] = make_double2(vv, wx);
       continue;
     }
     double ss = qok ? a0 * a0 + a1 * a1 + a2 * a2 + a3 * a3 : 0.0;
@@ -190,7 +191,7 @@ __global__ __launch_bounds__(kBlock, FM_FWD_MINW) void k_forward(TableView T, co
       continue;
     }
     if (MODE == kLossGrad) {
-      const double d = yhat - (double)label[s];
+      const double d = yhat - label[s];
       const int k = T.k;
       for (int64_t e = e0 + rs; e < e1; e += RPP) {
         const uint32_t id = col[e];
@@ -217,10 +218,10 @@ __global__ __launch_bounds__(kBlock, FM_FWD_MINW) void k_forward(TableView T, co
     if (rs == 0 && qok)
       *reinterpret_cast<float4*>(S_out + s * kp + g * 4) = make_float4((float)a0, (float)a1, (float)a2, (float)a3);
     if (tl == 0) {
-      const float y = label[s];
-      yl_out[s] = make_float2((float)yhat, y);
+      const double y = label[s];
+      yl_out[s] = make_double2(yhat, y);
       if (e1 > e0) {
-        const double d = yhat - (double)y;
+        const double d = yhat - y;
         loss_acc += d * d;  // pow(pred - label, 2.0), Model.scala:230
         nloss += 1.0;
       }
@@ -256,7 +257,7 @@ struct SegArgs {
   const uint2* sents;     // their entries {sample, x bits}, same order
   int64_t N;
   const float* S;    // per-sample rows of s_stride floats (vfxiSum first)
-  const float2* yl;  // {yhat, y} of sample s at yl[s * yl_stride]
+  const double2* yl;  // {yhat, y} of sample s at yl[s * yl_stride] (fp64)
   int64_t s_stride;
   int64_t yl_stride;
   double* part;      // [nranges][2][kp + 2] = [sum g_w | sum S*x*r (kp) | sum x*x*r]
@@ -341,7 +342,7 @@ __global__ __launch_bounds__(kBlock) void k_segment_update(SegArgs a) {
     }
     const uint32_t before = base > 0 ? a.skeys[base - 1] : kNone;
     const uint32_t after = base + kWaveEnt < a.N ? a.skeys[base + kWaveEnt] : kNone;
-    float2 yl[NP];
+    double2 yl[NP];
 #pragma unroll
     for (int i = 0; i < NP; ++i) {
       const uint32_t up = __shfl_up(key[i], 1);
@@ -357,7 +358,7 @@ __global__ __launch_bounds__(kBlock) void k_segment_update(SegArgs a) {
       const int l = li(i * 64 + lane);
       img_k[l] = make_uint2(key[i], (valid ? kFValid : 0u) | (end ? kFEnd : 0u) | (st ? kFStart : 0u));
       img_s[l] = (int)en[i].x;
-      yl[i] = valid ? a.yl[(int64_t)en[i].x * a.yl_stride] : make_float2(0.f, 0.f);
+      yl[i] = valid ? a.yl[(int64_t)en[i].x * a.yl_stride] : make_double2(0.0, 0.0);
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -391,7 +392,7 @@ __global__ __launch_bounds__(kBlock) void k_segment_update(SegArgs a) {
     for (int i = 0; i < NP; ++i) {
       const int l = li(i * 64 + lane);
       const double xd = (double)__uint_as_float(en[i].y);
-      const double yh = (double)yl[i].x, yy = (double)yl[i].y;
+      const double yh = yl[i].x, yy = yl[i].y;
       const double rj = yh - yy;
       img_d[l] = make_double2(xd * rj, (xd * xd) * rj);
       img_w[l] = xd * yh - yy;  // g_w = deltaWi * pred - label (SGD.scala:145)
@@ -976,20 +977,20 @@ void launch_fwd_t(const TableView& T, const BatchDev& b, StepWork& w, const Step
   }
   if (xo && xo->mode == kLossGrad) {
     hipLaunchKernelGGL((k_forward<GS, TEAM, kLossGrad, U>), grid, blk, 0, st, T, b.row_ptr.as<int64_t>(),
-                       b.col.as<uint32_t>(), b.ent.as<uint2>(), b.label.as<float>(), b.n_rows, p.w0, p.cumE, nullptr,
+                       b.col.as<uint32_t>(), b.ent.as<uint2>(), b.label.as<double>(), b.n_rows, p.w0, p.cumE, nullptr,
                        nullptr, nullptr, *xo);
     return;
   }
-  if (partial_out) {  // [n_rows][kp] vectors, then [n_rows] float2 scalars
+  if (partial_out) {  // [n_rows][kp] fp32 vectors, then [n_rows] double2 scalars
     hipLaunchKernelGGL((k_forward<GS, TEAM, kPartial, U>), grid, blk, 0, st, T, b.row_ptr.as<int64_t>(),
                        b.col.as<uint32_t>(), b.ent.as<uint2>(), nullptr, b.n_rows, p.w0, p.cumE, partial_out,
-                       reinterpret_cast<float2*>(partial_out + b.n_rows * T.kp), nullptr, none);
+                       reinterpret_cast<double2*>(partial_out + b.n_rows * T.kp), nullptr, none);
     return;
   }
   w.loss_part.ensure(sizeof(double2) * blocks);
   hipLaunchKernelGGL((k_forward<GS, TEAM, kTrain, U>), grid, blk, 0, st, T, b.row_ptr.as<int64_t>(),
-                     b.col.as<uint32_t>(), b.ent.as<uint2>(), b.label.as<float>(), b.n_rows, p.w0, p.cumE,
-                     w.S.as<float>(), w.yl.as<float2>(), w.loss_part.as<double2>(), none);
+                     b.col.as<uint32_t>(), b.ent.as<uint2>(), b.label.as<double>(), b.n_rows, p.w0, p.cumE,
+                     w.S.as<float>(), w.yl.as<double2>(), w.loss_part.as<double2>(), none);
 }
 
 }  // namespace
@@ -1035,7 +1036,7 @@ void launch_forward(const TableView& T, const BatchDev& b, StepWork& w, const St
 void launch_segment_update(const TableView& T, const BatchDev& b, StepWork& w, const StepParams& p,
                            const uint32_t* skeys, const uint2* sents, int64_t n_fwd_blocks,
                            double* stats_out, hipStream_t st, float* emit) {
-  SegSource src{w.S.as<float>(), T.kp, w.yl.as<float2>(), 1};
+  SegSource src{w.S.as<float>(), T.kp, w.yl.as<double2>(), 1};
   launch_segment_update(T, b.nnz, src, w, p, skeys, sents, n_fwd_blocks, stats_out, st, emit);
 }
 
@@ -1177,6 +1178,36 @@ void launch_loss_grad(const TableView& T, const BatchDev& b, double cumE, double
   StepWork unused;
   int64_t nblk = 0;
   launch_forward(T, b, unused, p, st, &nblk, nullptr, &xo);
+}
+
+// One team of 16 lanes per sample: its entries get {sample, x}; col, label and row_ptr are copied
+// alongside (grid-stride, the same pass).
+__global__ __launch_bounds__(kBlock) void k_explode(const int64_t* __restrict__ rp_in, const double* __restrict__ lab_in,
+                                                   const uint32_t* __restrict__ col_in, const float* __restrict__ x_in,
+                                                   int64_t B, int64_t* __restrict__ rp, double* __restrict__ lab,
+                                                   uint32_t* __restrict__ col, uint2* __restrict__ ent) {
+  constexpr int T = 16;
+  const int tl = threadIdx.x % T;
+  const int64_t gtid = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int64_t nthreads = (int64_t)gridDim.x * kBlock;
+  for (int64_t i = gtid; i <= B; i += nthreads) rp[i] = rp_in[i];
+  for (int64_t i = gtid; i < B; i += nthreads) lab[i] = lab_in[i];
+  for (int64_t s = gtid / T; s < B; s += nthreads / T) {
+    const int64_t e1 = rp_in[s + 1];
+    for (int64_t e = rp_in[s] + tl; e < e1; e += T) {
+      col[e] = col_in[e];
+      ent[e] = make_uint2((uint32_t)s, __float_as_uint(x_in[e]));
+    }
+  }
+}
+
+void launch_explode(const int64_t* row_ptr_in, const double* label_in, const uint32_t* col_in, const float* x_in,
+                    int64_t B, int64_t N, int64_t* row_ptr, double* label, uint32_t* col, uint2* ent,
+                    hipStream_t st) {
+  (void)N;
+  hipLaunchKernelGGL(k_explode, dim3(grid_for(std::max<int64_t>(B, 1) * 16, kBlock, 256 * 8)), dim3(kBlock), 0, st,
+                     row_ptr_in, label_in, col_in, x_in, B, row_ptr, label, col, ent);
+  FM_HIP_CHECK(hipGetLastError());
 }
 
 void launch_segment_sum(const uint32_t* skeys, const uint32_t* svals, int64_t n, const double* vecs, int32_t k,

@@ -26,12 +26,12 @@
 // sums are split per owner (fp32 on the wire), the per-feature gradient sums run over the
 // same entries in the same order.  Deterministic for a given R.
 // Traffic per rank and step (k = 16, z = 39, R = 8): entries 12 B each (off the critical path:
-// exchanged during the previous iteration), partials and S (kp + 2) * 4 B per (sample, owner)
+// exchanged during the previous iteration), partials and S (kp + 4) * 4 B per (sample, owner)
 // pair -- about 2 x 150 MB, against about 1 GB when rows and gradients of every distinct id
 // travel instead.
 // Wire buffers are structures of arrays over the pairs, so every k-vector is 16-B aligned and a
-// 64-B row at k = 16: partials [P][kp] sum v*x then [P] {sum v^2 x^2, sum w x}; S [P][kp] vfxiSum
-// then [P] {yhat, y}.
+// 64-B row at k = 16: partials [P][kp] fp32 sum v*x then [P] fp64 {sum v^2 x^2, sum w x}; S [P][kp]
+// fp32 vfxiSum then [P] fp64 {yhat, y}.
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
@@ -218,9 +218,9 @@ template <int GS>
 __global__ __launch_bounds__(kBlock) void k_shard_combine(const int32_t* __restrict__ pairidx,
                                                           const int64_t* __restrict__ poff, int R, int64_t B,
                                                           const float* __restrict__ part_vec,
-                                                          const float2* __restrict__ part_sc,
-                                                          const float* __restrict__ label, int kp, double w0,
-                                                          float* __restrict__ s_vec, float2* __restrict__ s_sc,
+                                                          const double2* __restrict__ part_sc,
+                                                          const double* __restrict__ label, int kp, double w0,
+                                                          float* __restrict__ s_vec, double2* __restrict__ s_sc,
                                                           double2* __restrict__ loss_part) {
   constexpr int TPB = kBlock / GS;
   const int tid = threadIdx.x, g = tid % GS;
@@ -233,9 +233,9 @@ __global__ __launch_bounds__(kBlock) void k_shard_combine(const int32_t* __restr
     for (int o = 0; o < R; ++o) {
       const int32_t ix = pi[o];
       if (ix >= 0) {
-        const float2 t = part_sc[poff[o] + ix];
-        vv += (double)t.x;
-        wx += (double)t.y;
+        const double2 t = part_sc[poff[o] + ix];
+        vv += t.x;
+        wx += t.y;
         any = true;
       }
     }
@@ -262,13 +262,13 @@ __global__ __launch_bounds__(kBlock) void k_shard_combine(const int32_t* __restr
     for (int o = 1; o < GS; o <<= 1) ss += __shfl_xor(ss, o);
     const double yhat = 0.5 * (ss - vv) + wx + w0;
     if (g == 0) {
-      const float y = label[s];
+      const double y = label[s];
       for (int o = 0; o < R; ++o) {
         const int32_t ix = pi[o];
-        if (ix >= 0) s_sc[poff[o] + ix] = make_float2((float)yhat, y);
+        if (ix >= 0) s_sc[poff[o] + ix] = make_double2(yhat, y);
       }
       if (any) {
-        const double d = yhat - (double)y;
+        const double d = yhat - y;
         loss_acc += d * d;
         nloss += 1.0;
       }
@@ -398,8 +398,9 @@ int fm_shard_route(fm_ctx* ctx, fm_batch* b, void* send_slot, void* send_ent, in
     hipLaunchKernelGGL(k_owner_offsets, dim3(1), dim3(64), 0, st, tot, R, S.poff.as<int64_t>());
     if (N > 0) {
       // wire keys owner << sb | slot with payload {pair index within the owner's block, x}; one
-      // stable pass over the owner bits partitions them (CSR order kept inside each owner)
-      const int sb = bits_for(std::max<int64_t>(ctx->rows - 1, 1));
+      // stable pass over the owner bits partitions them (CSR order kept inside each owner).  sb
+      // must hold the largest slot of ANY owner (owner 0 has the most rows), the same on every rank
+      const int sb = bits_for(std::max<int64_t>((ctx->cfg.num_features - 1) / R, 1));
       const int ob = bits_for(R - 1);
       FM_REQUIRE(sb + ob <= 32, "route key does not fit 32 bits");
       ctx->sh_pay.ensure(sizeof(uint2) * std::max<int64_t>(N, 4) + 16);
@@ -544,10 +545,10 @@ int fm_shard_combine(fm_ctx* ctx, fm_batch* b, const void* partials_in, void* s_
     const int64_t* poff = S.poff.as<int64_t>();
     const int kp = ctx->kp;
     const float* pin = reinterpret_cast<const float*>(partials_in);
-    const float2* psc = reinterpret_cast<const float2*>(pin ? pin + Ps * kp : nullptr);
+    const double2* psc = reinterpret_cast<const double2*>(pin ? pin + Ps * kp : nullptr);
     float* so = reinterpret_cast<float*>(s_send);
-    float2* ssc = reinterpret_cast<float2*>(so ? so + Ps * kp : nullptr);
-    const float* lab = b->dev.label.as<float>();
+    double2* ssc = reinterpret_cast<double2*>(so ? so + Ps * kp : nullptr);
+    const double* lab = b->dev.label.as<double>();
     double2* lp = ctx->work.loss_part.as<double2>();
     const double w0 = ctx->cfg.w0;
     const dim3 grid((unsigned)blocks), blk(kBlock);
@@ -584,7 +585,7 @@ int fm_shard_owner_update(fm_ctx* ctx, fm_batch* b, const void* s_recv, int32_t 
     FM_HIP_CHECK(hipStreamWaitEvent(st, S.ready_upd, 0));
     hipEvent_t e0 = ctx->prof_begin(st);
     const float* Srow = reinterpret_cast<const float*>(s_recv);  // [P][kp] S, then [P] {yhat, y}
-    SegSource src{Srow, ctx->kp, reinterpret_cast<const float2*>(Srow ? Srow + S.P * ctx->kp : nullptr), 1};
+    SegSource src{Srow, ctx->kp, reinterpret_cast<const double2*>(Srow ? Srow + S.P * ctx->kp : nullptr), 1};
     launch_segment_update(ctx->view(), n, src, ctx->work, p, S.skeys.as<uint32_t>(), S.sents.as<uint2>(),
                           S.loss_blocks, stats, st);
     ctx->prof_end("owner_update", e0, st);

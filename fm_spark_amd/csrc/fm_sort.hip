@@ -33,10 +33,10 @@ static_assert(kBlock == 256 || kBlock == 512, "sort block must be 256 or 512 thr
 constexpr int kWaves = kBlock / 64;
 constexpr int kMinRB = kBlock == 512 ? 9 : 8;  // the block scans hold R / kBlock >= 1 digits per thread
 #ifndef FM_SORT_ROUNDS
-#define FM_SORT_ROUNDS 8
+#define FM_SORT_ROUNDS (4096 / FM_SORT_BLOCK)  // 4096-key tiles whatever the block size
 #endif
 constexpr int kRounds = FM_SORT_ROUNDS;  // keys per thread per tile
-constexpr int kTile = kBlock * kRounds;  // 4096 keys per tile
+constexpr int kTile = kBlock * kRounds;  // 4096 keys per tile (unless FM_SORT_ROUNDS is overridden on purpose)
 constexpr int kMaxRadix = 1 << 10;
 
 // Tile of a block.  With FM_SORT_XCD the tiles of one XCD (blocks b = x mod 8 are dispatched

@@ -2,7 +2,8 @@
 
 * ``synthetic_batch`` — the Criteo-shaped synthetic workload of BASELINE.md / SURVEY.md §8(d):
   39 fields per sample (13 numeric with x = log1p(Poisson(3)) rounded to fp32, 26
-  categorical with x = 1.0).  Field f's feature id is splitmix64(f * 2^32 + rank) mod F
+  categorical with x = 1.0; ``exact=True`` keeps x and the regression labels in fp64, as Spark's
+  Double columns hold them).  Field f's feature id is splitmix64(f * 2^32 + rank) mod F
   with rank ~ Zipf(s) (s = 1.05, or 1.2 for the c5 skew); ids that collide inside a row are
   re-drawn, so every row holds 39 distinct ids in ascending order.  Labels are
   Bernoulli(0.25) ("binary") or <w*, x> + N(0, 0.1) ("regression", c5).
@@ -58,8 +59,11 @@ def _field_ids(field: int, ranks: np.ndarray, F: int) -> np.ndarray:
 
 
 def synthetic_batch(n_rows: int, num_features: int, *, seed: int = DEFAULT_SEED, batch_index: int = 0,
-                    zipf_s: float = 1.05, labels: str = "binary", w_star: np.ndarray | None = None) -> Batch:
-    """One mini-batch of the synthetic workload (deterministic in (seed, batch_index))."""
+                    zipf_s: float = 1.05, labels: str = "binary", w_star: np.ndarray | None = None,
+                    exact: bool = False) -> Batch:
+    """One mini-batch of the synthetic workload (deterministic in (seed, batch_index)).  exact:
+    numeric values and regression labels are not rounded to fp32 (the device rounds x to fp32 on
+    upload and keeps labels in fp64; parity tests of that rounding use this)."""
     F = int(num_features)
     if F < N_FIELDS:
         raise ValueError("num_features must be >= 39")
@@ -71,7 +75,7 @@ def synthetic_batch(n_rows: int, num_features: int, *, seed: int = DEFAULT_SEED,
         ids[:, f] = _field_ids(f, ranks[:, f], F)
     vals = np.ones((B, N_FIELDS), dtype=np.float64)
     pois = rng.poisson(3.0, size=(B, N_NUMERIC))
-    vals[:, :N_NUMERIC] = np.log1p(pois).astype(np.float32).astype(np.float64)
+    vals[:, :N_NUMERIC] = np.log1p(pois) if exact else np.log1p(pois).astype(np.float32).astype(np.float64)
     # re-draw colliding ids (rare: hash collisions mod F)
     srt = np.sort(ids, axis=1)
     bad = np.nonzero((srt[:, 1:] == srt[:, :-1]).any(axis=1))[0]
@@ -90,7 +94,8 @@ def synthetic_batch(n_rows: int, num_features: int, *, seed: int = DEFAULT_SEED,
         if w_star is None:
             raise ValueError("regression labels need w_star")
         y = (w_star[ids] * vals).sum(axis=1) + rng.normal(0.0, 0.1, B)
-        y = y.astype(np.float32).astype(np.float64)
+        if not exact:
+            y = y.astype(np.float32).astype(np.float64)
     else:
         raise ValueError(labels)
     row_ptr = np.arange(B + 1, dtype=np.int64) * N_FIELDS

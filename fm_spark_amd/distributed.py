@@ -20,7 +20,7 @@ so the next routing, entry exchange and slot sort overlap the current update.
 Every rank steps its own mini-batch; the iteration's miniBatchSize is the sum over ranks
 (weak scaling: the global batch grows with R).  The result equals one single-table step over
 the ranks' batches concatenated in rank order, up to fp summation order (deterministic for a
-given R).  Only entries (12 B) and twice kp + 2 floats per (sample, owner) pair cross xGMI
+given R).  Only entries (12 B) and twice kp + 4 words per (sample, owner) pair cross xGMI
 -- no table row or per-id gradient does.
 """
 
@@ -56,7 +56,7 @@ class HipShardEngine:
         N.check(self._lib.fm_set_side_stream(self.ctx.handle, C.c_void_p(self.side_stream.cuda_stream)),
                 "fm_set_side_stream")
         self.kp = (k + 3) // 4 * 4
-        self.width = self.kp + 2  # floats per pair on the wire: [P][kp] vectors, then [P][2] scalars
+        self.width = self.kp + 4  # 4-B words per pair on the wire: [P][kp] fp32 vectors, then [P] fp64 x 2 scalars
 
     def _empty(self, n, dtype):
         return self.torch.empty(max(int(n), 1), dtype=dtype, device=self.device)[: int(n)]
@@ -128,6 +128,17 @@ class HipShardEngine:
         return self.ctx.export_tables()
 
 
+def _global_rows(trainer, b) -> int:
+    """The all-reduced row count of b's iteration, kept on b until its step consumes it."""
+    gm = getattr(b, "_fm_global_rows", None)
+    if gm is None:
+        t = trainer.torch.tensor([int(b.n_rows)], dtype=trainer.torch.int64, device=trainer.device)
+        trainer.dist.all_reduce(t, group=trainer.group)
+        gm = int(t.item())
+        b._fm_global_rows = gm
+    return gm
+
+
 class _Plan:
     """One batch's exchange plan: what the batch-only phases produced (counts per peer and the
     received entries, which the owner phases read until the iteration's forward is done)."""
@@ -155,8 +166,6 @@ class ShardedTrainer:
         self.engine = engine if engine is not None else HipShardEngine(
             num_features, k, rank, world, device=device, seed=seed, init_sd=init_sd, w0=w0)
         self.device = self.engine.device
-        self._global_rows = {}
-        self._plans = {}
 
     # convenience passthroughs -------------------------------------------------------
     @property
@@ -177,13 +186,10 @@ class ShardedTrainer:
 
     # ------------------------------------------------------------------------------
     def global_rows(self, b) -> int:
-        """miniBatchSize of the iteration: the sum of every rank's rows (cached per batch)."""
-        key = id(b)
-        if key not in self._global_rows:
-            t = self.torch.tensor([int(b.n_rows)], dtype=self.torch.int64, device=self.device)
-            self.dist.all_reduce(t, group=self.group)
-            self._global_rows[key] = int(t.item())
-        return self._global_rows[key]
+        """miniBatchSize of the iteration: the sum of every rank's rows.  Cached on the batch object
+        itself until its step consumes it (a cache keyed by id(b) could hand a recycled id a stale
+        count, and the ranks would then disagree on whether to enter the collective)."""
+        return _global_rows(self, b)
 
     def _a2a(self, out, inp, out_splits, in_splits):
         self.dist.all_to_all_single(out, inp, output_split_sizes=[int(x) for x in out_splits],
@@ -193,12 +199,12 @@ class ShardedTrainer:
         return self.torch.empty(max(int(n), 1), dtype=dtype, device=self.device)[: int(n)]
 
     def _a2a_pairs(self, out, inp, out_pairs, in_pairs):
-        """All-to-all of a pair buffer in the wire layout (include/fm_hip.h): the [P][kp] vector
-        section, then the [P][2] scalar section, each exchanged with its own splits."""
+        """All-to-all of a pair buffer in the wire layout (include/fm_hip.h): the [P][kp] fp32 vector
+        section, then the [P][2] fp64 scalar section (4 words per pair), each with its own splits."""
         kp = self.engine.kp
         po, pi = int(np.sum(out_pairs)), int(np.sum(in_pairs))
         self._a2a(out[: po * kp], inp[: pi * kp], out_pairs * kp, in_pairs * kp)
-        self._a2a(out[po * kp:], inp[pi * kp:], out_pairs * 2, in_pairs * 2)
+        self._a2a(out[po * kp:], inp[pi * kp:], out_pairs * 4, in_pairs * 4)
 
     def _side(self):
         side = getattr(self.engine, "side", None)
@@ -208,8 +214,7 @@ class ShardedTrainer:
         """The batch-only phases of b's iteration (route, entry exchange, owner pair table and slot
         sort), enqueued on the side stream.  Every rank must prefetch the same iterations in the
         same order (the exchange is collective).  Idempotent until b's step consumes it."""
-        key = id(b)
-        if key in self._plans:
+        if getattr(b, "_fm_plan", None) is not None:
             return
         torch, R = self.torch, self.world
         with self._side():
@@ -226,7 +231,7 @@ class ShardedTrainer:
             recv_ent = self._empty(2 * ent_in.sum(), torch.int32)
             self._a2a(recv_ent, send_ent, 2 * ent_in, 2 * ent_out)
             self.engine.owner_prepare(b, recv_slot, recv_ent, ent_in, pair_in)
-        self._plans[key] = _Plan(ent_in, ent_out, pair_in, pair_out, (recv_slot, recv_ent))
+        b._fm_plan = _Plan(ent_in, ent_out, pair_in, pair_out, (recv_slot, recv_ent))
 
     def step(self, b, t: int, step_size: float, reg_param: float, sync: bool = True, prefetch=None) -> StepOut | None:
         """One iteration on this rank's batch b.  ``prefetch``: the batch of the next iteration,
@@ -234,13 +239,14 @@ class ShardedTrainer:
         pass the same schedule on every rank)."""
         W = self.engine.width
         gm = self.global_rows(b)
+        b._fm_global_rows = None  # consumed: a later step of the same batch re-counts
         if gm == 0:  # SGD.scala:126-128: every rank skips together
             self._drop_plan(b)
             if prefetch is not None:
                 self.prefetch(prefetch)
             return StepOut(0.0, 0, 0, 0, executed=False)
         self.prefetch(b)  # no-op when an earlier step already did
-        plan = self._plans.pop(id(b))
+        plan, b._fm_plan = b._fm_plan, None
         partials = self.engine.owner_forward(b, int(plan.pair_in.sum()))
         part_in = self._empty(plan.pair_out.sum() * W, self.torch.float32)
         self._a2a_pairs(part_in, partials, plan.pair_out, plan.pair_in)
@@ -265,7 +271,8 @@ class ShardedTrainer:
         plan.keep = None
 
     def _drop_plan(self, b):
-        plan = self._plans.pop(id(b), None)
+        plan = getattr(b, "_fm_plan", None)
+        b._fm_plan = None
         if plan is not None:
             self._retire(plan)
 
@@ -332,7 +339,6 @@ class ReplicatedTrainer:
         self.engine = engine if engine is not None else HipReplEngine(
             num_features, k, device=device, seed=seed, init_sd=init_sd, w0=w0)
         self.device = self.engine.device
-        self._global_rows = {}
 
     @property
     def ctx(self):
@@ -351,15 +357,11 @@ class ReplicatedTrainer:
         return self.engine.export_tables()
 
     def global_rows(self, b) -> int:
-        key = id(b)
-        if key not in self._global_rows:
-            t = self.torch.tensor([int(b.n_rows)], dtype=self.torch.int64, device=self.device)
-            self.dist.all_reduce(t, group=self.group)
-            self._global_rows[key] = int(t.item())
-        return self._global_rows[key]
+        return _global_rows(self, b)
 
     def step(self, b, t: int, step_size: float, reg_param: float, sync: bool = True) -> StepOut | None:
         gm = self.global_rows(b)
+        b._fm_global_rows = None
         if gm == 0:  # SGD.scala:126-128
             return StepOut(0.0, 0, 0, 0, executed=False)
         g = self.engine.grad_phase(b)

@@ -10,13 +10,17 @@ import torch
 
 
 def rows_to_soa(rows, kp):
-    """[P][kp + 2] rows -> the wire layout: [P][kp] vectors, then [P][2] scalars (flat)."""
-    return np.ascontiguousarray(np.concatenate([rows[:, :kp].reshape(-1), rows[:, kp:kp + 2].reshape(-1)]))
+    """[P][kp + 2] rows -> the wire layout (flat fp32 words): [P][kp] fp32 vectors, then [P][2]
+    fp64 scalars (each 2 words)."""
+    vec = np.asarray(rows[:, :kp], dtype=np.float32).reshape(-1)
+    sc = np.ascontiguousarray(np.asarray(rows[:, kp:kp + 2], dtype=np.float64)).reshape(-1).view(np.float32)
+    return np.ascontiguousarray(np.concatenate([vec, sc]))
 
 
 def soa_to_rows(flat, kp):
-    P = len(flat) // (kp + 2)
-    return np.concatenate([flat[: P * kp].reshape(P, kp), flat[P * kp:].reshape(P, 2)], axis=1)
+    P = len(flat) // (kp + 4)
+    sc = np.ascontiguousarray(flat[P * kp:]).view(np.float64).reshape(P, 2)
+    return np.concatenate([flat[: P * kp].reshape(P, kp).astype(np.float64), sc], axis=1)
 
 
 class NpBatch:
@@ -31,7 +35,7 @@ class NumpyShardEngine:
         self.device = torch.device("cpu")
         self.F, self.k, self.R, self.rank, self.w0 = num_features, k, world, rank, w0
         self.kp = (k + 3) // 4 * 4
-        self.width = self.kp + 2  # wire: [P][kp] vectors, then [P][2] scalars
+        self.width = self.kp + 4  # wire words: [P][kp] fp32 vectors, then [P][2] fp64 scalars
         self.rows = (num_features - rank + world - 1) // world
         self.w = np.zeros(self.rows)
         self.V = np.zeros((self.rows, k))
@@ -93,7 +97,7 @@ class NumpyShardEngine:
         has = np.diff(csr.row_ptr) > 0
         d = (yhat - csr.label)[has]
         b.loss = (float(np.sum(d * d)), int(has.sum()))
-        out = np.zeros((int(n_pairs_out), kp + 2), dtype=np.float32)
+        out = np.zeros((int(n_pairs_out), kp + 2), dtype=np.float64)
         for o in range(self.R):
             ix = b.pairidx[:, o]
             m = ix >= 0
@@ -124,7 +128,7 @@ class NumpyShardEngine:
         np.add.at(part[:, self.kp], pair, np.sum(V * V, axis=1) * x * x)
         np.add.at(part[:, self.kp + 1], pair, w * x)
         b.recv = (slots, x, pair)
-        return torch.from_numpy(rows_to_soa(part.astype(np.float32), self.kp))
+        return torch.from_numpy(rows_to_soa(part, self.kp))
 
     def owner_update(self, b, s_recv, t, step_size, reg_param, global_rows):
         if global_rows == 0:

@@ -23,13 +23,13 @@ def _concat(parts):
 
 
 def split_pairs(buf, counts, kp):
-    """A pair buffer in the wire layout ([P][kp] vectors, then [P][2] scalars) cut per peer."""
+    """A pair buffer in the wire layout ([P][kp] fp32 vectors, then [P][2] fp64 scalars = 4 words) cut per peer."""
     import torch
 
     counts = [int(c) for c in counts]
     P = sum(counts)
     vec = torch.split(buf[: P * kp], [c * kp for c in counts])
-    sc = torch.split(buf[P * kp:], [c * 2 for c in counts])
+    sc = torch.split(buf[P * kp:], [c * 4 for c in counts])
     return list(zip(vec, sc))
 
 
@@ -76,12 +76,14 @@ def _simulated_step(engines, batches, t, step_size, reg):
     return sum(e.last_stats()[0] for e in engines), sum(e.last_stats()[2] for e in engines)
 
 
-@pytest.mark.parametrize("R,k", [(1, 8), (2, 16), (3, 5), (4, 32)])
-def test_hip_shard_phases_match_single_table(gpu, R, k):
+# F = R * 2^s + 1 (513 at R = 2 and R = 4): owner 0 holds one slot more than the others, and that
+# slot (id F - 1, made hot) needs one more key bit than a rank with fewer rows would give it
+@pytest.mark.parametrize("R,k,F,hot", [(1, 8, 503, 11), (2, 16, 503, 11), (3, 5, 503, 11), (4, 32, 503, 11),
+                                       (2, 8, 513, 512), (4, 4, 513, 512)])
+def test_hip_shard_phases_match_single_table(gpu, R, k, F, hot):
     from fm_spark_amd._native import CSRHost
     from fm_spark_amd.distributed import HipShardEngine
 
-    F = 503
     _, ids, w, V = make_problem(3, 1, F, k, 1)
     engines = [HipShardEngine(F, k, r, R) for r in range(R)]
     for e in engines:
@@ -89,7 +91,7 @@ def test_hip_shard_phases_match_single_table(gpu, R, k):
     model = R_.Model.empty(F, k)
     model.load(ids, w, V)
     for t in range(1, 4):
-        parts = [make_problem(100 * t + r, 120 + 17 * r, F, k, 9, hot=11)[0] for r in range(R)]
+        parts = [make_problem(100 * t + r, 120 + 17 * r, F, k, 9, hot=hot)[0] for r in range(R)]
         bs = [e.batch(CSRHost(p.row_ptr, p.col, p.val, p.label)) for e, p in zip(engines, parts)]
         loss, nu = _simulated_step(engines, bs, t, 0.3, 1e-4)
         cat = _concat(parts)
