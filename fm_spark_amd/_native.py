@@ -72,6 +72,7 @@ SIGNATURES = {
     "fm_init_random": (C.c_int, [_P, _I32P, C.c_int64]),
     "fm_init_random_range": (C.c_int, [_P, C.c_int64, C.c_int64]),
     "fm_export_tables": (C.c_int, [_P, _I32P, _DP, _DP, C.c_int64, _I64P]),
+    "fm_export_rows": (C.c_int, [_P, _I32P, C.c_int64, _DP, _DP, C.POINTER(C.c_int8)]),
     "fm_num_present": (C.c_int64, [_P]),
     "fm_epoch": (C.c_int64, [_P]),
     "fm_batch_create": (C.c_int, [_P, C.POINTER(fm_csr), C.POINTER(_P)]),

@@ -441,6 +441,33 @@ int fm_export_tables(fm_ctx* ctx, int32_t* ids, double* w, double* V, int64_t ca
   });
 }
 
+int fm_export_rows(fm_ctx* ctx, const int32_t* ids, int64_t n, double* w, double* V, int8_t* present) {
+  return guarded(ctx, [&]() -> int {
+    FM_REQUIRE(n >= 0, "negative n");
+    if (n == 0) return FM_OK;
+    FM_REQUIRE(ids && w && V && present, "null argument");
+    const int R = ctx->cfg.shard_count;
+    for (int64_t i = 0; i < n; ++i) {
+      FM_REQUIRE(ids[i] >= 0 && ids[i] < ctx->cfg.num_features, "id out of [0, num_features)");
+      FM_REQUIRE(ids[i] % R == ctx->cfg.shard_index, "id not owned by this shard");
+    }
+    const int k = ctx->cfg.k;
+    DevBuf di, dw, dv, dp;
+    di.ensure(sizeof(int32_t) * n);
+    dw.ensure(sizeof(double) * n);
+    dv.ensure(sizeof(double) * n * k);
+    dp.ensure(sizeof(int8_t) * n);
+    FM_HIP_CHECK(hipMemcpyAsync(di.p, ids, sizeof(int32_t) * n, hipMemcpyHostToDevice, ctx->stream));
+    launch_gather_rows(ctx->view(), di.as<int32_t>(), n, ctx->cum_host.back(), dw.as<double>(), dv.as<double>(),
+                       dp.as<int8_t>(), ctx->stream);
+    FM_HIP_CHECK(hipMemcpyAsync(w, dw.p, sizeof(double) * n, hipMemcpyDeviceToHost, ctx->stream));
+    FM_HIP_CHECK(hipMemcpyAsync(V, dv.p, sizeof(double) * n * k, hipMemcpyDeviceToHost, ctx->stream));
+    FM_HIP_CHECK(hipMemcpyAsync(present, dp.p, sizeof(int8_t) * n, hipMemcpyDeviceToHost, ctx->stream));
+    FM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    return FM_OK;
+  });
+}
+
 int fm_batch_create(fm_ctx* ctx, const fm_csr* csr, fm_batch** out) {
   return guarded(ctx, [&]() -> int {
     FM_REQUIRE(out != nullptr, "null out");

@@ -177,6 +177,8 @@ void launch_init_random(const TableView& T, const int32_t* ids, int64_t n, int64
 void launch_load_rows(const TableView& T, const int32_t* ids, int64_t n, const double* w,
                       const double* V, int32_t epoch, double cumE, hipStream_t st);
 void launch_flush(const TableView& T, int32_t epoch, double cumE, hipStream_t st);
+void launch_gather_rows(const TableView& T, const int32_t* ids, int64_t n, double cumE, double* w, double* V,
+                        int8_t* present, hipStream_t st);
 void launch_table_reset(const TableView& T, hipStream_t st);
 void launch_predict(const TableView& T, const BatchDev& b, double cumE, double w0, double lo, double hi,
                     double* pred, hipStream_t st);

@@ -825,12 +825,21 @@ __device__ __forceinline__ float gauss_draw(uint64_t seed, int64_t id, int f, do
   return (float)(g * sd);
 }
 
+// ids != nullptr: the listed ids (those this shard owns); else every id in [id_begin, id_begin + n)
+// that this shard owns, walked slot by slot (i = the i-th owned id of the range)
 __global__ void k_init_random(TableView T, const int32_t* __restrict__ ids, int64_t n, int64_t id_begin,
                               uint64_t seed, double sd, int32_t epoch, double cumE) {
+  const int64_t R = T.shard_count;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t id = ids ? (int64_t)ids[i] : id_begin + i;
-    if (id % T.shard_count != T.shard_index) continue;
-    const int64_t slot = id / T.shard_count;
+    int64_t id;
+    if (ids) {
+      id = (int64_t)ids[i];
+      if (id % R != T.shard_index) continue;
+    } else {
+      const int64_t first = id_begin + ((T.shard_index - id_begin % R) % R + R) % R;  // first owned id >= id_begin
+      id = first + i * R;
+    }
+    const int64_t slot = id / R;
     if (slot >= T.rows) continue;
     RowHdr o;
     o.w = gauss_draw(seed, id, -1, sd);
@@ -874,6 +883,22 @@ __global__ void k_load_rows(TableView T, const int32_t* __restrict__ ids, int64_
     o.cum = cumE;
     for (int f = 0; f < T.kp; ++f) T.v(slot)[f] = f < T.k ? (float)V[i * T.k + f] : 0.f;
     store_hdr(T, slot, o);
+  }
+}
+
+// Rows by feature id (owned by this shard), brought current (pending L1 applied) without writing
+// the table: the model Datasets queried by id (Strength / FactorizedInteraction, Model.scala:281,289)
+__global__ void k_gather_rows(TableView T, const int32_t* __restrict__ ids, int64_t n, double cumE,
+                              double* __restrict__ w_out, double* __restrict__ V_out, int8_t* __restrict__ present) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t slot = (int64_t)ids[i] / T.shard_count;
+    const RowHdr h = *T.hdr(slot);
+    const bool pr = h.t >= 0;
+    const double a = pr ? cumE - h.cum : 0.0;
+    present[i] = pr ? 1 : 0;
+    w_out[i] = pr ? (double)(a > 0.0 ? shrink_f(h.w, a) : h.w) : 0.0;
+    const float* v = T.v(slot);
+    for (int f = 0; f < T.k; ++f) V_out[i * T.k + f] = pr ? (double)(a > 0.0 ? shrink_f(v[f], a) : v[f]) : 0.0;
   }
 }
 
@@ -1086,6 +1111,12 @@ void launch_segment_update(const TableView& T, int64_t N, const SegSource& src, 
 void launch_init_random(const TableView& T, const int32_t* ids, int64_t n, int64_t id_begin, uint64_t seed,
                         double sd, int32_t epoch, double cumE, hipStream_t st) {
   if (n <= 0) return;
+  if (!ids) {  // a range: only the ids this shard owns
+    const int64_t R = T.shard_count, end = id_begin + n;
+    const int64_t first = id_begin + ((T.shard_index - id_begin % R) % R + R) % R;
+    n = first < end ? (end - first + R - 1) / R : 0;
+    if (n <= 0) return;
+  }
   hipLaunchKernelGGL(k_init_random, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, st, T, ids, n, id_begin, seed, sd,
                      epoch, cumE);
   FM_HIP_CHECK(hipGetLastError());
@@ -1103,6 +1134,13 @@ void launch_load_rows(const TableView& T, const int32_t* ids, int64_t n, const d
                       int32_t epoch, double cumE, hipStream_t st) {
   if (n <= 0) return;
   hipLaunchKernelGGL(k_load_rows, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, st, T, ids, n, w, V, epoch, cumE);
+  FM_HIP_CHECK(hipGetLastError());
+}
+
+void launch_gather_rows(const TableView& T, const int32_t* ids, int64_t n, double cumE, double* w, double* V,
+                        int8_t* present, hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_gather_rows, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, st, T, ids, n, cumE, w, V, present);
   FM_HIP_CHECK(hipGetLastError());
 }
 

@@ -123,6 +123,18 @@ class FMContext:
                                                N.ptr(V, C.c_double), cnt, C.byref(n)), "fm_export_tables")
         return ids[:cnt], w[:cnt], V[:cnt]
 
+    def export_rows(self, ids):
+        """(w, V, present) of the given ids as they stand now (pending L1 applied), without a
+        whole-table export (fm_export_rows)."""
+        ids = np.ascontiguousarray(ids, dtype=np.int32)
+        n = len(ids)
+        w = np.zeros(max(n, 1))
+        V = np.zeros((max(n, 1), self.k))
+        pres = np.zeros(max(n, 1), dtype=np.int8)
+        N.check(self._lib.fm_export_rows(self.handle, N.ptr(ids, C.c_int32), n, N.ptr(w, C.c_double),
+                                         N.ptr(V, C.c_double), N.ptr(pres, C.c_int8)), "fm_export_rows")
+        return w[:n], V[:n], pres[:n].astype(bool)
+
     def num_present(self) -> int:
         return N.check(self._lib.fm_num_present(self.handle), "fm_num_present")
 

@@ -114,6 +114,11 @@ int fm_init_from_batch(fm_ctx* ctx, fm_batch* data, int64_t* n_present);
  * pending L1 shrink.  cap = capacity in rows; *n receives the number of present rows
  * (call with cap 0 to size).  V is row-major [n][k]. */
 int fm_export_tables(fm_ctx* ctx, int32_t* ids, double* w, double* V, int64_t cap, int64_t* n);
+/* The rows of the given ids (each owned by this context) as they stand now, pending L1 shrink
+ * applied, without exporting the whole table (the model Datasets queried by id: at F = Int.MaxValue
+ * a full export is 2^31 rows).  present[i] = 1 for a present row, else 0 and a zero row.  V is
+ * row-major [n][k]. */
+int fm_export_rows(fm_ctx* ctx, const int32_t* ids, int64_t n, double* w, double* V, int8_t* present);
 int64_t fm_num_present(fm_ctx* ctx);
 /* Number of executed (non-empty) SGD steps. */
 int64_t fm_epoch(fm_ctx* ctx);
