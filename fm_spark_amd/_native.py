@@ -16,6 +16,9 @@ _LIB_PATH = Path(__file__).resolve().parent / "lib" / "libfm_hip.so"
 
 FM_OK = 0
 FM_NOTHING_TO_DO = 1
+FM_PARALLEL_NONE, FM_PARALLEL_SHARDED, FM_PARALLEL_REPLICATED = 0, 1, 2
+FM_TRANSPORT_AUTO, FM_TRANSPORT_RCCL, FM_TRANSPORT_COPY = 0, 1, 2
+FM_MAX_LOCAL = 16
 
 
 class FMError(RuntimeError):
@@ -32,6 +35,13 @@ class fm_config(C.Structure):
         ("w0", C.c_double),
         ("shard_index", C.c_int32),
         ("shard_count", C.c_int32),
+        ("parallel", C.c_int32),
+        ("n_gpus", C.c_int32),
+        ("devices", C.c_int32 * FM_MAX_LOCAL),
+        ("transport", C.c_int32),
+        ("n_procs", C.c_int32),
+        ("proc_rank", C.c_int32),
+        ("comm_id", C.c_uint8 * 128),
     ]
 
 
@@ -65,6 +75,7 @@ SIGNATURES = {
     "fm_create": (C.c_int, [C.POINTER(fm_config), C.POINTER(_P)]),
     "fm_destroy": (None, [_P]),
     "fm_last_error": (C.c_char_p, []),
+    "fm_comm_unique_id": (C.c_int, [C.POINTER(C.c_uint8)]),
     "fm_set_stream": (C.c_int, [_P, _P]),
     "fm_sync": (C.c_int, [_P]),
     "fm_reserve": (C.c_int, [_P, C.c_int64, C.c_int64]),

@@ -16,7 +16,8 @@ INCLUDE = PKG.parent / "include"
 ARCH = os.environ.get("FM_HIP_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
-SOURCES = ["fm_kernels.hip", "fm_sort.hip", "fm_capi.hip", "fm_shard.hip", "fm_sampler.cpp", "fm_libsvm.cpp"]
+SOURCES = ["fm_kernels.hip", "fm_sort.hip", "fm_capi.hip", "fm_shard.hip", "fm_group.hip", "fm_sampler.cpp",
+           "fm_libsvm.cpp"]
 HEADERS = ["fm_internal.h", "fm_device.h", "fm_context.h"]
 
 CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function", "-Wno-unused-variable"]
@@ -52,7 +53,8 @@ def build(verbose: bool = False, force: bool = False, out: Path | None = None, d
                 print(" ".join(cmd), file=sys.stderr)
             subprocess.run(cmd, check=True)
     if force or _newer(lib, objs):
-        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", str(lib)]
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", str(lib),
+               "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.run(cmd, check=True)

@@ -266,6 +266,7 @@ const char* fm_last_error(void) { return g_last_error.c_str(); }
 int fm_create(const fm_config* cfg, fm_ctx** out) {
   return guarded_free([&]() -> int {
     FM_REQUIRE(cfg && out, "null argument");
+    if (cfg->parallel != FM_PARALLEL_NONE) return group_create(cfg, out);  // several ranks (fm_group.hip)
     FM_REQUIRE(cfg->num_features >= 1 && cfg->num_features <= (int64_t(1) << 31), "num_features must be in [1, 2^31]");
     FM_REQUIRE(cfg->k >= 1 && cfg->k <= 256, "dimFactorization must be in [1, 256]");
     FM_REQUIRE(cfg->shard_count >= 1 && cfg->shard_index >= 0 && cfg->shard_index < cfg->shard_count,
@@ -306,6 +307,13 @@ void fm_destroy(fm_ctx* ctx) {
 }
 
 int fm_set_stream(fm_ctx* ctx, void* s) {
+  if (ctx && ctx->group) {  // a multi-GPU context: only with one local rank, whose streams these become
+    if (ctx->cfg.n_gpus != 1) {
+      set_error("fm_set_stream on a context with several local ranks");
+      return FM_ERR_ARG;
+    }
+    return fm_set_stream(group_member0(ctx), s);
+  }
   return guarded(ctx, [&]() -> int {
     FM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
     if (ctx->own_stream && ctx->stream) FM_HIP_CHECK(hipStreamDestroy(ctx->stream));
@@ -317,6 +325,13 @@ int fm_set_stream(fm_ctx* ctx, void* s) {
 }
 
 int fm_set_side_stream(fm_ctx* ctx, void* s) {
+  if (ctx && ctx->group) {  // a multi-GPU context: only with one local rank, whose streams these become
+    if (ctx->cfg.n_gpus != 1) {
+      set_error("fm_set_side_stream on a context with several local ranks");
+      return FM_ERR_ARG;
+    }
+    return fm_set_side_stream(group_member0(ctx), s);
+  }
   return guarded(ctx, [&]() -> int {
     FM_HIP_CHECK(hipStreamSynchronize(ctx->side));
     ctx->side = s ? reinterpret_cast<hipStream_t>(s) : ctx->side_own;
@@ -326,6 +341,7 @@ int fm_set_side_stream(fm_ctx* ctx, void* s) {
 
 int fm_sync(fm_ctx* ctx) {
   return guarded(ctx, [&]() -> int {
+    if (ctx->group) return group_sync(ctx);
     FM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
     return FM_OK;
   });
@@ -334,6 +350,7 @@ int fm_sync(fm_ctx* ctx) {
 int fm_reserve(fm_ctx* ctx, int64_t max_rows, int64_t max_nnz) {
   return guarded(ctx, [&]() -> int {
     FM_REQUIRE(max_rows >= 0 && max_nnz >= 0, "negative reserve");
+    if (ctx->group) return group_reserve(ctx, max_rows, max_nnz);
     reserve_work(ctx, max_rows, max_nnz);
     return FM_OK;
   });
@@ -343,6 +360,7 @@ int fm_load_tables(fm_ctx* ctx, const int32_t* ids, int64_t n, const double* w, 
   return guarded(ctx, [&]() -> int {
     FM_REQUIRE(n >= 0, "negative n");
     if (n == 0) return FM_OK;
+    if (ctx->group) return group_load_tables(ctx, ids, n, w, V);
     FM_REQUIRE(ids && w && V, "null argument");
     for (int64_t i = 0; i < n; ++i)
       FM_REQUIRE(ids[i] >= 0 && ids[i] < ctx->cfg.num_features, "id out of [0, num_features)");
@@ -368,6 +386,7 @@ int fm_init_random(fm_ctx* ctx, const int32_t* ids, int64_t n) {
     FM_REQUIRE(n >= 0, "negative n");
     if (n == 0) return FM_OK;
     FM_REQUIRE(ids, "null ids");
+    if (ctx->group) return group_init_random(ctx, ids, n, 0, 0);
     for (int64_t i = 0; i < n; ++i)
       FM_REQUIRE(ids[i] >= 0 && ids[i] < ctx->cfg.num_features, "id out of [0, num_features)");
     DevBuf di;
@@ -384,6 +403,7 @@ int fm_init_random(fm_ctx* ctx, const int32_t* ids, int64_t n) {
 int fm_init_random_range(fm_ctx* ctx, int64_t b, int64_t e) {
   return guarded(ctx, [&]() -> int {
     FM_REQUIRE(b >= 0 && e >= b && e <= ctx->cfg.num_features, "bad id range");
+    if (ctx->group) return group_init_random(ctx, nullptr, 0, b, e);
     launch_init_random(ctx->view(), nullptr, e - b, b, ctx->cfg.seed, ctx->cfg.init_sd, ctx->epoch,
                        ctx->cum_host.back(), ctx->stream);
     FM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
@@ -394,6 +414,10 @@ int fm_init_random_range(fm_ctx* ctx, int64_t b, int64_t e) {
 int64_t fm_num_present(fm_ctx* ctx) {
   int64_t n = -1;
   int rc = guarded(ctx, [&]() -> int {
+    if (ctx->group) {
+      n = group_num_present(ctx);
+      return FM_OK;
+    }
     DevBuf d;
     d.ensure(sizeof(int64_t));
     launch_count_present(ctx->view(), d.as<int64_t>(), ctx->stream);
@@ -410,6 +434,7 @@ int64_t fm_epoch(fm_ctx* ctx) { return ctx ? ctx->epoch : -1; }
 int fm_export_tables(fm_ctx* ctx, int32_t* ids, double* w, double* V, int64_t cap, int64_t* n) {
   return guarded(ctx, [&]() -> int {
     FM_REQUIRE(n != nullptr && cap >= 0, "bad arguments");
+    if (ctx->group) return group_export_tables(ctx, ids, w, V, cap, n);
     launch_flush(ctx->view(), ctx->epoch, ctx->cum_host.back(), ctx->stream);  // apply pending L1 to every row
     FM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
     const int k = ctx->cfg.k, kp = ctx->kp, S = ctx->stride;
@@ -446,6 +471,7 @@ int fm_export_rows(fm_ctx* ctx, const int32_t* ids, int64_t n, double* w, double
     FM_REQUIRE(n >= 0, "negative n");
     if (n == 0) return FM_OK;
     FM_REQUIRE(ids && w && V && present, "null argument");
+    if (ctx->group) return group_export_rows(ctx, ids, n, w, V, present);
     const int R = ctx->cfg.shard_count;
     for (int64_t i = 0; i < n; ++i) {
       FM_REQUIRE(ids[i] >= 0 && ids[i] < ctx->cfg.num_features, "id out of [0, num_features)");
@@ -471,6 +497,7 @@ int fm_export_rows(fm_ctx* ctx, const int32_t* ids, int64_t n, double* w, double
 int fm_batch_create(fm_ctx* ctx, const fm_csr* csr, fm_batch** out) {
   return guarded(ctx, [&]() -> int {
     FM_REQUIRE(out != nullptr, "null out");
+    if (ctx->group) return group_batch_create(ctx, csr, out);
     std::unique_ptr<fm_batch> b(new fm_batch());
     upload_batch(ctx, csr, b.get(), true);
     *out = b.release();
@@ -489,6 +516,7 @@ void fm_batch_destroy(fm_batch* b) {
 int fm_batch_prepare(fm_ctx* ctx, fm_batch* b) {
   return guarded(ctx, [&]() -> int {
     FM_REQUIRE(b != nullptr && b->owner == ctx, "batch belongs to another context");
+    if (ctx->group) return group_batch_prepare(ctx, b);
     FM_REQUIRE(ctx->cfg.shard_count == 1, "fm_batch_prepare is for single-table contexts");
     const int64_t N = b->dev.nnz;
     if (N == 0) return FM_OK;
@@ -519,7 +547,10 @@ int64_t fm_batch_nnz(const fm_batch* b) { return b ? b->dev.nnz : -1; }
 
 int fm_step_batch(fm_ctx* ctx, fm_batch* batch, int32_t t, double step_size, double reg_param,
                   fm_step_out* out) {
-  return guarded(ctx, [&]() -> int { return step_impl(ctx, batch, t, step_size, reg_param, out); });
+  return guarded(ctx, [&]() -> int {
+    if (ctx->group) return group_step_batch(ctx, batch, t, step_size, reg_param, out);
+    return step_impl(ctx, batch, t, step_size, reg_param, out);
+  });
 }
 
 int fm_step(fm_ctx* ctx, const fm_csr* csr, int32_t t, double step_size, double reg_param, fm_step_out* out) {
@@ -532,8 +563,9 @@ int fm_step(fm_ctx* ctx, const fm_csr* csr, int32_t t, double step_size, double 
         out->n_loss_rows = 0;
         out->n_unique = 0;
       }
-      return FM_NOTHING_TO_DO;
+      if (!ctx->group) return FM_NOTHING_TO_DO;  // a group's other processes may hold rows: they agree below
     }
+    if (ctx->group) return group_step(ctx, csr, t, step_size, reg_param, out);
     // two upload slots used in turn: while the device runs step i from one slot, the host explodes
     // batch i + 1 into the other slot's pinned staging and its copies queue on the copy stream
     HostSlot& h = ctx->hslot[ctx->hnext];
@@ -562,6 +594,7 @@ int fm_step(fm_ctx* ctx, const fm_csr* csr, int32_t t, double step_size, double 
 int fm_loss_history(fm_ctx* ctx, double* loss, int64_t cap, int64_t* n) {
   return guarded(ctx, [&]() -> int {
     FM_REQUIRE(n != nullptr, "null n");
+    if (ctx->group) return group_loss_history(ctx, loss, cap, n);
     *n = ctx->epoch;
     if (cap == 0 || ctx->epoch == 0) return FM_OK;
     FM_REQUIRE(loss != nullptr, "null loss buffer");
@@ -577,6 +610,7 @@ int fm_loss_history(fm_ctx* ctx, double* loss, int64_t cap, int64_t* n) {
 int fm_predict(fm_ctx* ctx, const fm_csr* csr, double lo, double hi, double* pred) {
   return guarded(ctx, [&]() -> int {
     FM_REQUIRE(csr != nullptr && (csr->n_rows == 0 || pred), "null argument");
+    if (ctx->group) return group_predict(ctx, csr, lo, hi, pred);
     if (csr->n_rows == 0) return FM_OK;
     fm_batch* b = host_batch(ctx);
     upload_batch(ctx, csr, b, false);
@@ -593,6 +627,7 @@ int fm_predict(fm_ctx* ctx, const fm_csr* csr, double lo, double hi, double* pre
 int fm_predict_batch(fm_ctx* ctx, fm_batch* b, double lo, double hi, double* pred) {
   return guarded(ctx, [&]() -> int {
     FM_REQUIRE(b != nullptr && b->owner == ctx, "batch belongs to another context");
+    if (ctx->group) return group_predict_batch(ctx, b, lo, hi, pred);
     const int64_t B = b->dev.n_rows;
     FM_REQUIRE(B == 0 || pred, "null argument");
     if (B == 0) return FM_OK;
@@ -611,6 +646,7 @@ int fm_predict_batch(fm_ctx* ctx, fm_batch* b, double lo, double hi, double* pre
 int fm_init_from_batch(fm_ctx* ctx, fm_batch* b, int64_t* n_present) {
   return guarded(ctx, [&]() -> int {
     FM_REQUIRE(b != nullptr && b->owner == ctx, "batch belongs to another context");
+    if (ctx->group) return group_init_from_batch(ctx, b, n_present);
     launch_init_entries(ctx->view(), b->dev.col.as<uint32_t>(), b->dev.nnz, ctx->cfg.seed, ctx->cfg.init_sd, ctx->epoch,
                         ctx->cum_host.back(), ctx->stream);
     if (n_present) {
@@ -628,6 +664,11 @@ int fm_init_from_batch(fm_ctx* ctx, fm_batch* b, int64_t* n_present) {
 }
 
 int fm_loss_grad(fm_ctx* ctx, const fm_csr* csr, double* pred, double* loss, double* dw, double* dv) {
+  if (ctx && ctx->group) {
+    if (ctx->cfg.parallel == FM_PARALLEL_REPLICATED) return fm_loss_grad(group_member0(ctx), csr, pred, loss, dw, dv);
+    set_error("fm_loss_grad needs the whole table (a replicated or single-table context)");
+    return FM_ERR_ARG;
+  }
   return guarded(ctx, [&]() -> int {
     FM_REQUIRE(csr != nullptr, "null argument");
     if (csr->n_rows == 0 || csr->nnz == 0) return FM_OK;
@@ -658,6 +699,7 @@ int fm_loss_grad(fm_ctx* ctx, const fm_csr* csr, double* pred, double* loss, dou
 
 int fm_vector_sum_by_key(fm_ctx* ctx, const int32_t* keys, int64_t n, const double* vecs, int32_t k,
                          int32_t* out_keys, double* out_sums, int64_t* n_out) {
+  if (ctx && ctx->group) return fm_vector_sum_by_key(group_member0(ctx), keys, n, vecs, k, out_keys, out_sums, n_out);
   return guarded(ctx, [&]() -> int {
     FM_REQUIRE(n >= 0 && k >= 1 && n_out, "bad arguments");
     *n_out = 0;
@@ -697,6 +739,7 @@ int fm_vector_sum_by_key(fm_ctx* ctx, const int32_t* keys, int64_t n, const doub
 
 int fm_profile_enable(fm_ctx* ctx, int32_t on) {
   return guarded(ctx, [&]() -> int {
+    if (ctx->group) return group_profile(ctx, 0, on, nullptr, 0, nullptr, nullptr, 0, nullptr);
     ctx->prof = on != 0;
     return FM_OK;
   });
@@ -704,6 +747,7 @@ int fm_profile_enable(fm_ctx* ctx, int32_t on) {
 
 int fm_profile_reset(fm_ctx* ctx) {
   return guarded(ctx, [&]() -> int {
+    if (ctx->group) return group_profile(ctx, 1, 0, nullptr, 0, nullptr, nullptr, 0, nullptr);
     ctx->resolve_profile();
     ctx->prof_acc.clear();
     ctx->prof_order.clear();
@@ -715,6 +759,7 @@ int fm_profile_read(fm_ctx* ctx, char* names, int64_t names_cap, double* total_m
                     int64_t* n) {
   return guarded(ctx, [&]() -> int {
     FM_REQUIRE(n != nullptr, "null n");
+    if (ctx->group) return group_profile(ctx, 2, 0, names, names_cap, total_ms, launches, cap, n);
     ctx->resolve_profile();
     *n = (int64_t)ctx->prof_order.size();
     std::string joined;
@@ -739,6 +784,7 @@ int fm_profile_read(fm_ctx* ctx, char* names, int64_t names_cap, double* total_m
 
 int fm_repl_grad(fm_ctx* ctx, fm_batch* batch, void* grad) {
   return guarded(ctx, [&]() -> int {
+    FM_REQUIRE(!ctx->group, "a multi-GPU context runs its replicated step itself (fm_step / fm_step_batch)");
     FM_REQUIRE(grad != nullptr, "null gradient buffer");
     FM_REQUIRE(!ctx->repl_pending, "fm_repl_apply must follow fm_repl_grad");
     ctx->ensure_hist(ctx->epoch + 1);
@@ -753,6 +799,7 @@ int fm_repl_grad(fm_ctx* ctx, fm_batch* batch, void* grad) {
 int fm_repl_apply(fm_ctx* ctx, const void* grad, int32_t t, double step_size, double reg_param,
                   int64_t global_rows) {
   return guarded(ctx, [&]() -> int {
+    FM_REQUIRE(!ctx->group, "a multi-GPU context runs its replicated step itself (fm_step / fm_step_batch)");
     FM_REQUIRE(ctx->repl_pending, "fm_repl_grad must run first");
     FM_REQUIRE(global_rows >= 0, "negative global_rows");
     ctx->repl_pending = false;
@@ -789,6 +836,7 @@ int fm_repl_apply(fm_ctx* ctx, const void* grad, int32_t t, double step_size, do
 int fm_last_stats(fm_ctx* ctx, double* loss_sum, int64_t* n_loss_rows, int64_t* n_unique) {
   return guarded(ctx, [&]() -> int {
     FM_REQUIRE(loss_sum && n_loss_rows && n_unique, "null argument");
+    if (ctx->group) return group_last_stats(ctx, loss_sum, n_loss_rows, n_unique);
     FM_REQUIRE(ctx->epoch >= 1, "no step executed");
     double h[3];
     FM_HIP_CHECK(hipMemcpyAsync(h, ctx->loss_hist.as<double>() + 3 * (int64_t)(ctx->epoch - 1), sizeof(h),

@@ -75,6 +75,17 @@ struct ShardBatchState {
   }
 };
 
+// Multi-GPU context state (fm_group.hip): the ranks one fm_ctx drives, and a group batch's
+// per-rank parts.
+struct Group;
+struct GroupBatch;
+struct GroupDeleter {
+  void operator()(Group* g) const;
+};
+struct GroupBatchDeleter {
+  void operator()(GroupBatch* g) const;
+};
+
 }  // namespace fmhip
 
 using namespace fmhip;
@@ -91,7 +102,9 @@ struct fm_batch {
   hipEvent_t last_use = nullptr;  // recorded on the main stream after a step read skeys/sents
   bool prepared = false;
   std::unique_ptr<ShardBatchState> sh;  // sharded contexts only
+  std::unique_ptr<GroupBatch, GroupBatchDeleter> grp;  // a multi-GPU context's batch: its per-rank parts
   ~fm_batch() {
+    grp.reset();
     (void)hipSetDevice(device);
     if (sh) sh->release(device);
     if (ready) (void)hipEventSynchronize(ready);
@@ -111,6 +124,7 @@ struct fm_batch {
 struct fm_ctx {
   std::mutex mu;
   fm_config cfg{};
+  std::unique_ptr<Group, GroupDeleter> group;  // non-null: this context drives several ranks (fm_group.hip)
   int32_t kp = 0;
   int64_t rows = 0;  // local rows
   hipStream_t stream = nullptr;
@@ -227,6 +241,7 @@ struct fm_ctx {
   }
 
   ~fm_ctx() {
+    group.reset();
     (void)hipSetDevice(cfg.device);
     if (stream) (void)hipStreamSynchronize(stream);
     if (copy_stream) (void)hipStreamSynchronize(copy_stream);
@@ -322,5 +337,35 @@ inline int bits_for(int64_t max_value) {
 // shared host helpers (fm_capi.hip)
 void upload_batch(fm_ctx* ctx, const fm_csr* c, fm_batch* b, bool check_range);
 void reserve_work(fm_ctx* ctx, int64_t B, int64_t N);
+
+// sharded predict building blocks (fm_shard.hip), called by fm_group.hip with the member locked:
+// the owner partial pass with the per-pair count of present rows (Model.scala:103-112 inner
+// joins: absent ids contribute nothing), and the requester's predict epilogue
+// (Model.scala:78-86, 127-132): w0 for a row without a learned feature, else clamp.
+void shard_owner_partials(fm_ctx* ctx, fm_batch* b, void* partials_out, uint32_t* present_out);
+void shard_combine_predict(fm_ctx* ctx, fm_batch* b, const void* partials_in, const uint32_t* present_in,
+                           double lo, double hi, double* pred_dev);
+
+// multi-GPU contexts (fm_group.hip); each runs inside the group context's guarded()
+int group_create(const fm_config* cfg, fm_ctx** out);
+int group_batch_create(fm_ctx* ctx, const fm_csr* csr, fm_batch** out);
+int group_batch_prepare(fm_ctx* ctx, fm_batch* b);
+int group_step(fm_ctx* ctx, const fm_csr* csr, int32_t t, double step_size, double reg_param, fm_step_out* out);
+int group_step_batch(fm_ctx* ctx, fm_batch* b, int32_t t, double step_size, double reg_param, fm_step_out* out);
+int group_predict(fm_ctx* ctx, const fm_csr* csr, double lo, double hi, double* pred);
+int group_predict_batch(fm_ctx* ctx, fm_batch* b, double lo, double hi, double* pred);
+int group_load_tables(fm_ctx* ctx, const int32_t* ids, int64_t n, const double* w, const double* V);
+int group_init_random(fm_ctx* ctx, const int32_t* ids, int64_t n, int64_t id_begin, int64_t id_end);
+int group_init_from_batch(fm_ctx* ctx, fm_batch* b, int64_t* n_present);
+int group_export_tables(fm_ctx* ctx, int32_t* ids, double* w, double* V, int64_t cap, int64_t* n);
+int group_export_rows(fm_ctx* ctx, const int32_t* ids, int64_t n, double* w, double* V, int8_t* present);
+int64_t group_num_present(fm_ctx* ctx);
+int group_loss_history(fm_ctx* ctx, double* loss, int64_t cap, int64_t* n);
+int group_last_stats(fm_ctx* ctx, double* loss_sum, int64_t* n_loss_rows, int64_t* n_unique);
+int group_sync(fm_ctx* ctx);
+int group_reserve(fm_ctx* ctx, int64_t max_rows, int64_t max_nnz);
+int group_profile(fm_ctx* ctx, int op, int32_t on, char* names, int64_t names_cap, double* total_ms,
+                  int64_t* launches, int64_t cap, int64_t* n);
+fm_ctx* group_member0(fm_ctx* ctx);
 
 }  // namespace fmhip

@@ -1,0 +1,901 @@
+// Multi-GPU inside one fm_ctx: one host thread drives every rank of the job this process holds,
+// and the exchanges between ranks run inside the library over RCCL (xGMI on one node).
+//
+// SURVEY §8(b) Threading: "Multi-GPU lives inside one context (one host thread)": the caller is
+// the Spark driver, one JVM, so the multi-GPU step cannot need one process per GPU.  A context
+// created with fm_config.parallel = FM_PARALLEL_SHARDED / FM_PARALLEL_REPLICATED holds n_gpus
+// local ranks.  Each is an ordinary per-device fm_ctx (a "member": its share of the table, its
+// streams and workspaces); this file sequences the member phases of fm_shard.hip / fm_capi.hip
+// and moves the data between them.  The reference's shuffles it replaces:
+//   sharded  : S1/S2 (entries ⋈ w, V by featureId, Model.scala:155-164) -> the entry all-to-all;
+//              S3 (window by sampleId, :191) -> partial sums back to the requester;
+//              S5/S6 (gradient groupBy + outer join, SGD.scala:148-166) -> S rows to the owner,
+//              owner-local update (fm_shard.hip for the phases and the wire layout)
+//   replicated: S5 -> one all-reduce of the per-slot gradient sums (fm_repl_grad / fm_repl_apply)
+// A mini-batch handed to the context is split by rows, contiguously, over its local ranks; the
+// iteration's miniBatchSize is the sum over every rank of the job (SGD.scala:124).
+//
+// Transports.  RCCL: grouped ncclSend/ncclRecv for the all-to-alls (every peer at once, so an
+// all-to-all drives all 7 xGMI links of a GPU), ncclAllReduce / ncclAllGather for the gradient
+// and the counts; one communicator per stream role (main: the iteration's critical path; side:
+// the batch-only routing that runs one iteration ahead), each used in the same order on every
+// rank.  COPY (one process only): device-to-device copies between the ranks' buffers, bracketed
+// by event barriers across the ranks' streams; it also lets several ranks share one GPU, which
+// RCCL refuses -- that is how the in-process tests run an 8-rank job on one MI355X.
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <numeric>
+
+#include "fm_context.h"
+#include "fm_device.h"
+
+namespace fmhip {
+
+#define FM_RCCL_CHECK(expr)                                                                  \
+  do {                                                                                       \
+    ncclResult_t _r = (expr);                                                                \
+    if (_r != ncclSuccess)                                                                   \
+      throw ::fmhip::Error{FM_ERR_RCCL, std::string(#expr) + ": " + ncclGetErrorString(_r)}; \
+  } while (0)
+
+namespace {
+
+// a member call through the C-ABI: its error (and message) becomes the group's
+void mcheck(int rc, const char* what) {
+  if (rc < 0) throw Error{rc, std::string(what) + ": " + fm_last_error()};
+}
+
+constexpr int kBlock = 256;
+
+__global__ void k_slots_to_ids(const uint32_t* __restrict__ slot, int64_t n, uint32_t R, uint32_t shard,
+                               uint32_t* __restrict__ ids) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    ids[i] = slot[i] * R + shard;
+}
+
+__global__ void k_add_f32(float* __restrict__ dst, const float* __restrict__ src, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    dst[i] += src[i];
+}
+
+inline unsigned grid_of(int64_t n) {
+  int64_t g = (n + kBlock - 1) / kBlock;
+  return (unsigned)std::max<int64_t>(1, std::min<int64_t>(g, 256 * 16));
+}
+
+}  // namespace
+
+struct Rank {
+  fm_ctx* m = nullptr;  // the member context (owned)
+  int device = 0;
+  int global = 0;
+  ncclComm_t comm_main = nullptr, comm_side = nullptr;
+  hipEvent_t ev_main = nullptr, ev_side = nullptr;  // COPY transport barriers
+  DevBuf partials, part_in, s_send, s_recv;           // sharded wire buffers (main stream)
+  DevBuf pc_out, pc_in, pred;                         // sharded predict: present counts, scores
+  DevBuf grad, gtmp;                                  // replicated gradient buffer
+  DevBuf xg_send, xg_recv;                            // counts all-gather (RCCL)
+  Pinned xg_pin;
+  hipStream_t stream(bool side) const { return side ? m->side : m->stream; }
+  hipEvent_t event(bool side) const { return side ? ev_side : ev_main; }
+  ncclComm_t comm(bool side) const { return side ? comm_side : comm_main; }
+};
+
+struct GPart {
+  fm_batch* b = nullptr;  // the member's batch (owned)
+  int device = 0;
+  int64_t rows = 0, row0 = 0, nnz = 0;
+  DevBuf send_slot, send_ent, recv_slot, recv_ent;
+  std::vector<int64_t> ent_out, pair_out, ent_in, pair_in;  // per global peer
+};
+
+struct GroupBatch {
+  std::vector<GPart> parts;
+  int64_t rows = 0, nnz = 0, global_rows = 0;
+  bool prefetched = false;  // routed, exchanged and slot-sorted for its next step
+  ~GroupBatch() {
+    for (auto& p : parts) {
+      (void)hipSetDevice(p.device);
+      for (DevBuf* d : {&p.send_slot, &p.send_ent, &p.recv_slot, &p.recv_ent}) d->release();
+      if (p.b) fm_batch_destroy(p.b);
+      p.b = nullptr;
+    }
+  }
+};
+
+struct Group {
+  int mode = FM_PARALLEL_SHARDED;
+  int L = 0, R = 0, nprocs = 1, prank = 0;
+  bool rccl = false;
+  std::vector<Rank> ranks;
+  std::unique_ptr<fm_batch> host_b[2];  // fm_step / fm_predict uploads, used in turn
+  int hnext = 0;
+  bool sharded() const { return mode == FM_PARALLEL_SHARDED; }
+  ~Group() {
+    for (auto& h : host_b) h.reset();
+    for (auto& r : ranks) {
+      if (!r.m) continue;
+      (void)hipSetDevice(r.device);
+      (void)hipDeviceSynchronize();
+      if (r.comm_side) (void)ncclCommDestroy(r.comm_side);
+      if (r.comm_main) (void)ncclCommDestroy(r.comm_main);
+      for (DevBuf* d : {&r.partials, &r.part_in, &r.s_send, &r.s_recv, &r.pc_out, &r.pc_in, &r.pred, &r.grad, &r.gtmp,
+                        &r.xg_send, &r.xg_recv})
+        d->release();
+      if (r.ev_main) (void)hipEventDestroy(r.ev_main);
+      if (r.ev_side) (void)hipEventDestroy(r.ev_side);
+    }
+    for (auto& r : ranks)
+      if (r.m) fm_destroy(r.m);
+  }
+};
+
+void GroupDeleter::operator()(Group* g) const { delete g; }
+void GroupBatchDeleter::operator()(GroupBatch* g) const { delete g; }
+
+namespace {
+
+// run f with the member locked and its device current (internal, non-ABI member calls)
+template <class F>
+void on(Rank& r, F&& f) {
+  std::lock_guard<std::mutex> lk(r.m->mu);
+  FM_HIP_CHECK(hipSetDevice(r.device));
+  f();
+}
+
+void ensure_on(int device, DevBuf& b, size_t bytes) {
+  FM_HIP_CHECK(hipSetDevice(device));
+  b.ensure(bytes + 16);
+}
+
+Group& grp(fm_ctx* ctx) { return *ctx->group; }
+
+GroupBatch& gbatch(fm_ctx* ctx, fm_batch* b) {
+  FM_REQUIRE(b != nullptr && b->owner == ctx && b->grp, "batch belongs to another context");
+  return *b->grp;
+}
+
+// COPY transport: every rank's stream (side or main) waits for what every other rank's has queued
+void barrier(Group& g, bool side) {
+  for (auto& r : g.ranks) {
+    FM_HIP_CHECK(hipSetDevice(r.device));
+    FM_HIP_CHECK(hipEventRecord(r.event(side), r.stream(side)));
+  }
+  for (auto& r : g.ranks) {
+    FM_HIP_CHECK(hipSetDevice(r.device));
+    for (auto& q : g.ranks)
+      if (&q != &r) FM_HIP_CHECK(hipStreamWaitEvent(r.stream(side), q.event(side), 0));
+  }
+}
+
+// All-to-all-v between the job's ranks: local rank l sends out[l][p] elements of esize bytes to
+// global rank p (from send[l], peer-major) and receives in[l][p] from p (into recv[l], peer-major).
+void a2a(Group& g, bool side, const std::vector<const char*>& send, const std::vector<char*>& recv,
+         const std::vector<const int64_t*>& out, const std::vector<const int64_t*>& in, size_t esize) {
+  if (g.rccl) {
+    FM_RCCL_CHECK(ncclGroupStart());
+    for (int l = 0; l < g.L; ++l) {
+      Rank& r = g.ranks[l];
+      FM_HIP_CHECK(hipSetDevice(r.device));
+      size_t so = 0, ro = 0;
+      for (int p = 0; p < g.R; ++p) {
+        const size_t sb = (size_t)out[l][p] * esize, rb = (size_t)in[l][p] * esize;
+        if (sb) FM_RCCL_CHECK(ncclSend(send[l] + so, sb, ncclChar, p, r.comm(side), r.stream(side)));
+        if (rb) FM_RCCL_CHECK(ncclRecv(recv[l] + ro, rb, ncclChar, p, r.comm(side), r.stream(side)));
+        so += sb;
+        ro += rb;
+      }
+    }
+    FM_RCCL_CHECK(ncclGroupEnd());
+    return;
+  }
+  barrier(g, side);
+  for (int l = 0; l < g.L; ++l) {  // destination
+    Rank& r = g.ranks[l];
+    FM_HIP_CHECK(hipSetDevice(r.device));
+    size_t ro = 0;
+    for (int q = 0; q < g.L; ++q) {  // source (one process: global rank = local rank)
+      size_t so = 0;
+      for (int p = 0; p < l; ++p) so += (size_t)out[q][p] * esize;
+      const size_t bytes = (size_t)in[l][q] * esize;
+      if (bytes)
+        FM_HIP_CHECK(hipMemcpyAsync(recv[l] + ro, send[q] + so, bytes, hipMemcpyDefault, r.stream(side)));
+      ro += bytes;
+    }
+  }
+  barrier(g, side);
+}
+
+// Every rank's `width` int64 values -> all ranks' values on the host, rank-major [R][width].
+std::vector<int64_t> allgather(Group& g, const std::vector<std::vector<int64_t>>& local, int width) {
+  std::vector<int64_t> all((size_t)g.R * width, 0);
+  if (!g.rccl) {
+    for (int l = 0; l < g.L; ++l) std::copy(local[l].begin(), local[l].end(), all.begin() + (size_t)g.ranks[l].global * width);
+    return all;
+  }
+  const size_t bs = sizeof(int64_t) * width, br = bs * g.R;
+  for (int l = 0; l < g.L; ++l) {
+    Rank& r = g.ranks[l];
+    ensure_on(r.device, r.xg_send, bs);
+    ensure_on(r.device, r.xg_recv, br);
+    r.xg_pin.ensure(std::max(bs, br));
+    std::memcpy(r.xg_pin.p, local[l].data(), bs);
+    FM_HIP_CHECK(hipMemcpyAsync(r.xg_send.p, r.xg_pin.p, bs, hipMemcpyHostToDevice, r.stream(true)));
+  }
+  FM_RCCL_CHECK(ncclGroupStart());
+  for (int l = 0; l < g.L; ++l) {
+    Rank& r = g.ranks[l];
+    FM_HIP_CHECK(hipSetDevice(r.device));
+    FM_RCCL_CHECK(ncclAllGather(r.xg_send.p, r.xg_recv.p, width, ncclInt64, r.comm_side, r.stream(true)));
+  }
+  FM_RCCL_CHECK(ncclGroupEnd());
+  Rank& r0 = g.ranks[0];
+  FM_HIP_CHECK(hipSetDevice(r0.device));
+  FM_HIP_CHECK(hipMemcpyAsync(r0.xg_pin.p, r0.xg_recv.p, br, hipMemcpyDeviceToHost, r0.stream(true)));
+  for (auto& r : g.ranks) {
+    FM_HIP_CHECK(hipSetDevice(r.device));
+    FM_HIP_CHECK(hipStreamSynchronize(r.stream(true)));
+  }
+  std::memcpy(all.data(), r0.xg_pin.p, br);
+  return all;
+}
+
+// Split a host CSR by rows over the local ranks and upload each part into its member batch.
+void upload_parts(Group& g, const fm_csr* c, GroupBatch& gb, bool check_range) {
+  FM_REQUIRE(c != nullptr, "null fm_csr");
+  FM_REQUIRE(c->n_rows >= 0 && c->nnz >= 0, "negative n_rows / nnz");
+  FM_REQUIRE(c->n_rows == 0 || (c->row_ptr && c->label), "null row_ptr / label");
+  const int64_t B = c->n_rows;
+  if (B > 0) {
+    FM_REQUIRE(c->row_ptr[0] == 0 && c->row_ptr[B] == c->nnz, "row_ptr must run from 0 to nnz");
+    for (int64_t i = 0; i < B; ++i) FM_REQUIRE(c->row_ptr[i] <= c->row_ptr[i + 1], "row_ptr must be non-decreasing");
+  } else {
+    FM_REQUIRE(c->nnz == 0, "nnz > 0 with n_rows == 0");
+  }
+  gb.parts.resize(g.L);
+  gb.rows = B;
+  gb.nnz = c->nnz;
+  gb.prefetched = false;
+  std::vector<int64_t> rp;
+  std::vector<std::vector<int64_t>> rows(g.L, std::vector<int64_t>(1));
+  for (int l = 0; l < g.L; ++l) {
+    Rank& r = g.ranks[l];
+    GPart& p = gb.parts[l];
+    const int64_t r0 = B * l / g.L, r1 = B * (l + 1) / g.L;
+    const int64_t e0 = B > 0 ? c->row_ptr[r0] : 0, e1 = B > 0 ? c->row_ptr[r1] : 0;
+    rp.resize(r1 - r0 + 1);
+    for (int64_t i = r0; i <= r1; ++i) rp[i - r0] = B > 0 ? c->row_ptr[i] - e0 : 0;
+    fm_csr sub{};
+    sub.n_rows = r1 - r0;
+    sub.nnz = e1 - e0;
+    sub.row_ptr = rp.data();
+    sub.col = c->col ? c->col + e0 : nullptr;
+    sub.val = c->val ? c->val + e0 : nullptr;
+    sub.label = c->label ? c->label + r0 : nullptr;
+    if (!p.b) p.b = new fm_batch();
+    p.device = r.device;
+    on(r, [&] { upload_batch(r.m, &sub, p.b, check_range); });
+    p.rows = sub.n_rows;
+    p.row0 = r0;
+    p.nnz = sub.nnz;
+    rows[l][0] = p.rows;
+  }
+  const std::vector<int64_t> all = allgather(g, rows, 1);
+  gb.global_rows = std::accumulate(all.begin(), all.end(), int64_t(0));
+}
+
+// A new group batch (an fm_batch whose parts are member batches).
+fm_batch* new_group_batch(fm_ctx* ctx) {
+  std::unique_ptr<fm_batch> b(new fm_batch());
+  b->owner = ctx;
+  b->device = ctx->cfg.device;
+  b->grp.reset(new GroupBatch());
+  return b.release();
+}
+
+void sync_group_batch_view(fm_batch* b) {  // fm_batch_rows / fm_batch_nnz of the group batch
+  b->dev.n_rows = b->grp->rows;
+  b->dev.nnz = b->grp->nnz;
+}
+
+// The batch-only phases of a sharded iteration (fm_shard.hip phases 1 and 1b): route every part,
+// exchange the counts and the entries, build the owners' pair tables and slot orders.  Side
+// streams; the host waits for the routes' counts only (they size the exchange).
+void prefetch(Group& g, GroupBatch& gb) {
+  if (gb.prefetched) return;
+  const int R = g.R, L = g.L;
+  std::vector<std::vector<int64_t>> counts(L, std::vector<int64_t>(2 * R, 0));
+  for (int l = 0; l < L; ++l) {
+    Rank& r = g.ranks[l];
+    GPart& p = gb.parts[l];
+    ensure_on(r.device, p.send_slot, sizeof(uint32_t) * p.nnz);
+    ensure_on(r.device, p.send_ent, sizeof(uint2) * p.nnz);
+    mcheck(fm_shard_route(r.m, p.b, p.send_slot.p, p.send_ent.p, counts[l].data()), "fm_shard_route");
+  }
+  const std::vector<int64_t> all = allgather(g, counts, 2 * R);  // [source][2R]
+  std::vector<const char*> ss(L), se(L);
+  std::vector<char*> rs(L), re(L);
+  std::vector<const int64_t*> out(L), in(L);
+  std::vector<std::vector<int64_t>> out2(L), in2(L);
+  for (int l = 0; l < L; ++l) {
+    GPart& p = gb.parts[l];
+    const int gl = g.ranks[l].global;
+    p.ent_out.assign(counts[l].begin(), counts[l].begin() + R);
+    p.pair_out.assign(counts[l].begin() + R, counts[l].end());
+    p.ent_in.resize(R);
+    p.pair_in.resize(R);
+    for (int s = 0; s < R; ++s) {
+      p.ent_in[s] = all[(size_t)s * 2 * R + gl];
+      p.pair_in[s] = all[(size_t)s * 2 * R + R + gl];
+    }
+    const int64_t n_in = std::accumulate(p.ent_in.begin(), p.ent_in.end(), int64_t(0));
+    ensure_on(g.ranks[l].device, p.recv_slot, sizeof(uint32_t) * n_in);
+    ensure_on(g.ranks[l].device, p.recv_ent, sizeof(uint2) * n_in);
+    ss[l] = p.send_slot.as<char>();
+    se[l] = p.send_ent.as<char>();
+    rs[l] = p.recv_slot.as<char>();
+    re[l] = p.recv_ent.as<char>();
+    out[l] = p.ent_out.data();
+    in[l] = p.ent_in.data();
+  }
+  a2a(g, true, ss, rs, out, in, sizeof(uint32_t));
+  a2a(g, true, se, re, out, in, sizeof(uint2));
+  for (int l = 0; l < L; ++l) {
+    Rank& r = g.ranks[l];
+    GPart& p = gb.parts[l];
+    const int64_t n_in = std::accumulate(p.ent_in.begin(), p.ent_in.end(), int64_t(0));
+    mcheck(fm_shard_owner_prepare(r.m, p.b, p.recv_slot.p, p.recv_ent.p, n_in, p.ent_in.data(), p.pair_in.data()),
+           "fm_shard_owner_prepare");
+  }
+  gb.prefetched = true;
+}
+
+// the pair buffers of one direction in the wire layout: [P][kp] fp32 vectors, then [P][2] fp64
+// scalars -- two all-to-alls with the same pair counts
+void a2a_pairs(Group& g, int kp, const std::vector<DevBuf*>& send, const std::vector<int64_t>& sendP,
+               const std::vector<DevBuf*>& recv, const std::vector<int64_t>& recvP,
+               const std::vector<const int64_t*>& out, const std::vector<const int64_t*>& in) {
+  const int L = g.L;
+  std::vector<const char*> sv(L), sc(L);
+  std::vector<char*> rv(L), rc(L);
+  for (int l = 0; l < L; ++l) {
+    sv[l] = send[l]->as<char>();
+    sc[l] = send[l]->as<char>() + sizeof(float) * sendP[l] * kp;
+    rv[l] = recv[l]->as<char>();
+    rc[l] = recv[l]->as<char>() + sizeof(float) * recvP[l] * kp;
+  }
+  a2a(g, false, sv, rv, out, in, sizeof(float) * kp);
+  a2a(g, false, sc, rc, out, in, sizeof(double) * 2);
+}
+
+// per-step stats rows of the members (loss, loss rows, distinct ids) at epoch index e -> the job's
+void stats_row(Group& g, int64_t e, double* h) {
+  h[0] = h[1] = h[2] = 0.0;
+  const int nsum = g.rccl ? 1 : g.L;  // RCCL: the rows were all-reduced in place after the step
+  for (int l = 0; l < nsum; ++l) {
+    Rank& r = g.ranks[l];
+    double v[3];
+    on(r, [&] {
+      FM_HIP_CHECK(hipMemcpyAsync(v, r.m->loss_hist.as<double>() + 3 * e, sizeof(v), hipMemcpyDeviceToHost, r.m->stream));
+      FM_HIP_CHECK(hipStreamSynchronize(r.m->stream));
+    });
+    h[0] += v[0];
+    h[1] += v[1];
+    if (g.sharded() || l == 0) h[2] += v[2];  // replicated: every replica counts the same touched rows
+  }
+}
+
+// RCCL: the step's stats rows summed over the job in place (loss and loss rows; sharded also the
+// distinct ids, each owned by exactly one rank), on the main streams after the step
+void reduce_stats(Group& g, int64_t e) {
+  if (!g.rccl) return;
+  FM_RCCL_CHECK(ncclGroupStart());
+  for (auto& r : g.ranks) {
+    FM_HIP_CHECK(hipSetDevice(r.device));
+    double* row = r.m->loss_hist.as<double>() + 3 * e;
+    FM_RCCL_CHECK(ncclAllReduce(row, row, g.sharded() ? 3 : 2, ncclFloat64, ncclSum, r.comm_main, r.m->stream));
+  }
+  FM_RCCL_CHECK(ncclGroupEnd());
+}
+
+void fill_out(Group& g, fm_ctx* ctx, int64_t e, int64_t global_rows, fm_step_out* out) {
+  if (!out) return;
+  double h[3];
+  stats_row(g, e, h);
+  out->loss_sum = h[0];
+  out->n_loss_rows = (int64_t)h[1];
+  out->n_unique = (int64_t)h[2];
+  out->n_rows = global_rows;
+}
+
+int step_sharded(fm_ctx* ctx, Group& g, GroupBatch& gb, int32_t t, double step_size, double reg_param,
+                 fm_step_out* out) {
+  const int L = g.L, kp = ctx->kp, W = kp + 4;
+  prefetch(g, gb);
+  std::vector<int64_t> Pin(L), Pout(L);
+  std::vector<DevBuf*> parts(L), part_in(L), s_send(L), s_recv(L);
+  std::vector<const int64_t*> pin(L), pout(L);
+  for (int l = 0; l < L; ++l) {
+    Rank& r = g.ranks[l];
+    GPart& p = gb.parts[l];
+    Pin[l] = std::accumulate(p.pair_in.begin(), p.pair_in.end(), int64_t(0));
+    Pout[l] = std::accumulate(p.pair_out.begin(), p.pair_out.end(), int64_t(0));
+    ensure_on(r.device, r.partials, sizeof(float) * Pin[l] * W);
+    ensure_on(r.device, r.s_recv, sizeof(float) * Pin[l] * W);
+    ensure_on(r.device, r.part_in, sizeof(float) * Pout[l] * W);
+    ensure_on(r.device, r.s_send, sizeof(float) * Pout[l] * W);
+    parts[l] = &r.partials;
+    part_in[l] = &r.part_in;
+    s_send[l] = &r.s_send;
+    s_recv[l] = &r.s_recv;
+    pin[l] = p.pair_in.data();
+    pout[l] = p.pair_out.data();
+  }
+  // owners: partial sums per received pair
+  for (int l = 0; l < L; ++l)
+    mcheck(fm_shard_owner_forward(g.ranks[l].m, gb.parts[l].b, g.ranks[l].partials.p), "fm_shard_owner_forward");
+  // back to the requesters (owner l -> requester p: the pair_in[l][p] pairs it got from p)
+  a2a_pairs(g, kp, parts, Pin, part_in, Pout, pin, pout);
+  for (int l = 0; l < L; ++l)
+    mcheck(fm_shard_combine(g.ranks[l].m, gb.parts[l].b, g.ranks[l].part_in.p, g.ranks[l].s_send.p), "fm_shard_combine");
+  // S rows to the owners
+  a2a_pairs(g, kp, s_send, Pout, s_recv, Pin, pout, pin);
+  for (int l = 0; l < L; ++l)
+    mcheck(fm_shard_owner_update(g.ranks[l].m, gb.parts[l].b, g.ranks[l].s_recv.p, t, step_size, reg_param,
+                                 gb.global_rows),
+           "fm_shard_owner_update");
+  gb.prefetched = false;
+  const int64_t e = g.ranks[0].m->epoch - 1;
+  reduce_stats(g, e);
+  ctx->epoch = (int32_t)(e + 1);
+  fill_out(g, ctx, e, gb.global_rows, out);
+  return FM_OK;
+}
+
+int step_replicated(fm_ctx* ctx, Group& g, GroupBatch& gb, int32_t t, double step_size, double reg_param,
+                    fm_step_out* out) {
+  const int L = g.L;
+  const int64_t n = g.ranks[0].m->rows * (int64_t)(ctx->kp + 4);
+  for (int l = 0; l < L; ++l) {
+    Rank& r = g.ranks[l];
+    ensure_on(r.device, r.grad, sizeof(float) * n);
+    mcheck(fm_repl_grad(r.m, gb.parts[l].b, r.grad.p), "fm_repl_grad");
+  }
+  if (g.rccl) {
+    FM_RCCL_CHECK(ncclGroupStart());
+    for (auto& r : g.ranks) {
+      FM_HIP_CHECK(hipSetDevice(r.device));
+      FM_RCCL_CHECK(ncclAllReduce(r.grad.p, r.grad.p, n, ncclFloat32, ncclSum, r.comm_main, r.m->stream));
+    }
+    FM_RCCL_CHECK(ncclGroupEnd());
+  } else if (L > 1) {
+    // rank order sum on rank 0, then rank 0's sum to every rank: every replica applies the same bytes
+    barrier(g, false);
+    Rank& r0 = g.ranks[0];
+    ensure_on(r0.device, r0.gtmp, sizeof(float) * n);
+    for (int l = 1; l < L; ++l) {
+      FM_HIP_CHECK(hipSetDevice(r0.device));
+      FM_HIP_CHECK(hipMemcpyAsync(r0.gtmp.p, g.ranks[l].grad.p, sizeof(float) * n, hipMemcpyDefault, r0.m->stream));
+      hipLaunchKernelGGL(k_add_f32, dim3(grid_of(n)), dim3(kBlock), 0, r0.m->stream, r0.grad.as<float>(),
+                         r0.gtmp.as<float>(), n);
+      FM_HIP_CHECK(hipGetLastError());
+    }
+    for (int l = 1; l < L; ++l)
+      FM_HIP_CHECK(hipMemcpyAsync(g.ranks[l].grad.p, r0.grad.p, sizeof(float) * n, hipMemcpyDefault, r0.m->stream));
+    barrier(g, false);
+  }
+  for (int l = 0; l < L; ++l)
+    mcheck(fm_repl_apply(g.ranks[l].m, g.ranks[l].grad.p, t, step_size, reg_param, gb.global_rows), "fm_repl_apply");
+  const int64_t e = g.ranks[0].m->epoch - 1;
+  reduce_stats(g, e);
+  ctx->epoch = (int32_t)(e + 1);
+  fill_out(g, ctx, e, gb.global_rows, out);
+  return FM_OK;
+}
+
+int step_group_batch(fm_ctx* ctx, GroupBatch& gb, int32_t t, double step_size, double reg_param, fm_step_out* out) {
+  Group& g = grp(ctx);
+  if (gb.global_rows == 0) {  // SGD.scala:126-128: every rank of the job skips together
+    if (out) {
+      out->loss_sum = 0.0;
+      out->n_rows = out->n_loss_rows = out->n_unique = 0;
+    }
+    return FM_NOTHING_TO_DO;
+  }
+  FM_REQUIRE(t >= 1, "iteration index t must be >= 1");
+  FM_REQUIRE(std::isfinite(step_size) && std::isfinite(reg_param), "non-finite step size / regParam");
+  return g.sharded() ? step_sharded(ctx, g, gb, t, step_size, reg_param, out)
+                     : step_replicated(ctx, g, gb, t, step_size, reg_param, out);
+}
+
+// FactorizationMachinesModel.transform over a sharded table: route (ids outside the model
+// dropped) -> entries to the owners -> owner partial sums with present counts -> back ->
+// predict epilogue per sample.  pred: host [gb.rows].
+void predict_sharded(fm_ctx* ctx, Group& g, GroupBatch& gb, double lo, double hi, double* pred) {
+  const int L = g.L, kp = ctx->kp, W = kp + 4;
+  gb.prefetched = false;  // the route below replaces any pending training plan of this batch
+  prefetch(g, gb);
+  gb.prefetched = false;
+  std::vector<int64_t> Pin(L), Pout(L);
+  std::vector<DevBuf*> parts(L), part_in(L);
+  std::vector<const int64_t*> pin(L), pout(L);
+  std::vector<const char*> cs(L);
+  std::vector<char*> cr(L);
+  for (int l = 0; l < L; ++l) {
+    Rank& r = g.ranks[l];
+    GPart& p = gb.parts[l];
+    Pin[l] = std::accumulate(p.pair_in.begin(), p.pair_in.end(), int64_t(0));
+    Pout[l] = std::accumulate(p.pair_out.begin(), p.pair_out.end(), int64_t(0));
+    ensure_on(r.device, r.partials, sizeof(float) * Pin[l] * W);
+    ensure_on(r.device, r.part_in, sizeof(float) * Pout[l] * W);
+    ensure_on(r.device, r.pc_out, sizeof(uint32_t) * Pin[l]);
+    ensure_on(r.device, r.pc_in, sizeof(uint32_t) * Pout[l]);
+    ensure_on(r.device, r.pred, sizeof(double) * p.rows);
+    parts[l] = &r.partials;
+    part_in[l] = &r.part_in;
+    pin[l] = p.pair_in.data();
+    pout[l] = p.pair_out.data();
+    cs[l] = r.pc_out.as<char>();
+    cr[l] = r.pc_in.as<char>();
+    on(r, [&] { shard_owner_partials(r.m, p.b, r.partials.p, r.pc_out.as<uint32_t>()); });
+  }
+  a2a_pairs(g, kp, parts, Pin, part_in, Pout, pin, pout);
+  a2a(g, false, cs, cr, pin, pout, sizeof(uint32_t));
+  for (int l = 0; l < L; ++l) {
+    Rank& r = g.ranks[l];
+    GPart& p = gb.parts[l];
+    on(r, [&] {
+      shard_combine_predict(r.m, p.b, r.part_in.p, r.pc_in.as<uint32_t>(), lo, hi, r.pred.as<double>());
+      if (p.rows > 0)
+        FM_HIP_CHECK(hipMemcpyAsync(pred + p.row0, r.pred.p, sizeof(double) * p.rows, hipMemcpyDeviceToHost, r.m->stream));
+    });
+  }
+  for (auto& r : g.ranks) on(r, [&] { FM_HIP_CHECK(hipStreamSynchronize(r.m->stream)); });
+}
+
+void predict_group_batch(fm_ctx* ctx, GroupBatch& gb, double lo, double hi, double* pred) {
+  Group& g = grp(ctx);
+  if (gb.rows == 0) return;
+  FM_REQUIRE(pred != nullptr, "null argument");
+  if (g.sharded()) {
+    predict_sharded(ctx, g, gb, lo, hi, pred);
+    return;
+  }
+  for (int l = 0; l < g.L; ++l)
+    if (gb.parts[l].rows > 0)
+      mcheck(fm_predict_batch(g.ranks[l].m, gb.parts[l].b, lo, hi, pred + gb.parts[l].row0), "fm_predict_batch");
+}
+
+fm_batch* host_slot(fm_ctx* ctx) {
+  Group& g = grp(ctx);
+  auto& h = g.host_b[g.hnext];
+  g.hnext ^= 1;
+  if (!h) h.reset(new_group_batch(ctx));
+  return h.get();
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------ entry points
+int group_create(const fm_config* cfg, fm_ctx** out) {
+  FM_REQUIRE(cfg->parallel == FM_PARALLEL_SHARDED || cfg->parallel == FM_PARALLEL_REPLICATED, "bad parallel mode");
+  FM_REQUIRE(cfg->n_gpus >= 1 && cfg->n_gpus <= FM_MAX_LOCAL, "n_gpus must be in [1, FM_MAX_LOCAL]");
+  FM_REQUIRE(cfg->n_procs >= 1 && cfg->proc_rank >= 0 && cfg->proc_rank < cfg->n_procs, "bad n_procs / proc_rank");
+  const int L = cfg->n_gpus, R = cfg->n_procs * cfg->n_gpus;
+  FM_REQUIRE(cfg->parallel != FM_PARALLEL_SHARDED || R <= 64, "the sharded step supports at most 64 ranks");
+  bool repeat = false;
+  for (int a = 0; a < L; ++a)
+    for (int b = a + 1; b < L; ++b) repeat = repeat || cfg->devices[a] == cfg->devices[b];
+  int transport = cfg->transport;
+  if (transport == FM_TRANSPORT_AUTO) transport = (repeat && cfg->n_procs == 1) ? FM_TRANSPORT_COPY : FM_TRANSPORT_RCCL;
+  FM_REQUIRE(transport == FM_TRANSPORT_RCCL || transport == FM_TRANSPORT_COPY, "bad transport");
+  FM_REQUIRE(transport != FM_TRANSPORT_COPY || cfg->n_procs == 1, "the copy transport needs one process");
+  FM_REQUIRE(transport != FM_TRANSPORT_RCCL || !repeat, "RCCL needs a distinct device per rank");
+  std::unique_ptr<fm_ctx> c(new fm_ctx());
+  c->cfg = *cfg;
+  c->cfg.device = cfg->devices[0];
+  c->kp = (cfg->k + 3) / 4 * 4;
+  c->rows = 0;
+  c->group.reset(new Group());
+  Group& g = *c->group;
+  g.mode = cfg->parallel;
+  g.L = L;
+  g.R = R;
+  g.nprocs = cfg->n_procs;
+  g.prank = cfg->proc_rank;
+  g.rccl = transport == FM_TRANSPORT_RCCL;
+  g.ranks.resize(L);
+  for (int l = 0; l < L; ++l) {
+    Rank& r = g.ranks[l];
+    r.device = cfg->devices[l];
+    r.global = cfg->proc_rank * L + l;
+    fm_config mc = *cfg;
+    mc.parallel = FM_PARALLEL_NONE;
+    mc.n_gpus = 1;
+    mc.device = r.device;
+    mc.shard_index = g.sharded() ? r.global : 0;
+    mc.shard_count = g.sharded() ? R : 1;
+    mcheck(fm_create(&mc, &r.m), "fm_create (member)");
+    FM_HIP_CHECK(hipSetDevice(r.device));
+    FM_HIP_CHECK(hipEventCreateWithFlags(&r.ev_main, hipEventDisableTiming));
+    FM_HIP_CHECK(hipEventCreateWithFlags(&r.ev_side, hipEventDisableTiming));
+  }
+  for (auto& a : g.ranks)  // peer access between the distinct devices (copies, RCCL's P2P)
+    for (auto& b : g.ranks)
+      if (a.device != b.device) {
+        FM_HIP_CHECK(hipSetDevice(a.device));
+        const hipError_t e = hipDeviceEnablePeerAccess(b.device, 0);
+        if (e != hipSuccess) (void)hipGetLastError();  // already enabled, or no P2P: copies stage
+      }
+  if (g.rccl) {
+    ncclUniqueId id;
+    static_assert(sizeof(id) == sizeof(cfg->comm_id), "ncclUniqueId is 128 bytes");
+    if (cfg->n_procs == 1) FM_RCCL_CHECK(ncclGetUniqueId(&id));
+    else std::memcpy(&id, cfg->comm_id, sizeof(id));
+    FM_RCCL_CHECK(ncclGroupStart());
+    for (auto& r : g.ranks) {
+      FM_HIP_CHECK(hipSetDevice(r.device));
+      FM_RCCL_CHECK(ncclCommInitRank(&r.comm_main, R, id, r.global));
+    }
+    FM_RCCL_CHECK(ncclGroupEnd());
+    FM_RCCL_CHECK(ncclGroupStart());
+    for (auto& r : g.ranks) {
+      FM_HIP_CHECK(hipSetDevice(r.device));
+      FM_RCCL_CHECK(ncclCommSplit(r.comm_main, 0, r.global, &r.comm_side, nullptr));
+    }
+    FM_RCCL_CHECK(ncclGroupEnd());
+  }
+  *out = c.release();
+  return FM_OK;
+}
+
+fm_ctx* group_member0(fm_ctx* ctx) { return grp(ctx).ranks[0].m; }
+
+int group_batch_create(fm_ctx* ctx, const fm_csr* csr, fm_batch** out) {
+  FM_REQUIRE(out != nullptr, "null out");
+  std::unique_ptr<fm_batch> b(new_group_batch(ctx));
+  upload_parts(grp(ctx), csr, *b->grp, true);
+  sync_group_batch_view(b.get());
+  *out = b.release();
+  return FM_OK;
+}
+
+int group_batch_prepare(fm_ctx* ctx, fm_batch* b) {
+  Group& g = grp(ctx);
+  GroupBatch& gb = gbatch(ctx, b);
+  if (g.sharded()) {
+    prefetch(g, gb);
+  } else {
+    for (int l = 0; l < g.L; ++l) mcheck(fm_batch_prepare(g.ranks[l].m, gb.parts[l].b), "fm_batch_prepare");
+  }
+  return FM_OK;
+}
+
+int group_step_batch(fm_ctx* ctx, fm_batch* b, int32_t t, double step_size, double reg_param, fm_step_out* out) {
+  return step_group_batch(ctx, gbatch(ctx, b), t, step_size, reg_param, out);
+}
+
+int group_step(fm_ctx* ctx, const fm_csr* csr, int32_t t, double step_size, double reg_param, fm_step_out* out) {
+  fm_batch* b = host_slot(ctx);
+  upload_parts(grp(ctx), csr, *b->grp, true);
+  sync_group_batch_view(b);
+  return step_group_batch(ctx, *b->grp, t, step_size, reg_param, out);
+}
+
+int group_predict(fm_ctx* ctx, const fm_csr* csr, double lo, double hi, double* pred) {
+  FM_REQUIRE(csr != nullptr && (csr->n_rows == 0 || pred), "null argument");
+  fm_batch* b = host_slot(ctx);
+  upload_parts(grp(ctx), csr, *b->grp, false);
+  sync_group_batch_view(b);
+  predict_group_batch(ctx, *b->grp, lo, hi, pred);
+  return FM_OK;
+}
+
+int group_predict_batch(fm_ctx* ctx, fm_batch* b, double lo, double hi, double* pred) {
+  predict_group_batch(ctx, gbatch(ctx, b), lo, hi, pred);
+  return FM_OK;
+}
+
+int group_load_tables(fm_ctx* ctx, const int32_t* ids, int64_t n, const double* w, const double* V) {
+  for (auto& r : grp(ctx).ranks) mcheck(fm_load_tables(r.m, ids, n, w, V), "fm_load_tables");
+  return FM_OK;
+}
+
+int group_init_random(fm_ctx* ctx, const int32_t* ids, int64_t n, int64_t id_begin, int64_t id_end) {
+  for (auto& r : grp(ctx).ranks) {
+    if (ids) mcheck(fm_init_random(r.m, ids, n), "fm_init_random");
+    else mcheck(fm_init_random_range(r.m, id_begin, id_end), "fm_init_random_range");
+  }
+  return FM_OK;
+}
+
+int group_init_from_batch(fm_ctx* ctx, fm_batch* b, int64_t* n_present) {
+  Group& g = grp(ctx);
+  GroupBatch& gb = gbatch(ctx, b);
+  if (g.sharded()) {
+    // createInitialModel's distinct ids arrive at their owners through the step's own routing
+    prefetch(g, gb);
+    for (int l = 0; l < g.L; ++l) {
+      Rank& r = g.ranks[l];
+      GPart& p = gb.parts[l];
+      const int64_t n_in = std::accumulate(p.ent_in.begin(), p.ent_in.end(), int64_t(0));
+      if (n_in == 0) continue;
+      on(r, [&] {
+        FM_HIP_CHECK(hipStreamSynchronize(r.m->side));
+        DevBuf ids;
+        ids.ensure(sizeof(uint32_t) * n_in);
+        hipLaunchKernelGGL(k_slots_to_ids, dim3(grid_of(n_in)), dim3(kBlock), 0, r.m->stream, p.recv_slot.as<uint32_t>(),
+                           n_in, (uint32_t)g.R, (uint32_t)r.global, ids.as<uint32_t>());
+        launch_init_entries(r.m->view(), ids.as<uint32_t>(), n_in, r.m->cfg.seed, r.m->cfg.init_sd, r.m->epoch,
+                            r.m->cum_host.back(), r.m->stream);
+        FM_HIP_CHECK(hipStreamSynchronize(r.m->stream));
+        ids.release();
+      });
+    }
+  } else {
+    FM_REQUIRE(g.nprocs == 1, "replicated fm_init_from_batch needs one process (use fm_init_random_range)");
+    // every replica draws every id of every part (the draw depends on (seed, id, factor) only)
+    for (auto& r : g.ranks)
+      for (auto& p : gb.parts) {
+        if (p.nnz == 0) continue;
+        on(r, [&] {
+          DevBuf col;
+          col.ensure(sizeof(uint32_t) * p.nnz);
+          FM_HIP_CHECK(hipMemcpyAsync(col.p, p.b->dev.col.p, sizeof(uint32_t) * p.nnz, hipMemcpyDefault, r.m->stream));
+          launch_init_entries(r.m->view(), col.as<uint32_t>(), p.nnz, r.m->cfg.seed, r.m->cfg.init_sd, r.m->epoch,
+                              r.m->cum_host.back(), r.m->stream);
+          FM_HIP_CHECK(hipStreamSynchronize(r.m->stream));
+          col.release();
+        });
+      }
+  }
+  if (n_present) *n_present = group_num_present(ctx);
+  return FM_OK;
+}
+
+int64_t group_num_present(fm_ctx* ctx) {
+  Group& g = grp(ctx);
+  int64_t tot = 0;
+  for (int l = 0; l < (g.sharded() ? g.L : 1); ++l) {
+    const int64_t n = fm_num_present(g.ranks[l].m);
+    mcheck((int)std::min<int64_t>(n, 0), "fm_num_present");
+    tot += n;
+  }
+  return tot;
+}
+
+int group_export_tables(fm_ctx* ctx, int32_t* ids, double* w, double* V, int64_t cap, int64_t* n) {
+  Group& g = grp(ctx);
+  FM_REQUIRE(n != nullptr && cap >= 0, "bad arguments");
+  if (!g.sharded()) return fm_export_tables(g.ranks[0].m, ids, w, V, cap, n);
+  const int k = ctx->cfg.k;
+  std::vector<int64_t> cnt(g.L);
+  int64_t tot = 0;
+  for (int l = 0; l < g.L; ++l) {
+    mcheck(fm_export_tables(g.ranks[l].m, nullptr, nullptr, nullptr, 0, &cnt[l]), "fm_export_tables");
+    tot += cnt[l];
+  }
+  *n = tot;
+  if (cap == 0) return FM_OK;
+  FM_REQUIRE(cap >= tot && ids && w && V, "export buffers too small or null");
+  std::vector<int32_t> ai(tot);
+  std::vector<double> aw(tot), aV((size_t)tot * k);
+  int64_t o = 0;
+  for (int l = 0; l < g.L; ++l) {
+    int64_t got = 0;
+    if (cnt[l])
+      mcheck(fm_export_tables(g.ranks[l].m, ai.data() + o, aw.data() + o, aV.data() + o * k, cnt[l], &got),
+             "fm_export_tables");
+    o += cnt[l];
+  }
+  std::vector<int64_t> ord(tot);
+  std::iota(ord.begin(), ord.end(), int64_t(0));
+  std::sort(ord.begin(), ord.end(), [&](int64_t a, int64_t b) { return ai[a] < ai[b]; });
+  for (int64_t i = 0; i < tot; ++i) {
+    ids[i] = ai[ord[i]];
+    w[i] = aw[ord[i]];
+    std::memcpy(V + i * k, aV.data() + ord[i] * k, sizeof(double) * k);
+  }
+  return FM_OK;
+}
+
+int group_export_rows(fm_ctx* ctx, const int32_t* ids, int64_t n, double* w, double* V, int8_t* present) {
+  Group& g = grp(ctx);
+  if (!g.sharded()) return fm_export_rows(g.ranks[0].m, ids, n, w, V, present);
+  FM_REQUIRE(n >= 0, "negative n");
+  if (n == 0) return FM_OK;
+  FM_REQUIRE(ids && w && V && present, "null argument");
+  const int k = ctx->cfg.k;
+  std::vector<std::vector<int64_t>> pos(g.L);
+  for (int64_t i = 0; i < n; ++i) {
+    FM_REQUIRE(ids[i] >= 0 && ids[i] < ctx->cfg.num_features, "id out of [0, num_features)");
+    const int owner = (int)(ids[i] % g.R);
+    const int l = owner - g.prank * g.L;
+    FM_REQUIRE(l >= 0 && l < g.L, "id owned by a rank of another process");
+    pos[l].push_back(i);
+  }
+  for (int l = 0; l < g.L; ++l) {
+    const int64_t m = (int64_t)pos[l].size();
+    if (m == 0) continue;
+    std::vector<int32_t> si(m);
+    std::vector<double> sw(m), sV((size_t)m * k);
+    std::vector<int8_t> sp(m);
+    for (int64_t j = 0; j < m; ++j) si[j] = ids[pos[l][j]];
+    mcheck(fm_export_rows(g.ranks[l].m, si.data(), m, sw.data(), sV.data(), sp.data()), "fm_export_rows");
+    for (int64_t j = 0; j < m; ++j) {
+      const int64_t i = pos[l][j];
+      w[i] = sw[j];
+      present[i] = sp[j];
+      std::memcpy(V + i * k, sV.data() + j * k, sizeof(double) * k);
+    }
+  }
+  return FM_OK;
+}
+
+int group_loss_history(fm_ctx* ctx, double* loss, int64_t cap, int64_t* n) {
+  Group& g = grp(ctx);
+  FM_REQUIRE(n != nullptr, "null n");
+  *n = ctx->epoch;
+  if (cap == 0 || ctx->epoch == 0) return FM_OK;
+  FM_REQUIRE(loss != nullptr, "null loss buffer");
+  const int64_t m = std::min<int64_t>(cap, ctx->epoch);
+  for (int64_t e = 0; e < m; ++e) {
+    double h[3];
+    stats_row(g, e, h);
+    loss[e] = h[0];
+  }
+  return FM_OK;
+}
+
+int group_last_stats(fm_ctx* ctx, double* loss_sum, int64_t* n_loss_rows, int64_t* n_unique) {
+  FM_REQUIRE(loss_sum && n_loss_rows && n_unique, "null argument");
+  FM_REQUIRE(ctx->epoch >= 1, "no step executed");
+  double h[3];
+  stats_row(grp(ctx), ctx->epoch - 1, h);
+  *loss_sum = h[0];
+  *n_loss_rows = (int64_t)h[1];
+  *n_unique = (int64_t)h[2];
+  return FM_OK;
+}
+
+int group_sync(fm_ctx* ctx) {
+  for (auto& r : grp(ctx).ranks)
+    on(r, [&] {
+      FM_HIP_CHECK(hipStreamSynchronize(r.m->stream));
+      FM_HIP_CHECK(hipStreamSynchronize(r.m->side));
+    });
+  return FM_OK;
+}
+
+int group_reserve(fm_ctx* ctx, int64_t max_rows, int64_t max_nnz) {
+  Group& g = grp(ctx);
+  for (auto& r : g.ranks) mcheck(fm_reserve(r.m, max_rows / g.L + 1, max_nnz), "fm_reserve");
+  return FM_OK;
+}
+
+// op 0: enable(on) on every rank; 1: reset every rank; 2: read local rank 0's per-phase times
+int group_profile(fm_ctx* ctx, int op, int32_t on_, char* names, int64_t names_cap, double* total_ms,
+                  int64_t* launches, int64_t cap, int64_t* n) {
+  Group& g = grp(ctx);
+  if (op == 2) return fm_profile_read(g.ranks[0].m, names, names_cap, total_ms, launches, cap, n);
+  for (auto& r : g.ranks) {
+    if (op == 0) mcheck(fm_profile_enable(r.m, on_), "fm_profile_enable");
+    else mcheck(fm_profile_reset(r.m), "fm_profile_reset");
+  }
+  return FM_OK;
+}
+
+}  // namespace fmhip
+
+extern "C" int fm_comm_unique_id(uint8_t* id) {
+  return fmhip::guarded_free([&]() -> int {
+    FM_REQUIRE(id != nullptr, "null id");
+    ncclUniqueId u;
+    FM_RCCL_CHECK(ncclGetUniqueId(&u));
+    std::memcpy(id, &u, sizeof(u));
+    return FM_OK;
+  });
+}

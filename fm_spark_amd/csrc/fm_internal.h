@@ -145,10 +145,11 @@ struct FwdOut {
   double* dw = nullptr;
   double* dv = nullptr;
   int32_t* absent = nullptr;
+  uint32_t* pcount = nullptr;  // partial pass (sharded predict): present rows per pair
 };
-// partial_out != nullptr: the sharded owner's partial pass (fm_shard.hip): [pairs][kp] vectors
-// followed by [pairs] float2 scalars;
-// pred != nullptr: FactorizationMachinesModel.predict (p.w0, p.cumE used)
+// partial_out != nullptr: the sharded owner's partial pass (fm_shard.hip): [pairs][kp] fp32 vectors
+// followed by [pairs] double2 scalars (pred->pcount, if given: present rows per pair);
+// else pred != nullptr: FactorizationMachinesModel.predict / calcLossGrad (p.w0, p.cumE used)
 void launch_forward(const TableView& T, const BatchDev& b, StepWork& w, const StepParams& p,
                     hipStream_t st, int64_t* n_fwd_blocks, float* partial_out = nullptr,
                     const FwdOut* pred = nullptr);

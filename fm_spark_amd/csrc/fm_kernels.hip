@@ -150,7 +150,7 @@ __global__ __launch_bounds__(kBlock, FM_FWD_MINW) void k_forward(TableView T, co
 #pragma unroll
       for (int j = 0; j < U; ++j) {
         float w;
-        if (MODE == kPredict && g == 0 && h[j].t >= 0) ++npres;
+        if ((MODE == kPredict || PARTIAL) && g == 0 && h[j].t >= 0) ++npres;
         current_row(h[j], v[j], w, cumE);
         const double xd = x[j];
         // vfxi = v * x (Model.scala:179), VectorSum over the sample (:191)
@@ -173,12 +173,15 @@ __global__ __launch_bounds__(kBlock, FM_FWD_MINW) void k_forward(TableView T, co
     for (int o = 1; o < TEAM; o <<= 1) {
       vv += __shfl_xor(vv, o);
       wx += __shfl_xor(wx, o);
-      if (MODE == kPredict) npres += __shfl_xor(npres, o);
+      if (MODE == kPredict || PARTIAL) npres += __shfl_xor(npres, o);
     }
     if (PARTIAL) {  // vectors [pair][kp] in S_out, scalars {sum v^2 x^2, sum w x} in yl_out
       if (rs == 0 && qok)
         *reinterpret_cast<float4*>(S_out + s * kp + g * 4) = make_float4((float)a0, (float)a1, (float)a2, (float)a3);
-      if (tl == 0) yl_out[s] = make_double2(vv, wx);
+      if (tl == 0) {
+        yl_out[s] = make_double2(vv, wx);
+        if (xo.pcount) xo.pcount[s] = npres;
+      }
       continue;
     }
     double ss = qok ? a0 * a0 + a1 * a1 + a2 * a2 + a3 * a3 : 0.0;
@@ -994,6 +997,12 @@ void launch_fwd_t(const TableView& T, const BatchDev& b, StepWork& w, const Step
   *nblk = blocks;
   const dim3 grid((unsigned)blocks), blk(kBlock);
   const FwdOut none{};
+  if (partial_out) {  // [n_rows][kp] fp32 vectors, then [n_rows] double2 scalars (xo: the present counts)
+    hipLaunchKernelGGL((k_forward<GS, TEAM, kPartial, U>), grid, blk, 0, st, T, b.row_ptr.as<int64_t>(),
+                       b.col.as<uint32_t>(), b.ent.as<uint2>(), nullptr, b.n_rows, p.w0, p.cumE, partial_out,
+                       reinterpret_cast<double2*>(partial_out + b.n_rows * T.kp), nullptr, xo ? *xo : none);
+    return;
+  }
   if (xo && xo->mode == kPredict) {
     hipLaunchKernelGGL((k_forward<GS, TEAM, kPredict, U>), grid, blk, 0, st, T, b.row_ptr.as<int64_t>(),
                        b.col.as<uint32_t>(), b.ent.as<uint2>(), nullptr, b.n_rows, p.w0, p.cumE, nullptr, nullptr,
@@ -1004,12 +1013,6 @@ void launch_fwd_t(const TableView& T, const BatchDev& b, StepWork& w, const Step
     hipLaunchKernelGGL((k_forward<GS, TEAM, kLossGrad, U>), grid, blk, 0, st, T, b.row_ptr.as<int64_t>(),
                        b.col.as<uint32_t>(), b.ent.as<uint2>(), b.label.as<double>(), b.n_rows, p.w0, p.cumE, nullptr,
                        nullptr, nullptr, *xo);
-    return;
-  }
-  if (partial_out) {  // [n_rows][kp] fp32 vectors, then [n_rows] double2 scalars
-    hipLaunchKernelGGL((k_forward<GS, TEAM, kPartial, U>), grid, blk, 0, st, T, b.row_ptr.as<int64_t>(),
-                       b.col.as<uint32_t>(), b.ent.as<uint2>(), nullptr, b.n_rows, p.w0, p.cumE, partial_out,
-                       reinterpret_cast<double2*>(partial_out + b.n_rows * T.kp), nullptr, none);
     return;
   }
   w.loss_part.ensure(sizeof(double2) * blocks);
@@ -1024,22 +1027,22 @@ void launch_fwd_t(const TableView& T, const BatchDev& b, StepWork& w, const Step
 // is sized so one round of U = 4 passes covers a segment, instead of 16 lanes per segment.
 template <int GS>
 void launch_partial_t(const TableView& T, const BatchDev& b, StepWork& w, const StepParams& p, hipStream_t st,
-                      int64_t* nblk, float* partial_out) {
+                      int64_t* nblk, float* partial_out, const FwdOut* xo) {
   const double avg = b.n_rows > 0 ? (double)b.nnz / (double)b.n_rows : 0.0;
-  if (GS <= 16 && avg <= 4.0) launch_fwd_t<GS, GS, FM_FWD_U>(T, b, w, p, st, nblk, partial_out, nullptr);
-  else if (GS <= 16 && avg <= 8.0) launch_fwd_t<GS, (2 * GS > 16 ? 16 : 2 * GS), FM_FWD_U>(T, b, w, p, st, nblk, partial_out, nullptr);
-  else launch_fwd_t<GS, (GS > 16 ? GS : 16), FM_FWD_U>(T, b, w, p, st, nblk, partial_out, nullptr);
+  if (GS <= 16 && avg <= 4.0) launch_fwd_t<GS, GS, FM_FWD_U>(T, b, w, p, st, nblk, partial_out, xo);
+  else if (GS <= 16 && avg <= 8.0) launch_fwd_t<GS, (2 * GS > 16 ? 16 : 2 * GS), FM_FWD_U>(T, b, w, p, st, nblk, partial_out, xo);
+  else launch_fwd_t<GS, (GS > 16 ? GS : 16), FM_FWD_U>(T, b, w, p, st, nblk, partial_out, xo);
 }
 
 void launch_forward(const TableView& T, const BatchDev& b, StepWork& w, const StepParams& p, hipStream_t st,
                     int64_t* nblk, float* partial_out, const FwdOut* pred) {
   const int nq = T.kp / 4;
-  if (partial_out && !pred) {
-    if (nq <= 1) launch_partial_t<1>(T, b, w, p, st, nblk, partial_out);
-    else if (nq <= 2) launch_partial_t<2>(T, b, w, p, st, nblk, partial_out);
-    else if (nq <= 4) launch_partial_t<4>(T, b, w, p, st, nblk, partial_out);
-    else if (nq <= 8) launch_partial_t<8>(T, b, w, p, st, nblk, partial_out);
-    else if (nq <= 16) launch_partial_t<16>(T, b, w, p, st, nblk, partial_out);
+  if (partial_out) {
+    if (nq <= 1) launch_partial_t<1>(T, b, w, p, st, nblk, partial_out, pred);
+    else if (nq <= 2) launch_partial_t<2>(T, b, w, p, st, nblk, partial_out, pred);
+    else if (nq <= 4) launch_partial_t<4>(T, b, w, p, st, nblk, partial_out, pred);
+    else if (nq <= 8) launch_partial_t<8>(T, b, w, p, st, nblk, partial_out, pred);
+    else if (nq <= 16) launch_partial_t<16>(T, b, w, p, st, nblk, partial_out, pred);
     else if (nq <= 32) launch_fwd_t<32, 32, FM_FWD_U>(T, b, w, p, st, nblk, partial_out, pred);
     else if (nq <= 64) launch_fwd_t<64, 64, FM_FWD_U>(T, b, w, p, st, nblk, partial_out, pred);
     else FM_REQUIRE(false, "dimFactorization > 256 is not supported");

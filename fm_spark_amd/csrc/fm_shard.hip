@@ -70,10 +70,11 @@ __device__ __forceinline__ uint64_t team_or64(uint64_t m) {
 }
 
 // per sample (a team of lanes over its entries): the owners it touches (bit mask); per owner:
-// entry counts
+// entry counts.  Ids >= F (a predict batch's ids outside the model, dropped by the inner joins of
+// Model.scala:103-112) belong to no owner.
 __global__ __launch_bounds__(kBlock) void k_sample_mask(const int64_t* __restrict__ row_ptr,
                                                         const uint32_t* __restrict__ col, int64_t B, uint32_t R,
-                                                        uint64_t* __restrict__ mask,
+                                                        uint64_t F, uint64_t* __restrict__ mask,
                                                         unsigned long long* __restrict__ ecount) {
   constexpr int TPB = kBlock / kTeamR;
   __shared__ uint32_t cnt[kMaxR];
@@ -85,6 +86,7 @@ __global__ __launch_bounds__(kBlock) void k_sample_mask(const int64_t* __restric
     uint64_t m = 0;
     if (s < B) {
       for (int64_t e = row_ptr[s] + tl; e < row_ptr[s + 1]; e += kTeamR) {
+        if (col[e] >= F) continue;
         const uint32_t o = col[e] % R;
         m |= 1ull << o;
         atomicAdd(&cnt[o], 1u);
@@ -99,17 +101,22 @@ __global__ __launch_bounds__(kBlock) void k_sample_mask(const int64_t* __restric
 
 // per entry, in CSR order: key = owner << sb | slot and the wire payload {pair index of (sample,
 // owner) within the owner's block, x bits}, so one stable pass over the owner bits lays out the
-// send buffers
+// send buffers.  Ids >= F get owner R: they sort after every owner's block and are not sent.
 __global__ __launch_bounds__(kBlock) void k_route_keys(const int64_t* __restrict__ row_ptr,
                                                        const uint32_t* __restrict__ col,
                                                        const uint2* __restrict__ ent, int64_t B, uint32_t R, int sb,
-                                                       const int32_t* __restrict__ pairidx,
+                                                       uint64_t F, const int32_t* __restrict__ pairidx,
                                                        uint32_t* __restrict__ key, uint2* __restrict__ pay) {
   constexpr int TPB = kBlock / kTeamR;
   const int tl = threadIdx.x % kTeamR;
   for (int64_t s = (int64_t)blockIdx.x * TPB + threadIdx.x / kTeamR; s < B; s += (int64_t)gridDim.x * TPB) {
     for (int64_t e = row_ptr[s] + tl; e < row_ptr[s + 1]; e += kTeamR) {
       const uint32_t id = col[e];
+      if (id >= F) {
+        key[e] = R << sb;
+        pay[e] = make_uint2(0u, ent[e].y);
+        continue;
+      }
       const uint32_t o = id % R;
       key[e] = (o << sb) | (id / R);
       pay[e] = make_uint2((uint32_t)pairidx[s * R + o], ent[e].y);
@@ -295,6 +302,53 @@ __global__ __launch_bounds__(kBlock) void k_shard_combine(const int32_t* __restr
   }
 }
 
+// The same sums for FactorizationMachinesModel.predict (Model.scala:90-133) over a sharded table:
+// pcnt[pair] = the owner's present rows among the pair's entries (absent ids drop out, :103-112);
+// a sample with none scores globalBias unclamped (na.fill, :78-86), every other
+// least(greatest(yhat, minLabel), maxLabel) (:129-132).
+template <int GS>
+__global__ __launch_bounds__(kBlock) void k_shard_predict(const int32_t* __restrict__ pairidx,
+                                                          const int64_t* __restrict__ poff, int R, int64_t B,
+                                                          const float* __restrict__ part_vec,
+                                                          const double2* __restrict__ part_sc,
+                                                          const uint32_t* __restrict__ pcnt, int kp, double w0,
+                                                          double lo, double hi, double* __restrict__ pred) {
+  constexpr int TPB = kBlock / GS;
+  const int tid = threadIdx.x, g = tid % GS;
+  const int nq = kp >> 2;
+  for (int64_t s = (int64_t)blockIdx.x * TPB + tid / GS; s < B; s += (int64_t)gridDim.x * TPB) {
+    const int32_t* pi = pairidx + s * R;
+    double vv = 0.0, wx = 0.0, ss = 0.0;
+    uint32_t cnt = 0;
+    for (int o = 0; o < R; ++o) {
+      const int32_t ix = pi[o];
+      if (ix >= 0) {
+        const double2 t = part_sc[poff[o] + ix];
+        vv += t.x;
+        wx += t.y;
+        cnt += pcnt[poff[o] + ix];
+      }
+    }
+    for (int qc = 0; qc < nq; qc += GS) {
+      const int q = qc + g;
+      if (q >= nq) continue;
+      double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+      for (int o = 0; o < R; ++o) {
+        const int32_t ix = pi[o];
+        if (ix >= 0) {
+          const float4 t = reinterpret_cast<const float4*>(part_vec + (poff[o] + ix) * kp)[q];
+          a0 += (double)t.x; a1 += (double)t.y; a2 += (double)t.z; a3 += (double)t.w;
+        }
+      }
+      ss += a0 * a0 + a1 * a1 + a2 * a2 + a3 * a3;
+    }
+#pragma unroll
+    for (int o = 1; o < GS; o <<= 1) ss += __shfl_xor(ss, o);
+    const double yhat = 0.5 * (ss - vv) + wx + w0;
+    if (g == 0) pred[s] = cnt == 0 ? w0 : fmin(fmax(yhat, lo), hi);
+  }
+}
+
 inline unsigned blocks_for(int64_t threads, int64_t cap = 256 * 16) {
   int64_t b = (threads + kBlock - 1) / kBlock;
   if (b < 1) b = 1;
@@ -322,6 +376,10 @@ __global__ void k_owner_offsets(const unsigned long long* __restrict__ pairs, in
 
 }  // namespace
 
+// The owner partial pass of fm_shard_owner_forward; present_out (optional, [P] uint32): the pair's
+// present rows (sharded predict).
+void shard_owner_partials(fm_ctx* ctx, fm_batch* b, void* partials_out, uint32_t* present_out);
+
 }  // namespace fmhip
 
 using namespace fmhip;
@@ -346,6 +404,7 @@ StepParams shard_params(fm_ctx* ctx, int32_t t, double step_size, double reg_par
 // The batch's sharded state, created on first use with its events already "done".
 ShardBatchState& shard_state(fm_ctx* ctx, fm_batch* b) {
   FM_REQUIRE(b != nullptr && b->owner == ctx, "batch belongs to another context");
+  FM_REQUIRE(!ctx->group, "a multi-GPU context runs its sharded phases itself (fm_step / fm_step_batch)");
   FM_REQUIRE(ctx->cfg.shard_count >= 1, "bad context");
   if (!b->sh) {
     std::unique_ptr<ShardBatchState> s(new ShardBatchState());
@@ -385,9 +444,11 @@ int fm_shard_route(fm_ctx* ctx, fm_batch* b, void* send_slot, void* send_ent, in
     S.poff.ensure(sizeof(int64_t) * (R + 1));
     unsigned long long* tot = ctx->sh_tot.as<unsigned long long>();  // [R] pairs, [R] entries
     FM_HIP_CHECK(hipMemsetAsync(tot, 0, sizeof(unsigned long long) * 2 * R, st));
+    const uint64_t F = (uint64_t)ctx->cfg.num_features;
+    const bool drop = b->max_id >= (int64_t)F;  // a predict batch with ids outside the model
     if (B > 0) {
       hipLaunchKernelGGL(k_sample_mask, dim3(blocks_for(B * kTeamR)), dim3(kBlock), 0, st, b->dev.row_ptr.as<int64_t>(),
-                         b->dev.col.as<uint32_t>(), B, (uint32_t)R, ctx->sh_mask.as<uint64_t>(), tot + R);
+                         b->dev.col.as<uint32_t>(), B, (uint32_t)R, F, ctx->sh_mask.as<uint64_t>(), tot + R);
       hipLaunchKernelGGL(k_pair_count, dim3((unsigned)ntiles), dim3(kBlock), 0, st, ctx->sh_mask.as<uint64_t>(), B,
                          R, ntiles, ctx->sh_tcnt.as<uint32_t>());
       hipLaunchKernelGGL(k_rows_scan, dim3((unsigned)R), dim3(kBlock), 0, st, ctx->sh_tcnt.as<uint32_t>(), ntiles,
@@ -401,13 +462,13 @@ int fm_shard_route(fm_ctx* ctx, fm_batch* b, void* send_slot, void* send_ent, in
       // stable pass over the owner bits partitions them (CSR order kept inside each owner).  sb
       // must hold the largest slot of ANY owner (owner 0 has the most rows), the same on every rank
       const int sb = bits_for(std::max<int64_t>((ctx->cfg.num_features - 1) / R, 1));
-      const int ob = bits_for(R - 1);
+      const int ob = bits_for(drop ? R : R - 1);
       FM_REQUIRE(sb + ob <= 32, "route key does not fit 32 bits");
       ctx->sh_pay.ensure(sizeof(uint2) * std::max<int64_t>(N, 4) + 16);
       ctx->sh_skey.ensure(sizeof(uint32_t) * std::max<int64_t>(N, 4) + 16);
       hipLaunchKernelGGL(k_route_keys, dim3(blocks_for(B * kTeamR)), dim3(kBlock), 0, st,
                          b->dev.row_ptr.as<int64_t>(), b->dev.col.as<uint32_t>(), b->dev.ent.as<uint2>(), B,
-                         (uint32_t)R, sb, S.pairidx.as<int32_t>(), ctx->sh_okey.as<uint32_t>(),
+                         (uint32_t)R, sb, F, S.pairidx.as<int32_t>(), ctx->sh_okey.as<uint32_t>(),
                          ctx->sh_pay.as<uint2>());
       radix_sort_pairs64_bits(ctx->side_sort, ctx->sh_okey.as<uint32_t>(), ctx->sh_pay.as<uint2>(), N, sb, sb + ob, st,
                               ctx->sh_skey.as<uint32_t>(), reinterpret_cast<uint2*>(send_ent));
@@ -428,7 +489,7 @@ int fm_shard_route(fm_ctx* ctx, fm_batch* b, void* send_slot, void* send_ent, in
       S.pairs_out[o] = (int64_t)hc[o];
       ne += (int64_t)hc[R + o];
     }
-    FM_REQUIRE(ne == N, "route: inconsistent entry count");
+    FM_REQUIRE(drop ? ne <= N : ne == N, "route: inconsistent entry count");
     S.route_nnz = N;
     S.combined = false;
     return FM_OK;
@@ -497,31 +558,77 @@ int fm_shard_owner_prepare(fm_ctx* ctx, fm_batch* b, const void* recv_slot, cons
 
 int fm_shard_owner_forward(fm_ctx* ctx, fm_batch* b, void* partials_out) {
   return guarded(ctx, [&]() -> int {
-    ShardBatchState& S = shard_state(ctx, b);
-    FM_REQUIRE(S.prepared, "fm_shard_owner_prepare must run on this batch first");
-    FM_REQUIRE(S.P == 0 || partials_out, "null buffer");
-    hipStream_t st = ctx->stream;
-    FM_HIP_CHECK(hipStreamWaitEvent(st, S.ready_fwd, 0));
-    hipEvent_t e0 = ctx->prof_begin(st);
-    if (S.P > 0) {
-      // partial forward over the pairs, rows of the local table (lazy L1 caught up on read)
-      BatchDev view;
-      view.n_rows = S.P;
-      view.nnz = S.n;
-      view.row_ptr.p = S.pair_ptr.p;
-      view.col.p = const_cast<uint32_t*>(S.recv_slot);
-      view.ent.p = const_cast<uint2*>(S.recv_ent);
-      StepParams p{};
-      p.cumE = ctx->cum_host.back();
-      int64_t nblk = 0;
-      launch_forward(ctx->view(), view, ctx->work, p, st, &nblk, reinterpret_cast<float*>(partials_out));
-      view.row_ptr.p = view.col.p = view.ent.p = nullptr;  // borrowed
-      FM_HIP_CHECK(hipGetLastError());
-    }
-    ctx->prof_end("owner_forward", e0, st);
+    shard_owner_partials(ctx, b, partials_out, nullptr);
     return FM_OK;
   });
 }
+
+}  // extern "C"
+
+namespace fmhip {
+
+void shard_owner_partials(fm_ctx* ctx, fm_batch* b, void* partials_out, uint32_t* present_out) {
+  ShardBatchState& S = shard_state(ctx, b);
+  FM_REQUIRE(S.prepared, "fm_shard_owner_prepare must run on this batch first");
+  FM_REQUIRE(S.P == 0 || partials_out, "null buffer");
+  hipStream_t st = ctx->stream;
+  FM_HIP_CHECK(hipStreamWaitEvent(st, S.ready_fwd, 0));
+  hipEvent_t e0 = ctx->prof_begin(st);
+  if (S.P > 0) {
+    // partial forward over the pairs, rows of the local table (lazy L1 caught up on read)
+    BatchDev view;
+    view.n_rows = S.P;
+    view.nnz = S.n;
+    view.row_ptr.p = S.pair_ptr.p;
+    view.col.p = const_cast<uint32_t*>(S.recv_slot);
+    view.ent.p = const_cast<uint2*>(S.recv_ent);
+    StepParams p{};
+    p.cumE = ctx->cum_host.back();
+    int64_t nblk = 0;
+    FwdOut xo{};  // the partial pass (partial_out given); only the present counts are read
+    xo.pcount = present_out;
+    launch_forward(ctx->view(), view, ctx->work, p, st, &nblk, reinterpret_cast<float*>(partials_out), &xo);
+    view.row_ptr.p = view.col.p = view.ent.p = nullptr;  // borrowed
+    FM_HIP_CHECK(hipGetLastError());
+  }
+  ctx->prof_end("owner_forward", e0, st);
+}
+
+void shard_combine_predict(fm_ctx* ctx, fm_batch* b, const void* partials_in, const uint32_t* present_in,
+                           double lo, double hi, double* pred_dev) {
+  ShardBatchState& S = shard_state(ctx, b);
+  FM_REQUIRE(S.route_nnz == b->dev.nnz && (int)S.pairs_out.size() == ctx->cfg.shard_count,
+             "fm_shard_route must run on this batch first");
+  const int R = ctx->cfg.shard_count;
+  const int64_t B = b->dev.n_rows;
+  if (B == 0) return;
+  int64_t Ps = 0;
+  for (int o = 0; o < R; ++o) Ps += S.pairs_out[o];
+  FM_REQUIRE(Ps == 0 || (partials_in && present_in), "null buffer");
+  const int kp = ctx->kp;
+  const int GS = team_for(kp / 4);
+  int64_t blocks = std::max<int64_t>((B + kBlock / GS - 1) / (kBlock / GS), 1);
+  if (blocks > 256 * 8) blocks = 256 * 8;
+  const float* pv = reinterpret_cast<const float*>(partials_in);
+  const double2* ps = reinterpret_cast<const double2*>(pv ? pv + Ps * kp : nullptr);
+  const int32_t* pi = S.pairidx.as<int32_t>();
+  const int64_t* poff = S.poff.as<int64_t>();
+  const double w0 = ctx->cfg.w0;
+  hipStream_t st = ctx->stream;
+  const dim3 grid((unsigned)blocks), blk(kBlock);
+  switch (GS) {
+    case 1: hipLaunchKernelGGL(k_shard_predict<1>, grid, blk, 0, st, pi, poff, R, B, pv, ps, present_in, kp, w0, lo, hi, pred_dev); break;
+    case 2: hipLaunchKernelGGL(k_shard_predict<2>, grid, blk, 0, st, pi, poff, R, B, pv, ps, present_in, kp, w0, lo, hi, pred_dev); break;
+    case 4: hipLaunchKernelGGL(k_shard_predict<4>, grid, blk, 0, st, pi, poff, R, B, pv, ps, present_in, kp, w0, lo, hi, pred_dev); break;
+    case 8: hipLaunchKernelGGL(k_shard_predict<8>, grid, blk, 0, st, pi, poff, R, B, pv, ps, present_in, kp, w0, lo, hi, pred_dev); break;
+    default: hipLaunchKernelGGL(k_shard_predict<16>, grid, blk, 0, st, pi, poff, R, B, pv, ps, present_in, kp, w0, lo, hi, pred_dev); break;
+  }
+  FM_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace fmhip
+
+extern "C" {
 
 int fm_shard_combine(fm_ctx* ctx, fm_batch* b, const void* partials_in, void* s_send) {
   return guarded(ctx, [&]() -> int {

@@ -50,13 +50,51 @@ class DeviceBatch:
             pass
 
 
+def comm_unique_id() -> bytes:
+    """RCCL unique id (128 bytes) that process 0 of a multi-process job hands to the others
+    (fm_comm_unique_id)."""
+    lib = N.load()
+    buf = (C.c_uint8 * 128)()
+    N.check(lib.fm_comm_unique_id(buf), "fm_comm_unique_id")
+    return bytes(buf)
+
+
 class FMContext:
+    """One fm_ctx.  ``parallel`` = "sharded" / "replicated": the context drives ``n_gpus`` local
+    ranks on ``devices`` (default device, device + 1, ...) of a job of ``n_procs`` processes and runs
+    the multi-GPU step itself (include/fm_hip.h); ``transport`` "auto" | "rccl" | "copy"."""
+
+    _PAR = {None: N.FM_PARALLEL_NONE, "none": N.FM_PARALLEL_NONE, "sharded": N.FM_PARALLEL_SHARDED,
+            "replicated": N.FM_PARALLEL_REPLICATED}
+    _TR = {"auto": N.FM_TRANSPORT_AUTO, "rccl": N.FM_TRANSPORT_RCCL, "copy": N.FM_TRANSPORT_COPY}
+
     def __init__(self, num_features: int, k: int, *, device: int = 0, seed: int = 0, init_sd: float = 0.01,
-                 w0: float = 0.0, shard_index: int = 0, shard_count: int = 1):
+                 w0: float = 0.0, shard_index: int = 0, shard_count: int = 1, parallel: str | None = None,
+                 n_gpus: int = 1, devices=None, transport: str = "auto", n_procs: int = 1, proc_rank: int = 0,
+                 comm_id: bytes | None = None):
         self._lib = N.load()
         cfg = N.fm_config(num_features=int(num_features), k=int(k), device=int(device), seed=int(seed) & (2**64 - 1),
                           init_sd=float(init_sd), w0=float(w0), shard_index=int(shard_index),
                           shard_count=int(shard_count))
+        cfg.parallel = self._PAR[parallel]
+        cfg.n_gpus = int(n_gpus)
+        devs = list(devices) if devices is not None else [int(device) + i for i in range(int(n_gpus))]
+        if cfg.parallel != N.FM_PARALLEL_NONE and len(devs) != n_gpus:
+            raise ValueError("devices must list n_gpus devices")
+        for i, d in enumerate(devs[: N.FM_MAX_LOCAL]):
+            cfg.devices[i] = int(d)
+        if cfg.parallel != N.FM_PARALLEL_NONE:
+            cfg.device = int(devs[0])
+        cfg.transport = self._TR[transport]
+        cfg.n_procs = int(n_procs)
+        cfg.proc_rank = int(proc_rank)
+        if comm_id is not None:
+            if len(comm_id) != 128:
+                raise ValueError("comm_id must be 128 bytes")
+            for i, b in enumerate(comm_id):
+                cfg.comm_id[i] = b
+        self.parallel = parallel if parallel not in (None, "none") else None
+        self.n_gpus = int(n_gpus)
         h = C.c_void_p()
         N.check(self._lib.fm_create(C.byref(cfg), C.byref(h)), "fm_create")
         self.handle = h

@@ -15,7 +15,10 @@
  *     (FactorizationMachinesSGD.scala:126-128), negative = error; the message is available
  *     from fm_last_error() on the calling thread.  No C++ exception, abort or exit crosses
  *     this boundary;
- *   - one fm_ctx owns one device's tables (one process per GPU).  Calls on one context are
+ *   - one fm_ctx owns one device's tables, or -- fm_config.parallel != FM_PARALLEL_NONE -- every
+ *     rank of a multi-GPU job that this process drives: n_gpus devices from ONE host thread, the
+ *     table row-sharded (or replicated) across them, the exchanges done inside the library over
+ *     RCCL (xGMI), as SURVEY §8(b) Threading asks of the Spark driver.  Calls on one context are
  *     serialised by an internal mutex; independent contexts may run concurrently
  *     (CrossValidator keeps several models alive at once).
  *   - arithmetic: tables are fp32 on the device, accumulations fp64; inputs/outputs fp64.
@@ -34,7 +37,16 @@ extern "C" {
 #define FM_ERR_ARG (-1)
 #define FM_ERR_OOM (-2)
 #define FM_ERR_HIP (-3)
+#define FM_ERR_RCCL (-4)
 #define FM_ERR_STATE (-5)
+
+#define FM_PARALLEL_NONE 0       /* this context is one table (or one manual shard, shard_index/count) */
+#define FM_PARALLEL_SHARDED 1    /* rows sharded by id % R over the job's R ranks, owner-computes */
+#define FM_PARALLEL_REPLICATED 2 /* every rank holds the whole table; gradient all-reduce */
+#define FM_TRANSPORT_AUTO 0      /* RCCL, unless a device repeats in devices[] (then COPY) */
+#define FM_TRANSPORT_RCCL 1      /* RCCL send/recv and all-reduce over xGMI */
+#define FM_TRANSPORT_COPY 2      /* one process only: device-to-device copies between the ranks */
+#define FM_MAX_LOCAL 16
 
 typedef struct fm_ctx fm_ctx;
 typedef struct fm_batch fm_batch;
@@ -46,8 +58,18 @@ typedef struct fm_batch fm_batch;
  *                (FactorizationMachinesSGD.scala:246).
  * init_sd/seed : createInitialModel's N(0, initialSd^2) draw (FactorizationMachinesSGD.scala:234-241),
  *                made deterministic (the reference's draw is unseeded).
- * shard_index/shard_count : row sharding by feature hash; this context owns the ids with
- *                id % shard_count == shard_index (shard_count 1 = whole table). */
+ * shard_index/shard_count : (parallel == FM_PARALLEL_NONE) row sharding by feature hash for a
+ *                caller that drives the fm_shard_* phases itself; this context owns the ids with
+ *                id % shard_count == shard_index (shard_count 1 = whole table).
+ * parallel     : FM_PARALLEL_SHARDED / _REPLICATED: this context drives n_gpus local ranks
+ *                (devices[0..n_gpus)) of a job of R = n_procs * n_gpus ranks; global rank of local
+ *                rank l = proc_rank * n_gpus + l (every process uses the same n_gpus).  Mini-batches
+ *                given to it are split by rows, contiguously, over the local ranks; the global
+ *                miniBatchSize is the sum over all ranks (SGD.scala:124).  Replaces the shuffles
+ *                S1/S2/S5/S6 of SURVEY §2b (Model.scala:155-164, SGD.scala:148-166).
+ * transport    : how the ranks exchange (FM_TRANSPORT_*).  n_procs > 1 needs RCCL and comm_id:
+ *                process 0 calls fm_comm_unique_id and hands the 128 bytes to the others by any
+ *                channel (Spark broadcast, torch.distributed, a file). */
 typedef struct fm_config {
   int64_t num_features;
   int32_t k;
@@ -57,6 +79,13 @@ typedef struct fm_config {
   double w0;
   int32_t shard_index;
   int32_t shard_count;
+  int32_t parallel;
+  int32_t n_gpus;
+  int32_t devices[FM_MAX_LOCAL];
+  int32_t transport;
+  int32_t n_procs;
+  int32_t proc_rank;
+  uint8_t comm_id[128];
 } fm_config;
 
 /* One mini-batch in CSR form: the result of explode(udfVecToMap(features))
@@ -81,8 +110,14 @@ typedef struct fm_step_out {
 } fm_step_out;
 
 /* ---- context --------------------------------------------------------------------- */
-/* Replaces: new FactorizationMachinesModel(uid, k, globalBias, ...) (Model.scala:43-48). */
+/* Replaces: new FactorizationMachinesModel(uid, k, globalBias, ...) (Model.scala:43-48).
+ * A multi-GPU context (parallel != FM_PARALLEL_NONE) accepts every entry point below except the
+ * manual fm_shard_* / fm_repl_* phases, fm_set_stream / fm_set_side_stream (unless n_gpus == 1)
+ * and fm_loss_grad on a sharded table; the table entry points act on the rows this process's ranks
+ * hold (all rows when n_procs == 1). */
 int fm_create(const fm_config* cfg, fm_ctx** out);
+/* RCCL unique id for a job of several processes (ncclGetUniqueId), 128 bytes into id. */
+int fm_comm_unique_id(uint8_t* id);
 void fm_destroy(fm_ctx* ctx);
 const char* fm_last_error(void);
 /* Launch on an externally owned HIP stream (hipStream_t passed as void*); NULL = the device's

@@ -61,3 +61,30 @@ def test_null_arguments_are_errors_not_crashes():
     assert lib.fm_epoch(None) == -1
     lib.fm_destroy(None)
     lib.fm_batch_destroy(None)
+
+
+def test_config_layout_matches_header(tmp_path):
+    """fm_config as the C compiler lays it out == the ctypes mirror (the multi-GPU fields included)."""
+    src = tmp_path / "sz.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "fm_hip.h"\n'
+                   'int main(void){printf("%zu %zu %zu %zu %zu\\n", sizeof(fm_config), offsetof(fm_config, parallel),'
+                   ' offsetof(fm_config, devices), offsetof(fm_config, proc_rank), offsetof(fm_config, comm_id));'
+                   'return 0;}\n')
+    exe = tmp_path / "sz"
+    subprocess.run(["gcc", f"-I{HEADER.parent}", str(src), "-o", str(exe)], check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
+    F = N.fm_config
+    assert got == [C.sizeof(F), F.parallel.offset, F.devices.offset, F.proc_rank.offset, F.comm_id.offset]
+
+
+def test_multi_gpu_context_without_gpu_fails_loudly():
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    from fm_spark_amd.engine import FMContext
+
+    with pytest.raises(N.FMError):
+        FMContext(100, 4, parallel="sharded", n_gpus=2, devices=[0, 0])
+    with pytest.raises(N.FMError):  # the copy transport is for one process
+        FMContext(100, 4, parallel="sharded", n_gpus=1, n_procs=2, transport="copy")

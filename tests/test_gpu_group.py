@@ -1,0 +1,179 @@
+"""GPU: multi-GPU inside one fm_ctx (fm_config.parallel; csrc/fm_group.hip), driven through the
+C entry points alone -- no Python exchange code.
+
+The COPY transport lets R ranks share this box's one MI355X (RCCL refuses two ranks on one
+device), so the sharded and replicated jobs run at R = 1..8 in one process; the RCCL transport
+runs at R = 1 (the same grouped send/recv, all-gather and all-reduce calls, one rank).  Every
+job is compared with the fp64 oracle step over the concatenated mini-batch (the reference's one
+global mini-batch: SGD.scala:116-211), and the sharded transform with oracle.predict
+(Model.scala:69-133: ids outside or absent from the model dropped, w0 for rows left without a
+learned feature, clamp)."""
+
+import math
+
+import numpy as np
+import pytest
+
+from oracle import fm_ref as R_
+from problems import make_problem
+
+pytestmark = pytest.mark.gpu
+
+
+def _host(c):
+    from fm_spark_amd._native import CSRHost
+
+    return CSRHost(c.row_ptr, c.col, c.val, c.label)
+
+
+def _ctx(F, k, R, mode="sharded", transport="copy", **kw):
+    from fm_spark_amd.engine import FMContext
+
+    devs = [0] * R if transport == "copy" else list(range(R))
+    return FMContext(F, k, parallel=mode, n_gpus=R, devices=devs, transport=transport, **kw)
+
+
+def _check_tables(ctx, model):
+    gi, gw, gV = ctx.export_tables()
+    np.testing.assert_array_equal(gi, np.nonzero(model.present)[0])
+    np.testing.assert_allclose(gw, model.w[gi], rtol=1e-5, atol=1e-8)
+    np.testing.assert_allclose(gV, model.V[gi], rtol=1e-5, atol=1e-8)
+
+
+@pytest.mark.parametrize("R,k,F,hot,transport", [
+    (1, 8, 503, 11, "copy"), (2, 16, 503, 11, "copy"), (3, 5, 401, 7, "copy"), (4, 32, 513, 512, "copy"),
+    (8, 16, 1031, 1030, "copy"), (1, 16, 300, 2, "rccl"),
+])
+def test_group_sharded_step_matches_oracle(gpu, R, k, F, hot, transport):
+    _, ids, w, V = make_problem(3, 1, F, k, 1)
+    ctx = _ctx(F, k, R, transport=transport)
+    ctx.load_tables(ids, w, V)
+    model = R_.Model.empty(F, k)
+    model.load(ids, w, V)
+    # steps 1-2 from host CSRs (fm_step), 3-4 from device batches with the next one prepared
+    probs = [make_problem(40 + t, 150 + 13 * t, F, k, 9, hot=hot)[0] for t in range(1, 5)]
+    for t in (1, 2):
+        o = ctx.step(_host(probs[t - 1]), t, 0.3, 1e-4)
+        ref = R_.sgd_step_fast(model, probs[t - 1], t, 0.3, 1e-4)
+        assert o.loss_sum == pytest.approx(ref.loss_sum, rel=1e-5)
+        assert (o.n_rows, o.n_loss_rows, o.n_unique) == (ref.n_rows, ref.n_loss_rows, ref.n_unique)
+    bs = [ctx.batch(_host(p)) for p in probs[2:]]
+    bs[0].prepare()
+    for t in (3, 4):
+        o = ctx.step_batch(bs[t - 3], t, 0.3, 1e-4, sync=True)
+        if t == 3:
+            bs[1].prepare()  # routed, exchanged and slot-sorted behind step 3
+        ref = R_.sgd_step_fast(model, probs[t - 1], t, 0.3, 1e-4)
+        assert o.loss_sum == pytest.approx(ref.loss_sum, rel=1e-5)
+        assert o.n_unique == ref.n_unique
+    assert ctx.epoch == 4
+    hist = ctx.loss_history()
+    assert len(hist) == 4 and hist[-1] == pytest.approx(o.loss_sum, rel=1e-12)
+    _check_tables(ctx, model)
+    # rows by id through the owners
+    q = np.array([0, hot, F - 1, F // 2], dtype=np.int32)
+    rw, rV, rp = ctx.export_rows(q)
+    assert rp.all()
+    np.testing.assert_allclose(rw, model.w[q], rtol=1e-5, atol=1e-8)
+    np.testing.assert_allclose(rV, model.V[q], rtol=1e-5, atol=1e-8)
+    ctx.close()
+
+
+@pytest.mark.parametrize("R,k,transport", [(1, 8, "copy"), (3, 16, "copy"), (1, 16, "rccl")])
+def test_group_replicated_step_matches_oracle(gpu, R, k, transport):
+    F = 401
+    _, ids, w, V = make_problem(12, 1, F, k, 1)
+    ctx = _ctx(F, k, R, mode="replicated", transport=transport)
+    ctx.load_tables(ids, w, V)
+    model = R_.Model.empty(F, k)
+    model.load(ids, w, V)
+    for t in range(1, 4):
+        p = make_problem(300 * t, 200 + 11 * t, F, k, 7, hot=5)[0]
+        o = ctx.step(_host(p), t, 0.3, 1e-4)
+        ref = R_.sgd_step_fast(model, p, t, 0.3, 1e-4)
+        assert o.loss_sum == pytest.approx(ref.loss_sum, rel=1e-5)
+        assert (o.n_rows, o.n_loss_rows, o.n_unique) == (ref.n_rows, ref.n_loss_rows, ref.n_unique)
+    _check_tables(ctx, model)
+    ctx.close()
+
+
+def test_group_empty_batch_and_empty_rows(gpu):
+    """An empty global mini-batch is skipped by every rank (SGD.scala:126-128); rows without
+    entries count in miniBatchSize only; a part may hold no row at all."""
+    F, k, R = 97, 4, 3
+    _, ids, w, V = make_problem(8, 1, F, k, 1)
+    ctx = _ctx(F, k, R)
+    ctx.load_tables(ids, w, V)
+    model = R_.Model.empty(F, k)
+    model.load(ids, w, V)
+    empty = R_.CSR(np.zeros(1, np.int64), np.zeros(0, np.int32), np.zeros(0), np.zeros(0))
+    o = ctx.step(_host(empty), 1, 0.3, 1e-4)
+    assert not o.executed and ctx.epoch == 0
+    two = make_problem(9, 2, F, k, 5, empty_frac=0.0)[0]  # 2 rows over 3 ranks: one part is empty
+    o = ctx.step(_host(two), 1, 0.3, 1e-4)
+    ref = R_.sgd_step_fast(model, two, 1, 0.3, 1e-4)
+    assert o.loss_sum == pytest.approx(ref.loss_sum, rel=1e-5)
+    p = make_problem(10, 60, F, k, 5, hot=3, empty_frac=0.3)[0]
+    o = ctx.step(_host(p), 2, 0.3, 1e-4)
+    ref = R_.sgd_step_fast(model, p, 2, 0.3, 1e-4)
+    assert o.loss_sum == pytest.approx(ref.loss_sum, rel=1e-5) and o.n_rows == p.n_rows
+    _check_tables(ctx, model)
+    ctx.close()
+
+
+@pytest.mark.parametrize("R,transport", [(1, "copy"), (2, "copy"), (3, "copy"), (4, "copy"), (1, "rccl")])
+def test_group_sharded_predict_matches_oracle(gpu, R, transport):
+    """transform on a sharded table: ids >= F and ids absent from the model drop out, rows left
+    without a learned feature score w0 unclamped, the rest are clamped."""
+    F, k, w0 = 211, 8, 0.25
+    _, _, w, V = make_problem(5, 1, F, k, 1)
+    present = np.sort(np.random.default_rng(1).choice(F, size=150, replace=False)).astype(np.int32)
+    ctx = _ctx(F, k, R, transport=transport, w0=w0)
+    ctx.load_tables(present, w[present], V[present])
+    model = R_.Model.empty(F, k, w0=w0)
+    model.load(present, w[present], V[present])
+    p = make_problem(6, 300, F + 40, k, 6, empty_frac=0.15)[0]  # ids up to F + 39: some outside
+    lone = np.nonzero(~np.isin(np.arange(F), present))[0][:3]  # a row holding only absent ids
+    rp = np.concatenate([p.row_ptr, [p.row_ptr[-1] + len(lone)]]).astype(np.int64)
+    csr = R_.CSR(rp, np.concatenate([p.col, lone]).astype(np.int32), np.concatenate([p.val, np.ones(len(lone))]),
+                 np.concatenate([p.label, [0.0]]))
+    for lo, hi in ((0.0, 1.0), (-math.inf, math.inf)):
+        got = ctx.predict(_host(csr), lo, hi)
+        ref = R_.predict(model, csr, lo, hi, num_features=F)
+        np.testing.assert_allclose(got, ref, rtol=1e-5, atol=1e-7)
+    assert got[-1] == w0
+    ctx.close()
+
+
+def test_group_c3_r8_matches_single_table(gpu):
+    """Config c3's table (100M hashed features, k = 16) sharded over R = 8 ranks of one context
+    (COPY transport, every rank on this GPU): two iterations of 8 x 32K rows against the
+    single-table HIP step over the same global mini-batch; then transform of a third batch on both."""
+    from fm_spark_amd.data import synthetic_batch
+    from fm_spark_amd.engine import FMContext
+
+    F, k, R, B = 100_000_000, 16, 8, 8 * 32768
+    ref = FMContext(F, k, seed=5, init_sd=0.01)
+    grp = _ctx(F, k, R, seed=5, init_sd=0.01)
+    for t in (1, 2):
+        b = synthetic_batch(B, F, batch_index=500 + t)
+        rb = ref.batch(_host(b))
+        gb = grp.batch(_host(b))
+        n1 = ref.init_from_batch(rb)
+        n2 = grp.init_from_batch(gb)  # createInitialModel through the owners: the same seeded draw
+        assert n1 == n2
+        o = ref.step_batch(rb, t, 0.1, 1e-6, sync=True)
+        q = grp.step_batch(gb, t, 0.1, 1e-6, sync=True)
+        assert q.n_unique == o.n_unique == len(np.unique(b.col))
+        assert q.loss_sum == pytest.approx(o.loss_sum, rel=1e-9)
+    gi, gw, gV = ref.export_tables()
+    si, sw, sV = grp.export_tables()
+    np.testing.assert_array_equal(si, gi)
+    np.testing.assert_allclose(sw, gw, rtol=1e-5, atol=1e-8)
+    np.testing.assert_allclose(sV, gV, rtol=1e-5, atol=1e-8)
+    b3 = synthetic_batch(65536, F, batch_index=777)
+    pr = ref.predict(_host(b3), 0.0, 1.0)
+    pg = grp.predict(_host(b3), 0.0, 1.0)
+    np.testing.assert_allclose(pg, pr, rtol=1e-5, atol=1e-7)
+    ref.close()
+    grp.close()
