@@ -64,6 +64,10 @@ def parse():
                         "caller sees it) instead of device-resident batches; reported, never the headline")
     p.add_argument("--prefetch-depth", type=int, default=1,
                    help="single table: how many steps ahead a batch is sorted on the side stream")
+    p.add_argument("--trainer", default="lib", choices=["lib", "torch"],
+                   help="N > 1 / --force-sharded: 'lib' = one multi-GPU fm_ctx per process, the exchanges "
+                        "inside libfm_hip over RCCL (the C-ABI path); 'torch' = the torch.distributed test "
+                        "harness (fm_spark_amd/distributed.py) driving the fm_shard_* phases")
     p.add_argument("--host-path-steps", type=int, default=12,
                    help="N = 1: after the timed region, time this many fm_step calls with the host CSR "
                         "(PCIe-inclusive, what a JNI caller gets) for host_path_ms_per_step; 0 = skip")
@@ -75,6 +79,25 @@ def median_step_ms(events):
     median over >= 20 steps); the events sit on the stream the steps are launched on."""
     d = [events[i].elapsed_time(events[i + 1]) for i in range(len(events) - 1)]
     return float(np.median(d)) if d else None
+
+
+XGMI_LINK_GBS = 153.0  # per direction per link (MI355X: 7 links to the 7 peers of an 8-GPU node)
+
+
+def exchange_bytes(b, R, r, kp):
+    """Per iteration, what rank r sends over xGMI for its own batch b in the sharded step
+    (include/fm_hip.h wire formats): its entries to remote owners (4 B slot + 8 B {pair, x}), the
+    S rows back to them ((kp + 4) words per remote pair); as an owner it returns a partial row per
+    pair it received (about the same count by symmetry of the hashed ids)."""
+    ids = b.col.astype(np.int64)
+    owner = ids % R
+    sample = np.repeat(np.arange(b.n_rows, dtype=np.int64), np.diff(b.row_ptr))
+    pairs = np.unique(sample * R + owner)
+    ent_remote = int(np.count_nonzero(owner != r))
+    pair_remote = int(np.count_nonzero(pairs % R != r))
+    row = (kp + 4) * 4
+    return {"entries_B": 12 * ent_remote, "s_rows_B": row * pair_remote, "partials_B": row * pair_remote,
+            "remote_entries": ent_remote, "remote_pairs": pair_remote}
 
 
 def host_path_leg(ctx, host_batches, t, steps, torch):
@@ -271,6 +294,63 @@ def main():
                                          f", batches sorted {depth} steps ahead on the side stream") if prefetch else "")
         if args.host_path:
             parallelism += ", host CSR uploaded by fm_step every step (PCIe-inclusive)"
+    elif args.trainer == "lib":
+        from fm_spark_amd.engine import comm_unique_id
+
+        # one fm_ctx per process (n_gpus = 1 here: torch.distributed.run starts a process per GPU);
+        # rank 0's RCCL id reaches the others over the torch group, then every exchange of the
+        # step runs inside libfm_hip (fm_group.hip)
+        idt = torch.zeros(128, dtype=torch.uint8, device="cuda")
+        if rank == 0:
+            idt.copy_(torch.tensor(list(comm_unique_id()), dtype=torch.uint8))
+        dist.broadcast(idt, src=0)
+        cid = bytes(idt.cpu().tolist())
+        ctx = FMContext(F, k, seed=20261015, init_sd=INIT_SD, parallel="sharded", n_gpus=1, devices=[local_rank],
+                        transport="rccl", n_procs=world, proc_rank=rank, comm_id=cid)
+        main_stream = torch.cuda.Stream()
+        torch.cuda.set_stream(main_stream)
+        ctx.set_stream(main_stream.cuda_stream)
+        ctx.init_random_range(0, F)
+        dbatches = [ctx.batch(CSRHost(b.row_ptr, b.col, b.val, b.label)) for b in host_batches]
+        prefetch = not args.no_prefetch
+        nb = len(dbatches)
+        t = 0
+        uniques = []
+        for i in range(max(args.warmup, nb)):  # every batch once: its distinct ids (U) for the roofline
+            t += 1
+            uniques.append(ctx.step_batch(dbatches[i % nb], t, STEP_SIZE, REG_PARAM, sync=True).n_unique)
+        ctx.sync()
+        torch.cuda.synchronize()
+        dist.barrier()
+        if args.profile_kernels:
+            ctx.profile_reset()
+            ctx.profile_enable(True)
+        t_start = time.perf_counter()
+        # batch i + 1's route, entry exchange and slot sort are enqueued on the side stream behind
+        # step i (fm_batch_prepare): inside the timed region, off the critical path
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+        if prefetch:
+            dbatches[0].prepare()
+        for i in range(args.steps):
+            t += 1
+            evs[i].record(main_stream)
+            ctx.step_batch(dbatches[i % nb], t, STEP_SIZE, REG_PARAM, sync=False)
+            if prefetch and i + 1 < args.steps:
+                dbatches[(i + 1) % nb].prepare()
+        evs[args.steps].record(main_stream)
+        ctx.sync()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t_start
+        median_ms = median_step_ms(evs)
+        prof = ctx.profile_read() if args.profile_kernels else {}
+        ctx.profile_enable(False)
+        losses = ctx.loss_history()
+        assert os.environ.get("FM_ABLATE") or np.all(np.isfinite(losses)), "non-finite loss"
+        U_mean = float(np.mean(uniques)) / world  # rows one owner updates
+        xg = exchange_bytes(host_batches[0], world, rank, (k + 3) // 4 * 4)
+        parallelism = (f"row-sharded x{world}, owner-computes, one fm_ctx per process with the exchanges inside "
+                       f"libfm_hip (RCCL grouped send/recv of entries, partial sums and S rows)" +
+                       (", next batch routed, exchanged and slot-sorted during the current step" if prefetch else ""))
     else:
         from fm_spark_amd.distributed import ShardedTrainer
 
@@ -309,7 +389,9 @@ def main():
         losses = tr.ctx.loss_history()
         assert os.environ.get("FM_ABLATE") or np.all(np.isfinite(losses)), "non-finite loss"
         U_mean = float(np.mean(uniques)) / world if uniques else 0.0  # rows one owner updates
-        parallelism = (f"row-sharded x{world}, owner-computes (RCCL all-to-all of entries, partial sums, S)" +
+        xg = exchange_bytes(host_batches[0], world, rank, (k + 3) // 4 * 4)
+        parallelism = (f"row-sharded x{world}, owner-computes, torch.distributed harness (RCCL all-to-all of entries, "
+                       f"partial sums, S)" +
                        (", next batch routed, exchanged and slot-sorted during the current step" if prefetch else ""))
 
     if sharded:
@@ -360,6 +442,14 @@ def main():
             line["step_roofline"] = {"bytes_per_step": step_bytes,
                                      "achieved_GBs": step_bytes / (ms_per_step * 1e-3) / 1e9,
                                      "frac": step_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS}
+        if sharded:
+            step_s = (median_ms or ms_per_step) * 1e-3
+            egress = xg["entries_B"] + xg["s_rows_B"] + xg["partials_B"]
+            line["exchange"] = dict(xg, per="rank 0, per iteration, egress (ingress alike by symmetry)",
+                                    egress_B=egress, egress_GBs_at_step_time=egress / step_s / 1e9,
+                                    xgmi_peak_GBs=XGMI_LINK_GBS * max(world - 1, 0),
+                                    xgmi_frac_at_step_time=(egress / step_s / 1e9 / (XGMI_LINK_GBS * (world - 1))
+                                                            if world > 1 else None))
         if host_path:
             line["host_path_ms_per_step"] = host_path["median_ms_per_step"]
             line["host_path"] = host_path

@@ -273,6 +273,9 @@ class FactorizationMachinesSGD:
         "minLabel": 0.0, "maxLabel": 1.0, "initialSd": 0.01,
         # not in the reference: the init draw is unseeded there; device / seed here
         "seed": 0, "device": 0, "numFeatures": None,
+        # not in the reference: the table over several GPUs of this process (include/fm_hip.h
+        # fm_config.parallel), in place of Spark's hash-partitioned model Datasets
+        "parallel": None, "nGpus": 1, "devices": None, "transport": "auto",
     }
 
     def __init__(self, uid: str | None = None):
@@ -301,6 +304,15 @@ class FactorizationMachinesSGD:
     def setInitialSd(self, v): return self._set("initialSd", float(v))
     def setSeed(self, v): return self._set("seed", int(v))
     def setNumFeatures(self, v): return self._set("numFeatures", int(v))
+
+    def setParallel(self, mode, n_gpus: int = 1, devices=None, transport: str = "auto"):
+        """Train (and transform) on n_gpus GPUs of this process: mode "sharded" splits the table's
+        rows by id % R (owner-computes), "replicated" keeps a copy per GPU (gradient all-reduce);
+        the mini-batches split by rows across the GPUs.  transport "copy" shares one device."""
+        self._set("parallel", mode)
+        self._set("nGpus", int(n_gpus))
+        self._set("devices", None if devices is None else [int(d) for d in devices])
+        return self._set("transport", transport)
 
     def getDimFactorization(self): return self._params["dimFactorization"]
     def getMaxIter(self): return self._params["maxIter"]
@@ -333,7 +345,8 @@ class FactorizationMachinesSGD:
         labels = np.asarray(dataset[p["labelCol"]], dtype=np.float64)
         rp, col, val = _explode(vectors)
         F = p["numFeatures"] or (int(col.max()) + 1 if len(col) else 1)
-        ctx = FMContext(F, k, device=p["device"], seed=p["seed"], init_sd=p["initialSd"], w0=0.0)
+        ctx = FMContext(F, k, device=p["device"], seed=p["seed"], init_sd=p["initialSd"], w0=0.0,
+                        parallel=p["parallel"], n_gpus=p["nGpus"], devices=p["devices"], transport=p["transport"])
         if initial_tables is not None:
             ctx.load_tables(*initial_tables)
         elif len(col):

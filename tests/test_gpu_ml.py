@@ -92,3 +92,33 @@ def test_fit_default_init_is_seeded_and_deterministic(gpu):
         outs.append(m._ctx.export_tables())
     for a, b in zip(*outs):
         assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("mode", ["sharded", "replicated"])
+def test_fit_and_transform_on_several_gpus(gpu, mode):
+    """fit + transform with the table spread over 3 ranks of one context (one GPU, COPY
+    transport): the same model and predictions as the single-table fit, through the same
+    estimator API (randomSplit replay, createInitialModel on the device, clamp on transform)."""
+    from fm_spark_amd.data import synthetic_batch
+    from fm_spark_amd.ml import DataFrame, FactorizationMachinesSGD
+
+    b = synthetic_batch(3000, 4000, batch_index=11)
+    vecs = [SparseVector(4000, b.col[b.row_ptr[i]:b.row_ptr[i + 1]], b.val[b.row_ptr[i]:b.row_ptr[i + 1]])
+            for i in range(b.n_rows)]
+    df = DataFrame({"label": [float(y) for y in b.label], "features": vecs}, [1000, 1000, 1000])
+
+    def est():
+        return (FactorizationMachinesSGD().setDimFactorization(8).setMaxIter(4).setStepSize(0.5).setRegParam(1e-5)
+                .setNumFeatures(4000).setSeed(9))
+
+    single = est().fit(df)
+    multi = est().setParallel(mode, n_gpus=3, devices=[0, 0, 0], transport="copy").fit(df)
+    i1, w1, V1 = single._ctx.export_tables()
+    i2, w2, V2 = multi._ctx.export_tables()
+    np.testing.assert_array_equal(i2, i1)
+    np.testing.assert_allclose(w2, w1, rtol=1e-5, atol=1e-8)
+    np.testing.assert_allclose(V2, V1, rtol=1e-5, atol=1e-8)
+    np.testing.assert_allclose(multi._ctx.loss_history(), single._ctx.loss_history(), rtol=1e-6)
+    p1 = [r["prediction"] for r in single.transform(df).collect()]
+    p2 = [r["prediction"] for r in multi.transform(df).collect()]
+    np.testing.assert_allclose(p2, p1, rtol=1e-5, atol=1e-7)

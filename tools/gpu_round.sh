@@ -18,6 +18,9 @@ run pytest_gpu 900 python -u -m pytest tests -m gpu -q -rf --timeout 120 --timeo
 rc=$?; if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
 run bench 600 python bench.py --steps "$STEPS" --warmup 3 ${BENCH_ARGS:-} || exit $?
+if [ "${SHARDED:-0}" = "1" ]; then
+  run bench_sharded 600 python bench.py --steps "$STEPS" --warmup 3 --force-sharded --no-cpu-baseline || exit $?
+fi
 if [ "${PROF:-0}" = "1" ]; then
   export TMPDIR=/tmp
   run rocprof 600 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/prof -o run \
