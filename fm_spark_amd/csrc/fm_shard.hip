@@ -464,16 +464,25 @@ int fm_shard_route(fm_ctx* ctx, fm_batch* b, void* send_slot, void* send_ent, in
       const int sb = bits_for(std::max<int64_t>((ctx->cfg.num_features - 1) / R, 1));
       const int ob = bits_for(drop ? R : R - 1);
       FM_REQUIRE(sb + ob <= 32, "route key does not fit 32 bits");
-      ctx->sh_pay.ensure(sizeof(uint2) * std::max<int64_t>(N, 4) + 16);
-      ctx->sh_skey.ensure(sizeof(uint32_t) * std::max<int64_t>(N, 4) + 16);
-      hipLaunchKernelGGL(k_route_keys, dim3(blocks_for(B * kTeamR)), dim3(kBlock), 0, st,
-                         b->dev.row_ptr.as<int64_t>(), b->dev.col.as<uint32_t>(), b->dev.ent.as<uint2>(), B,
-                         (uint32_t)R, sb, F, S.pairidx.as<int32_t>(), ctx->sh_okey.as<uint32_t>(),
-                         ctx->sh_pay.as<uint2>());
-      radix_sort_pairs64_bits(ctx->side_sort, ctx->sh_okey.as<uint32_t>(), ctx->sh_pay.as<uint2>(), N, sb, sb + ob, st,
-                              ctx->sh_skey.as<uint32_t>(), reinterpret_cast<uint2*>(send_ent));
-      hipLaunchKernelGGL(k_key_slots, dim3(blocks_for(N)), dim3(kBlock), 0, st, ctx->sh_skey.as<uint32_t>(), N,
-                         (uint32_t)((sb >= 32) ? 0xFFFFFFFFu : ((1u << sb) - 1u)), reinterpret_cast<uint32_t*>(send_slot));
+      if (R == 1 && !drop) {
+        // one owner: CSR order is already the owner order and the key is the slot -- the keys and
+        // payloads go straight to the send buffers, no partition pass
+        hipLaunchKernelGGL(k_route_keys, dim3(blocks_for(B * kTeamR)), dim3(kBlock), 0, st,
+                           b->dev.row_ptr.as<int64_t>(), b->dev.col.as<uint32_t>(), b->dev.ent.as<uint2>(), B,
+                           (uint32_t)R, sb, F, S.pairidx.as<int32_t>(), reinterpret_cast<uint32_t*>(send_slot),
+                           reinterpret_cast<uint2*>(send_ent));
+      } else {
+        ctx->sh_pay.ensure(sizeof(uint2) * std::max<int64_t>(N, 4) + 16);
+        ctx->sh_skey.ensure(sizeof(uint32_t) * std::max<int64_t>(N, 4) + 16);
+        hipLaunchKernelGGL(k_route_keys, dim3(blocks_for(B * kTeamR)), dim3(kBlock), 0, st,
+                           b->dev.row_ptr.as<int64_t>(), b->dev.col.as<uint32_t>(), b->dev.ent.as<uint2>(), B,
+                           (uint32_t)R, sb, F, S.pairidx.as<int32_t>(), ctx->sh_okey.as<uint32_t>(),
+                           ctx->sh_pay.as<uint2>());
+        radix_sort_pairs64_bits(ctx->side_sort, ctx->sh_okey.as<uint32_t>(), ctx->sh_pay.as<uint2>(), N, sb, sb + ob, st,
+                                ctx->sh_skey.as<uint32_t>(), reinterpret_cast<uint2*>(send_ent));
+        hipLaunchKernelGGL(k_key_slots, dim3(blocks_for(N)), dim3(kBlock), 0, st, ctx->sh_skey.as<uint32_t>(), N,
+                           (uint32_t)((sb >= 32) ? 0xFFFFFFFFu : ((1u << sb) - 1u)), reinterpret_cast<uint32_t*>(send_slot));
+      }
     }
     FM_HIP_CHECK(hipGetLastError());
     ctx->prof_end("route", e0, st);
