@@ -169,7 +169,7 @@ fm_batch* host_batch(fm_ctx* ctx) {
 void reserve_work(fm_ctx* ctx, int64_t B, int64_t N) {
   StepWork& w = ctx->work;
   w.S.ensure(sizeof(float) * (size_t)std::max<int64_t>(B, 1) * ctx->kp);
-  w.yl.ensure(sizeof(double2) * (size_t)std::max<int64_t>(B, 1));
+  w.yl.ensure(sizeof(float2) * (size_t)std::max<int64_t>(B, 1));
   w.sort.ensure(std::max<int64_t>(N, 1));
   const int64_t nranges = (N + 255) / 256;  // update waves (fm_kernels.hip, kWaveEnt)
   w.part.ensure(sizeof(double) * (size_t)std::max<int64_t>(nranges, 1) * 2 * (ctx->kp + 2));
@@ -232,10 +232,24 @@ int step_impl(fm_ctx* ctx, fm_batch* b, int32_t t, double step_size, double reg_
   launch_forward(T, b->dev, ctx->work, p, ctx->stream, &nfwd);
   ctx->prof_end("forward", e0, ctx->stream);
   FM_HIP_CHECK(hipStreamWaitEvent(ctx->stream, prepared ? b->ready : ctx->ev_join, 0));
+#ifndef FM_SORT_GATE
+#define FM_SORT_GATE 0
+#endif
+  if (FM_SORT_GATE && prepared) {
+    // experiment: the update waits for whatever the side stream holds now (the next batch's sort,
+    // enqueued before this step), so that sort overlaps the forward and the update runs alone
+    FM_HIP_CHECK(hipEventRecord(ctx->ev_join, ctx->side));
+    FM_HIP_CHECK(hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));
+  }
   e0 = ctx->prof_begin(ctx->stream);
   double* stats = ctx->loss_hist.as<double>() + 3 * (int64_t)ctx->epoch;
   launch_segment_update(T, b->dev, ctx->work, p, skeys, sents, nfwd, stats, ctx->stream, emit);
-  FM_HIP_CHECK(hipEventRecord(ctx->ev_upd_done, ctx->stream));
+#ifndef FM_PREP_EAGER
+#define FM_PREP_EAGER 1
+#endif
+  // the shared sort workspace is read by the main stream only when the batch was sorted inline
+  // (not prepared): only then must the next fm_batch_prepare's sort wait for this update
+  if (!prepared || !FM_PREP_EAGER) FM_HIP_CHECK(hipEventRecord(ctx->ev_upd_done, ctx->stream));
   if (prepared) {
     FM_HIP_CHECK(hipEventRecord(b->last_use, ctx->stream));
     b->prepared = false;

@@ -132,7 +132,7 @@ struct fm_ctx {
   hipStream_t side = nullptr;  // the entry sort runs here, overlapped with the forward
   hipStream_t side_own = nullptr;  // the context's own side stream (fm_set_side_stream may replace side)
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-  hipEvent_t ev_upd_done = nullptr;  // last main-stream read of the shared sort workspace
+  hipEvent_t ev_upd_done = nullptr;  // last main-stream read of the shared sort workspace (an inline-sorted step)
   DevBuf rec;  // [rows * stride] float records (V row + header)
   int32_t stride = 0;
   std::vector<double> cum_host{0.0};  // cum[e] = sum of lambda over executed steps 1..e

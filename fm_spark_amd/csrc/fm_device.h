@@ -6,6 +6,28 @@
 
 namespace fmhip {
 
+// Cache-policy switches (experiments; 0 = plain accesses): FM_NT_ROWS nontemporal stores of the
+// update's row write-back, FM_NT_ENT nontemporal loads of the update's sorted entry stream,
+// FM_NT_SORT nontemporal stores of the sort's scatter.
+#ifndef FM_NT_ROWS
+#define FM_NT_ROWS 0
+#endif
+#ifndef FM_NT_ENT
+#define FM_NT_ENT 0
+#endif
+#ifndef FM_NT_SORT
+#define FM_NT_SORT 0
+#endif
+typedef float fm_f4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void st_row4(float* p, float4 v) {
+#if FM_NT_ROWS
+  __builtin_nontemporal_store(fm_f4v{v.x, v.y, v.z, v.w}, reinterpret_cast<fm_f4v*>(p));
+#else
+  *reinterpret_cast<float4*>(p) = v;
+#endif
+}
+
 __device__ __forceinline__ float shrink_f(float z, double a) {
   // signum(z) * max(0, |z| - a) (FactorizationMachinesSGD.scala:104, :179), in fp64.
   const double az = fabs((double)z) - a;

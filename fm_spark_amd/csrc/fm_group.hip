@@ -176,6 +176,24 @@ void barrier(Group& g, bool side) {
 void a2a(Group& g, bool side, const std::vector<const char*>& send, const std::vector<char*>& recv,
          const std::vector<const int64_t*>& out, const std::vector<const int64_t*>& in, size_t esize) {
   if (g.rccl) {
+    // the block a rank keeps for itself is a device copy on its own stream, not a send to itself
+    // through RCCL's channel buffers
+    for (int l = 0; l < g.L; ++l) {
+      Rank& r = g.ranks[l];
+      const int me = r.global;
+      size_t so = 0, ro = 0;
+      for (int p = 0; p < me; ++p) {
+        so += (size_t)out[l][p] * esize;
+        ro += (size_t)in[l][p] * esize;
+      }
+      const size_t bytes = (size_t)out[l][me] * esize;
+      FM_REQUIRE(bytes == (size_t)in[l][me] * esize, "a2a: the self block differs between send and receive");
+      if (bytes) {
+        FM_HIP_CHECK(hipSetDevice(r.device));
+        FM_HIP_CHECK(hipMemcpyAsync(recv[l] + ro, send[l] + so, bytes, hipMemcpyDeviceToDevice, r.stream(side)));
+      }
+    }
+    if (g.R == 1) return;
     FM_RCCL_CHECK(ncclGroupStart());
     for (int l = 0; l < g.L; ++l) {
       Rank& r = g.ranks[l];
@@ -183,8 +201,10 @@ void a2a(Group& g, bool side, const std::vector<const char*>& send, const std::v
       size_t so = 0, ro = 0;
       for (int p = 0; p < g.R; ++p) {
         const size_t sb = (size_t)out[l][p] * esize, rb = (size_t)in[l][p] * esize;
-        if (sb) FM_RCCL_CHECK(ncclSend(send[l] + so, sb, ncclChar, p, r.comm(side), r.stream(side)));
-        if (rb) FM_RCCL_CHECK(ncclRecv(recv[l] + ro, rb, ncclChar, p, r.comm(side), r.stream(side)));
+        if (p != r.global) {
+          if (sb) FM_RCCL_CHECK(ncclSend(send[l] + so, sb, ncclChar, p, r.comm(side), r.stream(side)));
+          if (rb) FM_RCCL_CHECK(ncclRecv(recv[l] + ro, rb, ncclChar, p, r.comm(side), r.stream(side)));
+        }
         so += sb;
         ro += rb;
       }
@@ -353,7 +373,7 @@ void prefetch(Group& g, GroupBatch& gb) {
   gb.prefetched = true;
 }
 
-// the pair buffers of one direction in the wire layout: [P][kp] fp32 vectors, then [P][2] fp64
+// the pair buffers of one direction in the wire layout: [P][kp] fp32 vectors, then [P][2] fp32
 // scalars -- two all-to-alls with the same pair counts
 void a2a_pairs(Group& g, int kp, const std::vector<DevBuf*>& send, const std::vector<int64_t>& sendP,
                const std::vector<DevBuf*>& recv, const std::vector<int64_t>& recvP,
@@ -368,7 +388,7 @@ void a2a_pairs(Group& g, int kp, const std::vector<DevBuf*>& send, const std::ve
     rc[l] = recv[l]->as<char>() + sizeof(float) * recvP[l] * kp;
   }
   a2a(g, false, sv, rv, out, in, sizeof(float) * kp);
-  a2a(g, false, sc, rc, out, in, sizeof(double) * 2);
+  a2a(g, false, sc, rc, out, in, sizeof(float) * 2);
 }
 
 // per-step stats rows of the members (loss, loss rows, distinct ids) at epoch index e -> the job's
@@ -413,7 +433,7 @@ void fill_out(Group& g, fm_ctx* ctx, int64_t e, int64_t global_rows, fm_step_out
 
 int step_sharded(fm_ctx* ctx, Group& g, GroupBatch& gb, int32_t t, double step_size, double reg_param,
                  fm_step_out* out) {
-  const int L = g.L, kp = ctx->kp, W = kp + 4;
+  const int L = g.L, kp = ctx->kp, W = kp + 2;
   prefetch(g, gb);
   std::vector<int64_t> Pin(L), Pout(L);
   std::vector<DevBuf*> parts(L), part_in(L), s_send(L), s_recv(L);
@@ -515,7 +535,7 @@ int step_group_batch(fm_ctx* ctx, GroupBatch& gb, int32_t t, double step_size, d
 // dropped) -> entries to the owners -> owner partial sums with present counts -> back ->
 // predict epilogue per sample.  pred: host [gb.rows].
 void predict_sharded(fm_ctx* ctx, Group& g, GroupBatch& gb, double lo, double hi, double* pred) {
-  const int L = g.L, kp = ctx->kp, W = kp + 4;
+  const int L = g.L, kp = ctx->kp, W = kp + 2;
   gb.prefetched = false;  // the route below replaces any pending training plan of this batch
   prefetch(g, gb);
   gb.prefetched = false;

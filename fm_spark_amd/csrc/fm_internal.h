@@ -115,7 +115,7 @@ struct BatchDev {
 
 struct StepWork {
   DevBuf S;         // [B * kp] float: per-sample vfxiSum
-  DevBuf yl;        // [B] double2 {yhat, y} (fp64: r = yhat - y enters every gradient)
+  DevBuf yl;        // [B] float2 {r, yhat}: r = yhat - y formed in fp64 from the fp64 label, then rounded
   DevBuf loss_part; // [n_fwd_blocks] double2 {loss, n_loss}
   DevBuf part;      // [ceil(N / 256) * 2 * (kp+2)] double partial gradients (one range per update wave)
   DevBuf ucnt;      // [n_update_blocks] uint32 distinct-id counts per block
@@ -148,7 +148,7 @@ struct FwdOut {
   uint32_t* pcount = nullptr;  // partial pass (sharded predict): present rows per pair
 };
 // partial_out != nullptr: the sharded owner's partial pass (fm_shard.hip): [pairs][kp] fp32 vectors
-// followed by [pairs] double2 scalars (pred->pcount, if given: present rows per pair);
+// followed by [pairs] float2 scalars (pred->pcount, if given: present rows per pair);
 // else pred != nullptr: FactorizationMachinesModel.predict / calcLossGrad (p.w0, p.cumE used)
 void launch_forward(const TableView& T, const BatchDev& b, StepWork& w, const StepParams& p,
                     hipStream_t st, int64_t* n_fwd_blocks, float* partial_out = nullptr,
@@ -157,7 +157,7 @@ void launch_forward(const TableView& T, const BatchDev& b, StepWork& w, const St
 struct SegSource {
   const float* S;
   int64_t s_stride;
-  const double2* yl;
+  const float2* yl;
   int64_t yl_stride;
 };
 // emit != nullptr (replicated mode): the per-slot gradient sums go to emit[rows][kp + 4] as

@@ -106,7 +106,7 @@ __global__ __launch_bounds__(kBlock, FM_FWD_MINW) void k_forward(TableView T, co
                                                     const uint2* __restrict__ ent,
                                                     const double* __restrict__ label, int64_t B,
                                                     double w0, double cumE, float* __restrict__ S_out,
-                                                    double2* __restrict__ yl_out, double2* __restrict__ loss_part,
+                                                    float2* __restrict__ yl_out, double2* __restrict__ loss_part,
                                                     FwdOut xo) {
   constexpr bool PARTIAL = MODE == kPartial;
   constexpr int RPP = TEAM / GS;  // entries per pass
@@ -179,7 +179,7 @@ __global__ __launch_bounds__(kBlock, FM_FWD_MINW) void k_forward(TableView T, co
       if (rs == 0 && qok)
         *reinterpret_cast<float4*>(S_out + s * kp + g * 4) = make_float4((float)a0, (float)a1, (float)a2, (float)a3);
       if (tl == 0) {
-        yl_out[s] = make_double2(vv, wx);
+        yl_out[s] = make_float2((float)vv, (float)wx);
         if (xo.pcount) xo.pcount[s] = npres;
       }
       continue;
@@ -222,7 +222,8 @@ __global__ __launch_bounds__(kBlock, FM_FWD_MINW) void k_forward(TableView T, co
       *reinterpret_cast<float4*>(S_out + s * kp + g * 4) = make_float4((float)a0, (float)a1, (float)a2, (float)a3);
     if (tl == 0) {
       const double y = label[s];
-      yl_out[s] = make_double2(yhat, y);
+      // r = pred - label in fp64 (SGD.scala:146), rounded once: relative error 2^-24 of r itself
+      yl_out[s] = make_float2((float)(yhat - y), (float)yhat);
       if (e1 > e0) {
         const double d = yhat - y;
         loss_acc += d * d;  // pow(pred - label, 2.0), Model.scala:230
@@ -260,7 +261,7 @@ struct SegArgs {
   const uint2* sents;     // their entries {sample, x bits}, same order
   int64_t N;
   const float* S;    // per-sample rows of s_stride floats (vfxiSum first)
-  const double2* yl;  // {yhat, y} of sample s at yl[s * yl_stride] (fp64)
+  const float2* yl;  // {r = yhat - y, yhat} of sample s at yl[s * yl_stride]
   int64_t s_stride;
   int64_t yl_stride;
   double* part;      // [nranges][2][kp + 2] = [sum g_w | sum S*x*r (kp) | sum x*x*r]
@@ -340,12 +341,22 @@ __global__ __launch_bounds__(kBlock) void k_segment_update(SegArgs a) {
     for (int i = 0; i < NP; ++i) {
       const int64_t p = base + i * 64 + lane;
       const bool v = p < a.N;
+#if FM_NT_ENT
+      key[i] = v ? __builtin_nontemporal_load(a.skeys + p) : kNone;
+      if (v) {
+        const unsigned long long q = __builtin_nontemporal_load(reinterpret_cast<const unsigned long long*>(a.sents) + p);
+        en[i] = make_uint2((uint32_t)q, (uint32_t)(q >> 32));
+      } else {
+        en[i] = make_uint2(0u, 0u);
+      }
+#else
       key[i] = v ? a.skeys[p] : kNone;
       en[i] = v ? a.sents[p] : make_uint2(0u, 0u);
+#endif
     }
     const uint32_t before = base > 0 ? a.skeys[base - 1] : kNone;
     const uint32_t after = base + kWaveEnt < a.N ? a.skeys[base + kWaveEnt] : kNone;
-    double2 yl[NP];
+    float2 yl[NP];
 #pragma unroll
     for (int i = 0; i < NP; ++i) {
       const uint32_t up = __shfl_up(key[i], 1);
@@ -361,7 +372,7 @@ __global__ __launch_bounds__(kBlock) void k_segment_update(SegArgs a) {
       const int l = li(i * 64 + lane);
       img_k[l] = make_uint2(key[i], (valid ? kFValid : 0u) | (end ? kFEnd : 0u) | (st ? kFStart : 0u));
       img_s[l] = (int)en[i].x;
-      yl[i] = valid ? a.yl[(int64_t)en[i].x * a.yl_stride] : make_double2(0.0, 0.0);
+      yl[i] = valid ? a.yl[(int64_t)en[i].x * a.yl_stride] : make_float2(0.f, 0.f);
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -395,10 +406,10 @@ __global__ __launch_bounds__(kBlock) void k_segment_update(SegArgs a) {
     for (int i = 0; i < NP; ++i) {
       const int l = li(i * 64 + lane);
       const double xd = (double)__uint_as_float(en[i].y);
-      const double yh = yl[i].x, yy = yl[i].y;
-      const double rj = yh - yy;
+      const double rj = (double)yl[i].x, yh = (double)yl[i].y;
       img_d[l] = make_double2(xd * rj, (xd * xd) * rj);
-      img_w[l] = xd * yh - yy;  // g_w = deltaWi * pred - label (SGD.scala:145)
+      // g_w = deltaWi * pred - label = x yhat - (yhat - r) (SGD.scala:145)
+      img_w[l] = (xd - 1.0) * yh + rj;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -426,7 +437,7 @@ __global__ __launch_bounds__(kBlock) void k_segment_update(SegArgs a) {
           // vec' = S_lambda(vec - sum * (eta / m))  (SGD.scala:153, :179)
           const float4 u = make_float4((float)fma(g0, -a.p.scale_v, (double)v.x), (float)fma(g1, -a.p.scale_v, (double)v.y),
                                        (float)fma(g2, -a.p.scale_v, (double)v.z), (float)fma(g3, -a.p.scale_v, (double)v.w));
-          *reinterpret_cast<float4*>(rec + c) = shrink4f(u, lamf);
+          st_row4(rec + c, shrink4f(u, lamf));
         }
       }
       if (a.emit) {
@@ -444,7 +455,7 @@ __global__ __launch_bounds__(kBlock) void k_segment_update(SegArgs a) {
           o.cum = a.p.cum_next;
           hv = *reinterpret_cast<const float4*>(&o);
         }
-        *reinterpret_cast<float4*>(rec + kp + i) = hv;
+        st_row4(rec + kp + i, hv);
       }
     };
 
@@ -997,10 +1008,10 @@ void launch_fwd_t(const TableView& T, const BatchDev& b, StepWork& w, const Step
   *nblk = blocks;
   const dim3 grid((unsigned)blocks), blk(kBlock);
   const FwdOut none{};
-  if (partial_out) {  // [n_rows][kp] fp32 vectors, then [n_rows] double2 scalars (xo: the present counts)
+  if (partial_out) {  // [n_rows][kp] fp32 vectors, then [n_rows] float2 scalars (xo: the present counts)
     hipLaunchKernelGGL((k_forward<GS, TEAM, kPartial, U>), grid, blk, 0, st, T, b.row_ptr.as<int64_t>(),
                        b.col.as<uint32_t>(), b.ent.as<uint2>(), nullptr, b.n_rows, p.w0, p.cumE, partial_out,
-                       reinterpret_cast<double2*>(partial_out + b.n_rows * T.kp), nullptr, xo ? *xo : none);
+                       reinterpret_cast<float2*>(partial_out + b.n_rows * T.kp), nullptr, xo ? *xo : none);
     return;
   }
   if (xo && xo->mode == kPredict) {
@@ -1018,7 +1029,7 @@ void launch_fwd_t(const TableView& T, const BatchDev& b, StepWork& w, const Step
   w.loss_part.ensure(sizeof(double2) * blocks);
   hipLaunchKernelGGL((k_forward<GS, TEAM, kTrain, U>), grid, blk, 0, st, T, b.row_ptr.as<int64_t>(),
                      b.col.as<uint32_t>(), b.ent.as<uint2>(), b.label.as<double>(), b.n_rows, p.w0, p.cumE,
-                     w.S.as<float>(), w.yl.as<double2>(), w.loss_part.as<double2>(), none);
+                     w.S.as<float>(), w.yl.as<float2>(), w.loss_part.as<double2>(), none);
 }
 
 }  // namespace
@@ -1064,7 +1075,7 @@ void launch_forward(const TableView& T, const BatchDev& b, StepWork& w, const St
 void launch_segment_update(const TableView& T, const BatchDev& b, StepWork& w, const StepParams& p,
                            const uint32_t* skeys, const uint2* sents, int64_t n_fwd_blocks,
                            double* stats_out, hipStream_t st, float* emit) {
-  SegSource src{w.S.as<float>(), T.kp, w.yl.as<double2>(), 1};
+  SegSource src{w.S.as<float>(), T.kp, w.yl.as<float2>(), 1};
   launch_segment_update(T, b.nnz, src, w, p, skeys, sents, n_fwd_blocks, stats_out, st, emit);
 }
 

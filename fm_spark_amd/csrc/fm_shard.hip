@@ -26,12 +26,12 @@
 // sums are split per owner (fp32 on the wire), the per-feature gradient sums run over the
 // same entries in the same order.  Deterministic for a given R.
 // Traffic per rank and step (k = 16, z = 39, R = 8): entries 12 B each (off the critical path:
-// exchanged during the previous iteration), partials and S (kp + 4) * 4 B per (sample, owner)
+// exchanged during the previous iteration), partials and S (kp + 2) * 4 B per (sample, owner)
 // pair -- about 2 x 150 MB, against about 1 GB when rows and gradients of every distinct id
 // travel instead.
 // Wire buffers are structures of arrays over the pairs, so every k-vector is 16-B aligned and a
-// 64-B row at k = 16: partials [P][kp] fp32 sum v*x then [P] fp64 {sum v^2 x^2, sum w x}; S [P][kp]
-// fp32 vfxiSum then [P] fp64 {yhat, y}.
+// 64-B row at k = 16: partials [P][kp] fp32 sum v*x then [P] fp32 {sum v^2 x^2, sum w x}; S [P][kp]
+// fp32 vfxiSum then [P] fp32 {r, yhat} (r = yhat - y formed in fp64 by the requester, then rounded).
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
@@ -225,9 +225,9 @@ template <int GS>
 __global__ __launch_bounds__(kBlock) void k_shard_combine(const int32_t* __restrict__ pairidx,
                                                           const int64_t* __restrict__ poff, int R, int64_t B,
                                                           const float* __restrict__ part_vec,
-                                                          const double2* __restrict__ part_sc,
+                                                          const float2* __restrict__ part_sc,
                                                           const double* __restrict__ label, int kp, double w0,
-                                                          float* __restrict__ s_vec, double2* __restrict__ s_sc,
+                                                          float* __restrict__ s_vec, float2* __restrict__ s_sc,
                                                           double2* __restrict__ loss_part) {
   constexpr int TPB = kBlock / GS;
   const int tid = threadIdx.x, g = tid % GS;
@@ -240,9 +240,9 @@ __global__ __launch_bounds__(kBlock) void k_shard_combine(const int32_t* __restr
     for (int o = 0; o < R; ++o) {
       const int32_t ix = pi[o];
       if (ix >= 0) {
-        const double2 t = part_sc[poff[o] + ix];
-        vv += t.x;
-        wx += t.y;
+        const float2 t = part_sc[poff[o] + ix];
+        vv += (double)t.x;
+        wx += (double)t.y;
         any = true;
       }
     }
@@ -272,7 +272,7 @@ __global__ __launch_bounds__(kBlock) void k_shard_combine(const int32_t* __restr
       const double y = label[s];
       for (int o = 0; o < R; ++o) {
         const int32_t ix = pi[o];
-        if (ix >= 0) s_sc[poff[o] + ix] = make_double2(yhat, y);
+        if (ix >= 0) s_sc[poff[o] + ix] = make_float2((float)(yhat - y), (float)yhat);  // {r, yhat}
       }
       if (any) {
         const double d = yhat - y;
@@ -310,7 +310,7 @@ template <int GS>
 __global__ __launch_bounds__(kBlock) void k_shard_predict(const int32_t* __restrict__ pairidx,
                                                           const int64_t* __restrict__ poff, int R, int64_t B,
                                                           const float* __restrict__ part_vec,
-                                                          const double2* __restrict__ part_sc,
+                                                          const float2* __restrict__ part_sc,
                                                           const uint32_t* __restrict__ pcnt, int kp, double w0,
                                                           double lo, double hi, double* __restrict__ pred) {
   constexpr int TPB = kBlock / GS;
@@ -323,9 +323,9 @@ __global__ __launch_bounds__(kBlock) void k_shard_predict(const int32_t* __restr
     for (int o = 0; o < R; ++o) {
       const int32_t ix = pi[o];
       if (ix >= 0) {
-        const double2 t = part_sc[poff[o] + ix];
-        vv += t.x;
-        wx += t.y;
+        const float2 t = part_sc[poff[o] + ix];
+        vv += (double)t.x;
+        wx += (double)t.y;
         cnt += pcnt[poff[o] + ix];
       }
     }
@@ -619,7 +619,7 @@ void shard_combine_predict(fm_ctx* ctx, fm_batch* b, const void* partials_in, co
   int64_t blocks = std::max<int64_t>((B + kBlock / GS - 1) / (kBlock / GS), 1);
   if (blocks > 256 * 8) blocks = 256 * 8;
   const float* pv = reinterpret_cast<const float*>(partials_in);
-  const double2* ps = reinterpret_cast<const double2*>(pv ? pv + Ps * kp : nullptr);
+  const float2* ps = reinterpret_cast<const float2*>(pv ? pv + Ps * kp : nullptr);
   const int32_t* pi = S.pairidx.as<int32_t>();
   const int64_t* poff = S.poff.as<int64_t>();
   const double w0 = ctx->cfg.w0;
@@ -661,9 +661,9 @@ int fm_shard_combine(fm_ctx* ctx, fm_batch* b, const void* partials_in, void* s_
     const int64_t* poff = S.poff.as<int64_t>();
     const int kp = ctx->kp;
     const float* pin = reinterpret_cast<const float*>(partials_in);
-    const double2* psc = reinterpret_cast<const double2*>(pin ? pin + Ps * kp : nullptr);
+    const float2* psc = reinterpret_cast<const float2*>(pin ? pin + Ps * kp : nullptr);
     float* so = reinterpret_cast<float*>(s_send);
-    double2* ssc = reinterpret_cast<double2*>(so ? so + Ps * kp : nullptr);
+    float2* ssc = reinterpret_cast<float2*>(so ? so + Ps * kp : nullptr);
     const double* lab = b->dev.label.as<double>();
     double2* lp = ctx->work.loss_part.as<double2>();
     const double w0 = ctx->cfg.w0;
@@ -701,7 +701,7 @@ int fm_shard_owner_update(fm_ctx* ctx, fm_batch* b, const void* s_recv, int32_t 
     FM_HIP_CHECK(hipStreamWaitEvent(st, S.ready_upd, 0));
     hipEvent_t e0 = ctx->prof_begin(st);
     const float* Srow = reinterpret_cast<const float*>(s_recv);  // [P][kp] S, then [P] {yhat, y}
-    SegSource src{Srow, ctx->kp, reinterpret_cast<const double2*>(Srow ? Srow + S.P * ctx->kp : nullptr), 1};
+    SegSource src{Srow, ctx->kp, reinterpret_cast<const float2*>(Srow ? Srow + S.P * ctx->kp : nullptr), 1};
     launch_segment_update(ctx->view(), n, src, ctx->work, p, S.skeys.as<uint32_t>(), S.sents.as<uint2>(),
                           S.loss_blocks, stats, st);
     ctx->prof_end("owner_update", e0, st);

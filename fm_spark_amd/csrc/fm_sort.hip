@@ -266,8 +266,20 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint32_t* __rest
     const uint32_t key = s_keys[j];
     const uint32_t d = (key >> shift) & M;
     const uint32_t dest = glob_off[d] + (uint32_t)j - tile_start[d];
+#if FM_NT_SORT
+    __builtin_nontemporal_store(key, keys_out + dest);
+    if constexpr (sizeof(P) == 8) {
+      const uint2 v = *reinterpret_cast<const uint2*>(&s_vals[j]);
+      __builtin_nontemporal_store((unsigned long long)v.x | ((unsigned long long)v.y << 32),
+                                  reinterpret_cast<unsigned long long*>(vals_out) + dest);
+    } else {
+      __builtin_nontemporal_store(*reinterpret_cast<const uint32_t*>(&s_vals[j]),
+                                  reinterpret_cast<uint32_t*>(vals_out) + dest);
+    }
+#else
     keys_out[dest] = key;
     vals_out[dest] = s_vals[j];
+#endif
   }
 }
 

@@ -20,7 +20,7 @@ so the next routing, entry exchange and slot sort overlap the current update.
 Every rank steps its own mini-batch; the iteration's miniBatchSize is the sum over ranks
 (weak scaling: the global batch grows with R).  The result equals one single-table step over
 the ranks' batches concatenated in rank order, up to fp summation order (deterministic for a
-given R).  Only entries (12 B) and twice kp + 4 words per (sample, owner) pair cross xGMI
+given R).  Only entries (12 B) and twice kp + 2 words per (sample, owner) pair cross xGMI
 -- no table row or per-id gradient does.
 """
 
@@ -56,7 +56,7 @@ class HipShardEngine:
         N.check(self._lib.fm_set_side_stream(self.ctx.handle, C.c_void_p(self.side_stream.cuda_stream)),
                 "fm_set_side_stream")
         self.kp = (k + 3) // 4 * 4
-        self.width = self.kp + 4  # 4-B words per pair on the wire: [P][kp] fp32 vectors, then [P] fp64 x 2 scalars
+        self.width = self.kp + 2  # fp32 words per pair on the wire: [P][kp] vectors, then [P][2] scalars
 
     def _empty(self, n, dtype):
         return self.torch.empty(max(int(n), 1), dtype=dtype, device=self.device)[: int(n)]
@@ -199,12 +199,12 @@ class ShardedTrainer:
         return self.torch.empty(max(int(n), 1), dtype=dtype, device=self.device)[: int(n)]
 
     def _a2a_pairs(self, out, inp, out_pairs, in_pairs):
-        """All-to-all of a pair buffer in the wire layout (include/fm_hip.h): the [P][kp] fp32 vector
-        section, then the [P][2] fp64 scalar section (4 words per pair), each with its own splits."""
+        """All-to-all of a pair buffer in the wire layout (include/fm_hip.h): the [P][kp] vector section,
+        then the [P][2] scalar section, each exchanged with its own splits."""
         kp = self.engine.kp
         po, pi = int(np.sum(out_pairs)), int(np.sum(in_pairs))
         self._a2a(out[: po * kp], inp[: pi * kp], out_pairs * kp, in_pairs * kp)
-        self._a2a(out[po * kp:], inp[pi * kp:], out_pairs * 4, in_pairs * 4)
+        self._a2a(out[po * kp:], inp[pi * kp:], out_pairs * 2, in_pairs * 2)
 
     def _side(self):
         side = getattr(self.engine, "side", None)

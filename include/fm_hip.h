@@ -261,10 +261,11 @@ int fm_xorshift_next_doubles(int64_t seed, int64_t n, double* out);
  * feature-keyed shuffles S1/S2/S5/S6 and the per-sample window of the reference plan
  * (Model.scala:155-164, :191, SGD.scala:148-166).
  * A "pair" is (sample of a source rank, owner holding some of its entries).  Wire buffers are fp32
- * structures of arrays over P pairs, kp + 4 four-byte words per pair (kp = roundup(k, 4)):
- *   partials = [P][kp] fp32 sum v*x, then [P][2] fp64 {sum v^2 x^2, sum w*x}
- *   S        = [P][kp] fp32 vfxiSum, then [P][2] fp64 {yhat, y}  (the residual yhat - y is formed
- *              in fp64 from the fp64 label, as the reference's Double column, SGD.scala:145-146)
+ * structures of arrays over P pairs, kp + 2 fp32 words per pair (kp = roundup(k, 4)):
+ *   partials = [P][kp] sum v*x, then [P][2] {sum v^2 x^2, sum w*x}
+ *   S        = [P][kp] vfxiSum, then [P][2] {r, yhat}  (the residual r = yhat - y is formed in fp64
+ *              from the fp64 label, as the reference's Double column, SGD.scala:145-146, and rounded
+ *              once; the owner forms g_w = x*yhat - y as (x - 1)*yhat + r)
  * so the exchange is two all-to-alls per direction (the vector section, the scalar section).
  * Every phase is keyed by `batch`, this rank's mini-batch of the iteration; its state lives with
  * the batch.  Phases 1 and 1b depend on the batch alone and run on the side stream

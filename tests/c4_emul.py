@@ -82,7 +82,7 @@ def route_to(tb: TBatch, o: int):
 
 def owner_partial_emul(tb: TBatch, o: int, k: int, kp: int):
     """Owner o's partial forward sums (as fm_shard_owner_forward writes them) over the rows of
-    `other_rows_t`: vec [P][kp] fp32 = sum v x, sc [P][2] fp64 = {sum v^2 x^2, sum w x}."""
+    `other_rows_t`: vec [P][kp] = sum v x, sc [P][2] = {sum v^2 x^2, sum w x}, fp32 on the wire."""
     _, _, has, pair_of, m = route_to(tb, o)
     P = int(has.sum())
     ids, x, s = tb.ids[m], tb.x32[m].to(torch.float64), tb.sample[m]
@@ -95,19 +95,17 @@ def owner_partial_emul(tb: TBatch, o: int, k: int, kp: int):
     sc = torch.zeros(P, 2, dtype=torch.float64, device=ids.device)
     sc[:, 0].index_add_(0, pidx, (V * V).sum(1) * x * x)
     sc[:, 1].index_add_(0, pidx, w * x)
-    return vec.to(torch.float32), sc, has, pair_of
+    return vec.to(torch.float32), sc.to(torch.float32), has, pair_of
 
 
 def wire(vec: torch.Tensor, sc: torch.Tensor) -> torch.Tensor:
-    """[P][kp] fp32 + [P][2] fp64 -> the flat fp32-word wire layout (include/fm_hip.h)."""
-    return torch.cat([vec.reshape(-1), sc.contiguous().reshape(-1).view(torch.float32)])
+    """[P][kp] + [P][2] -> the flat fp32 wire layout (include/fm_hip.h)."""
+    return torch.cat([vec.reshape(-1), sc.to(torch.float32).contiguous().reshape(-1)])
 
 
 def unwire(buf: torch.Tensor, kp: int):
-    P = buf.numel() // (kp + 4)
-    vec = buf[: P * kp].reshape(P, kp)
-    sc = buf[P * kp:].contiguous().view(torch.float64).reshape(P, 2)
-    return vec, sc
+    P = buf.numel() // (kp + 2)
+    return buf[: P * kp].reshape(P, kp), buf[P * kp:].reshape(P, 2)
 
 
 def combine_emul(tb: TBatch, parts, kp: int, w0: float = 0.0):
@@ -120,8 +118,8 @@ def combine_emul(tb: TBatch, parts, kp: int, w0: float = 0.0):
     for vec, sc, has, pair_of in parts:
         idx = pair_of[has]
         S[has] += vec[idx].to(torch.float64)
-        vv[has] += sc[idx, 0]
-        wx[has] += sc[idx, 1]
+        vv[has] += sc[idx, 0].to(torch.float64)
+        wx[has] += sc[idx, 1].to(torch.float64)
     yhat = 0.5 * ((S * S).sum(1) - vv) + wx + w0
     return S, yhat
 
@@ -157,7 +155,7 @@ def run_iteration(eng, b0_dev, tbs, t, step_size, reg_param, check_route=True):
         parts = [mine] + [owner_partial_emul(tb, o, k, kp) for o in range(1, R)]
         if r == 0:  # rank 0 combines its own batch on the device
             pin = torch.cat([torch.cat([p[0].reshape(-1) for p in parts]),
-                             torch.cat([p[1].contiguous().reshape(-1).view(torch.float32) for p in parts])])
+                             torch.cat([p[1].contiguous().reshape(-1) for p in parts])])
             s_send = eng.combine(b0_dev, pin, int(sum(int(p[2].sum()) for p in parts)))
             v_all, c_all = unwire(s_send, kp)
             p0 = int(routes[0][2].sum())
@@ -169,7 +167,7 @@ def run_iteration(eng, b0_dev, tbs, t, step_size, reg_param, check_route=True):
             S, yhat = combine_emul(tb, parts, kp)
             has = routes[r][2]
             s_vec.append(S[has].to(torch.float32))
-            s_sc.append(torch.stack([yhat[has], tb.label[has]], dim=1))
+            s_sc.append(torch.stack([yhat[has] - tb.label[has], yhat[has]], dim=1).to(torch.float32))
     s_recv = wire(torch.cat(s_vec), torch.cat(s_sc))
     gm = sum(tb.B for tb in tbs)
     eng.owner_update(b0_dev, s_recv, t, step_size, reg_param, gm)

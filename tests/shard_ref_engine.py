@@ -10,17 +10,14 @@ import torch
 
 
 def rows_to_soa(rows, kp):
-    """[P][kp + 2] rows -> the wire layout (flat fp32 words): [P][kp] fp32 vectors, then [P][2]
-    fp64 scalars (each 2 words)."""
-    vec = np.asarray(rows[:, :kp], dtype=np.float32).reshape(-1)
-    sc = np.ascontiguousarray(np.asarray(rows[:, kp:kp + 2], dtype=np.float64)).reshape(-1).view(np.float32)
-    return np.ascontiguousarray(np.concatenate([vec, sc]))
+    """[P][kp + 2] rows -> the fp32 wire layout: [P][kp] vectors, then [P][2] scalars (flat)."""
+    rows = np.asarray(rows, dtype=np.float32)
+    return np.ascontiguousarray(np.concatenate([rows[:, :kp].reshape(-1), rows[:, kp:kp + 2].reshape(-1)]))
 
 
 def soa_to_rows(flat, kp):
-    P = len(flat) // (kp + 4)
-    sc = np.ascontiguousarray(flat[P * kp:]).view(np.float64).reshape(P, 2)
-    return np.concatenate([flat[: P * kp].reshape(P, kp).astype(np.float64), sc], axis=1)
+    P = len(flat) // (kp + 2)
+    return np.concatenate([flat[: P * kp].reshape(P, kp), flat[P * kp:].reshape(P, 2)], axis=1).astype(np.float64)
 
 
 class NpBatch:
@@ -35,7 +32,7 @@ class NumpyShardEngine:
         self.device = torch.device("cpu")
         self.F, self.k, self.R, self.rank, self.w0 = num_features, k, world, rank, w0
         self.kp = (k + 3) // 4 * 4
-        self.width = self.kp + 4  # wire words: [P][kp] fp32 vectors, then [P][2] fp64 scalars
+        self.width = self.kp + 2  # wire: [P][kp] vectors, then [P][2] scalars
         self.rows = (num_features - rank + world - 1) // world
         self.w = np.zeros(self.rows)
         self.V = np.zeros((self.rows, k))
@@ -102,8 +99,8 @@ class NumpyShardEngine:
             ix = b.pairidx[:, o]
             m = ix >= 0
             out[poff[o] + ix[m], :kp] = S[m]
-            out[poff[o] + ix[m], kp] = yhat[m]
-            out[poff[o] + ix[m], kp + 1] = csr.label[m]
+            out[poff[o] + ix[m], kp] = yhat[m] - csr.label[m]  # r, formed in fp64
+            out[poff[o] + ix[m], kp + 1] = yhat[m]
         return torch.from_numpy(rows_to_soa(out, kp))
 
     # owner -----------------------------------------------------------------------
@@ -135,12 +132,12 @@ class NumpyShardEngine:
             return 1
         slots, x, pair = b.recv
         Srow = soa_to_rows(s_recv.numpy(), self.kp).astype(np.float64)
-        S, yhat, y = Srow[pair, : self.k], Srow[pair, self.kp], Srow[pair, self.kp + 1]
+        S, r, yhat = Srow[pair, : self.k], Srow[pair, self.kp], Srow[pair, self.kp + 1]
         eta = step_size / math.sqrt(t)
         lam = eta * reg_param
         V = self.V[slots]
-        gw = x * yhat - y  # SGD.scala:145
-        gv = (S * x[:, None] - V * x[:, None] * x[:, None]) * (yhat - y)[:, None]
+        gw = (x - 1.0) * yhat + r  # x * yhat - y with y = yhat - r (SGD.scala:145)
+        gv = (S * x[:, None] - V * x[:, None] * x[:, None]) * r[:, None]
         GW = np.zeros(self.rows)
         GV = np.zeros((self.rows, self.k))
         np.add.at(GW, slots, gw)

@@ -23,13 +23,13 @@ def _concat(parts):
 
 
 def split_pairs(buf, counts, kp):
-    """A pair buffer in the wire layout ([P][kp] fp32 vectors, then [P][2] fp64 scalars = 4 words) cut per peer."""
+    """A pair buffer in the wire layout ([P][kp] vectors, then [P][2] scalars) cut per peer."""
     import torch
 
     counts = [int(c) for c in counts]
     P = sum(counts)
     vec = torch.split(buf[: P * kp], [c * kp for c in counts])
-    sc = torch.split(buf[P * kp:], [c * 4 for c in counts])
+    sc = torch.split(buf[P * kp:], [c * 2 for c in counts])
     return list(zip(vec, sc))
 
 

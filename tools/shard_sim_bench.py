@@ -24,7 +24,7 @@ def split_pairs(buf, counts, kp):
     counts = [int(c) for c in counts]
     P = sum(counts)
     vec = torch.split(buf[: P * kp], [c * kp for c in counts])
-    sc = torch.split(buf[P * kp:], [c * 4 for c in counts])
+    sc = torch.split(buf[P * kp:], [c * 2 for c in counts])
     return list(zip(vec, sc))
 
 
