@@ -34,6 +34,8 @@ CONFIGS = {
     "c2": (1_000_000, 8, 65_536, 1.05, "synthetic Criteo-shaped 1M features, 39 nnz/row, k=8, batch 64K"),
     "c3": (100_000_000, 16, 262_144, 1.05, "synthetic hashed 100M features, 39 nnz/row, k=16, batch 256K"),
     "c4": (2_147_483_647, 32, 262_144, 1.05, "Int.MaxValue features, 39 nnz/row, k=32, batch 256K"),
+    # c5: the CrossValidator config's step (one grid point: k = 16; regression labels); hot rows
+    "c5": (1_000_000, 16, 65_536, 1.2, "Zipf(1.2) hashed 1M features, 39 nnz/row, k=16, batch 64K, regression"),
 }
 STEP_SIZE = 0.1
 REG_PARAM = 1e-6
@@ -222,7 +224,11 @@ def main():
         desc = f"override F={F} k={k} B={B} zipf={zipf_s} ({desc})"
         cfg = (F, k, B, zipf_s, desc)
     t0 = time.perf_counter()
-    host_batches = [synthetic_batch(B, F, batch_index=rank * 1000 + i, zipf_s=zipf_s) for i in range(args.batches)]
+    lab = {}
+    if args.config == "c5":  # y = <w*, x> + N(0, 0.1) (BASELINE.md synthetic data)
+        lab = dict(labels="regression", w_star=np.random.default_rng(20261015).normal(0.0, 0.1, F))
+    host_batches = [synthetic_batch(B, F, batch_index=rank * 1000 + i, zipf_s=zipf_s, **lab)
+                    for i in range(args.batches)]
     log(f"[rank {rank}] generated {args.batches} batches in {time.perf_counter() - t0:.1f}s")
     z = host_batches[0].nnz / B
 
