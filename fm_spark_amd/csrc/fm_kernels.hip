@@ -309,8 +309,13 @@ struct UpdGeom {
 //    it closes inside the wave; the wave's first piece (run begun in an earlier wave) and a run
 //    still open at the wave's end leave fp64 partials (slot 0 / slot 1), summed in wave order by
 //    k_segment_combine.  Every sum runs in a fixed order: the step is bitwise reproducible.
+#ifndef FM_UPD_MINW
+#define FM_UPD_MINW 4  // k <= 16: waves per SIMD the register allocation must allow (4 blocks/CU: the LDS
+                       // limit); without it the compiler took 130 VGPRs (3 waves/SIMD): update -8.6 %,
+                       // step -1.7 % (A/B 3 x 40 steps).  A 29-B LDS image + 5 waves spills: slower.
+#endif
 template <int Q, int NF, int D0>
-__global__ __launch_bounds__(kBlock) void k_segment_update(SegArgs a) {
+__global__ __launch_bounds__(kBlock, (NF == 1 && Q <= 4) ? FM_UPD_MINW : 1) void k_segment_update(SegArgs a) {
   using Geo = UpdGeom<Q, NF>;
   constexpr int NG = Geo::NG, RL = Geo::RL, PIECE = Geo::PIECE, NP = kWaveEnt / 64, C = 4 * NF;
   constexpr int D = D0 < RL ? D0 : RL;  // entries loaded ahead (divides RL)
