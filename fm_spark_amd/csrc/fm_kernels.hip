@@ -282,8 +282,10 @@ struct UpdGeom {
   static constexpr int RL = kWaveEnt / NG;
   static constexpr int KP = 4 * Q * NF;   // widest kp served
   static constexpr int PIECE = KP + 2;    // doubles per piece: [g_w | columns | b]
-  static constexpr int NGS = NG + 1;      // image row stride (entries): skewed against bank conflicts
-  static constexpr int IMG_N = RL * NGS;  // image slots
+  static constexpr int IMG_N = RL * NG;   // image slots: RL rows of NG, column g XOR-swizzled by the
+                                          // row against bank conflicts (no pad column: at k = 32 the
+                                          // pad cost the fourth block per CU)
+  static __device__ __forceinline__ int at(int row, int g) { return row * NG + (g ^ (row & (NG - 1))); }
   static constexpr int IMG = IMG_N * 36;  // {t, b} f64x2 | g_w f64 | {slot, flags} | sample
   static constexpr int PIECES = 2 * NG * PIECE * 8;
   static constexpr int BYTES = IMG > PIECES ? IMG : PIECES;
@@ -310,12 +312,13 @@ struct UpdGeom {
 //    still open at the wave's end leave fp64 partials (slot 0 / slot 1), summed in wave order by
 //    k_segment_combine.  Every sum runs in a fixed order: the step is bitwise reproducible.
 #ifndef FM_UPD_MINW
-#define FM_UPD_MINW 4  // k <= 16: waves per SIMD the register allocation must allow (4 blocks/CU: the LDS
-                       // limit); without it the compiler took 130 VGPRs (3 waves/SIMD): update -8.6 %,
-                       // step -1.7 % (A/B 3 x 40 steps).  A 29-B LDS image + 5 waves spills: slower.
+#define FM_UPD_MINW 4  // k <= 64 (NF = 1): waves per SIMD the register allocation must allow (4 blocks/CU:
+                       // the LDS limit); without it the compiler took 130 VGPRs at k = 16 (3 waves/SIMD):
+                       // update -8.6 %, step -1.7 % (A/B 3 x 40 steps).  A 29-B LDS image + 5 waves
+                       // spills: slower.
 #endif
 template <int Q, int NF, int D0>
-__global__ __launch_bounds__(kBlock, (NF == 1 && Q <= 4) ? FM_UPD_MINW : 1) void k_segment_update(SegArgs a) {
+__global__ __launch_bounds__(kBlock, NF == 1 ? FM_UPD_MINW : 1) void k_segment_update(SegArgs a) {
   using Geo = UpdGeom<Q, NF>;
   constexpr int NG = Geo::NG, RL = Geo::RL, PIECE = Geo::PIECE, NP = kWaveEnt / 64, C = 4 * NF;
   constexpr int D = D0 < RL ? D0 : RL;  // entries loaded ahead (divides RL)
@@ -324,7 +327,7 @@ __global__ __launch_bounds__(kBlock, (NF == 1 && Q <= 4) ? FM_UPD_MINW : 1) void
   __shared__ uint32_t wcnt[kBlock / 64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   unsigned char* smem = smem_all[wave];
-  constexpr int NGS = Geo::NGS, IN = Geo::IMG_N;
+  constexpr int IN = Geo::IMG_N;
   double2* img_d = reinterpret_cast<double2*>(smem);            // {x r, x^2 r}
   double* img_w = reinterpret_cast<double*>(smem + IN * 16);     // x yhat - y
   uint2* img_k = reinterpret_cast<uint2*>(smem + IN * 24);       // {slot, flags}
@@ -336,7 +339,7 @@ __global__ __launch_bounds__(kBlock, (NF == 1 && Q <= 4) ? FM_UPD_MINW : 1) void
   const int64_t base = wid * kWaveEnt;
   const uint32_t kNone = 0xFFFFFFFFu;
   uint32_t ucount = 0;
-  auto li = [](int e) { return (e % RL) * NGS + e / RL; };
+  auto li = [](int e) { return Geo::at(e % RL, e / RL); };
 
   if (base < a.N) {  // wave-uniform
     // ---------------- phase 1: one lane per entry
@@ -390,7 +393,7 @@ __global__ __launch_bounds__(kBlock, (NF == 1 && Q <= 4) ? FM_UPD_MINW : 1) void
     auto prefetch = [&](int b0, float4 (&Sp)[D][NF], float4 (&Vp)[D][NF], float4 (&Hp)[D]) {
 #pragma unroll
       for (int u = 0; u < D; ++u) {
-        const int l = (b0 + u) * NGS + g;  // li(g * RL + b0 + u)
+        const int l = Geo::at(b0 + u, g);  // li(g * RL + b0 + u)
         const uint2 kf = img_k[l];
         const int s = img_s[l];
         const bool valid = (kf.y & kFValid) != 0, end = (kf.y & kFEnd) != 0;
@@ -474,7 +477,7 @@ __global__ __launch_bounds__(kBlock, (NF == 1 && Q <= 4) ? FM_UPD_MINW : 1) void
     auto consume = [&](int b0, const float4 (&Sp)[D][NF], const float4 (&Vp)[D][NF], const float4 (&Hp)[D]) {
 #pragma unroll
       for (int u = 0; u < D; ++u) {
-        const int l = (b0 + u) * NGS + g;
+        const int l = Geo::at(b0 + u, g);
         const uint2 kf = img_k[l];
         if (!(kf.y & kFValid)) continue;
         const double2 tb = img_d[l];

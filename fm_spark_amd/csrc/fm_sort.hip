@@ -12,6 +12,8 @@
 //             block stages the tile in LDS in digit order, then writes runs coalesced; tiles
 //             are mapped to XCDs in contiguous groups.
 // HBM traffic per pass: 4 B (count) + (4 + P) B read + (4 + P) B write per pair.
+#include <type_traits>
+
 #include "fm_internal.h"
 
 namespace fmhip {
@@ -169,9 +171,13 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint32_t* __rest
   constexpr int R = 1 << RB;
   constexpr uint32_t M = R - 1;
   constexpr int D = R / kBlock;  // digits per thread in the block scans
+  // per-wave digit counts and their prefixes stay below the 4096-key tile: 16-bit counters for the
+  // 10-bit digits keep the block at 74 KB of LDS, two blocks per CU (32-bit: 90 KB, one block)
+  using HistT = typename std::conditional<(RB >= 10), uint16_t, uint32_t>::type;
+  static_assert(kTile < 65536 || RB < 10, "16-bit tile histograms need tiles below 64K keys");
   __shared__ uint32_t s_keys[kTile];
   __shared__ P s_vals[kTile];
-  __shared__ uint32_t wave_hist[kWaves][R];
+  __shared__ HistT wave_hist[kWaves][R];
   __shared__ uint32_t tile_start[R];
   __shared__ uint32_t glob_off[R];
   __shared__ uint32_t wsum[kWaves];
@@ -181,7 +187,7 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint32_t* __rest
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 #pragma unroll
   for (int w = 0; w < kWaves; ++w)
-    for (int d = tid; d < R; d += kBlock) wave_hist[w][d] = 0u;
+    for (int d = tid; d < R; d += kBlock) wave_hist[w][d] = 0;
 
   // global base of (digit, this tile): exclusive scan of digit totals + row prefix.
   {
@@ -222,7 +228,7 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint32_t* __rest
     const uint32_t cnt = (uint32_t)__popcll(peers);
     const uint32_t prev = wave_hist[wave][d];
     __builtin_amdgcn_wave_barrier();
-    if (valid && below == 0) wave_hist[wave][d] = prev + cnt;
+    if (valid && below == 0) wave_hist[wave][d] = (HistT)(prev + cnt);
     __builtin_amdgcn_wave_barrier();
     my_rank[r] = valid ? prev + below : 0xFFFFFFFFu;
   }
@@ -238,7 +244,7 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint32_t* __rest
 #pragma unroll
       for (int w = 0; w < kWaves; ++w) {
         const uint32_t c = wave_hist[w][d];
-        wave_hist[w][d] = acc;
+        wave_hist[w][d] = (HistT)acc;
         acc += c;
       }
       v[i] = acc;
