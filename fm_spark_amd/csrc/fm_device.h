@@ -20,6 +20,15 @@ namespace fmhip {
 #endif
 typedef float fm_f4v __attribute__((ext_vector_type(4)));
 
+// Block barrier that orders LDS only: the waits it implies are lgkmcnt, not vmcnt, so global
+// loads issued ahead and global stores still draining stay in flight across it (__syncthreads'
+// workgroup fence waits for every outstanding global access of the wave).
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 __device__ __forceinline__ void st_row4(float* p, float4 v) {
 #if FM_NT_ROWS
   __builtin_nontemporal_store(fm_f4v{v.x, v.y, v.z, v.w}, reinterpret_cast<fm_f4v*>(p));

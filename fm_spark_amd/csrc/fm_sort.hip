@@ -5,7 +5,8 @@
 // up contiguous and in their original (CSR) order, so every per-feature sum downstream runs
 // in a fixed order and the step is bitwise reproducible.
 //
-// Per pass (RB-bit digit, 9..10 bits: 27-bit feature slots take 3 passes of 9 bits):
+// Per pass (RB-bit digit, 9..10 bits: 27-bit feature slots take 3 passes of 9 bits; tiles of both
+// kernels grouped by XCD):
 //   count   : one 512-thread block per 4096-key tile, LDS histogram  -> counts[digit][tile]
 //   scan    : one block per digit, exclusive scan along tiles        -> counts, digit totals
 //   scatter : each wave ranks its 512 keys with RB ballots per round (wave64 match), the
@@ -14,6 +15,7 @@
 // HBM traffic per pass: 4 B (count) + (4 + P) B read + (4 + P) B write per pair.
 #include <type_traits>
 
+#include "fm_device.h"
 #include "fm_internal.h"
 
 namespace fmhip {
@@ -23,8 +25,15 @@ namespace {
 #ifndef FM_SORT_MAXRB
 #define FM_SORT_MAXRB 10
 #endif
-#ifndef FM_SORT_XCD
-#define FM_SORT_XCD 1
+
+#ifndef FM_SORT_CWAVE
+#define FM_SORT_CWAVE 0  // count: one LDS histogram per wave (less same-address atomic contention)
+#endif
+#ifndef FM_SORT_H16
+#define FM_SORT_H16 0  // 16-bit tile histograms for every digit width (always for 10-bit digits)
+#endif
+#ifndef FM_SORT_CXCD
+#define FM_SORT_CXCD 1  // count: tiles mapped to XCDs like the scatter's (a count row's line is written by one L2)
 #endif
 
 #ifndef FM_SORT_BLOCK
@@ -46,21 +55,11 @@ constexpr int kMaxRadix = 1 << 10;
 // and leave it as whole 64-B granules (a partly written granule costs a read-modify-write in
 // HBM; tools/traffic_cal.hip).
 __device__ __forceinline__ int64_t tile_of_block(int64_t ntiles) {
-#if FM_SORT_XCD
   const int64_t per = (ntiles + 7) / 8;
   return (int64_t)(blockIdx.x % 8) * per + blockIdx.x / 8;
-#else
-  return blockIdx.x;
-#endif
 }
 
-inline int64_t blocks_for_tiles(int64_t ntiles) {
-#if FM_SORT_XCD
-  return (ntiles + 7) / 8 * 8;
-#else
-  return ntiles;
-#endif
-}
+inline int64_t blocks_for_tiles(int64_t ntiles) { return (ntiles + 7) / 8 * 8; }
 
 template <int RB>
 __global__ __launch_bounds__(kBlock) void k_radix_count(const uint32_t* __restrict__ keys, int64_t n,
@@ -68,12 +67,19 @@ __global__ __launch_bounds__(kBlock) void k_radix_count(const uint32_t* __restri
                                                         int64_t ntiles) {
   constexpr int R = 1 << RB;
   constexpr uint32_t M = R - 1;
-  __shared__ uint32_t hist[R];
-  for (int d = threadIdx.x; d < R; d += kBlock) hist[d] = 0;
-  __syncthreads();
+  constexpr int HW = FM_SORT_CWAVE ? kWaves : 1;
+  __shared__ uint32_t hist_all[HW][R];
+  uint32_t* hist = hist_all[FM_SORT_CWAVE ? (threadIdx.x >> 6) : 0];
+#if FM_SORT_CXCD
+  const int64_t tile = tile_of_block(ntiles);
+  if (tile >= ntiles) return;  // block-uniform
+#else
   const int64_t tile = blockIdx.x;
+#endif
+  for (int d = threadIdx.x; d < HW * R; d += kBlock) hist_all[d / R][d % R] = 0;
+  lds_barrier();
   const int64_t base = tile * kTile;
-  if (base + kTile <= n) {
+  if (kRounds % 4 == 0 && base + kTile <= n) {
     const uint4* k4 = reinterpret_cast<const uint4*>(keys + base);
 #pragma unroll
     for (int i = 0; i < kRounds / 4; ++i) {
@@ -89,8 +95,13 @@ __global__ __launch_bounds__(kBlock) void k_radix_count(const uint32_t* __restri
       if (idx < n) atomicAdd(&hist[(keys[idx] >> shift) & M], 1u);
     }
   }
-  __syncthreads();
-  for (int d = threadIdx.x; d < R; d += kBlock) counts[(int64_t)d * ntiles + tile] = hist[d];
+  lds_barrier();
+  for (int d = threadIdx.x; d < R; d += kBlock) {
+    uint32_t c = 0;
+#pragma unroll
+    for (int w = 0; w < HW; ++w) c += hist_all[w][d];
+    counts[(int64_t)d * ntiles + tile] = c;
+  }
 }
 
 __device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v, int lane) {
@@ -114,7 +125,7 @@ __global__ __launch_bounds__(kBlock) void k_radix_scan_rows(uint32_t* __restrict
     const uint32_t v = i < ntiles ? row[i] : 0u;
     const uint32_t incl = wave_incl_scan_u32(v, lane);
     if (lane == 63) wsum[wave] = incl;
-    __syncthreads();
+    lds_barrier();
     uint32_t wpre = 0, tot = 0;
 #pragma unroll
     for (int w = 0; w < kWaves; ++w) {
@@ -124,7 +135,7 @@ __global__ __launch_bounds__(kBlock) void k_radix_scan_rows(uint32_t* __restrict
     }
     if (i < ntiles) row[i] = carry + wpre + incl - v;
     carry += tot;
-    __syncthreads();
+    lds_barrier();
   }
   if (threadIdx.x == 0) digit_tot[blockIdx.x] = carry;
 }
@@ -137,7 +148,7 @@ __device__ __forceinline__ void block_excl_scan(uint32_t (&v)[D], uint32_t* wsum
   for (int i = 0; i < D; ++i) t += v[i];
   const uint32_t incl = wave_incl_scan_u32(t, lane);
   if (lane == 63) wsum[wave] = incl;
-  __syncthreads();
+  lds_barrier();
   uint32_t run = incl - t;
 #pragma unroll
   for (int w = 0; w < kWaves; ++w) run += (w < wave) ? wsum[w] : 0u;
@@ -173,7 +184,7 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint32_t* __rest
   constexpr int D = R / kBlock;  // digits per thread in the block scans
   // per-wave digit counts and their prefixes stay below the 4096-key tile: 16-bit counters for the
   // 10-bit digits keep the block at 74 KB of LDS, two blocks per CU (32-bit: 90 KB, one block)
-  using HistT = typename std::conditional<(RB >= 10), uint16_t, uint32_t>::type;
+  using HistT = typename std::conditional<(RB >= 10 || FM_SORT_H16), uint16_t, uint32_t>::type;
   static_assert(kTile < 65536 || RB < 10, "16-bit tile histograms need tiles below 64K keys");
   __shared__ uint32_t s_keys[kTile];
   __shared__ P s_vals[kTile];
@@ -185,26 +196,12 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint32_t* __rest
   const int64_t tile = tile_of_block(ntiles);
   if (tile >= ntiles) return;  // block-uniform
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-#pragma unroll
-  for (int w = 0; w < kWaves; ++w)
-    for (int d = tid; d < R; d += kBlock) wave_hist[w][d] = 0;
-
-  // global base of (digit, this tile): exclusive scan of digit totals + row prefix.
-  {
-    uint32_t v[D];
-#pragma unroll
-    for (int i = 0; i < D; ++i) v[i] = digit_tot[tid * D + i];
-    block_excl_scan<D>(v, wsum, lane, wave);
-#pragma unroll
-    for (int i = 0; i < D; ++i) glob_off[tid * D + i] = v[i] + counts[(int64_t)(tid * D + i) * ntiles + tile];
-  }
-  __syncthreads();
-
+  const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   const int64_t tile_base = tile * kTile;
   const int64_t wbase = tile_base + (int64_t)wave * (kTile / kWaves);
-  const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   uint32_t my_key[kRounds], my_rank[kRounds];
   P my_val[kRounds];
+  // the tile's loads first: in flight while the digit offsets below are read and scanned
 #pragma unroll
   for (int r = 0; r < kRounds; ++r) {
     const int64_t idx = wbase + (int64_t)r * 64 + lane;
@@ -212,80 +209,107 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint32_t* __rest
     my_key[r] = valid ? keys_in[idx] : 0u;
     my_val[r] = valid ? (vals_in ? vals_in[idx] : implicit_payload<P>(idx)) : P{};
   }
-#pragma unroll
-  for (int r = 0; r < kRounds; ++r) {
-    const int64_t idx = wbase + (int64_t)r * 64 + lane;
-    const bool valid = idx < n;
-    const uint32_t d = (my_key[r] >> shift) & M;
-    uint64_t peers = __ballot(valid);
-#pragma unroll
-    for (int b = 0; b < RB; ++b) {
-      const bool bit = (d >> b) & 1u;
-      const uint64_t m = __ballot(bit);
-      peers &= bit ? m : ~m;
-    }
-    const uint32_t below = (uint32_t)__popcll(peers & lt_mask);
-    const uint32_t cnt = (uint32_t)__popcll(peers);
-    const uint32_t prev = wave_hist[wave][d];
-    __builtin_amdgcn_wave_barrier();
-    if (valid && below == 0) wave_hist[wave][d] = (HistT)(prev + cnt);
-    __builtin_amdgcn_wave_barrier();
-    my_rank[r] = valid ? prev + below : 0xFFFFFFFFu;
-  }
-  __syncthreads();
-
-  // per-digit wave bases (exclusive over waves) and the tile's digit starts.
   {
-    uint32_t v[D];
 #pragma unroll
-    for (int i = 0; i < D; ++i) {
-      const int d = tid * D + i;
-      uint32_t acc = 0;
+    for (int w = 0; w < kWaves; ++w)
+      for (int d = tid; d < R; d += kBlock) wave_hist[w][d] = 0;
+
+    // global base of (digit, this tile): exclusive scan of digit totals + row prefix.
+    {
+      uint32_t v[D];
 #pragma unroll
-      for (int w = 0; w < kWaves; ++w) {
-        const uint32_t c = wave_hist[w][d];
-        wave_hist[w][d] = (HistT)acc;
-        acc += c;
-      }
-      v[i] = acc;
+      for (int i = 0; i < D; ++i) v[i] = digit_tot[tid * D + i];
+      block_excl_scan<D>(v, wsum, lane, wave);
+#pragma unroll
+      for (int i = 0; i < D; ++i) glob_off[tid * D + i] = v[i] + counts[(int64_t)(tid * D + i) * ntiles + tile];
     }
-    block_excl_scan<D>(v, wsum, lane, wave);
-#pragma unroll
-    for (int i = 0; i < D; ++i) tile_start[tid * D + i] = v[i];
-  }
-  __syncthreads();
+    lds_barrier();
 
 #pragma unroll
-  for (int r = 0; r < kRounds; ++r) {
-    if (my_rank[r] != 0xFFFFFFFFu) {
+    for (int r = 0; r < kRounds; ++r) {
+      const int64_t idx = wbase + (int64_t)r * 64 + lane;
+      const bool valid = idx < n;
       const uint32_t d = (my_key[r] >> shift) & M;
-      const uint32_t pos = tile_start[d] + wave_hist[wave][d] + my_rank[r];
-      s_keys[pos] = my_key[r];
-      s_vals[pos] = my_val[r];
+      uint64_t peers = __ballot(valid);
+#pragma unroll
+      for (int b = 0; b < RB; ++b) {
+        const bool bit = (d >> b) & 1u;
+        const uint64_t m = __ballot(bit);
+        peers &= bit ? m : ~m;
+      }
+      const uint32_t below = (uint32_t)__popcll(peers & lt_mask);
+      const uint32_t cnt = (uint32_t)__popcll(peers);
+      const uint32_t prev = wave_hist[wave][d];
+      __builtin_amdgcn_wave_barrier();
+      if (valid && below == 0) wave_hist[wave][d] = (HistT)(prev + cnt);
+      __builtin_amdgcn_wave_barrier();
+      my_rank[r] = valid ? prev + below : 0xFFFFFFFFu;
     }
-  }
-  __syncthreads();
+    lds_barrier();
 
-  const int64_t rem = n - tile_base;
-  const int tile_n = rem < kTile ? (int)rem : kTile;
-  for (int j = tid; j < tile_n; j += kBlock) {
-    const uint32_t key = s_keys[j];
-    const uint32_t d = (key >> shift) & M;
-    const uint32_t dest = glob_off[d] + (uint32_t)j - tile_start[d];
-#if FM_NT_SORT
-    __builtin_nontemporal_store(key, keys_out + dest);
-    if constexpr (sizeof(P) == 8) {
-      const uint2 v = *reinterpret_cast<const uint2*>(&s_vals[j]);
-      __builtin_nontemporal_store((unsigned long long)v.x | ((unsigned long long)v.y << 32),
-                                  reinterpret_cast<unsigned long long*>(vals_out) + dest);
-    } else {
-      __builtin_nontemporal_store(*reinterpret_cast<const uint32_t*>(&s_vals[j]),
-                                  reinterpret_cast<uint32_t*>(vals_out) + dest);
+    // per-digit wave bases (exclusive over waves) and the tile's digit starts.
+    {
+      uint32_t v[D];
+#pragma unroll
+      for (int i = 0; i < D; ++i) {
+        const int d = tid * D + i;
+        uint32_t acc = 0;
+#pragma unroll
+        for (int w = 0; w < kWaves; ++w) {
+          const uint32_t c = wave_hist[w][d];
+          wave_hist[w][d] = (HistT)acc;
+          acc += c;
+        }
+        v[i] = acc;
+      }
+      block_excl_scan<D>(v, wsum, lane, wave);
+#pragma unroll
+      for (int i = 0; i < D; ++i) {
+        tile_start[tid * D + i] = v[i];
+        glob_off[tid * D + i] -= v[i];  // destination of staged element j of digit d: glob_off[d] + j
+      }
     }
+    lds_barrier();
+
+#pragma unroll
+    for (int r = 0; r < kRounds; ++r) {
+      if (my_rank[r] != 0xFFFFFFFFu) {
+        const uint32_t d = (my_key[r] >> shift) & M;
+        const uint32_t pos = tile_start[d] + wave_hist[wave][d] + my_rank[r];
+        s_keys[pos] = my_key[r];
+        s_vals[pos] = my_val[r];
+      }
+    }
+    lds_barrier();
+
+    const int64_t rem = n - tile_base;
+    const int tile_n = rem < kTile ? (int)rem : kTile;
+#pragma unroll
+    for (int r = 0; r < kRounds; ++r) {  // unrolled: the rounds' LDS reads are issued together
+      const int j = r * kBlock + tid;
+      if (j >= tile_n) break;
+      const uint32_t key = s_keys[j];
+      const uint32_t d = (key >> shift) & M;
+#ifdef FM_SORT_ABL_LINEAR  // measurement only (wrong order): tile written in place
+      const uint32_t dest = (uint32_t)(tile_base + j) + 0u * glob_off[d];
 #else
-    keys_out[dest] = key;
-    vals_out[dest] = s_vals[j];
+      const uint32_t dest = glob_off[d] + (uint32_t)j;
 #endif
+#if FM_NT_SORT
+      __builtin_nontemporal_store(key, keys_out + dest);
+      if constexpr (sizeof(P) == 8) {
+        const uint2 v = *reinterpret_cast<const uint2*>(&s_vals[j]);
+        __builtin_nontemporal_store((unsigned long long)v.x | ((unsigned long long)v.y << 32),
+                                    reinterpret_cast<unsigned long long*>(vals_out) + dest);
+      } else {
+        __builtin_nontemporal_store(*reinterpret_cast<const uint32_t*>(&s_vals[j]),
+                                    reinterpret_cast<uint32_t*>(vals_out) + dest);
+      }
+#else
+      keys_out[dest] = key;
+      vals_out[dest] = s_vals[j];
+#endif
+    }
   }
 }
 
@@ -307,7 +331,7 @@ void SortWork::ensure(int64_t n) {
 template <class P, int RB>
 static void radix_pass_impl(const uint32_t* kin, const P* vin, uint32_t* ko, P* vo, int64_t n, int shift,
                        SortWork& w, int64_t ntiles, hipStream_t st) {
-  hipLaunchKernelGGL(k_radix_count<RB>, dim3((unsigned)ntiles), dim3(kBlock), 0, st, kin, n, shift,
+  hipLaunchKernelGGL(k_radix_count<RB>, dim3((unsigned)(FM_SORT_CXCD ? blocks_for_tiles(ntiles) : ntiles)), dim3(kBlock), 0, st, kin, n, shift,
                      w.counts.as<uint32_t>(), ntiles);
   hipLaunchKernelGGL(k_radix_scan_rows, dim3(1u << RB), dim3(kBlock), 0, st, w.counts.as<uint32_t>(), ntiles,
                      w.digit_tot.as<uint32_t>());
