@@ -51,6 +51,7 @@ struct ShardBatchState {
   int64_t route_nnz = -1;
   DevBuf poff;                     // [R+1] int64 owner blocks of the partial / S rows
   int64_t loss_blocks = 0;
+  hipEvent_t fwd_e0 = nullptr;  // owner_forward profile start (chunked passes)
   bool combined = false;
   // owner: fm_shard_owner_prepare -> fm_shard_owner_forward -> fm_shard_owner_update
   bool prepared = false;
@@ -342,7 +343,10 @@ void reserve_work(fm_ctx* ctx, int64_t B, int64_t N);
 // the owner partial pass with the per-pair count of present rows (Model.scala:103-112 inner
 // joins: absent ids contribute nothing), and the requester's predict epilogue
 // (Model.scala:78-86, 127-132): w0 for a row without a learned feature, else clamp.
-void shard_owner_partials(fm_ctx* ctx, fm_batch* b, void* partials_out, uint32_t* present_out);
+// chunk c of C (C > 1): only the chunk's pairs of every source (FwdOut::ch_*), for an exchange that
+// sends each chunk while the next is computed; the profile event covers the last chunk
+void shard_owner_partials(fm_ctx* ctx, fm_batch* b, void* partials_out, uint32_t* present_out, int chunk = 0,
+                          int chunks = 1);
 void shard_combine_predict(fm_ctx* ctx, fm_batch* b, const void* partials_in, const uint32_t* present_in,
                            double lo, double hi, double* pred_dev);
 

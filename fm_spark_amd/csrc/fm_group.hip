@@ -26,6 +26,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <numeric>
 
@@ -79,10 +80,15 @@ struct Rank {
   DevBuf grad, gtmp;                                  // replicated gradient buffer
   DevBuf xg_send, xg_recv;                            // counts all-gather (RCCL)
   Pinned xg_pin;
-  hipStream_t stream(bool side) const { return side ? m->side : m->stream; }
-  hipEvent_t event(bool side) const { return side ? ev_side : ev_main; }
-  ncclComm_t comm(bool side) const { return side ? comm_side : comm_main; }
+  // chunked partial exchange of the sharded step (R > 1): its own stream, on the main communicator
+  hipStream_t xstream = nullptr;
+  hipEvent_t ev_x = nullptr, ev_fwd = nullptr, ev_xdone = nullptr;
+  // lanes: 0 main stream, 1 side stream (batch-only work), 2 the exchange stream
+  hipStream_t stream(int lane) const { return lane == 2 ? xstream : lane ? m->side : m->stream; }
+  hipEvent_t event(int lane) const { return lane == 2 ? ev_x : lane ? ev_side : ev_main; }
+  ncclComm_t comm(int lane) const { return lane == 1 ? comm_side : comm_main; }
 };
+constexpr int kLaneMain = 0, kLaneSide = 1, kLaneXchg = 2;
 
 struct GPart {
   fm_batch* b = nullptr;  // the member's batch (owned)
@@ -127,6 +133,9 @@ struct Group {
         d->release();
       if (r.ev_main) (void)hipEventDestroy(r.ev_main);
       if (r.ev_side) (void)hipEventDestroy(r.ev_side);
+      for (hipEvent_t e : {r.ev_x, r.ev_fwd, r.ev_xdone})
+        if (e) (void)hipEventDestroy(e);
+      if (r.xstream) (void)hipStreamDestroy(r.xstream);
     }
     for (auto& r : ranks)
       if (r.m) fm_destroy(r.m);
@@ -159,7 +168,7 @@ GroupBatch& gbatch(fm_ctx* ctx, fm_batch* b) {
 }
 
 // COPY transport: every rank's stream (side or main) waits for what every other rank's has queued
-void barrier(Group& g, bool side) {
+void barrier(Group& g, int side) {
   for (auto& r : g.ranks) {
     FM_HIP_CHECK(hipSetDevice(r.device));
     FM_HIP_CHECK(hipEventRecord(r.event(side), r.stream(side)));
@@ -171,62 +180,99 @@ void barrier(Group& g, bool side) {
   }
 }
 
-// All-to-all-v between the job's ranks: local rank l sends out[l][p] elements of esize bytes to
-// global rank p (from send[l], peer-major) and receives in[l][p] from p (into recv[l], peer-major).
-void a2a(Group& g, bool side, const std::vector<const char*>& send, const std::vector<char*>& recv,
-         const std::vector<const int64_t*>& out, const std::vector<const int64_t*>& in, size_t esize) {
+// One buffer pair of an all-to-all-v (element size esize; per local rank l, send[l] and recv[l]).
+struct A2ASeg {
+  const std::vector<const char*>& send;
+  const std::vector<char*>& recv;
+  size_t esize;
+};
+// Per local rank l and global peer p (in elements): send sc[l][p] from send[l] + so[l][p] to p, and
+// receive rc[l][p] from p into recv[l] + ro[l][p].
+struct A2APlan {
+  std::vector<std::vector<int64_t>> so, sc, ro, rc;
+};
+
+// All-to-all-v of one or more segments with the same plan between the job's ranks, on `lane`;
+// with RCCL every segment's sends and receives go in one group.
+void a2a_plan(Group& g, int lane, const std::vector<A2ASeg>& segs, const A2APlan& pl) {
   if (g.rccl) {
     // the block a rank keeps for itself is a device copy on its own stream, not a send to itself
     // through RCCL's channel buffers
-    for (int l = 0; l < g.L; ++l) {
-      Rank& r = g.ranks[l];
-      const int me = r.global;
-      size_t so = 0, ro = 0;
-      for (int p = 0; p < me; ++p) {
-        so += (size_t)out[l][p] * esize;
-        ro += (size_t)in[l][p] * esize;
-      }
-      const size_t bytes = (size_t)out[l][me] * esize;
-      FM_REQUIRE(bytes == (size_t)in[l][me] * esize, "a2a: the self block differs between send and receive");
-      if (bytes) {
-        FM_HIP_CHECK(hipSetDevice(r.device));
-        FM_HIP_CHECK(hipMemcpyAsync(recv[l] + ro, send[l] + so, bytes, hipMemcpyDeviceToDevice, r.stream(side)));
+    for (const A2ASeg& s : segs) {
+      for (int l = 0; l < g.L; ++l) {
+        Rank& r = g.ranks[l];
+        const int me = r.global;
+        FM_REQUIRE(pl.sc[l][me] == pl.rc[l][me], "a2a: the self block differs between send and receive");
+        const size_t bytes = (size_t)pl.sc[l][me] * s.esize;
+        if (bytes) {
+          FM_HIP_CHECK(hipSetDevice(r.device));
+          FM_HIP_CHECK(hipMemcpyAsync(s.recv[l] + (size_t)pl.ro[l][me] * s.esize, s.send[l] + (size_t)pl.so[l][me] * s.esize,
+                                      bytes, hipMemcpyDeviceToDevice, r.stream(lane)));
+        }
       }
     }
     if (g.R == 1) return;
     FM_RCCL_CHECK(ncclGroupStart());
-    for (int l = 0; l < g.L; ++l) {
-      Rank& r = g.ranks[l];
-      FM_HIP_CHECK(hipSetDevice(r.device));
-      size_t so = 0, ro = 0;
-      for (int p = 0; p < g.R; ++p) {
-        const size_t sb = (size_t)out[l][p] * esize, rb = (size_t)in[l][p] * esize;
-        if (p != r.global) {
-          if (sb) FM_RCCL_CHECK(ncclSend(send[l] + so, sb, ncclChar, p, r.comm(side), r.stream(side)));
-          if (rb) FM_RCCL_CHECK(ncclRecv(recv[l] + ro, rb, ncclChar, p, r.comm(side), r.stream(side)));
+    for (const A2ASeg& s : segs) {
+      for (int l = 0; l < g.L; ++l) {
+        Rank& r = g.ranks[l];
+        FM_HIP_CHECK(hipSetDevice(r.device));
+        for (int p = 0; p < g.R; ++p) {
+          if (p == r.global) continue;
+          const size_t sb = (size_t)pl.sc[l][p] * s.esize, rb = (size_t)pl.rc[l][p] * s.esize;
+          if (sb)
+            FM_RCCL_CHECK(ncclSend(s.send[l] + (size_t)pl.so[l][p] * s.esize, sb, ncclChar, p, r.comm(lane), r.stream(lane)));
+          if (rb)
+            FM_RCCL_CHECK(ncclRecv(s.recv[l] + (size_t)pl.ro[l][p] * s.esize, rb, ncclChar, p, r.comm(lane), r.stream(lane)));
         }
-        so += sb;
-        ro += rb;
       }
     }
     FM_RCCL_CHECK(ncclGroupEnd());
     return;
   }
-  barrier(g, side);
-  for (int l = 0; l < g.L; ++l) {  // destination
-    Rank& r = g.ranks[l];
-    FM_HIP_CHECK(hipSetDevice(r.device));
-    size_t ro = 0;
-    for (int q = 0; q < g.L; ++q) {  // source (one process: global rank = local rank)
-      size_t so = 0;
-      for (int p = 0; p < l; ++p) so += (size_t)out[q][p] * esize;
-      const size_t bytes = (size_t)in[l][q] * esize;
-      if (bytes)
-        FM_HIP_CHECK(hipMemcpyAsync(recv[l] + ro, send[q] + so, bytes, hipMemcpyDefault, r.stream(side)));
-      ro += bytes;
+  barrier(g, lane);
+  for (const A2ASeg& s : segs) {
+    for (int l = 0; l < g.L; ++l) {  // destination
+      Rank& r = g.ranks[l];
+      FM_HIP_CHECK(hipSetDevice(r.device));
+      for (int q = 0; q < g.L; ++q) {  // source (one process: global rank = local rank)
+        FM_REQUIRE(pl.sc[q][l] == pl.rc[l][q], "a2a: send and receive counts differ");
+        const size_t bytes = (size_t)pl.rc[l][q] * s.esize;
+        if (bytes)
+          FM_HIP_CHECK(hipMemcpyAsync(s.recv[l] + (size_t)pl.ro[l][q] * s.esize, s.send[q] + (size_t)pl.so[q][l] * s.esize,
+                                      bytes, hipMemcpyDefault, r.stream(lane)));
+      }
     }
   }
-  barrier(g, side);
+  barrier(g, lane);
+}
+
+// The plan of a packed all-to-all-v: blocks peer-major in both buffers, out[l][p] / in[l][p] elements.
+A2APlan packed_plan(Group& g, const std::vector<const int64_t*>& out, const std::vector<const int64_t*>& in) {
+  A2APlan pl;
+  for (auto* v : {&pl.so, &pl.sc, &pl.ro, &pl.rc}) v->assign(g.L, std::vector<int64_t>(g.R, 0));
+  for (int l = 0; l < g.L; ++l) {
+    int64_t so = 0, ro = 0;
+    for (int p = 0; p < g.R; ++p) {
+      pl.so[l][p] = so;
+      pl.sc[l][p] = out[l][p];
+      pl.ro[l][p] = ro;
+      pl.rc[l][p] = in[l][p];
+      so += out[l][p];
+      ro += in[l][p];
+    }
+  }
+  return pl;
+}
+
+void a2a_multi(Group& g, int lane, const std::vector<A2ASeg>& segs, const std::vector<const int64_t*>& out,
+               const std::vector<const int64_t*>& in) {
+  a2a_plan(g, lane, segs, packed_plan(g, out, in));
+}
+
+void a2a(Group& g, int lane, const std::vector<const char*>& send, const std::vector<char*>& recv,
+         const std::vector<const int64_t*>& out, const std::vector<const int64_t*>& in, size_t esize) {
+  a2a_multi(g, lane, {A2ASeg{send, recv, esize}}, out, in);
 }
 
 // Every rank's `width` int64 values -> all ranks' values on the host, rank-major [R][width].
@@ -361,8 +407,7 @@ void prefetch(Group& g, GroupBatch& gb) {
     out[l] = p.ent_out.data();
     in[l] = p.ent_in.data();
   }
-  a2a(g, true, ss, rs, out, in, sizeof(uint32_t));
-  a2a(g, true, se, re, out, in, sizeof(uint2));
+  a2a_multi(g, true, {A2ASeg{ss, rs, sizeof(uint32_t)}, A2ASeg{se, re, sizeof(uint2)}}, out, in);
   for (int l = 0; l < L; ++l) {
     Rank& r = g.ranks[l];
     GPart& p = gb.parts[l];
@@ -387,8 +432,7 @@ void a2a_pairs(Group& g, int kp, const std::vector<DevBuf*>& send, const std::ve
     rv[l] = recv[l]->as<char>();
     rc[l] = recv[l]->as<char>() + sizeof(float) * recvP[l] * kp;
   }
-  a2a(g, false, sv, rv, out, in, sizeof(float) * kp);
-  a2a(g, false, sc, rc, out, in, sizeof(float) * 2);
+  a2a_multi(g, false, {A2ASeg{sv, rv, sizeof(float) * kp}, A2ASeg{sc, rc, sizeof(float) * 2}}, out, in);
 }
 
 // per-step stats rows of the members (loss, loss rows, distinct ids) at epoch index e -> the job's
@@ -431,6 +475,74 @@ void fill_out(Group& g, fm_ctx* ctx, int64_t e, int64_t global_rows, fm_step_out
   out->n_rows = global_rows;
 }
 
+// Chunks of the owners' partial pass whose exchange overlaps the next chunk's compute
+// (FM_XCHG_CHUNKS, default 4; 1 = one pass, then one all-to-all).  Only with R > 1.
+int xchg_chunks(const Group& g) {
+  if (g.R <= 1 || g.R > kMaxChunkSources) return 1;
+  const char* e = std::getenv("FM_XCHG_CHUNKS");  // read per step: tests switch it
+  const int v = e ? std::atoi(e) : 4;
+  return std::max(1, std::min(v, 64));
+}
+
+void ensure_xchg(Group& g) {
+  for (auto& r : g.ranks) {
+    if (r.xstream) continue;
+    FM_HIP_CHECK(hipSetDevice(r.device));
+    FM_HIP_CHECK(hipStreamCreateWithFlags(&r.xstream, hipStreamNonBlocking));
+    for (hipEvent_t* e : {&r.ev_x, &r.ev_fwd, &r.ev_xdone}) FM_HIP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+  }
+}
+
+// The owners' partial pass in C chunks, each chunk's partial rows sent to their requesters on the
+// exchange stream while the next chunk is computed.  Chunk c of the P pairs of a (owner, requester)
+// block is [P c / C, P (c + 1) / C) on both sides (the owner's pair_in[p] = the requester's pair_out[o]).
+void forward_exchange_chunked(Group& g, GroupBatch& gb, int kp, int C, const std::vector<int64_t>& Pin,
+                              const std::vector<int64_t>& Pout) {
+  const int L = g.L, R = g.R;
+  ensure_xchg(g);
+  std::vector<const char*> sv(L), sc(L);
+  std::vector<char*> rv(L), rc(L);
+  std::vector<std::vector<int64_t>> ioff(L, std::vector<int64_t>(R + 1, 0)), ooff(L, std::vector<int64_t>(R + 1, 0));
+  for (int l = 0; l < L; ++l) {
+    Rank& r = g.ranks[l];
+    GPart& p = gb.parts[l];
+    sv[l] = r.partials.as<char>();
+    sc[l] = r.partials.as<char>() + sizeof(float) * Pin[l] * kp;
+    rv[l] = r.part_in.as<char>();
+    rc[l] = r.part_in.as<char>() + sizeof(float) * Pout[l] * kp;
+    for (int q = 0; q < R; ++q) {
+      ioff[l][q + 1] = ioff[l][q] + p.pair_in[q];
+      ooff[l][q + 1] = ooff[l][q] + p.pair_out[q];
+    }
+  }
+  A2APlan pl;
+  for (auto* v : {&pl.so, &pl.sc, &pl.ro, &pl.rc}) v->assign(L, std::vector<int64_t>(R, 0));
+  for (int c = 0; c < C; ++c) {
+    for (int l = 0; l < L; ++l) {
+      Rank& r = g.ranks[l];
+      on(r, [&] {
+        shard_owner_partials(r.m, gb.parts[l].b, r.partials.p, nullptr, c, C);
+        FM_HIP_CHECK(hipEventRecord(r.ev_fwd, r.m->stream));
+        FM_HIP_CHECK(hipStreamWaitEvent(r.xstream, r.ev_fwd, 0));
+      });
+      const GPart& p = gb.parts[l];
+      for (int q = 0; q < R; ++q) {
+        const int64_t Pi = p.pair_in[q], Po = p.pair_out[q];
+        pl.so[l][q] = ioff[l][q] + Pi * c / C;
+        pl.sc[l][q] = Pi * (c + 1) / C - Pi * c / C;
+        pl.ro[l][q] = ooff[l][q] + Po * c / C;
+        pl.rc[l][q] = Po * (c + 1) / C - Po * c / C;
+      }
+    }
+    a2a_plan(g, kLaneXchg, {A2ASeg{sv, rv, sizeof(float) * kp}, A2ASeg{sc, rc, sizeof(float) * 2}}, pl);
+  }
+  for (auto& r : g.ranks) {  // the combine reads what the exchange stream received
+    FM_HIP_CHECK(hipSetDevice(r.device));
+    FM_HIP_CHECK(hipEventRecord(r.ev_xdone, r.xstream));
+    FM_HIP_CHECK(hipStreamWaitEvent(r.m->stream, r.ev_xdone, 0));
+  }
+}
+
 int step_sharded(fm_ctx* ctx, Group& g, GroupBatch& gb, int32_t t, double step_size, double reg_param,
                  fm_step_out* out) {
   const int L = g.L, kp = ctx->kp, W = kp + 2;
@@ -454,11 +566,16 @@ int step_sharded(fm_ctx* ctx, Group& g, GroupBatch& gb, int32_t t, double step_s
     pin[l] = p.pair_in.data();
     pout[l] = p.pair_out.data();
   }
-  // owners: partial sums per received pair
-  for (int l = 0; l < L; ++l)
-    mcheck(fm_shard_owner_forward(g.ranks[l].m, gb.parts[l].b, g.ranks[l].partials.p), "fm_shard_owner_forward");
-  // back to the requesters (owner l -> requester p: the pair_in[l][p] pairs it got from p)
-  a2a_pairs(g, kp, parts, Pin, part_in, Pout, pin, pout);
+  const int C = xchg_chunks(g);
+  if (C > 1) {
+    forward_exchange_chunked(g, gb, kp, C, Pin, Pout);
+  } else {
+    // owners: partial sums per received pair
+    for (int l = 0; l < L; ++l)
+      mcheck(fm_shard_owner_forward(g.ranks[l].m, gb.parts[l].b, g.ranks[l].partials.p), "fm_shard_owner_forward");
+    // back to the requesters (owner l -> requester p: the pair_in[l][p] pairs it got from p)
+    a2a_pairs(g, kp, parts, Pin, part_in, Pout, pin, pout);
+  }
   for (int l = 0; l < L; ++l)
     mcheck(fm_shard_combine(g.ranks[l].m, gb.parts[l].b, g.ranks[l].part_in.p, g.ranks[l].s_send.p), "fm_shard_combine");
   // S rows to the owners

@@ -146,7 +146,12 @@ struct FwdOut {
   double* dv = nullptr;
   int32_t* absent = nullptr;
   uint32_t* pcount = nullptr;  // partial pass (sharded predict): present rows per pair
+  // partial pass over chunk ch_c of ch_C (ch_C > 1): of every source r < ch_R, the pairs
+  // [off[r] + P_r ch_c / ch_C, off[r] + P_r (ch_c + 1) / ch_C), P_r = off[r + 1] - off[r] (device off)
+  const int64_t* ch_off = nullptr;
+  int32_t ch_R = 0, ch_c = 0, ch_C = 1;
 };
+constexpr int kMaxChunkSources = 64;  // sources a chunked partial pass can split
 // partial_out != nullptr: the sharded owner's partial pass (fm_shard.hip): [pairs][kp] fp32 vectors
 // followed by [pairs] float2 scalars (pred->pcount, if given: present rows per pair);
 // else pred != nullptr: FactorizationMachinesModel.predict / calcLossGrad (p.w0, p.cumE used)

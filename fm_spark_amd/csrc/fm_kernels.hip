@@ -118,8 +118,33 @@ __global__ __launch_bounds__(kBlock, FM_FWD_MINW) void k_forward(TableView T, co
   const int kp = T.kp;
   const bool qok = g * 4 < kp;
   double loss_acc = 0.0, nloss = 0.0;
+  // kPartial over one chunk of the pairs: the chunk's pairs numbered source by source
+  __shared__ int64_t ch_base[PARTIAL ? kMaxChunkSources + 1 : 1], ch_start[PARTIAL ? kMaxChunkSources : 1];
+  const bool chunked = PARTIAL && xo.ch_C > 1;
+  int64_t Bl = B;
+  if (chunked) {
+    if (tid == 0) {
+      int64_t acc = 0;
+      for (int r = 0; r < xo.ch_R; ++r) {
+        const int64_t p0 = xo.ch_off[r], P = xo.ch_off[r + 1] - p0;
+        const int64_t lo = P * xo.ch_c / xo.ch_C, hi = P * (xo.ch_c + 1) / xo.ch_C;
+        ch_start[r] = p0 + lo;
+        ch_base[r] = acc;
+        acc += hi - lo;
+      }
+      ch_base[xo.ch_R] = acc;
+    }
+    __syncthreads();
+    Bl = ch_base[xo.ch_R];
+  }
 
-  for (int64_t s = (int64_t)blockIdx.x * TPB + tid / TEAM; s < B; s += (int64_t)gridDim.x * TPB) {
+  for (int64_t sl = (int64_t)blockIdx.x * TPB + tid / TEAM; sl < Bl; sl += (int64_t)gridDim.x * TPB) {
+    int64_t s = sl;
+    if (chunked) {
+      int r = 0;
+      while (sl >= ch_base[r + 1]) ++r;
+      s = ch_start[r] + (sl - ch_base[r]);
+    }
     const int64_t e0 = row_ptr[s], e1 = row_ptr[s + 1];
     double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0, vv = 0.0, wx = 0.0;
     uint32_t npres = 0;  // kPredict: learned entries of the sample (this lane's share)

@@ -378,7 +378,8 @@ __global__ void k_owner_offsets(const unsigned long long* __restrict__ pairs, in
 
 // The owner partial pass of fm_shard_owner_forward; present_out (optional, [P] uint32): the pair's
 // present rows (sharded predict).
-void shard_owner_partials(fm_ctx* ctx, fm_batch* b, void* partials_out, uint32_t* present_out);
+void shard_owner_partials(fm_ctx* ctx, fm_batch* b, void* partials_out, uint32_t* present_out, int chunk,
+                          int chunks);
 
 }  // namespace fmhip
 
@@ -576,13 +577,17 @@ int fm_shard_owner_forward(fm_ctx* ctx, fm_batch* b, void* partials_out) {
 
 namespace fmhip {
 
-void shard_owner_partials(fm_ctx* ctx, fm_batch* b, void* partials_out, uint32_t* present_out) {
+void shard_owner_partials(fm_ctx* ctx, fm_batch* b, void* partials_out, uint32_t* present_out, int chunk,
+                          int chunks) {
   ShardBatchState& S = shard_state(ctx, b);
   FM_REQUIRE(S.prepared, "fm_shard_owner_prepare must run on this batch first");
   FM_REQUIRE(S.P == 0 || partials_out, "null buffer");
+  const int R = ctx->cfg.shard_count;
+  FM_REQUIRE(chunks >= 1 && chunk >= 0 && chunk < chunks && (chunks == 1 || R <= kMaxChunkSources),
+             "bad owner-forward chunk");
   hipStream_t st = ctx->stream;
   FM_HIP_CHECK(hipStreamWaitEvent(st, S.ready_fwd, 0));
-  hipEvent_t e0 = ctx->prof_begin(st);
+  if (chunk == 0) S.fwd_e0 = ctx->prof_begin(st);  // the profile spans every chunk
   if (S.P > 0) {
     // partial forward over the pairs, rows of the local table (lazy L1 caught up on read)
     BatchDev view;
@@ -594,13 +599,22 @@ void shard_owner_partials(fm_ctx* ctx, fm_batch* b, void* partials_out, uint32_t
     StepParams p{};
     p.cumE = ctx->cum_host.back();
     int64_t nblk = 0;
-    FwdOut xo{};  // the partial pass (partial_out given); only the present counts are read
+    FwdOut xo{};  // the partial pass (partial_out given); only the present counts and the chunk are read
     xo.pcount = present_out;
+    if (chunks > 1) {
+      xo.ch_off = S.src_off.as<int64_t>() + (R + 1);  // the sources' pair offsets (owner_prepare)
+      xo.ch_R = R;
+      xo.ch_c = chunk;
+      xo.ch_C = chunks;
+    }
     launch_forward(ctx->view(), view, ctx->work, p, st, &nblk, reinterpret_cast<float*>(partials_out), &xo);
     view.row_ptr.p = view.col.p = view.ent.p = nullptr;  // borrowed
     FM_HIP_CHECK(hipGetLastError());
   }
-  ctx->prof_end("owner_forward", e0, st);
+  if (chunk + 1 == chunks) {
+    ctx->prof_end("owner_forward", S.fwd_e0, st);
+    S.fwd_e0 = nullptr;
+  }
 }
 
 void shard_combine_predict(fm_ctx* ctx, fm_batch* b, const void* partials_in, const uint32_t* present_in,

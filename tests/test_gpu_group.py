@@ -79,6 +79,27 @@ def test_group_sharded_step_matches_oracle(gpu, R, k, F, hot, transport):
     ctx.close()
 
 
+@pytest.mark.parametrize("chunks", ["1", "3", "16"])
+def test_group_sharded_exchange_chunks(gpu, chunks, monkeypatch):
+    """The owners' partial pass in C chunks whose exchange overlaps the next chunk's compute
+    (FM_XCHG_CHUNKS; default 4): any C gives the oracle step, including chunks with no pairs."""
+    monkeypatch.setenv("FM_XCHG_CHUNKS", chunks)
+    F, k, R = 257, 8, 4
+    _, ids, w, V = make_problem(21, 1, F, k, 1)
+    ctx = _ctx(F, k, R)
+    ctx.load_tables(ids, w, V)
+    model = R_.Model.empty(F, k)
+    model.load(ids, w, V)
+    for t, rows in ((1, 90), (2, 7), (3, 140)):  # 7 rows: most (owner, requester) blocks hold < 16 pairs
+        p = make_problem(60 + t, rows, F, k, 6, hot=3)[0]
+        o = ctx.step(_host(p), t, 0.3, 1e-4)
+        ref = R_.sgd_step_fast(model, p, t, 0.3, 1e-4)
+        assert o.loss_sum == pytest.approx(ref.loss_sum, rel=1e-5)
+        assert o.n_unique == ref.n_unique
+    _check_tables(ctx, model)
+    ctx.close()
+
+
 @pytest.mark.parametrize("R,k,transport", [(1, 8, "copy"), (3, 16, "copy"), (1, 16, "rccl")])
 def test_group_replicated_step_matches_oracle(gpu, R, k, transport):
     F = 401
