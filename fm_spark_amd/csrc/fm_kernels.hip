@@ -41,6 +41,14 @@ constexpr int kWaveEnt = 256;  // sorted entries per update wave
 #define FM_UPD_D 2
 #endif
 constexpr int kUpdD = FM_UPD_D;  // entries whose rows a lane group loads per step
+#ifndef FM_UPD_D4
+#define FM_UPD_D4 1  // k = 13..16 (4 lanes per entry, paired row stores): one entry ahead keeps the kernel
+#endif               // at 116 VGPRs; two spill under the 4-wave cap (A/B: step 1.11 vs 1.14 ms)
+constexpr int kUpdD4 = FM_UPD_D4;
+#ifndef FM_UPD_D2
+#define FM_UPD_D2 1  // k = 5..8 (2 lanes per entry, paired row stores): two ahead spill under the 4-wave cap
+#endif
+constexpr int kUpdD2 = FM_UPD_D2;
 
 // experiment switches (tools/variants.sh; all 0 in the product build): drop the update's S-row
 // loads, row loads or row stores to measure what each costs
@@ -336,6 +344,9 @@ struct UpdGeom {
 //    it closes inside the wave; the wave's first piece (run begun in an earlier wave) and a run
 //    still open at the wave's end leave fp64 partials (slot 0 / slot 1), summed in wave order by
 //    k_segment_combine.  Every sum runs in a fixed order: the step is bitwise reproducible.
+#ifndef FM_UPD_PAIRST
+#define FM_UPD_PAIRST 1  // k = 13..16: each updated row written by one 8-lane 128-B store (see flush_pair)
+#endif
 #ifndef FM_UPD_MINW
 #define FM_UPD_MINW 4  // k <= 64 (NF = 1): waves per SIMD the register allocation must allow (4 blocks/CU:
                        // the LDS limit); without it the compiler took 130 VGPRs at k = 16 (3 waves/SIMD):
@@ -448,14 +459,37 @@ __global__ __launch_bounds__(kBlock, NF == 1 ? FM_UPD_MINW : 1) void k_segment_u
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
+    // Paired row stores (kp = 4Q, Q = 2 or 4: records of V (16Q B) + a header granule of the same
+    // size, i.e. k = 5..8 in 64 B and k = 13..16 in 128 B): the new row of a run closed in phase 2
+    // is kept in registers and written at the end of the entry step by 2Q lanes, the group's Q (V)
+    // and its neighbour group's Q (header + zero pad), so every row leaves in ONE store
+    // instruction covering its whole record instead of two half-record ones.
+    constexpr bool kPairCfg = FM_UPD_PAIRST && (Q == 2 || Q == 4) && NF == 1;
+    const bool paired = kPairCfg && kp == 4 * Q && !a.emit && !FM_ABL_NOWR;  // wave-uniform
+    float4 pend_v = make_float4(0.f, 0.f, 0.f, 0.f);
+    float pend_w = 0.f;             // the row's new w (its header is {w, epoch + 1, cum_next})
+    uint32_t pend_slot = kNone;     // kNone: nothing pending
+
     // apply (or emit) a closed run: the row brought current (absent rows are all zero with
     // cum = 0, so they need no case of their own), then SGD.scala:150-181
-    auto close_run = [&](uint32_t slot, const float4 (&vq)[NF], float4 hq, const double (&A)[C], double b, double gw) {
+    auto close_run = [&](uint32_t slot, const float4 (&vq)[NF], float4 hq, const double (&A)[C], double b, double gw,
+                         bool defer) {
       const RowHdr h = *reinterpret_cast<const RowHdr*>(&hq);
       const float acf = (float)(a.p.cumE - h.cum);  // pending L1 of the row
       const float lamf = (float)a.p.lam;
       float* rec = T.v(slot);
       if (FM_ABL_NOWR) return;
+      if (kPairCfg && defer) {  // this lane's V quad and (lane q = 0) the header, written by flush_pair
+        const float4 v = shrink4f(vq[0], acf);
+        const double g0 = A[0] - (double)v.x * b, g1 = A[1] - (double)v.y * b;
+        const double g2 = A[2] - (double)v.z * b, g3 = A[3] - (double)v.w * b;
+        const float4 u = make_float4((float)fma(g0, -a.p.scale_v, (double)v.x), (float)fma(g1, -a.p.scale_v, (double)v.y),
+                                     (float)fma(g2, -a.p.scale_v, (double)v.z), (float)fma(g3, -a.p.scale_v, (double)v.w));
+        pend_v = shrink4f(u, lamf);
+        pend_w = upd_w(shrink1f(h.w, acf), gw, a.p);  // SGD.scala:150, :171
+        pend_slot = slot;
+        return;
+      }
 #pragma unroll
       for (int n = 0; n < NF; ++n) {
         const int c = 4 * (q + Q * n);
@@ -491,6 +525,29 @@ __global__ __launch_bounds__(kBlock, NF == 1 ? FM_UPD_MINW : 1) void k_segment_u
         st_row4(rec + kp + i, hv);
       }
     };
+    // the rows closed in this entry step (all lanes, converged): even groups' rows, then odd
+    // groups'; the partner group (lane ^ Q) writes the header granule of the row
+    auto flush_pair = [&]() {
+      // ds_swizzle bit mode within 32 lanes: and 0x1F, or 0, xor Q -> lane ^ Q
+      auto swz = [](uint32_t v) { return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x1F | (Q << 10)); };
+      const uint32_t p_slot = swz(pend_slot);
+      const float p_w = __uint_as_float(swz(__float_as_uint(pend_w)));
+      float4 p_h = make_float4(0.f, 0.f, 0.f, 0.f);  // the partner row's header granule: lane q = 0 the header
+      if (q == 0) {
+        RowHdr o;
+        o.w = p_w;
+        o.t = a.p.epoch + 1;
+        o.cum = a.p.cum_next;
+        p_h = *reinterpret_cast<const float4*>(&o);
+      }
+#pragma unroll
+      for (int pass = 0; pass < 2; ++pass) {
+        const bool writer = (g & 1) == pass;
+        const uint32_t slot = writer ? pend_slot : p_slot;
+        if (slot != kNone) st_row4(T.v(slot) + (writer ? 4 * q : kp + 4 * q), writer ? pend_v : p_h);
+      }
+      pend_slot = kNone;
+    };
 
     double acc[C], hacc[C];
 #pragma unroll
@@ -504,7 +561,7 @@ __global__ __launch_bounds__(kBlock, NF == 1 ? FM_UPD_MINW : 1) void k_segment_u
       for (int u = 0; u < D; ++u) {
         const int l = Geo::at(b0 + u, g);
         const uint2 kf = img_k[l];
-        if (!(kf.y & kFValid)) continue;
+        if (kf.y & kFValid) {
         const double2 tb = img_d[l];
         const double t = tb.x;
         if (kf.y & kFStart) started = true;
@@ -521,7 +578,7 @@ __global__ __launch_bounds__(kBlock, NF == 1 ? FM_UPD_MINW : 1) void k_segment_u
         accw += img_w[l];
         if (kf.y & kFEnd) {
           if (started) {
-            close_run(kf.x, Vp[u], Hp[u], acc, accb, accw);
+            close_run(kf.x, Vp[u], Hp[u], acc, accb, accw, paired);
           } else {  // the head piece closes
 #pragma unroll
             for (int j = 0; j < C; ++j) hacc[j] = acc[j];
@@ -536,6 +593,8 @@ __global__ __launch_bounds__(kBlock, NF == 1 ? FM_UPD_MINW : 1) void k_segment_u
           started = false;
           open = false;
         }
+        }
+        if (kPairCfg && paired) flush_pair();  // converged: every lane of the wave
       }
     };
 #pragma unroll 1
@@ -623,7 +682,7 @@ __global__ __launch_bounds__(kBlock, NF == 1 ? FM_UPD_MINW : 1) void k_segment_u
           vq[n] = c < kp ? *reinterpret_cast<const float4*>(T.v(lastkey) + c) : make_float4(0.f, 0.f, 0.f, 0.f);
         }
         const float4 hq = *reinterpret_cast<const float4*>(T.hdr(lastkey));
-        close_run(lastkey, vq, hq, acc, accb, accw);
+        close_run(lastkey, vq, hq, acc, accb, accw, false);
       } else {
         write_part(1, acc, accb, accw);  // still open at the wave's end
       }
@@ -1140,8 +1199,8 @@ void launch_segment_update(const TableView& T, int64_t N, const SegSource& src, 
     const dim3 grid((unsigned)ublocks), blk(kBlock);
     const int nq = T.kp / 4;  // column quads
     if (nq <= 1) hipLaunchKernelGGL((k_segment_update<1, 1, kUpdD>), grid, blk, 0, st, a);
-    else if (nq <= 2) hipLaunchKernelGGL((k_segment_update<2, 1, kUpdD>), grid, blk, 0, st, a);
-    else if (nq <= 4) hipLaunchKernelGGL((k_segment_update<4, 1, kUpdD>), grid, blk, 0, st, a);
+    else if (nq <= 2) hipLaunchKernelGGL((k_segment_update<2, 1, kUpdD2>), grid, blk, 0, st, a);
+    else if (nq <= 4) hipLaunchKernelGGL((k_segment_update<4, 1, kUpdD4>), grid, blk, 0, st, a);
     else if (nq <= 8) hipLaunchKernelGGL((k_segment_update<8, 1, kUpdD>), grid, blk, 0, st, a);
     else if (nq <= 16) hipLaunchKernelGGL((k_segment_update<16, 1, kUpdD>), grid, blk, 0, st, a);
     else if (nq <= 32) hipLaunchKernelGGL((k_segment_update<16, 2, 2>), grid, blk, 0, st, a);
