@@ -51,14 +51,20 @@ static void parallel_chunks(int64_t n, int64_t min_per_thread, F&& f) {
   for (auto& x : th) x.join();
 }
 
-// Host CSR -> pinned staging [row_ptr int64 B+1][label f64 B][col u32 N][x f32 N]: 8 B per
-// entry cross PCIe; the device rebuilds each entry's sample index from row_ptr (k_explode) into
-// the exploded {sample, x} entries of Model.scala:148-153.  Validated on the way; host threads
-// write the staging directly.  check_range: ids must be owned by this context's table
-// (training); otherwise any non-negative int32 id is accepted (predict drops unknown ids).
+// Host CSR -> pinned staging [row_ptr int64 B+1][label f64 B][xoff int32 B][col u32 N][x f32 N]:
+// values that round to 1.0f (one-hot / categorical fields) are not sent -- the id's bit 31 (free:
+// ids are non-negative int32) marks an entry whose fp32 value follows in the x area, and xoff[i]
+// is where row i's values start; each host thread packs its rows' values from its first entry's
+// position on, and only those runs are copied -- so 4 B per unit entry and 8 B per other entry
+// cross PCIe.  The device rebuilds each entry's sample index and value (k_explode) into the exploded
+// {sample, x} entries of Model.scala:148-153.  Validated on the way; host threads write the
+// staging directly.  check_range: ids must be owned by this context's table (training); otherwise
+// any non-negative int32 id is accepted (predict drops unknown ids).
 struct Staged {
-  int64_t B = 0, N = 0, max_id = -1;
-  size_t o_lab = 0, o_col = 0, o_x = 0, bytes = 0;
+  int64_t B = 0, N = 0, M = 0, max_id = -1;
+  size_t o_lab = 0, o_xoff = 0, o_col = 0, o_x = 0, bytes = 0;  // bytes: the image through col
+  int nruns = 0;
+  int64_t run_at[16] = {0}, run_n[16] = {0};  // packed value runs in the x area (floats)
 };
 
 static Staged stage_csr(fm_ctx* ctx, const fm_csr* c, bool check_range, Pinned& pin) {
@@ -80,13 +86,14 @@ static Staged stage_csr(fm_ctx* ctx, const fm_csr* c, bool check_range, Pinned& 
     FM_REQUIRE(N == 0, "nnz > 0 with n_rows == 0");
   }
   g.o_lab = sizeof(int64_t) * (B + 1);
-  g.o_col = (g.o_lab + sizeof(double) * B + 15) / 16 * 16;
+  g.o_xoff = g.o_lab + sizeof(double) * B;
+  g.o_col = (g.o_xoff + sizeof(int32_t) * B + 15) / 16 * 16;
   g.o_x = (g.o_col + sizeof(uint32_t) * N + 15) / 16 * 16;
-  g.bytes = g.o_x + sizeof(float) * N;
-  pin.ensure(g.bytes + 16);
+  pin.ensure(g.o_x + sizeof(float) * N + 16);  // M <= N
   char* base = reinterpret_cast<char*>(pin.p);
   int64_t* rp = reinterpret_cast<int64_t*>(base);
   double* lab = reinterpret_cast<double*>(base + g.o_lab);
+  int32_t* xoff = reinterpret_cast<int32_t*>(base + g.o_xoff);
   uint32_t* col = reinterpret_cast<uint32_t*>(base + g.o_col);
   float* xs = reinterpret_cast<float*>(base + g.o_x);
   if (B > 0) std::memcpy(rp, c->row_ptr, sizeof(int64_t) * (B + 1));
@@ -94,20 +101,31 @@ static Staged stage_csr(fm_ctx* ctx, const fm_csr* c, bool check_range, Pinned& 
   const int64_t F = ctx->cfg.num_features;
   std::atomic<int> bad{0};  // 1 negative id, 2 id >= num_features
   std::atomic<int64_t> mx{-1};
+  // one pass over row chunks: ids (bit 31 = a value follows), labels, the chunk's values packed
+  // from its first entry's position on
+  std::atomic<int> nrun{0};
   parallel_chunks(B, 4096, [&](int64_t r0, int64_t r1) {
-    int64_t lmx = -1;
+    const int64_t x0 = B > 0 ? c->row_ptr[r0] : 0;
+    int64_t lmx = -1, m = x0;
     int lbad = 0;
     for (int64_t i = r0; i < r1; ++i) {
       lab[i] = c->label[i];  // Double, as the reference's label column (SGD.scala:145-146)
+      xoff[i] = (int32_t)m;
       for (int64_t e = c->row_ptr[i]; e < c->row_ptr[i + 1]; ++e) {
         const int32_t id = c->col[e];
         if (id < 0) lbad |= 1;
         else if (check_range && id >= F) lbad |= 2;
-        col[e] = (uint32_t)id;
+        const float x = (float)c->val[e];
+        const uint32_t valued = x != 1.0f;
+        col[e] = (uint32_t)id | (valued << 31);
+        xs[m] = x;  // branch-free: the slot is taken only by a value that is not 1
+        m += valued;
         lmx = std::max<int64_t>(lmx, id);
-        xs[e] = (float)c->val[e];
       }
     }
+    const int ri = nrun.fetch_add(1);
+    g.run_at[ri] = x0;
+    g.run_n[ri] = m - x0;
     if (lbad) bad.fetch_or(lbad);
     int64_t cur = mx.load();
     while (lmx > cur && !mx.compare_exchange_weak(cur, lmx)) {
@@ -115,6 +133,9 @@ static Staged stage_csr(fm_ctx* ctx, const fm_csr* c, bool check_range, Pinned& 
   });
   FM_REQUIRE(!(bad.load() & 1), "negative feature id");
   FM_REQUIRE(!(bad.load() & 2), "feature id >= num_features");
+  g.nruns = nrun.load();
+  for (int r = 0; r < g.nruns; ++r) g.M += g.run_n[r];
+  g.bytes = g.o_col + sizeof(uint32_t) * N;
   g.max_id = mx.load();
   return g;
 }
@@ -124,7 +145,7 @@ static bool batch_fits(const fm_batch* b, const Staged& g) {
          b->dev.col.bytes >= sizeof(uint32_t) * std::max<int64_t>(g.N, 4) + 16 &&
          b->dev.ent.bytes >= sizeof(uint32_t) * 2 * std::max<int64_t>(g.N, 4) + 16 &&
          b->dev.label.bytes >= sizeof(double) * std::max<int64_t>(g.B, 4) + 16 &&
-         b->up.bytes >= g.bytes + 16;
+         b->up.bytes >= g.o_x + sizeof(float) * g.N + 16;
 }
 
 // b's device buffers (grown, never shrunk) filled from the staging by one async copy on st (into
@@ -141,13 +162,18 @@ static void copy_staged(fm_ctx* ctx, const Staged& g, const Pinned& pin, fm_batc
   b->dev.col.ensure(sizeof(uint32_t) * std::max<int64_t>(N, 4) + 16);
   b->dev.ent.ensure(sizeof(uint32_t) * 2 * std::max<int64_t>(N, 4) + 16);
   b->dev.label.ensure(sizeof(double) * std::max<int64_t>(B, 4) + 16);
-  b->up.ensure(g.bytes + 16);
+  b->up.ensure(g.o_x + sizeof(float) * N + 16);
   FM_HIP_CHECK(hipMemcpyAsync(b->up.p, pin.p, g.bytes, hipMemcpyHostToDevice, st));
+  for (int r = 0; r < g.nruns; ++r)  // the packed value runs, each where its rows' xoff point
+    if (g.run_n[r] > 0)
+      FM_HIP_CHECK(hipMemcpyAsync(b->up.as<char>() + g.o_x + sizeof(float) * g.run_at[r],
+                                  reinterpret_cast<const char*>(pin.p) + g.o_x + sizeof(float) * g.run_at[r],
+                                  sizeof(float) * g.run_n[r], hipMemcpyHostToDevice, st));
   const char* up = b->up.as<char>();
   launch_explode(reinterpret_cast<const int64_t*>(up), reinterpret_cast<const double*>(up + g.o_lab),
-                 reinterpret_cast<const uint32_t*>(up + g.o_col), reinterpret_cast<const float*>(up + g.o_x), B, N,
-                 b->dev.row_ptr.as<int64_t>(), b->dev.label.as<double>(), b->dev.col.as<uint32_t>(),
-                 b->dev.ent.as<uint2>(), st);
+                 reinterpret_cast<const int32_t*>(up + g.o_xoff), reinterpret_cast<const uint32_t*>(up + g.o_col),
+                 reinterpret_cast<const float*>(up + g.o_x), B, N, b->dev.row_ptr.as<int64_t>(),
+                 b->dev.label.as<double>(), b->dev.col.as<uint32_t>(), b->dev.ent.as<uint2>(), st);
 }
 
 // Synchronous upload (fm_batch_create, fm_predict, fm_loss_grad): staged in the context's

@@ -196,10 +196,11 @@ void launch_segment_sum(const uint32_t* skeys, const uint32_t* svals, int64_t n,
                         int32_t k, uint32_t* run_index, int32_t* out_keys, double* out_sums,
                         int64_t* n_out_dev, hipStream_t st);
 void launch_count_present(const TableView& T, int64_t* out, hipStream_t st);
-// the uploaded CSR image (row_ptr, label, col, x) -> the device batch: row_ptr / label / col copied,
-// ent[e] = {sample of e, x bits} rebuilt from row_ptr (the explode of Model.scala:148-153)
-void launch_explode(const int64_t* row_ptr_in, const double* label_in, const uint32_t* col_in, const float* x_in,
-                    int64_t B, int64_t N, int64_t* row_ptr, double* label, uint32_t* col, uint2* ent,
+// the uploaded CSR image (row_ptr, label, xoff, col with bit 31 = a value follows, the compact
+// non-unit values) -> the device batch: row_ptr / label / col copied, ent[e] = {sample of e, x
+// bits} rebuilt from row_ptr and the compact values (the explode of Model.scala:148-153)
+void launch_explode(const int64_t* row_ptr_in, const double* label_in, const int32_t* xoff, const uint32_t* col_in,
+                    const float* x_in, int64_t B, int64_t N, int64_t* row_ptr, double* label, uint32_t* col, uint2* ent,
                     hipStream_t st);
 
 }  // namespace fmhip

@@ -347,6 +347,9 @@ struct UpdGeom {
 #ifndef FM_UPD_PAIRST
 #define FM_UPD_PAIRST 1  // k = 13..16: each updated row written by one 8-lane 128-B store (see flush_pair)
 #endif
+#ifndef FM_UPD_PAIR8
+#define FM_UPD_PAIR8 0  // k = 29..32 too (8 lanes V + 4 lanes header granule in one instruction)
+#endif
 #ifndef FM_UPD_MINW
 #define FM_UPD_MINW 4  // k <= 64 (NF = 1): waves per SIMD the register allocation must allow (4 blocks/CU:
                        // the LDS limit); without it the compiler took 130 VGPRs at k = 16 (3 waves/SIMD):
@@ -464,7 +467,7 @@ __global__ __launch_bounds__(kBlock, NF == 1 ? FM_UPD_MINW : 1) void k_segment_u
     // is kept in registers and written at the end of the entry step by 2Q lanes, the group's Q (V)
     // and its neighbour group's Q (header + zero pad), so every row leaves in ONE store
     // instruction covering its whole record instead of two half-record ones.
-    constexpr bool kPairCfg = FM_UPD_PAIRST && (Q == 2 || Q == 4) && NF == 1;
+    constexpr bool kPairCfg = FM_UPD_PAIRST && (Q == 2 || Q == 4 || (Q == 8 && FM_UPD_PAIR8)) && NF == 1;
     const bool paired = kPairCfg && kp == 4 * Q && !a.emit && !FM_ABL_NOWR;  // wave-uniform
     float4 pend_v = make_float4(0.f, 0.f, 0.f, 0.f);
     float pend_w = 0.f;             // the row's new w (its header is {w, epoch + 1, cum_next})
@@ -527,6 +530,7 @@ __global__ __launch_bounds__(kBlock, NF == 1 ? FM_UPD_MINW : 1) void k_segment_u
     };
     // the rows closed in this entry step (all lanes, converged): even groups' rows, then odd
     // groups'; the partner group (lane ^ Q) writes the header granule of the row
+    const int pair_span = 4 + ((16 - ((kp + 4) & 15)) & 15);
     auto flush_pair = [&]() {
       // ds_swizzle bit mode within 32 lanes: and 0x1F, or 0, xor Q -> lane ^ Q
       auto swz = [](uint32_t v) { return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x1F | (Q << 10)); };
@@ -544,7 +548,8 @@ __global__ __launch_bounds__(kBlock, NF == 1 ? FM_UPD_MINW : 1) void k_segment_u
       for (int pass = 0; pass < 2; ++pass) {
         const bool writer = (g & 1) == pass;
         const uint32_t slot = writer ? pend_slot : p_slot;
-        if (slot != kNone) st_row4(T.v(slot) + (writer ? 4 * q : kp + 4 * q), writer ? pend_v : p_h);
+        // the header granule is 4 + pad floats: 4Q of them at kp = 4Q <= 16, 16 at kp = 32
+        if (slot != kNone && (writer || 4 * q < pair_span)) st_row4(T.v(slot) + (writer ? 4 * q : kp + 4 * q), writer ? pend_v : p_h);
       }
       pend_slot = kNone;
     };
@@ -1324,33 +1329,47 @@ void launch_loss_grad(const TableView& T, const BatchDev& b, double cumE, double
   launch_forward(T, b, unused, p, st, &nblk, nullptr, &xo);
 }
 
-// One team of 16 lanes per sample: its entries get {sample, x}; col, label and row_ptr are copied
-// alongside (grid-stride, the same pass).
+// One team of 16 lanes per sample: its entries get {sample, x}, x = 1 unless the id's bit 31 says
+// the value follows in the row's run of compact values (xoff); col (bit 31 cleared), label and
+// row_ptr are copied alongside (grid-stride, the same pass).
 __global__ __launch_bounds__(kBlock) void k_explode(const int64_t* __restrict__ rp_in, const double* __restrict__ lab_in,
-                                                   const uint32_t* __restrict__ col_in, const float* __restrict__ x_in,
-                                                   int64_t B, int64_t* __restrict__ rp, double* __restrict__ lab,
-                                                   uint32_t* __restrict__ col, uint2* __restrict__ ent) {
+                                                   const int32_t* __restrict__ xoff, const uint32_t* __restrict__ col_in,
+                                                   const float* __restrict__ x_in, int64_t B, int64_t* __restrict__ rp,
+                                                   double* __restrict__ lab, uint32_t* __restrict__ col,
+                                                   uint2* __restrict__ ent) {
   constexpr int T = 16;
   const int tl = threadIdx.x % T;
+  const int lane = threadIdx.x & 63;
+  const uint64_t team_bits = 0xFFFFull << (lane & ~(T - 1));
+  const uint64_t below = team_bits & ((1ull << lane) - 1ull);
   const int64_t gtid = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const int64_t nthreads = (int64_t)gridDim.x * kBlock;
   for (int64_t i = gtid; i <= B; i += nthreads) rp[i] = rp_in[i];
   for (int64_t i = gtid; i < B; i += nthreads) lab[i] = lab_in[i];
   for (int64_t s = gtid / T; s < B; s += nthreads / T) {
     const int64_t e1 = rp_in[s + 1];
-    for (int64_t e = rp_in[s] + tl; e < e1; e += T) {
-      col[e] = col_in[e];
-      ent[e] = make_uint2((uint32_t)s, __float_as_uint(x_in[e]));
+    int64_t xo = xoff[s];
+    for (int64_t eb = rp_in[s]; eb < e1; eb += T) {  // the team's lanes take the same trips
+      const int64_t e = eb + tl;
+      const uint32_t c = e < e1 ? col_in[e] : 0u;
+      const bool valued = (c >> 31) != 0u;
+      const uint64_t m = __ballot(valued);
+      const float x = valued ? x_in[xo + __popcll(m & below)] : 1.0f;
+      xo += __popcll(m & team_bits);
+      if (e < e1) {
+        col[e] = c & 0x7FFFFFFFu;
+        ent[e] = make_uint2((uint32_t)s, __float_as_uint(x));
+      }
     }
   }
 }
 
-void launch_explode(const int64_t* row_ptr_in, const double* label_in, const uint32_t* col_in, const float* x_in,
-                    int64_t B, int64_t N, int64_t* row_ptr, double* label, uint32_t* col, uint2* ent,
+void launch_explode(const int64_t* row_ptr_in, const double* label_in, const int32_t* xoff, const uint32_t* col_in,
+                    const float* x_in, int64_t B, int64_t N, int64_t* row_ptr, double* label, uint32_t* col, uint2* ent,
                     hipStream_t st) {
   (void)N;
   hipLaunchKernelGGL(k_explode, dim3(grid_for(std::max<int64_t>(B, 1) * 16, kBlock, 256 * 8)), dim3(kBlock), 0, st,
-                     row_ptr_in, label_in, col_in, x_in, B, row_ptr, label, col, ent);
+                     row_ptr_in, label_in, xoff, col_in, x_in, B, row_ptr, label, col, ent);
   FM_HIP_CHECK(hipGetLastError());
 }
 

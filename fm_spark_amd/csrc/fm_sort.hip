@@ -209,107 +209,105 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint32_t* __rest
     my_key[r] = valid ? keys_in[idx] : 0u;
     my_val[r] = valid ? (vals_in ? vals_in[idx] : implicit_payload<P>(idx)) : P{};
   }
+#pragma unroll
+  for (int w = 0; w < kWaves; ++w)
+    for (int d = tid; d < R; d += kBlock) wave_hist[w][d] = 0;
+
+  // global base of (digit, this tile): exclusive scan of digit totals + row prefix.
   {
+    uint32_t v[D];
 #pragma unroll
-    for (int w = 0; w < kWaves; ++w)
-      for (int d = tid; d < R; d += kBlock) wave_hist[w][d] = 0;
+    for (int i = 0; i < D; ++i) v[i] = digit_tot[tid * D + i];
+    block_excl_scan<D>(v, wsum, lane, wave);
+#pragma unroll
+    for (int i = 0; i < D; ++i) glob_off[tid * D + i] = v[i] + counts[(int64_t)(tid * D + i) * ntiles + tile];
+  }
+  lds_barrier();
 
-    // global base of (digit, this tile): exclusive scan of digit totals + row prefix.
-    {
-      uint32_t v[D];
 #pragma unroll
-      for (int i = 0; i < D; ++i) v[i] = digit_tot[tid * D + i];
-      block_excl_scan<D>(v, wsum, lane, wave);
+  for (int r = 0; r < kRounds; ++r) {
+    const int64_t idx = wbase + (int64_t)r * 64 + lane;
+    const bool valid = idx < n;
+    const uint32_t d = (my_key[r] >> shift) & M;
+    uint64_t peers = __ballot(valid);
 #pragma unroll
-      for (int i = 0; i < D; ++i) glob_off[tid * D + i] = v[i] + counts[(int64_t)(tid * D + i) * ntiles + tile];
+    for (int b = 0; b < RB; ++b) {
+      const bool bit = (d >> b) & 1u;
+      const uint64_t m = __ballot(bit);
+      peers &= bit ? m : ~m;
     }
-    lds_barrier();
+    const uint32_t below = (uint32_t)__popcll(peers & lt_mask);
+    const uint32_t cnt = (uint32_t)__popcll(peers);
+    const uint32_t prev = wave_hist[wave][d];
+    __builtin_amdgcn_wave_barrier();
+    if (valid && below == 0) wave_hist[wave][d] = (HistT)(prev + cnt);
+    __builtin_amdgcn_wave_barrier();
+    my_rank[r] = valid ? prev + below : 0xFFFFFFFFu;
+  }
+  lds_barrier();
+
+  // per-digit wave bases (exclusive over waves) and the tile's digit starts.
+  {
+    uint32_t v[D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+      const int d = tid * D + i;
+      uint32_t acc = 0;
+#pragma unroll
+      for (int w = 0; w < kWaves; ++w) {
+        const uint32_t c = wave_hist[w][d];
+        wave_hist[w][d] = (HistT)acc;
+        acc += c;
+      }
+      v[i] = acc;
+    }
+    block_excl_scan<D>(v, wsum, lane, wave);
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+      tile_start[tid * D + i] = v[i];
+      glob_off[tid * D + i] -= v[i];  // destination of staged element j of digit d: glob_off[d] + j
+    }
+  }
+  lds_barrier();
 
 #pragma unroll
-    for (int r = 0; r < kRounds; ++r) {
-      const int64_t idx = wbase + (int64_t)r * 64 + lane;
-      const bool valid = idx < n;
+  for (int r = 0; r < kRounds; ++r) {
+    if (my_rank[r] != 0xFFFFFFFFu) {
       const uint32_t d = (my_key[r] >> shift) & M;
-      uint64_t peers = __ballot(valid);
-#pragma unroll
-      for (int b = 0; b < RB; ++b) {
-        const bool bit = (d >> b) & 1u;
-        const uint64_t m = __ballot(bit);
-        peers &= bit ? m : ~m;
-      }
-      const uint32_t below = (uint32_t)__popcll(peers & lt_mask);
-      const uint32_t cnt = (uint32_t)__popcll(peers);
-      const uint32_t prev = wave_hist[wave][d];
-      __builtin_amdgcn_wave_barrier();
-      if (valid && below == 0) wave_hist[wave][d] = (HistT)(prev + cnt);
-      __builtin_amdgcn_wave_barrier();
-      my_rank[r] = valid ? prev + below : 0xFFFFFFFFu;
+      const uint32_t pos = tile_start[d] + wave_hist[wave][d] + my_rank[r];
+      s_keys[pos] = my_key[r];
+      s_vals[pos] = my_val[r];
     }
-    lds_barrier();
+  }
+  lds_barrier();
 
-    // per-digit wave bases (exclusive over waves) and the tile's digit starts.
-    {
-      uint32_t v[D];
+  const int64_t rem = n - tile_base;
+  const int tile_n = rem < kTile ? (int)rem : kTile;
 #pragma unroll
-      for (int i = 0; i < D; ++i) {
-        const int d = tid * D + i;
-        uint32_t acc = 0;
-#pragma unroll
-        for (int w = 0; w < kWaves; ++w) {
-          const uint32_t c = wave_hist[w][d];
-          wave_hist[w][d] = (HistT)acc;
-          acc += c;
-        }
-        v[i] = acc;
-      }
-      block_excl_scan<D>(v, wsum, lane, wave);
-#pragma unroll
-      for (int i = 0; i < D; ++i) {
-        tile_start[tid * D + i] = v[i];
-        glob_off[tid * D + i] -= v[i];  // destination of staged element j of digit d: glob_off[d] + j
-      }
-    }
-    lds_barrier();
-
-#pragma unroll
-    for (int r = 0; r < kRounds; ++r) {
-      if (my_rank[r] != 0xFFFFFFFFu) {
-        const uint32_t d = (my_key[r] >> shift) & M;
-        const uint32_t pos = tile_start[d] + wave_hist[wave][d] + my_rank[r];
-        s_keys[pos] = my_key[r];
-        s_vals[pos] = my_val[r];
-      }
-    }
-    lds_barrier();
-
-    const int64_t rem = n - tile_base;
-    const int tile_n = rem < kTile ? (int)rem : kTile;
-#pragma unroll
-    for (int r = 0; r < kRounds; ++r) {  // unrolled: the rounds' LDS reads are issued together
-      const int j = r * kBlock + tid;
-      if (j >= tile_n) break;
-      const uint32_t key = s_keys[j];
-      const uint32_t d = (key >> shift) & M;
+  for (int r = 0; r < kRounds; ++r) {  // unrolled: the rounds' LDS reads are issued together
+    const int j = r * kBlock + tid;
+    if (j >= tile_n) break;
+    const uint32_t key = s_keys[j];
+    const uint32_t d = (key >> shift) & M;
 #ifdef FM_SORT_ABL_LINEAR  // measurement only (wrong order): tile written in place
-      const uint32_t dest = (uint32_t)(tile_base + j) + 0u * glob_off[d];
+    const uint32_t dest = (uint32_t)(tile_base + j) + 0u * glob_off[d];
 #else
-      const uint32_t dest = glob_off[d] + (uint32_t)j;
+    const uint32_t dest = glob_off[d] + (uint32_t)j;
 #endif
 #if FM_NT_SORT
-      __builtin_nontemporal_store(key, keys_out + dest);
-      if constexpr (sizeof(P) == 8) {
-        const uint2 v = *reinterpret_cast<const uint2*>(&s_vals[j]);
-        __builtin_nontemporal_store((unsigned long long)v.x | ((unsigned long long)v.y << 32),
-                                    reinterpret_cast<unsigned long long*>(vals_out) + dest);
-      } else {
-        __builtin_nontemporal_store(*reinterpret_cast<const uint32_t*>(&s_vals[j]),
-                                    reinterpret_cast<uint32_t*>(vals_out) + dest);
-      }
-#else
-      keys_out[dest] = key;
-      vals_out[dest] = s_vals[j];
-#endif
+    __builtin_nontemporal_store(key, keys_out + dest);
+    if constexpr (sizeof(P) == 8) {
+      const uint2 v = *reinterpret_cast<const uint2*>(&s_vals[j]);
+      __builtin_nontemporal_store((unsigned long long)v.x | ((unsigned long long)v.y << 32),
+                                  reinterpret_cast<unsigned long long*>(vals_out) + dest);
+    } else {
+      __builtin_nontemporal_store(*reinterpret_cast<const uint32_t*>(&s_vals[j]),
+                                  reinterpret_cast<uint32_t*>(vals_out) + dest);
     }
+#else
+    keys_out[dest] = key;
+    vals_out[dest] = s_vals[j];
+#endif
   }
 }
 

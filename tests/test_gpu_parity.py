@@ -119,6 +119,32 @@ def test_loss_grad_matches_oracle(gpu, k):
     np.testing.assert_allclose(gdv, rdv, rtol=1e-5, atol=1e-9)
 
 
+def test_upload_unit_values_elided(gpu):
+    """The host upload sends only the values that do not round to 1.0f (bit 31 of the id marks
+    them) and the device rebuilds every entry's x: calcLossGrad's deltaWi = x (Model.scala:200)
+    returns the device's x of every entry, which must be the fp32 rounding of the input exactly --
+    unit, near-unit, negative, explicit-zero and large values, rows of only unit or only valued
+    entries, empty rows, and rows longer than the 16-lane team."""
+    from fm_spark_amd.engine import FMContext
+
+    rng = np.random.default_rng(31)
+    F, k = 3000, 4
+    lens = [0, 1, 5, 16, 17, 40, 0, 33, 3, 64]
+    row_ptr = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    nnz = int(row_ptr[-1])
+    col = np.concatenate([rng.choice(F, size=n, replace=False) for n in lens]).astype(np.int32)
+    pool = np.array([1.0, 1.0 + 1e-12, 1.0 - 1e-10, 1.0000001, 2.5, -1.0, 0.0, 1e6, np.nextafter(1.0, 2.0)])
+    val = rng.choice(pool, size=nnz)
+    val[row_ptr[2]:row_ptr[3]] = 1.0  # a row of unit values only
+    val[row_ptr[3]:row_ptr[4]] = 2.5  # a row of valued entries only
+    label = rng.normal(size=len(lens))
+    ctx = FMContext(F, k)
+    ctx.load_tables(np.arange(F, dtype=np.int32), rng.normal(0, 0.1, F), rng.normal(0, 0.1, (F, k)))
+    _, _, dw, _ = ctx.loss_grad(to_host(R.CSR(row_ptr, col, val, label)))
+    np.testing.assert_array_equal(dw, val.astype(np.float32).astype(np.float64))
+    ctx.close()
+
+
 @pytest.mark.parametrize("k", [1, 2, 3, 4, 8, 10, 16, 32, 48, 72, 136, 256])
 def test_step_parity_k(gpu, k):
     F = 97
