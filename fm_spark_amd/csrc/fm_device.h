@@ -15,6 +15,32 @@ namespace fmhip {
 #ifndef FM_NT_ENT
 #define FM_NT_ENT 0
 #endif
+#ifndef FM_NT_CSR
+#define FM_NT_CSR 0  // nontemporal loads of the forward's CSR stream (col, ent)
+#endif
+#ifndef FM_NT_SORTLD
+#define FM_NT_SORTLD 0  // nontemporal loads of the sort's key / payload streams (count and scatter)
+#endif
+template <class T>
+__device__ __forceinline__ T ld_stream(const T* p, bool nt) {
+  if (nt) return __builtin_nontemporal_load(p);
+  return *p;
+}
+__device__ __forceinline__ uint4 ld_stream(const uint4* p, bool nt) {
+  if (nt) {
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 q = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+    return make_uint4(q.x, q.y, q.z, q.w);
+  }
+  return *p;
+}
+__device__ __forceinline__ uint2 ld_stream(const uint2* p, bool nt) {
+  if (nt) {
+    const unsigned long long q = __builtin_nontemporal_load(reinterpret_cast<const unsigned long long*>(p));
+    return make_uint2((uint32_t)q, (uint32_t)(q >> 32));
+  }
+  return *p;
+}
 #ifndef FM_NT_SORT
 #define FM_NT_SORT 0
 #endif

@@ -164,9 +164,9 @@ __global__ __launch_bounds__(kBlock, FM_FWD_MINW) void k_forward(TableView T, co
       for (int j = 0; j < U; ++j) {
         const int64_t e = eb + j * RPP;
         ok[j] = e < e1;
-        id[j] = ok[j] ? col[e] : 0u;
+        id[j] = ok[j] ? ld_stream(col + e, FM_NT_CSR) : 0u;
         if (MODE == kPredict) ok[j] = ok[j] && id[j] < (uint64_t)T.rows;
-        x[j] = ok[j] ? __uint_as_float(ent[e].y) : 0.f;
+        x[j] = ok[j] ? __uint_as_float(ld_stream(ent + e, FM_NT_CSR).y) : 0.f;
       }
       RowHdr h[U];
       float4 v[U];

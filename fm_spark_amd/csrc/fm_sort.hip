@@ -83,7 +83,7 @@ __global__ __launch_bounds__(kBlock) void k_radix_count(const uint32_t* __restri
     const uint4* k4 = reinterpret_cast<const uint4*>(keys + base);
 #pragma unroll
     for (int i = 0; i < kRounds / 4; ++i) {
-      const uint4 q = k4[i * kBlock + threadIdx.x];
+      const uint4 q = ld_stream(k4 + i * kBlock + threadIdx.x, FM_NT_SORTLD);
       atomicAdd(&hist[(q.x >> shift) & M], 1u);
       atomicAdd(&hist[(q.y >> shift) & M], 1u);
       atomicAdd(&hist[(q.z >> shift) & M], 1u);
@@ -206,8 +206,8 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint32_t* __rest
   for (int r = 0; r < kRounds; ++r) {
     const int64_t idx = wbase + (int64_t)r * 64 + lane;
     const bool valid = idx < n;
-    my_key[r] = valid ? keys_in[idx] : 0u;
-    my_val[r] = valid ? (vals_in ? vals_in[idx] : implicit_payload<P>(idx)) : P{};
+    my_key[r] = valid ? ld_stream(keys_in + idx, FM_NT_SORTLD) : 0u;
+    my_val[r] = valid ? (vals_in ? ld_stream(vals_in + idx, FM_NT_SORTLD) : implicit_payload<P>(idx)) : P{};
   }
 #pragma unroll
   for (int w = 0; w < kWaves; ++w)
