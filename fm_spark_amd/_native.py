@@ -98,6 +98,7 @@ SIGNATURES = {
     "fm_predict_batch": (C.c_int, [_P, _P, C.c_double, C.c_double, _DP]),
     "fm_init_from_batch": (C.c_int, [_P, _P, _I64P]),
     "fm_loss_grad": (C.c_int, [_P, C.POINTER(fm_csr), _DP, _DP, _DP, _DP]),
+    "fm_calc_loss_grad": (C.c_int, [_P, C.POINTER(fm_csr), C.c_double, C.c_uint64, _DP, _DP, _DP, _DP]),
     "fm_vector_sum_by_key": (C.c_int, [_P, _I32P, C.c_int64, _DP, C.c_int32, _I32P, _DP, _I64P]),
     "fm_profile_enable": (C.c_int, [_P, C.c_int32]),
     "fm_profile_read": (C.c_int, [_P, C.c_char_p, C.c_int64, _DP, _I64P, C.c_int64, _I64P]),

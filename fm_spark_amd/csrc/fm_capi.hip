@@ -703,9 +703,11 @@ int fm_init_from_batch(fm_ctx* ctx, fm_batch* b, int64_t* n_present) {
   });
 }
 
-int fm_loss_grad(fm_ctx* ctx, const fm_csr* csr, double* pred, double* loss, double* dw, double* dv) {
+static int loss_grad_impl(fm_ctx* ctx, const fm_csr* csr, double fill_sd, uint64_t seed, double* pred, double* loss,
+                          double* dw, double* dv) {
   if (ctx && ctx->group) {
-    if (ctx->cfg.parallel == FM_PARALLEL_REPLICATED) return fm_loss_grad(group_member0(ctx), csr, pred, loss, dw, dv);
+    if (ctx->cfg.parallel == FM_PARALLEL_REPLICATED)
+      return loss_grad_impl(group_member0(ctx), csr, fill_sd, seed, pred, loss, dw, dv);
     set_error("fm_loss_grad needs the whole table (a replicated or single-table context)");
     return FM_ERR_ARG;
   }
@@ -713,7 +715,8 @@ int fm_loss_grad(fm_ctx* ctx, const fm_csr* csr, double* pred, double* loss, dou
     FM_REQUIRE(csr != nullptr, "null argument");
     if (csr->n_rows == 0 || csr->nnz == 0) return FM_OK;
     fm_batch* b = host_batch(ctx);
-    upload_batch(ctx, csr, b, true);
+    // the fill covers ids the table cannot hold too (ids >= num_features, the left outer join)
+    upload_batch(ctx, csr, b, fill_sd <= 0.0);
     const int64_t N = csr->nnz;
     const int k = ctx->cfg.k;
     DevBuf dpred, dloss, ddw, ddv, dabs;
@@ -724,17 +727,30 @@ int fm_loss_grad(fm_ctx* ctx, const fm_csr* csr, double* pred, double* loss, dou
     dabs.ensure(sizeof(int32_t));
     FM_HIP_CHECK(hipMemsetAsync(dabs.p, 0, sizeof(int32_t), ctx->stream));
     launch_loss_grad(ctx->view(), b->dev, ctx->cum_host.back(), ctx->cfg.w0, dpred.as<double>(), dloss.as<double>(),
-                     ddw.as<double>(), ddv.as<double>(), dabs.as<int32_t>(), ctx->stream);
+                     ddw.as<double>(), ddv.as<double>(), dabs.as<int32_t>(), ctx->stream, fill_sd, seed);
     int32_t absent = 0;
     FM_HIP_CHECK(hipMemcpyAsync(&absent, dabs.p, sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
     FM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
-    FM_REQUIRE(absent == 0, "batch references feature ids absent from the model");
+    FM_REQUIRE(fill_sd > 0.0 || absent == 0, "batch references feature ids absent from the model");
     if (pred) FM_HIP_CHECK(hipMemcpy(pred, dpred.p, sizeof(double) * N, hipMemcpyDeviceToHost));
     if (loss) FM_HIP_CHECK(hipMemcpy(loss, dloss.p, sizeof(double) * N, hipMemcpyDeviceToHost));
     if (dw) FM_HIP_CHECK(hipMemcpy(dw, ddw.p, sizeof(double) * N, hipMemcpyDeviceToHost));
     if (dv) FM_HIP_CHECK(hipMemcpy(dv, ddv.p, sizeof(double) * N * k, hipMemcpyDeviceToHost));
     return FM_OK;
   });
+}
+
+int fm_loss_grad(fm_ctx* ctx, const fm_csr* csr, double* pred, double* loss, double* dw, double* dv) {
+  return loss_grad_impl(ctx, csr, 0.0, 0, pred, loss, dw, dv);
+}
+
+int fm_calc_loss_grad(fm_ctx* ctx, const fm_csr* csr, double initial_sd, uint64_t seed, double* pred, double* loss,
+                      double* dw, double* dv) {
+  if (!(initial_sd > 0.0) || !std::isfinite(initial_sd)) {
+    set_error("requirement failed: initSd (initial Standard Deviation) must be > 0.0");
+    return FM_ERR_ARG;
+  }
+  return loss_grad_impl(ctx, csr, initial_sd, seed, pred, loss, dw, dv);
 }
 
 int fm_vector_sum_by_key(fm_ctx* ctx, const int32_t* keys, int64_t n, const double* vecs, int32_t k,

@@ -150,6 +150,11 @@ struct FwdOut {
   // [off[r] + P_r ch_c / ch_C, off[r] + P_r (ch_c + 1) / ch_C), P_r = off[r + 1] - off[r] (device off)
   const int64_t* ch_off = nullptr;
   int32_t ch_R = 0, ch_c = 0, ch_C = 1;
+  // loss-grad mode: fill_sd > 0 gives an entry whose id the model lacks its own N(0, fill_sd^2)
+  // w and v draws (calcLossGrad's coalesce with randn / udfInitVec, Model.scala:144-146,170-171),
+  // keyed by (fill_seed, entry index, column)
+  double fill_sd = 0.0;
+  uint64_t fill_seed = 0;
 };
 constexpr int kMaxChunkSources = 64;  // sources a chunked partial pass can split
 // partial_out != nullptr: the sharded owner's partial pass (fm_shard.hip): [pairs][kp] fp32 vectors
@@ -191,7 +196,8 @@ void launch_predict(const TableView& T, const BatchDev& b, double cumE, double w
 void launch_init_entries(const TableView& T, const uint32_t* col, int64_t n, uint64_t seed, double sd,
                          int32_t epoch, double cumE, hipStream_t st);
 void launch_loss_grad(const TableView& T, const BatchDev& b, double cumE, double w0, double* pred,
-                      double* loss, double* dw, double* dv, int32_t* absent_flag, hipStream_t st);
+                      double* loss, double* dw, double* dv, int32_t* absent_flag, hipStream_t st,
+                      double fill_sd = 0.0, uint64_t fill_seed = 0);
 void launch_segment_sum(const uint32_t* skeys, const uint32_t* svals, int64_t n, const double* vecs,
                         int32_t k, uint32_t* run_index, int32_t* out_keys, double* out_sums,
                         int64_t* n_out_dev, hipStream_t st);

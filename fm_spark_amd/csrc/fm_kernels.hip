@@ -77,6 +77,24 @@ __device__ __forceinline__ void current_row(const RowHdr& h, float4& v, float& w
   }
 }
 
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+// N(0, sd^2) draw keyed by (seed, feature id, factor f; f = -1 for w).  Box-Muller in fp64.
+__device__ __forceinline__ float gauss_draw(uint64_t seed, int64_t id, int f, double sd) {
+  const uint64_t c = ((uint64_t)id << 10) ^ (uint64_t)(f + 1);
+  const uint64_t h1 = splitmix64(seed ^ splitmix64(c));
+  const uint64_t h2 = splitmix64(h1 ^ 0x632BE59BD9B4E019ull);
+  const double u1 = (double)((h1 >> 11) + 1) * 0x1.0p-53;
+  const double u2 = (double)(h2 >> 11) * 0x1.0p-53;
+  const double g = sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2);
+  return (float)(g * sd);
+}
+
 // ------------------------------------------------------------------------ forward
 // MODE kTrain: the step's forward (S, {yhat, y}, loss partials).
 // MODE kPartial: the sharded owner's pass (fm_shard.hip).  "Samples" are (source rank, sample)
@@ -126,6 +144,15 @@ __global__ __launch_bounds__(kBlock, FM_FWD_MINW) void k_forward(TableView T, co
   const int kp = T.kp;
   const bool qok = g * 4 < kp;
   double loss_acc = 0.0, nloss = 0.0;
+  // calcLossGrad's draw for an entry whose id the model lacks (columns 4g .. 4g + 3 of k; f = -1: w)
+  auto fill_row = [&](int64_t e, float4& v, float& w) {
+    const int c = 4 * g, k = T.k;
+    v = make_float4(c + 0 < k ? gauss_draw(xo.fill_seed, e, c + 0, xo.fill_sd) : 0.f,
+                    c + 1 < k ? gauss_draw(xo.fill_seed, e, c + 1, xo.fill_sd) : 0.f,
+                    c + 2 < k ? gauss_draw(xo.fill_seed, e, c + 2, xo.fill_sd) : 0.f,
+                    c + 3 < k ? gauss_draw(xo.fill_seed, e, c + 3, xo.fill_sd) : 0.f);
+    w = gauss_draw(xo.fill_seed, e, -1, xo.fill_sd);
+  };
   // kPartial over one chunk of the pairs: the chunk's pairs numbered source by source
   __shared__ int64_t ch_base[PARTIAL ? kMaxChunkSources + 1 : 1], ch_start[PARTIAL ? kMaxChunkSources : 1];
   const bool chunked = PARTIAL && xo.ch_C > 1;
@@ -172,7 +199,8 @@ __global__ __launch_bounds__(kBlock, FM_FWD_MINW) void k_forward(TableView T, co
       float4 v[U];
 #pragma unroll
       for (int j = 0; j < U; ++j) {
-        if (ok[j]) {
+        // loss-grad with the fill takes ids beyond the table (the left outer join): absent rows
+        if (ok[j] && (MODE != kLossGrad || id[j] < (uint64_t)T.rows)) {
           h[j] = *T.hdr(id[j]);
           v[j] = qok ? reinterpret_cast<const float4*>(T.v(id[j]))[g] : make_float4(0.f, 0.f, 0.f, 0.f);
         } else {
@@ -185,6 +213,7 @@ __global__ __launch_bounds__(kBlock, FM_FWD_MINW) void k_forward(TableView T, co
         float w;
         if ((MODE == kPredict || PARTIAL) && g == 0 && h[j].t >= 0) ++npres;
         current_row(h[j], v[j], w, cumE);
+        if (MODE == kLossGrad && xo.fill_sd > 0.0 && ok[j] && h[j].t < 0) fill_row(eb + j * RPP, v[j], w);
         const double xd = x[j];
         // vfxi = v * x (Model.scala:179), VectorSum over the sample (:191)
         a0 += (double)v[j].x * xd; a1 += (double)v[j].y * xd;
@@ -232,10 +261,12 @@ __global__ __launch_bounds__(kBlock, FM_FWD_MINW) void k_forward(TableView T, co
       for (int64_t e = e0 + rs; e < e1; e += RPP) {
         const uint32_t id = col[e];
         const double xd = (double)__uint_as_float(ent[e].y);
-        const RowHdr h = *T.hdr(id);
-        float4 v = qok ? reinterpret_cast<const float4*>(T.v(id))[g] : make_float4(0.f, 0.f, 0.f, 0.f);
+        const bool inr = id < (uint64_t)T.rows;
+        const RowHdr h = inr ? *T.hdr(id) : RowHdr{0.f, -1, 0.0};
+        float4 v = qok && inr ? reinterpret_cast<const float4*>(T.v(id))[g] : make_float4(0.f, 0.f, 0.f, 0.f);
         float w;
         current_row(h, v, w, cumE);
+        if (xo.fill_sd > 0.0 && h.t < 0) fill_row(e, v, w);
         if (g == 0) {
           if (h.t < 0) *xo.absent = 1;
           xo.pred[e] = yhat;    // prediction (Model.scala:221)
@@ -918,24 +949,6 @@ __global__ __launch_bounds__(kBlock) void k_repl_apply(TableView T, const float*
 }
 
 // ---------------------------------------------------------------- table utilities
-__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
-  x += 0x9E3779B97F4A7C15ull;
-  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
-  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
-  return x ^ (x >> 31);
-}
-
-// N(0, sd^2) draw keyed by (seed, feature id, factor f; f = -1 for w).  Box-Muller in fp64.
-__device__ __forceinline__ float gauss_draw(uint64_t seed, int64_t id, int f, double sd) {
-  const uint64_t c = ((uint64_t)id << 10) ^ (uint64_t)(f + 1);
-  const uint64_t h1 = splitmix64(seed ^ splitmix64(c));
-  const uint64_t h2 = splitmix64(h1 ^ 0x632BE59BD9B4E019ull);
-  const double u1 = (double)((h1 >> 11) + 1) * 0x1.0p-53;
-  const double u2 = (double)(h2 >> 11) * 0x1.0p-53;
-  const double g = sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2);
-  return (float)(g * sd);
-}
-
 // ids != nullptr: the listed ids (those this shard owns); else every id in [id_begin, id_begin + n)
 // that this shard owns, walked slot by slot (i = the i-th owned id of the range)
 __global__ void k_init_random(TableView T, const int32_t* __restrict__ ids, int64_t n, int64_t id_begin,
@@ -1311,7 +1324,7 @@ void launch_predict(const TableView& T, const BatchDev& b, double cumE, double w
 }
 
 void launch_loss_grad(const TableView& T, const BatchDev& b, double cumE, double w0, double* pred, double* loss,
-                      double* dw, double* dv, int32_t* absent_flag, hipStream_t st) {
+                      double* dw, double* dv, int32_t* absent_flag, hipStream_t st, double fill_sd, uint64_t fill_seed) {
   FM_REQUIRE(T.shard_count == 1, "fm_loss_grad needs the whole table (shard_count == 1)");
   if (b.n_rows <= 0) return;
   StepParams p{};
@@ -1324,6 +1337,8 @@ void launch_loss_grad(const TableView& T, const BatchDev& b, double cumE, double
   xo.dw = dw;
   xo.dv = dv;
   xo.absent = absent_flag;
+  xo.fill_sd = fill_sd;
+  xo.fill_seed = fill_seed;
   StepWork unused;
   int64_t nblk = 0;
   launch_forward(T, b, unused, p, st, &nblk, nullptr, &xo);

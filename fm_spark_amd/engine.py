@@ -232,12 +232,19 @@ class FMContext:
                                            N.ptr(out, C.c_double)), "fm_predict_batch")
         return out[: b.n_rows]
 
-    def loss_grad(self, csr: N.CSRHost):
+    def loss_grad(self, csr: N.CSRHost, initial_sd: float | None = None, seed: int = 0):
+        """calcLossGrad per entry (pred, loss, deltaWi, deltaVi).  initial_sd: ids the model lacks
+        get their own N(0, initial_sd^2) draws per entry (fm_calc_loss_grad, keyed by seed); None:
+        such ids are an error (fm_loss_grad)."""
         n = max(csr.nnz, 1)
         pred, loss, dw = np.zeros(n), np.zeros(n), np.zeros(n)
         dv = np.zeros((n, self.k))
-        N.check(self._lib.fm_loss_grad(self.handle, C.byref(csr.c), N.ptr(pred, C.c_double), N.ptr(loss, C.c_double),
-                                       N.ptr(dw, C.c_double), N.ptr(dv, C.c_double)), "fm_loss_grad")
+        outs = (N.ptr(pred, C.c_double), N.ptr(loss, C.c_double), N.ptr(dw, C.c_double), N.ptr(dv, C.c_double))
+        if initial_sd is None:
+            N.check(self._lib.fm_loss_grad(self.handle, C.byref(csr.c), *outs), "fm_loss_grad")
+        else:
+            N.check(self._lib.fm_calc_loss_grad(self.handle, C.byref(csr.c), float(initial_sd), int(seed) & (2**64 - 1),
+                                                *outs), "fm_calc_loss_grad")
         m = csr.nnz
         return pred[:m], loss[:m], dw[:m], dv[:m]
 

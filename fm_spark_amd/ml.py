@@ -231,9 +231,11 @@ class FactorizationMachinesModel:
         pred = self._ctx.predict(csr, self.getMinLabel(), self.getMaxLabel())
         return dataset.with_column(self._params["predictionCol"], [float(p) for p in pred])
 
-    def calcLossGrad(self, dfSampleIndexed: DataFrame, initialSd: float) -> DataFrame:
+    def calcLossGrad(self, dfSampleIndexed: DataFrame, initialSd: float, seed: int = 0) -> DataFrame:
         """Model.scala:135-234: one row per active entry with columns label, sampleId,
-        featureId, prediction, loss, deltaWi, deltaVi (deltaVi before the (pred - label) factor)."""
+        featureId, prediction, loss, deltaWi, deltaVi (deltaVi before the (pred - label) factor).
+        Ids the model lacks get per-entry N(0, initialSd^2) draws (:144-146, 170-171); the
+        reference's draws are unseeded, here they are keyed by `seed` and the entry."""
         if not initialSd > 0.0:
             raise ValueError("requirement failed: initSd (initial Standard Deviation) must be > 0.0")
         fcol, lcol = self._params["featuresCol"], self._params["labelCol"]
@@ -241,7 +243,7 @@ class FactorizationMachinesModel:
         rp, col, val = _explode(dfSampleIndexed[fcol])
         labels = np.asarray(dfSampleIndexed[lcol], dtype=np.float64)
         csr = N.CSRHost(rp, col, val, labels)
-        pred, loss, dw, dv = self._ctx.loss_grad(csr)
+        pred, loss, dw, dv = self._ctx.loss_grad(csr, initial_sd=initialSd, seed=seed)
         rows = np.repeat(np.arange(len(labels)), np.diff(rp))
         sids = dfSampleIndexed["sampleId"] if "sampleId" in dfSampleIndexed.columns else list(range(len(labels)))
         return DataFrame({

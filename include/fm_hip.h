@@ -208,6 +208,13 @@ int fm_predict_batch(fm_ctx* ctx, fm_batch* batch, double min_label, double max_
  * unseeded random draw, Model.scala:170-171, which is never reached from fit). */
 int fm_loss_grad(fm_ctx* ctx, const fm_csr* csr, double* pred, double* loss, double* delta_w,
                  double* delta_v);
+/* calcLossGrad(dfSampleIndexed, initialSd) with the reference's fill for ids the model lacks
+ * (Model.scala:144-146, 170-171: coalesce(strength, randn() * initialSd) and udfInitVec() per
+ * joined row): every entry whose id is absent (or >= num_features) gets its own w and v drawn
+ * from N(0, initial_sd^2) -- keyed by (seed, entry index in CSR order, column), so a call is
+ * reproducible where the reference's draws are unseeded.  initial_sd must be > 0 (:136). */
+int fm_calc_loss_grad(fm_ctx* ctx, const fm_csr* csr, double initial_sd, uint64_t seed, double* pred,
+                      double* loss, double* delta_w, double* delta_v);
 /* VectorSum UDAF + groupBy (FactorizationMachines.scala:45-81): for every distinct key,
  * the element-wise fp64 sum of its k-vectors in input order.  Output ascending by key;
  * *n_out = number of distinct keys (<= n).  Runs the device sort + segmented reduction. */

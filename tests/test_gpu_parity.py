@@ -119,6 +119,61 @@ def test_loss_grad_matches_oracle(gpu, k):
     np.testing.assert_allclose(gdv, rdv, rtol=1e-5, atol=1e-9)
 
 
+def _gauss_draw(seed, e, f, sd):
+    """numpy restatement of the device's keyed N(0, sd^2) draw (fm_kernels.hip gauss_draw)."""
+    u64 = np.uint64
+    e = np.asarray(e, dtype=np.uint64)
+
+    def splitmix64(x):
+        x = x + u64(0x9E3779B97F4A7C15)
+        x = (x ^ (x >> u64(30))) * u64(0xBF58476D1CE4E5B9)
+        x = (x ^ (x >> u64(27))) * u64(0x94D049BB133111EB)
+        return x ^ (x >> u64(31))
+
+    with np.errstate(over="ignore"):
+        c = (e << u64(10)) ^ u64(f + 1)
+        h1 = splitmix64(u64(seed) ^ splitmix64(c))
+        h2 = splitmix64(h1 ^ u64(0x632BE59BD9B4E019))
+    u1 = ((h1 >> u64(11)) + u64(1)).astype(np.float64) * 2.0**-53
+    u2 = (h2 >> u64(11)).astype(np.float64) * 2.0**-53
+    return (np.sqrt(-2.0 * np.log(u1)) * np.cos(6.283185307179586 * u2) * sd).astype(np.float32)
+
+
+def test_calc_loss_grad_fills_absent_ids(gpu):
+    """calcLossGrad(df, initialSd) (Model.scala:135-234): entries whose id the model lacks --
+    absent rows and ids >= numFeatures alike (the left outer joins, :155-164) -- get their own
+    N(0, initialSd^2) strength and vector (coalesce with randn / udfInitVec, :144-146, 170-171),
+    keyed here by (seed, entry).  Checked against the oracle with every such entry relabelled as a
+    feature of its own holding the drawn row; fm_loss_grad without the fill still refuses them."""
+    from fm_spark_amd.engine import FMContext
+
+    F, k, sd, seed = 200, 5, 0.05, 7
+    csr, ids, w, V = make_problem(41, 250, F + 20, k, 7, hot=3)  # ids up to F + 19
+    keep = ids[(ids % 4 != 1) & (ids < F)]
+    ctx = FMContext(F, k)
+    ctx.load_tables(keep, w[keep], V[keep])
+    got = ctx.loss_grad(to_host(csr), initial_sd=sd, seed=seed)
+    with pytest.raises(Exception, match="absent from the model|>= num_features"):
+        ctx.loss_grad(to_host(csr))
+    e_abs = np.nonzero(~np.isin(csr.col, keep))[0]
+    assert len(e_abs) > 0 and (csr.col[e_abs] >= F).any()
+    col = csr.col.astype(np.int64).copy()
+    col[e_abs] = F + 20 + np.arange(len(e_abs))
+    model = R.Model.empty(F + 20 + len(e_abs), k)
+    model.load(keep, w[keep], V[keep])
+    wd = _gauss_draw(seed, e_abs, -1, sd).astype(np.float64)
+    Vd = np.stack([_gauss_draw(seed, e_abs, f, sd) for f in range(k)], axis=1).astype(np.float64)
+    model.load(col[e_abs], wd, Vd)
+    ref = R.loss_grad(model, R.CSR(csr.row_ptr, col.astype(np.int32), csr.val, csr.label))
+    for g, r in zip(got, ref):
+        np.testing.assert_allclose(g, r, rtol=1e-5, atol=1e-9)
+    again = ctx.loss_grad(to_host(csr), initial_sd=sd, seed=seed)
+    other = ctx.loss_grad(to_host(csr), initial_sd=sd, seed=seed + 1)
+    assert all(np.array_equal(a, b) for a, b in zip(got, again))
+    assert not np.array_equal(got[3], other[3])
+    ctx.close()
+
+
 def test_upload_unit_values_elided(gpu):
     """The host upload sends only the values that do not round to 1.0f (bit 31 of the id marks
     them) and the device rebuilds every entry's x: calcLossGrad's deltaWi = x (Model.scala:200)
