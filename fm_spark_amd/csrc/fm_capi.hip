@@ -194,7 +194,7 @@ fm_batch* host_batch(fm_ctx* ctx) {
 
 void reserve_work(fm_ctx* ctx, int64_t B, int64_t N) {
   StepWork& w = ctx->work;
-  w.S.ensure(sizeof(float) * (size_t)std::max<int64_t>(B, 1) * ctx->kp);
+  w.S.ensure(sizeof(float) * (size_t)std::max<int64_t>(B, 1) * s_rec_floats(ctx->kp));
   w.yl.ensure(sizeof(float2) * (size_t)std::max<int64_t>(B, 1));
   w.sort.ensure(std::max<int64_t>(N, 1));
   const int64_t nranges = (N + 255) / 256;  // update waves (fm_kernels.hip, kWaveEnt)

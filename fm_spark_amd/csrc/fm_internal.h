@@ -113,6 +113,15 @@ struct BatchDev {
   DevBuf row_ptr, col, ent, label;  // int64 [B+1], uint32 [N] feature slot, uint2 [N], double [B]
 };
 
+// The single-table step's per-sample record: S (kp floats) and, for kp <= 16, the sample's
+// {r, yhat} in the same 64-B (kp <= 12) or 128-B (kp = 16) record, so the update's S gather and
+// {r, yhat} load hit one line (FM_S_REC); wider rows keep {r, yhat} in StepWork::yl.
+#ifndef FM_S_REC
+#define FM_S_REC 1
+#endif
+inline bool s_rec_yl(int kp) { return FM_S_REC && kp <= 16; }
+inline int s_rec_floats(int kp) { return s_rec_yl(kp) ? (kp + 2 <= 16 ? 16 : 32) : kp; }
+
 struct StepWork {
   DevBuf S;         // [B * kp] float: per-sample vfxiSum
   DevBuf yl;        // [B] float2 {r, yhat}: r = yhat - y formed in fp64 from the fp64 label, then rounded

@@ -132,7 +132,8 @@ __global__ __launch_bounds__(kBlock, FM_FWD_MINW) void k_forward(TableView T, co
                                                     const uint2* __restrict__ ent,
                                                     const double* __restrict__ label, int64_t B,
                                                     double w0, double cumE, float* __restrict__ S_out,
-                                                    float2* __restrict__ yl_out, double2* __restrict__ loss_part,
+                                                    float2* __restrict__ yl_out, int64_t sstr, int64_t ystr,
+                                                    double2* __restrict__ loss_part,
                                                     FwdOut xo) {
   constexpr bool PARTIAL = MODE == kPartial;
   constexpr int RPP = TEAM / GS;  // entries per pass
@@ -239,9 +240,9 @@ __global__ __launch_bounds__(kBlock, FM_FWD_MINW) void k_forward(TableView T, co
     }
     if (PARTIAL) {  // vectors [pair][kp] in S_out, scalars {sum v^2 x^2, sum w x} in yl_out
       if (rs == 0 && qok)
-        *reinterpret_cast<float4*>(S_out + s * kp + g * 4) = make_float4((float)a0, (float)a1, (float)a2, (float)a3);
+        *reinterpret_cast<float4*>(S_out + s * sstr + g * 4) = make_float4((float)a0, (float)a1, (float)a2, (float)a3);
       if (tl == 0) {
-        yl_out[s] = make_float2((float)vv, (float)wx);
+        yl_out[s * ystr] = make_float2((float)vv, (float)wx);
         if (xo.pcount) xo.pcount[s] = npres;
       }
       continue;
@@ -283,11 +284,11 @@ __global__ __launch_bounds__(kBlock, FM_FWD_MINW) void k_forward(TableView T, co
       continue;
     }
     if (rs == 0 && qok)
-      *reinterpret_cast<float4*>(S_out + s * kp + g * 4) = make_float4((float)a0, (float)a1, (float)a2, (float)a3);
+      *reinterpret_cast<float4*>(S_out + s * sstr + g * 4) = make_float4((float)a0, (float)a1, (float)a2, (float)a3);
     if (tl == 0) {
       const double y = label[s];
       // r = pred - label in fp64 (SGD.scala:146), rounded once: relative error 2^-24 of r itself
-      yl_out[s] = make_float2((float)(yhat - y), (float)yhat);
+      yl_out[s * ystr] = make_float2((float)(yhat - y), (float)yhat);
       if (e1 > e0) {
         const double d = yhat - y;
         loss_acc += d * d;  // pow(pred - label, 2.0), Model.scala:230
@@ -338,6 +339,10 @@ struct SegArgs {
 
 constexpr uint32_t kFValid = 1u, kFEnd = 2u, kFStart = 4u;
 
+#ifndef FM_UPD_YL2
+#define FM_UPD_YL2 1  // the sample's {r, yhat} loaded in phase 2 with its S row (same 64/128-B record
+#endif                // in the single-table layout) instead of one lane per entry in phase 1
+
 // Lane-group geometry: Q lanes per entry, NF float4 column quads per lane (columns
 // 4 (q + Q n) .. + 3), NG = 64 / Q groups per wave, RL = 256 / NG entries per group.
 template <int Q, int NF>
@@ -350,7 +355,8 @@ struct UpdGeom {
                                           // row against bank conflicts (no pad column: at k = 32 the
                                           // pad cost the fourth block per CU)
   static __device__ __forceinline__ int at(int row, int g) { return row * NG + (g ^ (row & (NG - 1))); }
-  static constexpr int IMG = IMG_N * 36;  // {t, b} f64x2 | g_w f64 | {slot, flags} | sample
+  // FM_UPD_YL2: {slot, flags} | sample | x (16 B); else {t, b} f64x2 | g_w f64 | {slot, flags} | sample
+  static constexpr int IMG = IMG_N * (FM_UPD_YL2 ? 16 : 36);
   static constexpr int PIECES = 2 * NG * PIECE * 8;
   static constexpr int BYTES = IMG > PIECES ? IMG : PIECES;
 };
@@ -362,12 +368,12 @@ struct UpdGeom {
 // when the run closes.  g_w = x * yhat - y per entry (SGD.scala:145).
 //
 // One wave per 256 sorted entries.
-//  Phase 1, one lane per entry: run structure (ballots) and the entry's scalars
-//    t = x r, x^2 r and x yhat - y (fp64) from the sample's {yhat, y}, staged in the wave's LDS
-//    image (36 B per entry, step-major so that a step's entries are contiguous).
+//  Phase 1, one lane per entry: run structure (ballots), staged in the wave's LDS image with the
+//    entry's sample and x (16 B per entry, step-major so that a step's entries are contiguous).
 //  Phase 2, NG lane groups of Q lanes (float4 column quads per lane): group g walks its RL
-//    consecutive entries in order, accumulating A, b and g_w in fp64 from the S rows of D
-//    entries loaded ahead (with the V row + header of those that close a run).  A run that
+//    consecutive entries in order, accumulating A, b and g_w in fp64 from the S rows and {r, yhat}
+//    of D entries loaded ahead (one record per sample in the single-table step, FM_S_REC; with
+//    the V row + header of those that close a run): t = x r, x^2 r and x yhat - y per entry.  A run that
 //    begins and closes inside the group's entries is applied in place (update + L1,
 //    SGD.scala:150-181, or its gradient emitted in replicated mode).
 //  Phase 3: the pieces cut by group boundaries meet in LDS: the group holding a run's start
@@ -398,10 +404,16 @@ __global__ __launch_bounds__(kBlock, NF == 1 ? FM_UPD_MINW : 1) void k_segment_u
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   unsigned char* smem = smem_all[wave];
   constexpr int IN = Geo::IMG_N;
+#if FM_UPD_YL2
+  uint2* img_k = reinterpret_cast<uint2*>(smem);                 // {slot, flags}
+  int* img_s = reinterpret_cast<int*>(smem + IN * 8);            // sample
+  float* img_x = reinterpret_cast<float*>(smem + IN * 12);       // x
+#else
   double2* img_d = reinterpret_cast<double2*>(smem);            // {x r, x^2 r}
   double* img_w = reinterpret_cast<double*>(smem + IN * 16);     // x yhat - y
   uint2* img_k = reinterpret_cast<uint2*>(smem + IN * 24);       // {slot, flags}
   int* img_s = reinterpret_cast<int*>(smem + IN * 32);           // sample
+#endif
   int* pflag = pflag_all[wave];
   const TableView& T = a.T;
   const int kp = T.kp;
@@ -434,7 +446,9 @@ __global__ __launch_bounds__(kBlock, NF == 1 ? FM_UPD_MINW : 1) void k_segment_u
     }
     const uint32_t before = base > 0 ? a.skeys[base - 1] : kNone;
     const uint32_t after = base + kWaveEnt < a.N ? a.skeys[base + kWaveEnt] : kNone;
+#if !FM_UPD_YL2
     float2 yl[NP];
+#endif
 #pragma unroll
     for (int i = 0; i < NP; ++i) {
       const uint32_t up = __shfl_up(key[i], 1);
@@ -450,7 +464,11 @@ __global__ __launch_bounds__(kBlock, NF == 1 ? FM_UPD_MINW : 1) void k_segment_u
       const int l = li(i * 64 + lane);
       img_k[l] = make_uint2(key[i], (valid ? kFValid : 0u) | (end ? kFEnd : 0u) | (st ? kFStart : 0u));
       img_s[l] = (int)en[i].x;
+#if FM_UPD_YL2
+      img_x[l] = __uint_as_float(en[i].y);
+#else
       yl[i] = valid ? a.yl[(int64_t)en[i].x * a.yl_stride] : make_float2(0.f, 0.f);
+#endif
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -460,7 +478,8 @@ __global__ __launch_bounds__(kBlock, NF == 1 ? FM_UPD_MINW : 1) void k_segment_u
     const int g = lane / Q, q = lane % Q;
     // two buffers of D entries: the rows of the next step are in flight while a step is consumed
     float4 Sp0[D][NF], Vp0[D][NF], Hp0[D], Sp1[D][NF], Vp1[D][NF], Hp1[D];
-    auto prefetch = [&](int b0, float4 (&Sp)[D][NF], float4 (&Vp)[D][NF], float4 (&Hp)[D]) {
+    float2 Yp0[D], Yp1[D];  // FM_UPD_YL2: the samples' {r, yhat}
+    auto prefetch = [&](int b0, float4 (&Sp)[D][NF], float4 (&Vp)[D][NF], float4 (&Hp)[D], float2 (&Yp)[D]) {
 #pragma unroll
       for (int u = 0; u < D; ++u) {
         const int l = Geo::at(b0 + u, g);  // li(g * RL + b0 + u)
@@ -477,9 +496,11 @@ __global__ __launch_bounds__(kBlock, NF == 1 ? FM_UPD_MINW : 1) void k_segment_u
         }
         Hp[u] = (valid && end && !FM_ABL_NOROW) ? *reinterpret_cast<const float4*>(T.hdr(kf.x))
                                : make_float4(0.f, __int_as_float(-1), 0.f, 0.f);
+        if (FM_UPD_YL2) Yp[u] = valid ? a.yl[(int64_t)s * a.yl_stride] : make_float2(0.f, 0.f);
       }
     };
-    prefetch(0, Sp0, Vp0, Hp0);  // in flight together with phase 1's {yhat, y} reads
+    prefetch(0, Sp0, Vp0, Hp0, Yp0);  // in flight together with phase 1's {yhat, y} reads
+#if !FM_UPD_YL2
 #pragma unroll
     for (int i = 0; i < NP; ++i) {
       const int l = li(i * 64 + lane);
@@ -492,6 +513,7 @@ __global__ __launch_bounds__(kBlock, NF == 1 ? FM_UPD_MINW : 1) void k_segment_u
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#endif
 
     // Paired row stores (kp = 4Q, Q = 2 or 4: records of V (16Q B) + a header granule of the same
     // size, i.e. k = 5..8 in 64 B and k = 13..16 in 128 B): the new row of a run closed in phase 2
@@ -592,14 +614,24 @@ __global__ __launch_bounds__(kBlock, NF == 1 ? FM_UPD_MINW : 1) void k_segment_u
     int hst = 0;  // the group's head piece: 0 none, 1 open through the group's end, 2 closed
     bool started = false, open = false;
     uint32_t lastkey = kNone;
-    auto consume = [&](int b0, const float4 (&Sp)[D][NF], const float4 (&Vp)[D][NF], const float4 (&Hp)[D]) {
+    auto consume = [&](int b0, const float4 (&Sp)[D][NF], const float4 (&Vp)[D][NF], const float4 (&Hp)[D],
+                       const float2 (&Yp)[D]) {
 #pragma unroll
       for (int u = 0; u < D; ++u) {
         const int l = Geo::at(b0 + u, g);
         const uint2 kf = img_k[l];
         if (kf.y & kFValid) {
+#if FM_UPD_YL2
+        // t = x r, x^2 r and g_w = deltaWi * pred - label = x yhat - (yhat - r) (SGD.scala:145)
+        const double xd = (double)img_x[l], rj = (double)Yp[u].x, yh = (double)Yp[u].y;
+        const double t = xd * rj;
+        const double2 tb = make_double2(t, (xd * xd) * rj);
+        const double gwe = (xd - 1.0) * yh + rj;
+#else
         const double2 tb = img_d[l];
         const double t = tb.x;
+        const double gwe = img_w[l];
+#endif
         if (kf.y & kFStart) started = true;
         open = true;
         lastkey = kf.x;
@@ -611,7 +643,7 @@ __global__ __launch_bounds__(kBlock, NF == 1 ? FM_UPD_MINW : 1) void k_segment_u
           acc[4 * n + 3] = fma((double)Sp[u][n].w, t, acc[4 * n + 3]);
         }
         accb += tb.y;
-        accw += img_w[l];
+        accw += gwe;
         if (kf.y & kFEnd) {
           if (started) {
             close_run(kf.x, Vp[u], Hp[u], acc, accb, accw, paired);
@@ -635,11 +667,11 @@ __global__ __launch_bounds__(kBlock, NF == 1 ? FM_UPD_MINW : 1) void k_segment_u
     };
 #pragma unroll 1
     for (int b0 = 0; b0 < RL; b0 += 2 * D) {
-      if (b0 + D < RL) prefetch(b0 + D, Sp1, Vp1, Hp1);
-      consume(b0, Sp0, Vp0, Hp0);
+      if (b0 + D < RL) prefetch(b0 + D, Sp1, Vp1, Hp1, Yp1);
+      consume(b0, Sp0, Vp0, Hp0, Yp0);
       if (b0 + D < RL) {
-        if (b0 + 2 * D < RL) prefetch(b0 + 2 * D, Sp0, Vp0, Hp0);
-        consume(b0 + D, Sp1, Vp1, Hp1);
+        if (b0 + 2 * D < RL) prefetch(b0 + 2 * D, Sp0, Vp0, Hp0, Yp0);
+        consume(b0 + D, Sp1, Vp1, Hp1, Yp1);
       }
     }
     const bool tail = open && started;  // the open piece began in this group
@@ -1121,25 +1153,28 @@ void launch_fwd_t(const TableView& T, const BatchDev& b, StepWork& w, const Step
   if (partial_out) {  // [n_rows][kp] fp32 vectors, then [n_rows] float2 scalars (xo: the present counts)
     hipLaunchKernelGGL((k_forward<GS, TEAM, kPartial, U>), grid, blk, 0, st, T, b.row_ptr.as<int64_t>(),
                        b.col.as<uint32_t>(), b.ent.as<uint2>(), nullptr, b.n_rows, p.w0, p.cumE, partial_out,
-                       reinterpret_cast<float2*>(partial_out + b.n_rows * T.kp), nullptr, xo ? *xo : none);
+                       reinterpret_cast<float2*>(partial_out + b.n_rows * T.kp), (int64_t)T.kp, (int64_t)1, nullptr,
+                       xo ? *xo : none);
     return;
   }
   if (xo && xo->mode == kPredict) {
     hipLaunchKernelGGL((k_forward<GS, TEAM, kPredict, U>), grid, blk, 0, st, T, b.row_ptr.as<int64_t>(),
                        b.col.as<uint32_t>(), b.ent.as<uint2>(), nullptr, b.n_rows, p.w0, p.cumE, nullptr, nullptr,
-                       nullptr, *xo);
+                       (int64_t)T.kp, (int64_t)1, nullptr, *xo);
     return;
   }
   if (xo && xo->mode == kLossGrad) {
     hipLaunchKernelGGL((k_forward<GS, TEAM, kLossGrad, U>), grid, blk, 0, st, T, b.row_ptr.as<int64_t>(),
                        b.col.as<uint32_t>(), b.ent.as<uint2>(), b.label.as<double>(), b.n_rows, p.w0, p.cumE, nullptr,
-                       nullptr, nullptr, *xo);
+                       nullptr, (int64_t)T.kp, (int64_t)1, nullptr, *xo);
     return;
   }
   w.loss_part.ensure(sizeof(double2) * blocks);
   hipLaunchKernelGGL((k_forward<GS, TEAM, kTrain, U>), grid, blk, 0, st, T, b.row_ptr.as<int64_t>(),
                      b.col.as<uint32_t>(), b.ent.as<uint2>(), b.label.as<double>(), b.n_rows, p.w0, p.cumE,
-                     w.S.as<float>(), w.yl.as<float2>(), w.loss_part.as<double2>(), none);
+                     w.S.as<float>(), s_rec_yl(T.kp) ? reinterpret_cast<float2*>(w.S.as<float>() + T.kp) : w.yl.as<float2>(),
+                     (int64_t)s_rec_floats(T.kp), s_rec_yl(T.kp) ? (int64_t)s_rec_floats(T.kp) / 2 : (int64_t)1,
+                     w.loss_part.as<double2>(), none);
 }
 
 }  // namespace
@@ -1185,7 +1220,9 @@ void launch_forward(const TableView& T, const BatchDev& b, StepWork& w, const St
 void launch_segment_update(const TableView& T, const BatchDev& b, StepWork& w, const StepParams& p,
                            const uint32_t* skeys, const uint2* sents, int64_t n_fwd_blocks,
                            double* stats_out, hipStream_t st, float* emit) {
-  SegSource src{w.S.as<float>(), T.kp, w.yl.as<float2>(), 1};
+  SegSource src{w.S.as<float>(), s_rec_floats(T.kp),
+                 s_rec_yl(T.kp) ? reinterpret_cast<const float2*>(w.S.as<float>() + T.kp) : w.yl.as<float2>(),
+                 s_rec_yl(T.kp) ? s_rec_floats(T.kp) / 2 : 1};
   launch_segment_update(T, b.nnz, src, w, p, skeys, sents, n_fwd_blocks, stats_out, st, emit);
 }
 
