@@ -339,6 +339,9 @@ struct SegArgs {
 
 constexpr uint32_t kFValid = 1u, kFEnd = 2u, kFStart = 4u;
 
+#ifndef FM_UPD_LEAN
+#define FM_UPD_LEAN 1  // single-buffered loads + head pieces in LDS: 90 VGPRs, 5 waves/SIMD at k = 16 (step -3.5 %)
+#endif
 #ifndef FM_UPD_YL2
 #define FM_UPD_YL2 1  // the sample's {r, yhat} loaded in phase 2 with its S row (same 64/128-B record
 #endif                // in the single-table layout) instead of one lane per entry in phase 1
@@ -358,7 +361,10 @@ struct UpdGeom {
   // FM_UPD_YL2: {slot, flags} | sample | x (16 B); else {t, b} f64x2 | g_w f64 | {slot, flags} | sample
   static constexpr int IMG = IMG_N * (FM_UPD_YL2 ? 16 : 36);
   static constexpr int PIECES = 2 * NG * PIECE * 8;
-  static constexpr int BYTES = IMG > PIECES ? IMG : PIECES;
+  // FM_UPD_LEAN: the groups' head pieces go to their own region after the image as they close
+  // (one slot per group) instead of living in registers until phase 3
+  static constexpr int HEADS = NG * PIECE * 8;
+  static constexpr int BYTES = FM_UPD_LEAN ? IMG + HEADS : (IMG > PIECES ? IMG : PIECES);
 };
 
 // The interaction gradient of one entry (Model.scala:201-204, SGD.scala:146) is
@@ -607,10 +613,29 @@ __global__ __launch_bounds__(kBlock, NF == 1 ? FM_UPD_MINW : 1) void k_segment_u
       pend_slot = kNone;
     };
 
+#if FM_UPD_LEAN
+    double* heads = reinterpret_cast<double*>(smem + Geo::IMG);  // [NG][PIECE]
+    auto put_head = [&](const double (&A)[C], double b, double gw) {
+      double* ph = heads + g * PIECE;
+#pragma unroll
+      for (int n = 0; n < NF; ++n)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) ph[1 + 4 * (q + Q * n) + j] = A[4 * n + j];
+      if (q == 0) {
+        ph[0] = gw;
+        ph[PIECE - 1] = b;
+      }
+    };
+    double acc[C];
+#pragma unroll
+    for (int j = 0; j < C; ++j) acc[j] = 0.0;
+    double accb = 0.0, accw = 0.0;
+#else
     double acc[C], hacc[C];
 #pragma unroll
     for (int j = 0; j < C; ++j) acc[j] = hacc[j] = 0.0;
     double accb = 0.0, accw = 0.0, hb = 0.0, hw = 0.0;
+#endif
     int hst = 0;  // the group's head piece: 0 none, 1 open through the group's end, 2 closed
     bool started = false, open = false;
     uint32_t lastkey = kNone;
@@ -648,10 +673,14 @@ __global__ __launch_bounds__(kBlock, NF == 1 ? FM_UPD_MINW : 1) void k_segment_u
           if (started) {
             close_run(kf.x, Vp[u], Hp[u], acc, accb, accw, paired);
           } else {  // the head piece closes
+#if FM_UPD_LEAN
+            put_head(acc, accb, accw);
+#else
 #pragma unroll
             for (int j = 0; j < C; ++j) hacc[j] = acc[j];
             hb = accb;
             hw = accw;
+#endif
             hst = 2;
           }
 #pragma unroll
@@ -665,6 +694,13 @@ __global__ __launch_bounds__(kBlock, NF == 1 ? FM_UPD_MINW : 1) void k_segment_u
         if (kPairCfg && paired) flush_pair();  // converged: every lane of the wave
       }
     };
+#if FM_UPD_LEAN
+#pragma unroll 1
+    for (int b0 = D; b0 <= RL; b0 += D) {  // the first step's loads are in flight already
+      consume(b0 - D, Sp0, Vp0, Hp0, Yp0);
+      if (b0 < RL) prefetch(b0, Sp0, Vp0, Hp0, Yp0);
+    }
+#else
 #pragma unroll 1
     for (int b0 = 0; b0 < RL; b0 += 2 * D) {
       if (b0 + D < RL) prefetch(b0 + D, Sp1, Vp1, Hp1, Yp1);
@@ -674,12 +710,17 @@ __global__ __launch_bounds__(kBlock, NF == 1 ? FM_UPD_MINW : 1) void k_segment_u
         consume(b0 + D, Sp1, Vp1, Hp1, Yp1);
       }
     }
+#endif
     const bool tail = open && started;  // the open piece began in this group
     if (open && !started) {             // the head piece runs through the group's end
+#if FM_UPD_LEAN
+      put_head(acc, accb, accw);
+#else
 #pragma unroll
       for (int j = 0; j < C; ++j) hacc[j] = acc[j];
       hb = accb;
       hw = accw;
+#endif
       hst = 1;
     }
 
@@ -687,7 +728,12 @@ __global__ __launch_bounds__(kBlock, NF == 1 ? FM_UPD_MINW : 1) void k_segment_u
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#if FM_UPD_LEAN
+    double* pc = heads;  // head piece of group g at pc + g * PIECE, written in phase 2
+    constexpr int PS = 1;
+#else
     double* pc = reinterpret_cast<double*>(smem);
+    constexpr int PS = 2;
     if (hst) {
       double* ph = pc + (2 * g) * PIECE;
 #pragma unroll
@@ -699,6 +745,7 @@ __global__ __launch_bounds__(kBlock, NF == 1 ? FM_UPD_MINW : 1) void k_segment_u
         ph[PIECE - 1] = hb;
       }
     }
+#endif
     if (q == 0) pflag[2 * g] = hst;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -708,7 +755,7 @@ __global__ __launch_bounds__(kBlock, NF == 1 ? FM_UPD_MINW : 1) void k_segment_u
       for (int g2 = from; g2 < NG; ++g2) {
         const int f2 = pflag[2 * g2];
         if (f2 == 0) return false;  // unreachable: an open piece always continues into a head piece
-        const double* ph = pc + (2 * g2) * PIECE;
+        const double* ph = pc + (PS * g2) * PIECE;
 #pragma unroll
         for (int n = 0; n < NF; ++n)
 #pragma unroll
@@ -738,6 +785,13 @@ __global__ __launch_bounds__(kBlock, NF == 1 ? FM_UPD_MINW : 1) void k_segment_u
       }
     };
     if (g == 0 && hst) {  // the wave's first piece: its run began in an earlier wave
+#if FM_UPD_LEAN
+      double hacc[C], hb = pc[PIECE - 1], hw = pc[0];
+#pragma unroll
+      for (int n = 0; n < NF; ++n)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) hacc[4 * n + j] = pc[1 + 4 * (q + Q * n) + j];
+#endif
       if (hst == 1) extend(hacc, hb, hw, 1);
       write_part(0, hacc, hb, hw);
     }
