@@ -50,8 +50,8 @@ constexpr int kUpdD4 = FM_UPD_D4;
 #endif
 constexpr int kUpdD2 = FM_UPD_D2;
 
-// experiment switches (tools/variants.sh; all 0 in the product build): drop the update's S-row
-// loads, row loads or row stores to measure what each costs
+// experiment switches (tools/variants.sh; all 0 in the product build): drop the update's
+// per-sample record loads (S row and {r, yhat}), row loads or row stores to measure what each costs
 #ifndef FM_ABL_NOS
 #define FM_ABL_NOS 0
 #endif
@@ -502,7 +502,7 @@ __global__ __launch_bounds__(kBlock, NF == 1 ? FM_UPD_MINW : 1) void k_segment_u
         }
         Hp[u] = (valid && end && !FM_ABL_NOROW) ? *reinterpret_cast<const float4*>(T.hdr(kf.x))
                                : make_float4(0.f, __int_as_float(-1), 0.f, 0.f);
-        if (FM_UPD_YL2) Yp[u] = valid ? a.yl[(int64_t)s * a.yl_stride] : make_float2(0.f, 0.f);
+        if (FM_UPD_YL2) Yp[u] = valid && !FM_ABL_NOS ? a.yl[(int64_t)s * a.yl_stride] : make_float2(0.f, 0.f);
       }
     };
     prefetch(0, Sp0, Vp0, Hp0, Yp0);  // in flight together with phase 1's {yhat, y} reads
