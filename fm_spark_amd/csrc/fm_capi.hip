@@ -144,6 +144,7 @@ static bool batch_fits(const fm_batch* b, const Staged& g) {
   return b->dev.row_ptr.bytes >= sizeof(int64_t) * (g.B + 1) &&
          b->dev.col.bytes >= sizeof(uint32_t) * std::max<int64_t>(g.N, 4) + 16 &&
          b->dev.ent.bytes >= sizeof(uint32_t) * 2 * std::max<int64_t>(g.N, 4) + 16 &&
+         b->dev.xs.bytes >= sizeof(float) * std::max<int64_t>(g.N, 4) + 16 &&
          b->dev.label.bytes >= sizeof(double) * std::max<int64_t>(g.B, 4) + 16 &&
          b->up.bytes >= g.o_x + sizeof(float) * g.N + 16;
 }
@@ -161,6 +162,7 @@ static void copy_staged(fm_ctx* ctx, const Staged& g, const Pinned& pin, fm_batc
   b->dev.row_ptr.ensure(sizeof(int64_t) * (B + 1));
   b->dev.col.ensure(sizeof(uint32_t) * std::max<int64_t>(N, 4) + 16);
   b->dev.ent.ensure(sizeof(uint32_t) * 2 * std::max<int64_t>(N, 4) + 16);
+  b->dev.xs.ensure(sizeof(float) * std::max<int64_t>(N, 4) + 16);
   b->dev.label.ensure(sizeof(double) * std::max<int64_t>(B, 4) + 16);
   b->up.ensure(g.o_x + sizeof(float) * N + 16);
   FM_HIP_CHECK(hipMemcpyAsync(b->up.p, pin.p, g.bytes, hipMemcpyHostToDevice, st));
@@ -173,7 +175,7 @@ static void copy_staged(fm_ctx* ctx, const Staged& g, const Pinned& pin, fm_batc
   launch_explode(reinterpret_cast<const int64_t*>(up), reinterpret_cast<const double*>(up + g.o_lab),
                  reinterpret_cast<const int32_t*>(up + g.o_xoff), reinterpret_cast<const uint32_t*>(up + g.o_col),
                  reinterpret_cast<const float*>(up + g.o_x), B, N, b->dev.row_ptr.as<int64_t>(),
-                 b->dev.label.as<double>(), b->dev.col.as<uint32_t>(), b->dev.ent.as<uint2>(), st);
+                 b->dev.label.as<double>(), b->dev.col.as<uint32_t>(), b->dev.ent.as<uint2>(), b->dev.xs.as<float>(), st);
 }
 
 // Synchronous upload (fm_batch_create, fm_predict, fm_loss_grad): staged in the context's

@@ -118,6 +118,7 @@ struct fm_batch {
     dev.row_ptr.release();
     dev.col.release();
     dev.ent.release();
+    dev.xs.release();
     dev.label.release();
   }
 };

@@ -111,6 +111,7 @@ void radix_sort_pairs64_bits(SortWork& w, const uint32_t* keys_in, const uint2* 
 struct BatchDev {
   int64_t n_rows = 0, nnz = 0;
   DevBuf row_ptr, col, ent, label;  // int64 [B+1], uint32 [N] feature slot, uint2 [N], double [B]
+  DevBuf xs;                         // fp32 [N]: x alone, the forward's stream (8 B per entry with col)
 };
 
 // The single-table step's per-sample record: S (kp floats) and, for kp <= 16, the sample's
@@ -216,6 +217,6 @@ void launch_count_present(const TableView& T, int64_t* out, hipStream_t st);
 // bits} rebuilt from row_ptr and the compact values (the explode of Model.scala:148-153)
 void launch_explode(const int64_t* row_ptr_in, const double* label_in, const int32_t* xoff, const uint32_t* col_in,
                     const float* x_in, int64_t B, int64_t N, int64_t* row_ptr, double* label, uint32_t* col, uint2* ent,
-                    hipStream_t st);
+                    float* xs, hipStream_t st);
 
 }  // namespace fmhip

@@ -129,7 +129,7 @@ constexpr int kTrain = 0, kPartial = 1, kPredict = 2, kLossGrad = 3;
 template <int GS, int TEAM, int MODE, int U>
 __global__ __launch_bounds__(kBlock, FM_FWD_MINW) void k_forward(TableView T, const int64_t* __restrict__ row_ptr,
                                                     const uint32_t* __restrict__ col,
-                                                    const uint2* __restrict__ ent,
+                                                    const uint2* __restrict__ ent, const float* __restrict__ xs,
                                                     const double* __restrict__ label, int64_t B,
                                                     double w0, double cumE, float* __restrict__ S_out,
                                                     float2* __restrict__ yl_out, int64_t sstr, int64_t ystr,
@@ -194,7 +194,8 @@ __global__ __launch_bounds__(kBlock, FM_FWD_MINW) void k_forward(TableView T, co
         ok[j] = e < e1;
         id[j] = ok[j] ? ld_stream(col + e, FM_NT_CSR) : 0u;
         if (MODE == kPredict) ok[j] = ok[j] && id[j] < (uint64_t)T.rows;
-        x[j] = ok[j] ? __uint_as_float(ld_stream(ent + e, FM_NT_CSR).y) : 0.f;
+        // the batch's x stream (4 B per entry); the partial pass's entries carry x themselves
+        x[j] = ok[j] ? (PARTIAL ? __uint_as_float(ld_stream(ent + e, FM_NT_CSR).y) : ld_stream(xs + e, FM_NT_CSR)) : 0.f;
       }
       RowHdr h[U];
       float4 v[U];
@@ -261,7 +262,7 @@ __global__ __launch_bounds__(kBlock, FM_FWD_MINW) void k_forward(TableView T, co
       const int k = T.k;
       for (int64_t e = e0 + rs; e < e1; e += RPP) {
         const uint32_t id = col[e];
-        const double xd = (double)__uint_as_float(ent[e].y);
+        const double xd = (double)xs[e];
         const bool inr = id < (uint64_t)T.rows;
         const RowHdr h = inr ? *T.hdr(id) : RowHdr{0.f, -1, 0.0};
         float4 v = qok && inr ? reinterpret_cast<const float4*>(T.v(id))[g] : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1206,26 +1207,26 @@ void launch_fwd_t(const TableView& T, const BatchDev& b, StepWork& w, const Step
   const FwdOut none{};
   if (partial_out) {  // [n_rows][kp] fp32 vectors, then [n_rows] float2 scalars (xo: the present counts)
     hipLaunchKernelGGL((k_forward<GS, TEAM, kPartial, U>), grid, blk, 0, st, T, b.row_ptr.as<int64_t>(),
-                       b.col.as<uint32_t>(), b.ent.as<uint2>(), nullptr, b.n_rows, p.w0, p.cumE, partial_out,
+                       b.col.as<uint32_t>(), b.ent.as<uint2>(), nullptr, nullptr, b.n_rows, p.w0, p.cumE, partial_out,
                        reinterpret_cast<float2*>(partial_out + b.n_rows * T.kp), (int64_t)T.kp, (int64_t)1, nullptr,
                        xo ? *xo : none);
     return;
   }
   if (xo && xo->mode == kPredict) {
     hipLaunchKernelGGL((k_forward<GS, TEAM, kPredict, U>), grid, blk, 0, st, T, b.row_ptr.as<int64_t>(),
-                       b.col.as<uint32_t>(), b.ent.as<uint2>(), nullptr, b.n_rows, p.w0, p.cumE, nullptr, nullptr,
+                       b.col.as<uint32_t>(), b.ent.as<uint2>(), b.xs.as<float>(), nullptr, b.n_rows, p.w0, p.cumE, nullptr, nullptr,
                        (int64_t)T.kp, (int64_t)1, nullptr, *xo);
     return;
   }
   if (xo && xo->mode == kLossGrad) {
     hipLaunchKernelGGL((k_forward<GS, TEAM, kLossGrad, U>), grid, blk, 0, st, T, b.row_ptr.as<int64_t>(),
-                       b.col.as<uint32_t>(), b.ent.as<uint2>(), b.label.as<double>(), b.n_rows, p.w0, p.cumE, nullptr,
+                       b.col.as<uint32_t>(), b.ent.as<uint2>(), b.xs.as<float>(), b.label.as<double>(), b.n_rows, p.w0, p.cumE, nullptr,
                        nullptr, (int64_t)T.kp, (int64_t)1, nullptr, *xo);
     return;
   }
   w.loss_part.ensure(sizeof(double2) * blocks);
   hipLaunchKernelGGL((k_forward<GS, TEAM, kTrain, U>), grid, blk, 0, st, T, b.row_ptr.as<int64_t>(),
-                     b.col.as<uint32_t>(), b.ent.as<uint2>(), b.label.as<double>(), b.n_rows, p.w0, p.cumE,
+                     b.col.as<uint32_t>(), b.ent.as<uint2>(), b.xs.as<float>(), b.label.as<double>(), b.n_rows, p.w0, p.cumE,
                      w.S.as<float>(), s_rec_yl(T.kp) ? reinterpret_cast<float2*>(w.S.as<float>() + T.kp) : w.yl.as<float2>(),
                      (int64_t)s_rec_floats(T.kp), s_rec_yl(T.kp) ? (int64_t)s_rec_floats(T.kp) / 2 : (int64_t)1,
                      w.loss_part.as<double2>(), none);
@@ -1442,7 +1443,7 @@ __global__ __launch_bounds__(kBlock) void k_explode(const int64_t* __restrict__ 
                                                    const int32_t* __restrict__ xoff, const uint32_t* __restrict__ col_in,
                                                    const float* __restrict__ x_in, int64_t B, int64_t* __restrict__ rp,
                                                    double* __restrict__ lab, uint32_t* __restrict__ col,
-                                                   uint2* __restrict__ ent) {
+                                                   uint2* __restrict__ ent, float* __restrict__ xs) {
   constexpr int T = 16;
   const int tl = threadIdx.x % T;
   const int lane = threadIdx.x & 63;
@@ -1465,6 +1466,7 @@ __global__ __launch_bounds__(kBlock) void k_explode(const int64_t* __restrict__ 
       if (e < e1) {
         col[e] = c & 0x7FFFFFFFu;
         ent[e] = make_uint2((uint32_t)s, __float_as_uint(x));
+        xs[e] = x;
       }
     }
   }
@@ -1472,10 +1474,10 @@ __global__ __launch_bounds__(kBlock) void k_explode(const int64_t* __restrict__ 
 
 void launch_explode(const int64_t* row_ptr_in, const double* label_in, const int32_t* xoff, const uint32_t* col_in,
                     const float* x_in, int64_t B, int64_t N, int64_t* row_ptr, double* label, uint32_t* col, uint2* ent,
-                    hipStream_t st) {
+                    float* xs, hipStream_t st) {
   (void)N;
   hipLaunchKernelGGL(k_explode, dim3(grid_for(std::max<int64_t>(B, 1) * 16, kBlock, 256 * 8)), dim3(kBlock), 0, st,
-                     row_ptr_in, label_in, xoff, col_in, x_in, B, row_ptr, label, col, ent);
+                     row_ptr_in, label_in, xoff, col_in, x_in, B, row_ptr, label, col, ent, xs);
   FM_HIP_CHECK(hipGetLastError());
 }
 
