@@ -324,7 +324,16 @@ int fm_create(const fm_config* cfg, fm_ctx** out) {
     c->rows = (cfg->num_features - cfg->shard_index + cfg->shard_count - 1) / cfg->shard_count;
     FM_HIP_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     c->own_stream = true;
-    FM_HIP_CHECK(hipStreamCreateWithFlags(&c->side_own, hipStreamNonBlocking));
+    // FM_SIDE_PRIO=1: the side stream (the next batch's sort) at the greatest priority, so its
+    // blocks are dispatched before the update's as CUs free up (experiment switch)
+    const char* sp = std::getenv("FM_SIDE_PRIO");
+    if (sp && std::atoi(sp) != 0) {
+      int least = 0, greatest = 0;
+      FM_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+      FM_HIP_CHECK(hipStreamCreateWithPriority(&c->side_own, hipStreamNonBlocking, greatest));
+    } else {
+      FM_HIP_CHECK(hipStreamCreateWithFlags(&c->side_own, hipStreamNonBlocking));
+    }
     c->side = c->side_own;
     FM_HIP_CHECK(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
     FM_HIP_CHECK(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));

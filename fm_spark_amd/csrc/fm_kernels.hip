@@ -340,6 +340,9 @@ struct SegArgs {
 
 constexpr uint32_t kFValid = 1u, kFEnd = 2u, kFStart = 4u;
 
+#ifndef FM_UPD_GRID
+#define FM_UPD_GRID 0  // update blocks at most (0: one per 1024 sorted entries); a cap leaves CU room for the side stream
+#endif
 #ifndef FM_UPD_LEAN
 #define FM_UPD_LEAN 1  // single-buffered loads + head pieces in LDS: 90 VGPRs, 5 waves/SIMD at k = 16 (step -3.5 %)
 #endif
@@ -424,11 +427,14 @@ __global__ __launch_bounds__(kBlock, NF == 1 ? FM_UPD_MINW : 1) void k_segment_u
   int* pflag = pflag_all[wave];
   const TableView& T = a.T;
   const int kp = T.kp;
-  const int64_t wid = (int64_t)blockIdx.x * (kBlock / 64) + wave;
-  const int64_t base = wid * kWaveEnt;
   const uint32_t kNone = 0xFFFFFFFFu;
-  uint32_t ucount = 0;
   auto li = [](int e) { return Geo::at(e % RL, e / RL); };
+  // logical blocks of 4 waves x 256 entries; a capped grid (FM_UPD_GRID) walks them in turn
+  const int64_t nlblk = (a.N + (int64_t)kWaveEnt * (kBlock / 64) - 1) / ((int64_t)kWaveEnt * (kBlock / 64));
+  for (int64_t lblk = blockIdx.x; lblk < nlblk; lblk += gridDim.x) {
+  const int64_t wid = lblk * (kBlock / 64) + wave;
+  const int64_t base = wid * kWaveEnt;
+  uint32_t ucount = 0;
 
   if (base < a.N) {  // wave-uniform
     // ---------------- phase 1: one lane per entry
@@ -817,7 +823,9 @@ __global__ __launch_bounds__(kBlock, NF == 1 ? FM_UPD_MINW : 1) void k_segment_u
     uint32_t t = 0;
 #pragma unroll
     for (int w = 0; w < kBlock / 64; ++w) t += wcnt[w];
-    a.ucnt[blockIdx.x] = t;
+    a.ucnt[lblk] = t;
+  }
+  __syncthreads();  // the image and the counts are reused by the next logical block
   }
 }
 
@@ -1306,7 +1314,8 @@ void launch_segment_update(const TableView& T, int64_t N, const SegSource& src, 
   a.ucnt = w.ucnt.as<uint32_t>();
   a.emit = emit;
   if (ublocks > 0) {
-    const dim3 grid((unsigned)ublocks), blk(kBlock);
+    const int64_t gcap = FM_UPD_GRID > 0 && ublocks > FM_UPD_GRID ? FM_UPD_GRID : ublocks;
+    const dim3 grid((unsigned)gcap), blk(kBlock);
     const int nq = T.kp / 4;  // column quads
     if (nq <= 1) hipLaunchKernelGGL((k_segment_update<1, 1, kUpdD>), grid, blk, 0, st, a);
     else if (nq <= 2) hipLaunchKernelGGL((k_segment_update<2, 1, kUpdD2>), grid, blk, 0, st, a);
