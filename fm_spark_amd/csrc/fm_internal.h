@@ -83,7 +83,7 @@ struct DevBuf {
 
 // ------------------------------------------------------------------- radix sort
 struct SortWork {
-  DevBuf keys_a, keys_b, vals_a, vals_b, counts, digit_tot;
+  DevBuf keys_a, keys_b, vals_a, vals_b, counts, digit_tot, scratch;
   int64_t cap = 0;
   void ensure(int64_t n);
 };

@@ -311,6 +311,240 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint32_t* __rest
   }
 }
 
+// ----------------------------------------------------------------------------- bucket sort
+// Two-phase stable sort for large inputs with 12..28-bit keys.  Phase 1 is one radix pass above
+// (count / scan / scatter) on the top H bits: every key lands in its bucket, in input order.
+// Phase 2 runs one block per bucket over the low L = key_bits - H bits: two LSD passes (one when
+// L <= 9) whose intermediate order stays in LDS as one packed word per entry, {sub-key << (32 - L)
+// | index in bucket}; the last pass writes the bucket's keys and gathers its payloads from the
+// bucket's own (L2-resident) range.  A bucket larger than the LDS image (a hot feature's run) keeps
+// that intermediate order in a global scratch instead and is processed in LDS-sized chunks.
+// HBM bytes per pair (P = 8): 4 + 12 + 12 (phase 1) + 12 + 12 (phase 2) = 52, against 84 for
+// three LSD passes.
+#ifndef FM_BKT_CAP
+#define FM_BKT_CAP 15360
+#endif
+#ifndef FM_BKT_G
+#define FM_BKT_G 8  // rounds of 64 entries per wave whose loads are issued together
+#endif
+constexpr int kBB = 512;                      // phase-2 block: 8 waves
+constexpr int kBW = kBB / 64;
+constexpr int kBktCap = FM_BKT_CAP;           // a bucket up to this size keeps its order in LDS
+constexpr int kBktMaxRB = 9;                  // digit bits of one in-bucket pass (<= 512 digits: one per thread)
+static_assert(kBktCap <= 16384, "packed LDS words hold a 14-bit index next to an 18-bit sub-key");
+
+struct BktShared {
+  uint32_t arr[kBktCap];                // packed {sub, idx} in the order of the previous pass
+  uint32_t cnt[kBW][1 << kBktMaxRB];    // per-wave digit counts -> running destinations
+  uint32_t wsum[kBW];
+};
+
+enum BktSrc { kSrcKeys = 0, kSrcLds = 1, kSrcScratch = 2 };
+enum BktDst { kDstLds = 0, kDstScratch = 1, kDstOut = 2 };
+
+__device__ __forceinline__ uint64_t digit_peers(uint32_t d, bool valid, int rb) {
+  uint64_t peers = __ballot(valid);
+  for (int b = 0; b < rb; ++b) {
+    const bool bit = (d >> b) & 1u;
+    const uint64_t m = __ballot(bit);
+    peers &= bit ? m : ~m;
+  }
+  return peers;
+}
+
+// Exclusive scan of one value per thread over the 512-thread block.
+__device__ __forceinline__ uint32_t bkt_excl_scan(uint32_t v, uint32_t* wsum, int lane, int wave) {
+  const uint32_t incl = wave_incl_scan_u32(v, lane);
+  if (lane == 63) wsum[wave] = incl;
+  lds_barrier();
+  uint32_t pre = incl - v;
+#pragma unroll
+  for (int w = 0; w < kBW; ++w) pre += (w < wave) ? wsum[w] : 0u;
+  lds_barrier();
+  return pre;
+}
+
+template <bool GSYNC>
+__device__ __forceinline__ void bkt_sync() {
+  if (GSYNC)
+    __syncthreads();  // the pass exchanges through global scratch: workgroup fence on global too
+  else
+    lds_barrier();
+}
+
+template <class P>
+struct BktIO {
+  const uint32_t* keys;  // bucket's keys (phase-1 output)
+  const P* vals;         // bucket's payloads (phase-1 output)
+  uint32_t* okeys;
+  P* ovals;
+  uint2* scratch;        // {sub, idx} per entry (oversized buckets)
+  uint32_t hi;           // bucket << L
+  uint32_t lmask;        // (1 << L) - 1
+  int ib;                // 32 - L: index bits of the packed LDS word
+};
+
+// One stable counting pass over the m entries of a bucket by digit (sub >> shift) & (2^rb - 1),
+// from SRC to DST.  Wave w owns the contiguous part [w p, (w + 1) p) of the bucket: a histogram
+// sweep, a scan over (digit, wave), then a rank sweep with wave-private running counts.  Both
+// sweeps take G rounds of 64 entries at a time so that their loads (and the last pass's payload
+// gathers) are in flight together.
+template <int SRC, int DST, bool GSYNC, class P>
+__device__ __forceinline__ void bucket_pass(BktShared& S, const BktIO<P>& io, uint32_t m, int shift, int rb) {
+  constexpr int G = FM_BKT_G;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int R = 1 << rb;
+  const uint32_t M = (uint32_t)R - 1u;
+  const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  const uint32_t imask = (io.ib >= 32) ? 0xFFFFFFFFu : ((1u << io.ib) - 1u);
+  const uint32_t part = ((m + kBW - 1) / kBW + 63u) & ~63u;
+  const uint32_t lo = min(m, (uint32_t)wave * part), hi = min(m, lo + part);
+
+  auto load = [&](uint32_t e, uint32_t& sub, uint32_t& idx) {
+    if (SRC == kSrcKeys) {
+      sub = io.keys[e] & io.lmask;
+      idx = e;
+    } else if (SRC == kSrcLds) {
+      const uint32_t v = S.arr[e];
+      sub = v >> io.ib;
+      idx = v & imask;
+    } else {
+      const uint2 v = io.scratch[e];
+      sub = v.x;
+      idx = v.y;
+    }
+  };
+
+  for (int d = tid; d < kBW * R; d += kBB) S.cnt[d / R][d % R] = 0;
+  bkt_sync<GSYNC>();
+  for (uint32_t e0 = lo; e0 < hi; e0 += 64 * G) {
+    uint32_t sub[G];
+#pragma unroll
+    for (int u = 0; u < G; ++u) {
+      const uint32_t e = e0 + u * 64 + lane;
+      uint32_t idx;
+      sub[u] = 0;
+      if (e < hi) load(e, sub[u], idx);
+    }
+#pragma unroll
+    for (int u = 0; u < G; ++u) {
+      const uint32_t e = e0 + u * 64 + lane;
+      const bool valid = e < hi;
+      const uint32_t d = (sub[u] >> shift) & M;
+      const uint64_t peers = digit_peers(d, valid, rb);
+      if (valid && __popcll(peers & lt_mask) == 0) S.cnt[wave][d] += (uint32_t)__popcll(peers);
+    }
+  }
+  bkt_sync<GSYNC>();
+  // destinations of (digit, wave): the digit's base + the counts of the earlier waves
+  uint32_t t = 0;
+  if (tid < R) {
+#pragma unroll
+    for (int w = 0; w < kBW; ++w) {
+      const uint32_t x = S.cnt[w][tid];
+      S.cnt[w][tid] = t;
+      t += x;
+    }
+  }
+  const uint32_t base = bkt_excl_scan(t, S.wsum, lane, wave);
+  if (tid < R) {
+#pragma unroll
+    for (int w = 0; w < kBW; ++w) S.cnt[w][tid] += base;
+  }
+  lds_barrier();
+  for (uint32_t e0 = lo; e0 < hi; e0 += 64 * G) {
+    uint32_t sub[G], idx[G], pos[G];
+#pragma unroll
+    for (int u = 0; u < G; ++u) {
+      const uint32_t e = e0 + u * 64 + lane;
+      sub[u] = 0;
+      idx[u] = 0;
+      if (e < hi) load(e, sub[u], idx[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < G; ++u) {
+      const uint32_t e = e0 + u * 64 + lane;
+      const bool valid = e < hi;
+      const uint32_t d = (sub[u] >> shift) & M;
+      const uint64_t peers = digit_peers(d, valid, rb);
+      const uint32_t below = (uint32_t)__popcll(peers & lt_mask);
+      const uint32_t prev = S.cnt[wave][d];
+      __builtin_amdgcn_wave_barrier();
+      if (valid && below == 0) S.cnt[wave][d] = prev + (uint32_t)__popcll(peers);
+      __builtin_amdgcn_wave_barrier();
+      pos[u] = prev + below;
+    }
+    if (DST == kDstOut) {
+      P v[G];
+#pragma unroll
+      for (int u = 0; u < G; ++u)
+        if (e0 + u * 64 + lane < hi) v[u] = io.vals[idx[u]];
+#pragma unroll
+      for (int u = 0; u < G; ++u) {
+        if (e0 + u * 64 + lane < hi) {
+          io.okeys[pos[u]] = io.hi | sub[u];
+          io.ovals[pos[u]] = v[u];
+        }
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < G; ++u) {
+        if (e0 + u * 64 + lane < hi) {
+          if (DST == kDstLds)
+            S.arr[pos[u]] = (sub[u] << io.ib) | idx[u];
+          else
+            io.scratch[pos[u]] = make_uint2(sub[u], idx[u]);
+        }
+      }
+    }
+  }
+  bkt_sync<GSYNC>();  // the next pass reads what this one wrote and resets cnt
+}
+
+// Phase 2: block b sorts bucket b (btot[b] entries starting at the sum of the buckets below it).
+template <class P>
+__global__ __launch_bounds__(kBB) void k_bucket_sort(const uint32_t* __restrict__ keys_in, const P* __restrict__ vals_in,
+                                                     uint32_t* __restrict__ keys_out, P* __restrict__ vals_out,
+                                                     const uint32_t* __restrict__ btot, int L,
+                                                     uint2* __restrict__ scratch) {
+  __shared__ BktShared S;
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  uint32_t acc = 0;
+  for (int i = tid; i < b; i += kBB) acc += btot[i];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+  if (lane == 0) S.wsum[wave] = acc;
+  lds_barrier();
+  uint32_t start = 0;
+#pragma unroll
+  for (int w = 0; w < kBW; ++w) start += S.wsum[w];
+  const uint32_t m = btot[b];
+  if (m == 0) return;  // block-uniform
+  lds_barrier();       // wsum is reused by the scans
+  BktIO<P> io;
+  io.keys = keys_in + start;
+  io.vals = vals_in + start;
+  io.okeys = keys_out + start;
+  io.ovals = vals_out + start;
+  io.scratch = scratch + start;
+  io.hi = (uint32_t)b << L;
+  io.lmask = (1u << L) - 1u;
+  io.ib = 32 - L;
+  if (L <= kBktMaxRB) {
+    bucket_pass<kSrcKeys, kDstOut, false>(S, io, m, 0, L);
+  } else {
+    const int rb0 = L / 2, rb1 = L - rb0;
+    if (m <= (uint32_t)kBktCap) {
+      bucket_pass<kSrcKeys, kDstLds, false>(S, io, m, 0, rb0);
+      bucket_pass<kSrcLds, kDstOut, false>(S, io, m, rb0, rb1);
+    } else {
+      bucket_pass<kSrcKeys, kDstScratch, true>(S, io, m, 0, rb0);
+      bucket_pass<kSrcScratch, kDstOut, true>(S, io, m, rb0, rb1);
+    }
+  }
+}
+
 }  // namespace
 
 void SortWork::ensure(int64_t n) {
@@ -320,6 +554,7 @@ void SortWork::ensure(int64_t n) {
   keys_b.ensure(sizeof(uint32_t) * c);
   vals_a.ensure(sizeof(uint64_t) * c);  // payloads up to 8 bytes
   vals_b.ensure(sizeof(uint64_t) * c);
+  scratch.ensure(sizeof(uint2) * c);  // {sub, idx} of oversized buckets (bucket sort)
   const int64_t ntiles = (c + kTile - 1) / kTile;
   counts.ensure(sizeof(uint32_t) * kMaxRadix * ntiles);
   digit_tot.ensure(sizeof(uint32_t) * kMaxRadix);
@@ -360,6 +595,27 @@ inline int digit_bits(int key_bits, int* passes) {
   return rb;
 }
 
+// Top-bit count of the bucket sort (0: the LSD passes).  Buckets average n / 2^H entries (about
+// 5K - 10K, below the LDS image of kBktCap); the low L = key_bits - H bits take one or two in-bucket
+// passes of <= 9 bits.  Needs a payload array (the index payload of radix_sort_pairs stays LSD) and
+// keys from bit 0.
+#ifndef FM_SORT_BUCKET
+#define FM_SORT_BUCKET 0  // default off until the GPU A/B lands (FM_SORT_BUCKET=1 at run time switches it on)
+#endif
+#ifndef FM_SORT_BUCKET_MIN
+#define FM_SORT_BUCKET_MIN (1 << 20)
+#endif
+static int bucket_hi_bits(int64_t n, int key_bits, int lo_bit, bool has_vals) {
+  const char* env = getenv("FM_SORT_BUCKET");  // read per call: tests and A/B runs switch it
+  const bool on = env ? atoi(env) != 0 : FM_SORT_BUCKET != 0;
+  const char* env_min = getenv("FM_SORT_BUCKET_MIN");
+  const int64_t min_n = env_min ? atoll(env_min) : (int64_t)FM_SORT_BUCKET_MIN;
+  if (!on || !has_vals || lo_bit != 0 || n < min_n || n < 1) return 0;
+  if (key_bits < 12 || key_bits > 10 + 2 * kBktMaxRB) return 0;
+  const int H = (n / 512 > 8192 || key_bits - 9 > 2 * kBktMaxRB) ? 10 : 9;
+  return key_bits - H >= 1 ? H : 0;
+}
+
 template <class P>
 static void radix_sort_impl(SortWork& w, const uint32_t* keys_in, const P* vals_in, int64_t n, int key_bits,
                             hipStream_t st, const uint32_t** keys_out, const P** vals_out,
@@ -382,6 +638,27 @@ static void radix_sort_impl(SortWork& w, const uint32_t* keys_in, const P* vals_
   int which = 0;
   // the count kernel reads keys as uint4 when the tile is full: needs 16-byte alignment
   const bool aligned = (reinterpret_cast<uintptr_t>(keys_in) & 15u) == 0;
+  const int H = bucket_hi_bits(n, key_bits, lo_bit, vals_in != nullptr);
+  if (H > 0) {
+    // phase 1: one pass on the top H bits into kbuf[0]; phase 2: one block per bucket
+    const int L = key_bits - H;
+    if (!aligned) {
+      FM_HIP_CHECK(hipMemcpyAsync(kbuf[1], keys_in, sizeof(uint32_t) * n, hipMemcpyDeviceToDevice, st));
+      kin = kbuf[1];
+    }
+    if (H == 9)
+      radix_pass<P, 9>(kin, vin, kbuf[0], vbuf[0], n, L, w, ntiles, st);
+    else
+      radix_pass<P, 10>(kin, vin, kbuf[0], vbuf[0], n, L, w, ntiles, st);
+    uint32_t* ko = final_keys ? final_keys : kbuf[1];
+    P* vo = final_vals ? final_vals : vbuf[1];
+    hipLaunchKernelGGL(k_bucket_sort<P>, dim3(1u << H), dim3(kBB), 0, st, kbuf[0], vbuf[0], ko, vo,
+                       w.digit_tot.as<uint32_t>(), L, w.scratch.as<uint2>());
+    FM_HIP_CHECK(hipGetLastError());
+    *keys_out = ko;
+    *vals_out = vo;
+    return;
+  }
   for (int p = 0; p < passes; ++p) {
     const int shift = lo_bit + rb * p;
     if (p == 0 && !aligned) {

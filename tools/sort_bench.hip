@@ -24,10 +24,17 @@ int main(int argc, char** argv) {
   std::mt19937_64 rng(1);
   std::vector<uint32_t> keys(n);
   std::vector<uint2> vals(n);
+  // skew: 0 = 40% of keys from 1000 hot keys, the rest uniform; 1 = uniform; 2 = 60% on one key
+  const int skew = argc > 3 ? atoi(argv[3]) : 0;
   for (int64_t i = 0; i < n; ++i) {
-    // 40% of keys from a small hot set (Zipf-like skew), the rest uniform
     uint64_t r = rng();
-    keys[i] = (r % 10 < 4) ? (uint32_t)((r >> 8) % 1000) * 99991u % (1u << bits) : (uint32_t)((r >> 8) % (1u << bits));
+    const uint32_t uni = (uint32_t)((r >> 8) % (1ull << bits));
+    if (skew == 0)
+      keys[i] = (r % 10 < 4) ? (uint32_t)((r >> 8) % 1000) * 99991u % (1u << bits) : uni;
+    else if (skew == 2)
+      keys[i] = (r % 10 < 6) ? 12345u % (1u << bits) : uni;
+    else
+      keys[i] = uni;
     vals[i] = make_uint2((uint32_t)i, (uint32_t)(r >> 32));
   }
   uint32_t *dk, *dk2;
@@ -54,27 +61,34 @@ int main(int argc, char** argv) {
   float ms;
   CK(hipEventElapsedTime(&ms, a, b));
   printf("rocprim radix_sort_pairs n=%lld bits=%d: %.3f ms\n", (long long)n, bits, ms / R);
-  // ours
-  fmhip::SortWork sw;
-  const uint32_t* ok;
-  const uint2* ov;
-  for (int w = 0; w < 3; ++w) fmhip::radix_sort_pairs64(sw, dk, dv, n, bits, st, &ok, &ov);
-  CK(hipEventRecord(a, st));
-  for (int r = 0; r < R; ++r) fmhip::radix_sort_pairs64(sw, dk, dv, n, bits, st, &ok, &ov);
-  CK(hipEventRecord(b, st));
-  CK(hipEventSynchronize(b));
-  CK(hipEventElapsedTime(&ms, a, b));
-  printf("fm_hip radix_sort_pairs64 n=%lld bits=%d: %.3f ms\n", (long long)n, bits, ms / R);
-  // check equality
+  // ours: the LSD passes (FM_SORT_BUCKET=0) and the bucket sort (=1, forced at any n)
   std::vector<uint32_t> k1(n), k2(n);
   std::vector<uint2> v1(n), v2(n);
   CK(hipMemcpy(k1.data(), dk2, 4 * n, hipMemcpyDeviceToHost));
-  CK(hipMemcpy(k2.data(), ok, 4 * n, hipMemcpyDeviceToHost));
   CK(hipMemcpy(v1.data(), dv2, 8 * n, hipMemcpyDeviceToHost));
-  CK(hipMemcpy(v2.data(), ov, 8 * n, hipMemcpyDeviceToHost));
-  int64_t bad = 0;
-  for (int64_t i = 0; i < n; ++i) bad += (k1[i] != k2[i]) || (v1[i].x != v2[i].x) || (v1[i].y != v2[i].y);
-  printf("mismatches vs rocprim (both stable): %lld\n", (long long)bad);
+  int64_t bad_total = 0;
+  for (int mode = 0; mode < 2; ++mode) {
+    setenv("FM_SORT_BUCKET", mode ? "1" : "0", 1);
+    setenv("FM_SORT_BUCKET_MIN", "0", 1);
+    fmhip::SortWork sw;
+    const uint32_t* ok;
+    const uint2* ov;
+    for (int w = 0; w < 3; ++w) fmhip::radix_sort_pairs64(sw, dk, dv, n, bits, st, &ok, &ov);
+    CK(hipEventRecord(a, st));
+    for (int r = 0; r < R; ++r) fmhip::radix_sort_pairs64(sw, dk, dv, n, bits, st, &ok, &ov);
+    CK(hipEventRecord(b, st));
+    CK(hipEventSynchronize(b));
+    CK(hipEventElapsedTime(&ms, a, b));
+    printf("fm_hip radix_sort_pairs64 %s n=%lld bits=%d skew=%d: %.3f ms\n", mode ? "bucket" : "lsd", (long long)n, bits,
+           skew, ms / R);
+    CK(hipMemcpy(k2.data(), ok, 4 * n, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(v2.data(), ov, 8 * n, hipMemcpyDeviceToHost));
+    int64_t bad = 0;
+    for (int64_t i = 0; i < n; ++i) bad += (k1[i] != k2[i]) || (v1[i].x != v2[i].x) || (v1[i].y != v2[i].y);
+    printf("mismatches vs rocprim (%s, both stable): %lld\n", mode ? "bucket" : "lsd", (long long)bad);
+    bad_total += bad;
+  }
+  if (getenv("SORT_CHECK_ONLY")) return bad_total ? 1 : 0;
   // rocPRIM keys-only sort of packed 64-bit words (key << 24 | entry index): one stream per pass
   {
     std::vector<uint64_t> pk(n);
