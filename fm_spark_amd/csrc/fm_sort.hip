@@ -321,17 +321,21 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint32_t* __rest
 // that intermediate order in a global scratch instead and is processed in LDS-sized chunks.
 // HBM bytes per pair (P = 8): 4 + 12 + 12 (phase 1) + 12 + 12 (phase 2) = 52, against 84 for
 // three LSD passes.
+#ifndef FM_BKT_BLOCK
+#define FM_BKT_BLOCK 1024  // phase-2 block: 16 waves, one block per CU (the LDS image takes 120 KB)
+#endif
 #ifndef FM_BKT_CAP
-#define FM_BKT_CAP 15360
+#define FM_BKT_CAP (30 * FM_BKT_BLOCK)
 #endif
 #ifndef FM_BKT_G
 #define FM_BKT_G 8  // rounds of 64 entries per wave whose loads are issued together
 #endif
-constexpr int kBB = 512;                      // phase-2 block: 8 waves
+constexpr int kBB = FM_BKT_BLOCK;             // phase-2 block
 constexpr int kBW = kBB / 64;
 constexpr int kBktCap = FM_BKT_CAP;           // a bucket up to this size keeps its order in LDS
 constexpr int kBktMaxRB = 9;                  // digit bits of one in-bucket pass (<= 512 digits: one per thread)
-static_assert(kBktCap <= 16384, "packed LDS words hold a 14-bit index next to an 18-bit sub-key");
+static_assert(kBktCap <= 32768, "packed LDS words hold a 15-bit index next to a 17-bit sub-key");
+static_assert(kBB == 512 || kBB == 1024, "phase-2 block of 8 or 16 waves");
 
 struct BktShared {
   uint32_t arr[kBktCap];                // packed {sub, idx} in the order of the previous pass
@@ -340,7 +344,7 @@ struct BktShared {
 };
 
 enum BktSrc { kSrcKeys = 0, kSrcLds = 1, kSrcScratch = 2 };
-enum BktDst { kDstLds = 0, kDstScratch = 1, kDstOut = 2 };
+enum BktDst { kDstLds = 0, kDstScratch = 1, kDstOut = 2 };  // kSrcLds / kDstLds: chunked variants, unused
 
 __device__ __forceinline__ uint64_t digit_peers(uint32_t d, bool valid, int rb) {
   uint64_t peers = __ballot(valid);
@@ -501,14 +505,103 @@ __device__ __forceinline__ void bucket_pass(BktShared& S, const BktIO<P>& io, ui
   bkt_sync<GSYNC>();  // the next pass reads what this one wrote and resets cnt
 }
 
+// In-LDS pass for a bucket of m <= kBktCap entries, in place in S.arr: each lane holds its wave's
+// part of the bucket in registers (packed {sub << ib | idx} words, read from the bucket's keys on the
+// first pass), ranks it with one ballot sweep whose wave-private running counts end as the wave's
+// digit histogram, and once every part is read and the (digit, wave) bases are scanned, stores each
+// word at its destination.
+constexpr int kBktNR = kBktCap / kBB;  // words per lane at most
+static_assert(kBktCap % kBB == 0, "the LDS image must be a multiple of the block");
+
+template <bool FROM_KEYS, class P>
+__device__ __forceinline__ void bucket_pass_lds(BktShared& S, const BktIO<P>& io, uint32_t m, int shift) {
+  constexpr int rb = kBktMaxRB;  // digits (sub >> shift) & 511: bits above L are zero
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  constexpr int R = 1 << rb;
+  const uint32_t M = (uint32_t)R - 1u;
+  const int dsh = io.ib + shift;
+  const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  const uint32_t part = ((m + kBW - 1) / kBW + 63u) & ~63u;
+  const uint32_t lo = min(m, (uint32_t)wave * part);
+  const int nvw = (int)(min(m, lo + part) - lo);
+  uint32_t v[kBktNR], loc[kBktNR];
+#pragma unroll
+  for (int r = 0; r < kBktNR; ++r) {
+    const uint32_t e = lo + r * 64 + lane;
+    v[r] = 0;
+    if (r * 64 + lane < nvw) v[r] = FROM_KEYS ? (((io.keys[e] & io.lmask) << io.ib) | e) : S.arr[e];
+  }
+  for (int d = tid; d < kBW * R; d += kBB) S.cnt[d / R][d % R] = 0;
+  lds_barrier();  // every part is in registers: S.arr may be overwritten below
+#pragma unroll
+  for (int r = 0; r < kBktNR; ++r) {
+    if (r * 64 >= nvw) break;
+    const bool valid = r * 64 + lane < nvw;
+    const uint32_t d = (v[r] >> dsh) & M;
+    const uint64_t peers = digit_peers(d, valid, rb);
+    const uint32_t below = (uint32_t)__popcll(peers & lt_mask);
+    const uint32_t prev = S.cnt[wave][d];
+    __builtin_amdgcn_wave_barrier();
+    if (valid && below == 0) S.cnt[wave][d] = prev + (uint32_t)__popcll(peers);
+    __builtin_amdgcn_wave_barrier();
+    loc[r] = prev + below;
+  }
+  lds_barrier();
+  uint32_t t = 0;
+  if (tid < R) {
+#pragma unroll
+    for (int w = 0; w < kBW; ++w) {
+      const uint32_t x = S.cnt[w][tid];
+      S.cnt[w][tid] = t;
+      t += x;
+    }
+  }
+  const uint32_t base = bkt_excl_scan(t, S.wsum, lane, wave);
+  if (tid < R) {
+#pragma unroll
+    for (int w = 0; w < kBW; ++w) S.cnt[w][tid] += base;
+  }
+  lds_barrier();
+#pragma unroll
+  for (int r = 0; r < kBktNR; ++r) {
+    if (r * 64 + lane < nvw) S.arr[S.cnt[wave][(v[r] >> dsh) & M] + loc[r]] = v[r];
+  }
+  lds_barrier();
+}
+
+// Phase-2 dispatch order: buckets that outgrow the LDS image (hot features: their block walks the
+// bucket through global scratch, several times longer) first, so they start with the first wave of
+// blocks instead of forming the kernel's tail; then the rest in bucket order.  One block.
+__global__ __launch_bounds__(kBB) void k_bucket_order(const uint32_t* __restrict__ btot, int nb,
+                                                      uint32_t* __restrict__ order) {
+  __shared__ uint32_t wsum[kBW];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  uint32_t carry = 0;  // block-uniform
+  for (int pass = 0; pass < 2; ++pass) {
+    for (int b0 = 0; b0 < nb; b0 += kBB) {
+      const int b = b0 + tid;
+      const bool big = b < nb && btot[b] > (uint32_t)kBktCap / 2;  // the largest first (c4: 16K image)
+      const uint32_t f = (b < nb && (pass == 0 ? big : !big)) ? 1u : 0u;
+      const uint32_t pre = bkt_excl_scan(f, wsum, lane, wave);
+      if (f) order[carry + pre] = (uint32_t)b;
+      uint32_t t = 0;
+#pragma unroll
+      for (int w = 0; w < kBW; ++w) t += wsum[w];
+      lds_barrier();
+      carry += t;
+    }
+  }
+}
+
 // Phase 2: block b sorts bucket b (btot[b] entries starting at the sum of the buckets below it).
 template <class P>
 __global__ __launch_bounds__(kBB) void k_bucket_sort(const uint32_t* __restrict__ keys_in, const P* __restrict__ vals_in,
                                                      uint32_t* __restrict__ keys_out, P* __restrict__ vals_out,
                                                      const uint32_t* __restrict__ btot, int L,
-                                                     uint2* __restrict__ scratch) {
+                                                     uint2* __restrict__ scratch,
+                                                     const uint32_t* __restrict__ order) {
   __shared__ BktShared S;
-  const int b = blockIdx.x;
+  const int b = order ? (int)order[blockIdx.x] : (int)blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   uint32_t acc = 0;
   for (int i = tid; i < b; i += kBB) acc += btot[i];
@@ -531,17 +624,39 @@ __global__ __launch_bounds__(kBB) void k_bucket_sort(const uint32_t* __restrict_
   io.hi = (uint32_t)b << L;
   io.lmask = (1u << L) - 1u;
   io.ib = 32 - L;
-  if (L <= kBktMaxRB) {
+  const int rb0 = L <= kBktMaxRB ? L : L / 2, rb1 = L - rb0;
+  // the packed word holds the index in ib = 32 - L bits: 15 at c3's L = 17, 14 at c4's L = 18
+  const uint32_t cap = min((uint32_t)kBktCap, 1u << min(io.ib, 31));
+  if (m <= cap) {
+    bucket_pass_lds<true>(S, io, m, 0);
+    if (L > kBktMaxRB) bucket_pass_lds<false>(S, io, m, kBktMaxRB);
+    // the bucket in order in S.arr: coalesced key and payload writes, payloads gathered by index
+    // from the bucket's own range
+    const uint32_t imask = (io.ib >= 32) ? 0xFFFFFFFFu : ((1u << io.ib) - 1u);
+    constexpr int U = 4;
+    for (uint32_t j0 = 0; j0 < m; j0 += U * kBB) {
+      uint32_t w[U];
+      P pv[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t j = j0 + u * kBB + tid;
+        w[u] = j < m ? S.arr[j] : 0u;
+        if (j < m) pv[u] = io.vals[w[u] & imask];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t j = j0 + u * kBB + tid;
+        if (j < m) {
+          io.okeys[j] = io.hi | (w[u] >> io.ib);
+          io.ovals[j] = pv[u];
+        }
+      }
+    }
+  } else if (rb1 == 0) {
     bucket_pass<kSrcKeys, kDstOut, false>(S, io, m, 0, L);
   } else {
-    const int rb0 = L / 2, rb1 = L - rb0;
-    if (m <= (uint32_t)kBktCap) {
-      bucket_pass<kSrcKeys, kDstLds, false>(S, io, m, 0, rb0);
-      bucket_pass<kSrcLds, kDstOut, false>(S, io, m, rb0, rb1);
-    } else {
-      bucket_pass<kSrcKeys, kDstScratch, true>(S, io, m, 0, rb0);
-      bucket_pass<kSrcScratch, kDstOut, true>(S, io, m, rb0, rb1);
-    }
+    bucket_pass<kSrcKeys, kDstScratch, true>(S, io, m, 0, rb0);
+    bucket_pass<kSrcScratch, kDstOut, true>(S, io, m, rb0, rb1);
   }
 }
 
@@ -557,7 +672,7 @@ void SortWork::ensure(int64_t n) {
   scratch.ensure(sizeof(uint2) * c);  // {sub, idx} of oversized buckets (bucket sort)
   const int64_t ntiles = (c + kTile - 1) / kTile;
   counts.ensure(sizeof(uint32_t) * kMaxRadix * ntiles);
-  digit_tot.ensure(sizeof(uint32_t) * kMaxRadix);
+  digit_tot.ensure(sizeof(uint32_t) * kMaxRadix * 2);  // digit totals + the bucket sort's block order
   cap = c;
 }
 
@@ -652,8 +767,11 @@ static void radix_sort_impl(SortWork& w, const uint32_t* keys_in, const P* vals_
       radix_pass<P, 10>(kin, vin, kbuf[0], vbuf[0], n, L, w, ntiles, st);
     uint32_t* ko = final_keys ? final_keys : kbuf[1];
     P* vo = final_vals ? final_vals : vbuf[1];
+    // the bucket order lives past the digit totals (kMaxRadix words each)
+    uint32_t* order = w.digit_tot.as<uint32_t>() + kMaxRadix;
+    hipLaunchKernelGGL(k_bucket_order, dim3(1), dim3(kBB), 0, st, w.digit_tot.as<uint32_t>(), 1 << H, order);
     hipLaunchKernelGGL(k_bucket_sort<P>, dim3(1u << H), dim3(kBB), 0, st, kbuf[0], vbuf[0], ko, vo,
-                       w.digit_tot.as<uint32_t>(), L, w.scratch.as<uint2>());
+                       w.digit_tot.as<uint32_t>(), L, w.scratch.as<uint2>(), (const uint32_t*)order);
     FM_HIP_CHECK(hipGetLastError());
     *keys_out = ko;
     *vals_out = vo;

@@ -42,7 +42,7 @@ def test_bucket_sort_step_matches_lsd_bitwise(monkeypatch, gpu, F, n_rows, mean_
     assert_tables(model, g_b)
     for (gb, rb), (gl, _) in zip(losses_b, losses_l):
         assert gb == gl
-        np.testing.assert_allclose(gb, rb, rtol=1e-9)
+        np.testing.assert_allclose(gb, rb, rtol=1e-6)
     for a, b in zip(g_b, g_l):
         assert np.array_equal(a, b)
 
@@ -65,7 +65,7 @@ def test_bucket_sort_prepared_batch(monkeypatch, gpu):
     for i, (c, b) in enumerate(zip(csrs, dbs)):
         ro = R.sgd_step_fast(model, c, i + 1, 0.2, 1e-5)
         go = ctx.step_batch(b, i + 1, 0.2, 1e-5)
-        np.testing.assert_allclose(go.loss_sum, ro.loss_sum, rtol=1e-9)
+        np.testing.assert_allclose(go.loss_sum, ro.loss_sum, rtol=1e-6)
         assert go.n_unique == ro.n_unique
     assert_tables(model, ctx.export_tables())
     ctx.close()

@@ -4,6 +4,7 @@
 #include <cstring>
 #include <rocprim/device/device_radix_sort.hpp>
 
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <random>
@@ -33,6 +34,16 @@ int main(int argc, char** argv) {
       keys[i] = (r % 10 < 4) ? (uint32_t)((r >> 8) % 1000) * 99991u % (1u << bits) : uni;
     else if (skew == 2)
       keys[i] = (r % 10 < 6) ? 12345u % (1u << bits) : uni;
+    else if (skew == 3) {  // c3-like: 39 fields, rank with the Zipf(1.05) tail P(rank >= r) = r^-0.05, hashed
+      const double u = (double)(rng() >> 11) * (1.0 / 9007199254740992.0);
+      double rk = std::pow(1.0 - u, -20.0);
+      if (rk > 1e12) rk = 1e12;
+      uint64_t z = ((uint64_t)(i % 39) << 40) + (uint64_t)rk + 0x9E3779B97F4A7C15ull;
+      z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+      z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+      z ^= z >> 31;
+      keys[i] = (uint32_t)(z % (1ull << bits));
+    }
     else
       keys[i] = uni;
     vals[i] = make_uint2((uint32_t)i, (uint32_t)(r >> 32));
