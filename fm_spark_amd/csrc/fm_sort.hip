@@ -61,13 +61,23 @@ __device__ __forceinline__ int64_t tile_of_block(int64_t ntiles) {
 
 inline int64_t blocks_for_tiles(int64_t ntiles) { return (ntiles + 7) / 8 * 8; }
 
+// Experiment switch: the count and scan kernels on small blocks (4 waves; one wave per digit row),
+// which slot into the room the step's 4-wave forward / update blocks free (in the step an 8-wave
+// count or scan block takes 30 - 95 us instead of 7 - 17 alone).  Measured slower: the step is
+// throughput-bound, not bound by these kernels' wait for CU room.
+#ifndef FM_SORT_SMALLBLK
+#define FM_SORT_SMALLBLK 0  // measured: c3 step 1.069-1.072 vs 1.053-1.062 ms with the 8-wave blocks (off)
+#endif
+constexpr int kCntBlock = FM_SORT_SMALLBLK ? 256 : kBlock;
+static_assert(kTile % (4 * kCntBlock) == 0, "count block must divide the tile into uint4 rounds");
+
 template <int RB>
-__global__ __launch_bounds__(kBlock) void k_radix_count(const uint32_t* __restrict__ keys, int64_t n,
-                                                        int shift, uint32_t* __restrict__ counts,
-                                                        int64_t ntiles) {
+__global__ __launch_bounds__(kCntBlock) void k_radix_count(const uint32_t* __restrict__ keys, int64_t n,
+                                                           int shift, uint32_t* __restrict__ counts,
+                                                           int64_t ntiles) {
   constexpr int R = 1 << RB;
   constexpr uint32_t M = R - 1;
-  constexpr int HW = FM_SORT_CWAVE ? kWaves : 1;
+  constexpr int HW = FM_SORT_CWAVE ? kCntBlock / 64 : 1;
   __shared__ uint32_t hist_all[HW][R];
   uint32_t* hist = hist_all[FM_SORT_CWAVE ? (threadIdx.x >> 6) : 0];
 #if FM_SORT_CXCD
@@ -76,27 +86,27 @@ __global__ __launch_bounds__(kBlock) void k_radix_count(const uint32_t* __restri
 #else
   const int64_t tile = blockIdx.x;
 #endif
-  for (int d = threadIdx.x; d < HW * R; d += kBlock) hist_all[d / R][d % R] = 0;
+  for (int d = threadIdx.x; d < HW * R; d += kCntBlock) hist_all[d / R][d % R] = 0;
   lds_barrier();
   const int64_t base = tile * kTile;
-  if (kRounds % 4 == 0 && base + kTile <= n) {
+  if (base + kTile <= n) {
     const uint4* k4 = reinterpret_cast<const uint4*>(keys + base);
 #pragma unroll
-    for (int i = 0; i < kRounds / 4; ++i) {
-      const uint4 q = ld_stream(k4 + i * kBlock + threadIdx.x, FM_NT_SORTLD);
+    for (int i = 0; i < kTile / (4 * kCntBlock); ++i) {
+      const uint4 q = ld_stream(k4 + i * kCntBlock + threadIdx.x, FM_NT_SORTLD);
       atomicAdd(&hist[(q.x >> shift) & M], 1u);
       atomicAdd(&hist[(q.y >> shift) & M], 1u);
       atomicAdd(&hist[(q.z >> shift) & M], 1u);
       atomicAdd(&hist[(q.w >> shift) & M], 1u);
     }
   } else {
-    for (int i = 0; i < kRounds; ++i) {
-      const int64_t idx = base + (int64_t)i * kBlock + threadIdx.x;
+    for (int i = 0; i < kTile / kCntBlock; ++i) {
+      const int64_t idx = base + (int64_t)i * kCntBlock + threadIdx.x;
       if (idx < n) atomicAdd(&hist[(keys[idx] >> shift) & M], 1u);
     }
   }
   lds_barrier();
-  for (int d = threadIdx.x; d < R; d += kBlock) {
+  for (int d = threadIdx.x; d < R; d += kCntBlock) {
     uint32_t c = 0;
 #pragma unroll
     for (int w = 0; w < HW; ++w) c += hist_all[w][d];
@@ -138,6 +148,38 @@ __global__ __launch_bounds__(kBlock) void k_radix_scan_rows(uint32_t* __restrict
     lds_barrier();
   }
   if (threadIdx.x == 0) digit_tot[blockIdx.x] = carry;
+}
+
+// The same scan with one wave per digit row (4 rows per 256-thread block): each lane takes 8
+// consecutive tile counts per round, all loads of a round in flight together.
+__global__ __launch_bounds__(256) void k_radix_scan_rows_w(uint32_t* __restrict__ counts, int64_t ntiles,
+                                                           uint32_t* __restrict__ digit_tot, int R) {
+  constexpr int J = 8;
+  const int lane = threadIdx.x & 63;
+  const int d = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (d >= R) return;  // wave-uniform
+  uint32_t* row = counts + (int64_t)d * ntiles;
+  uint32_t carry = 0;
+  for (int64_t c0 = 0; c0 < ntiles; c0 += 64 * J) {
+    const int64_t b = c0 + (int64_t)lane * J;
+    uint32_t v[J];
+#pragma unroll
+    for (int j = 0; j < J; ++j) v[j] = b + j < ntiles ? row[b + j] : 0u;
+    uint32_t sum = 0;
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      const uint32_t x = v[j];
+      v[j] = sum;
+      sum += x;
+    }
+    const uint32_t incl = wave_incl_scan_u32(sum, lane);
+    const uint32_t pre = carry + incl - sum;
+#pragma unroll
+    for (int j = 0; j < J; ++j)
+      if (b + j < ntiles) row[b + j] = pre + v[j];
+    carry += __shfl(incl, 63);
+  }
+  if (lane == 0) digit_tot[d] = carry;
 }
 
 // Block-wide exclusive scan of R values held as D = R / kBlock consecutive values per thread.
@@ -679,10 +721,14 @@ void SortWork::ensure(int64_t n) {
 template <class P, int RB>
 static void radix_pass_impl(const uint32_t* kin, const P* vin, uint32_t* ko, P* vo, int64_t n, int shift,
                        SortWork& w, int64_t ntiles, hipStream_t st) {
-  hipLaunchKernelGGL(k_radix_count<RB>, dim3((unsigned)(FM_SORT_CXCD ? blocks_for_tiles(ntiles) : ntiles)), dim3(kBlock), 0, st, kin, n, shift,
+  hipLaunchKernelGGL(k_radix_count<RB>, dim3((unsigned)(FM_SORT_CXCD ? blocks_for_tiles(ntiles) : ntiles)), dim3(kCntBlock), 0, st, kin, n, shift,
                      w.counts.as<uint32_t>(), ntiles);
-  hipLaunchKernelGGL(k_radix_scan_rows, dim3(1u << RB), dim3(kBlock), 0, st, w.counts.as<uint32_t>(), ntiles,
-                     w.digit_tot.as<uint32_t>());
+  if (FM_SORT_SMALLBLK)
+    hipLaunchKernelGGL(k_radix_scan_rows_w, dim3((1u << RB) / 4), dim3(256), 0, st, w.counts.as<uint32_t>(), ntiles,
+                       w.digit_tot.as<uint32_t>(), 1 << RB);
+  else
+    hipLaunchKernelGGL(k_radix_scan_rows, dim3(1u << RB), dim3(kBlock), 0, st, w.counts.as<uint32_t>(), ntiles,
+                       w.digit_tot.as<uint32_t>());
   hipLaunchKernelGGL((k_radix_scatter<P, RB>), dim3((unsigned)blocks_for_tiles(ntiles)), dim3(kBlock), 0, st, kin,
                      vin, ko, vo, n, shift, w.counts.as<uint32_t>(), w.digit_tot.as<uint32_t>(), ntiles);
   FM_HIP_CHECK(hipGetLastError());

@@ -5,7 +5,7 @@ Both sorts are stable by feature slot, so the step that consumes them must come 
 the same; each case also runs against the fp64 oracle.  FM_SORT_BUCKET_MIN=0 forces the bucket
 path at test sizes (it normally starts at 1M entries); FM_SORT_BUCKET=0 selects the LSD passes.
 Cases cover one in-bucket pass (slots of <= 9 + 9 bits), two passes, and a hot feature whose
-bucket outgrows the LDS image (15360 entries) and takes the global-scratch route.
+bucket outgrows the LDS image (30720 entries) and takes the global-scratch route.
 """
 
 import numpy as np
@@ -30,7 +30,8 @@ def _run(monkeypatch, bucket, csrs, F, k, ids, w, V):
         (5000, 1500, 12, None),       # 13-bit slots: one in-bucket pass of 4 bits
         (300000, 3000, 20, 7),        # 19-bit slots: two in-bucket passes (5 + 5 bits)
         ((1 << 21) + 5, 2500, 16, 123),  # 22-bit slots
-        (70000, 20000, 6, 4242),      # hot id in ~90 % of rows: an 18K-entry bucket (global scratch)
+        (70000, 20000, 6, 4242),      # hot id in ~90 % of rows: an 18K-entry bucket
+        (70000, 40000, 4, 4243),      # hot id in ~90 % of 40K rows: a 36K-entry bucket (global scratch)
     ],
 )
 def test_bucket_sort_step_matches_lsd_bitwise(monkeypatch, gpu, F, n_rows, mean_nnz, hot):
