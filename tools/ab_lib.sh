@@ -1,5 +1,6 @@
 #!/bin/bash
-# GPU box: alternating c3 step A/B of the default library against tools/_variants/$B (median of 40 steps).
+# GPU box: alternating c3 step A/B of the default library against tools/_variants/$B (median of 40 steps;
+# B may name several variants).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/ab
