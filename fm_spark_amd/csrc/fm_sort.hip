@@ -711,7 +711,6 @@ void SortWork::ensure(int64_t n) {
   keys_b.ensure(sizeof(uint32_t) * c);
   vals_a.ensure(sizeof(uint64_t) * c);  // payloads up to 8 bytes
   vals_b.ensure(sizeof(uint64_t) * c);
-  scratch.ensure(sizeof(uint2) * c);  // {sub, idx} of oversized buckets (bucket sort)
   const int64_t ntiles = (c + kTile - 1) / kTile;
   counts.ensure(sizeof(uint32_t) * kMaxRadix * ntiles);
   digit_tot.ensure(sizeof(uint32_t) * kMaxRadix * 2);  // digit totals + the bucket sort's block order
@@ -811,6 +810,7 @@ static void radix_sort_impl(SortWork& w, const uint32_t* keys_in, const P* vals_
       radix_pass<P, 9>(kin, vin, kbuf[0], vbuf[0], n, L, w, ntiles, st);
     else
       radix_pass<P, 10>(kin, vin, kbuf[0], vbuf[0], n, L, w, ntiles, st);
+    w.scratch.ensure(sizeof(uint2) * w.cap);  // {sub, idx} of oversized buckets, only on this path
     uint32_t* ko = final_keys ? final_keys : kbuf[1];
     P* vo = final_vals ? final_vals : vbuf[1];
     // the bucket order lives past the digit totals (kMaxRadix words each)
