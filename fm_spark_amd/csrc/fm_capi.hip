@@ -61,7 +61,7 @@ static void parallel_chunks(int64_t n, int64_t min_per_thread, F&& f) {
 // staging directly.  check_range: ids must be owned by this context's table (training); otherwise
 // any non-negative int32 id is accepted (predict drops unknown ids).
 struct Staged {
-  int64_t B = 0, N = 0, M = 0, max_id = -1;
+  int64_t B = 0, N = 0, M = 0, max_id = -1, max_len = 0;
   size_t o_lab = 0, o_xoff = 0, o_col = 0, o_x = 0, bytes = 0;  // bytes: the image through col
   int nruns = 0;
   int64_t run_at[16] = {0}, run_n[16] = {0};  // packed value runs in the x area (floats)
@@ -100,16 +100,17 @@ static Staged stage_csr(fm_ctx* ctx, const fm_csr* c, bool check_range, Pinned& 
   else rp[0] = 0;
   const int64_t F = ctx->cfg.num_features;
   std::atomic<int> bad{0};  // 1 negative id, 2 id >= num_features
-  std::atomic<int64_t> mx{-1};
+  std::atomic<int64_t> mx{-1}, mlen{0};
   // one pass over row chunks: ids (bit 31 = a value follows), labels, the chunk's values packed
   // from its first entry's position on
   std::atomic<int> nrun{0};
   parallel_chunks(B, 4096, [&](int64_t r0, int64_t r1) {
     const int64_t x0 = B > 0 ? c->row_ptr[r0] : 0;
-    int64_t lmx = -1, m = x0;
+    int64_t lmx = -1, m = x0, llen = 0;
     int lbad = 0;
     for (int64_t i = r0; i < r1; ++i) {
       lab[i] = c->label[i];  // Double, as the reference's label column (SGD.scala:145-146)
+      llen = std::max<int64_t>(llen, c->row_ptr[i + 1] - c->row_ptr[i]);
       xoff[i] = (int32_t)m;
       for (int64_t e = c->row_ptr[i]; e < c->row_ptr[i + 1]; ++e) {
         const int32_t id = c->col[e];
@@ -130,6 +131,9 @@ static Staged stage_csr(fm_ctx* ctx, const fm_csr* c, bool check_range, Pinned& 
     int64_t cur = mx.load();
     while (lmx > cur && !mx.compare_exchange_weak(cur, lmx)) {
     }
+    cur = mlen.load();
+    while (llen > cur && !mlen.compare_exchange_weak(cur, llen)) {
+    }
   });
   FM_REQUIRE(!(bad.load() & 1), "negative feature id");
   FM_REQUIRE(!(bad.load() & 2), "feature id >= num_features");
@@ -137,7 +141,26 @@ static Staged stage_csr(fm_ctx* ctx, const fm_csr* c, bool check_range, Pinned& 
   for (int r = 0; r < g.nruns; ++r) g.M += g.run_n[r];
   g.bytes = g.o_col + sizeof(uint32_t) * N;
   g.max_id = mx.load();
+  g.max_len = mlen.load();
   return g;
+}
+
+// Singleton fusion (FM_FUSE_SINGLE=1; off by default): prepared batches get per-entry singleton flags
+// and the forward applies those rows' updates (fm_kernels.hip k_forward<kTrainFused>,
+// k_segment_update skip_single).  Bit-exact, but measured slower: the forward's
+// extra row read and store per singleton are latency-exposed.
+static bool fuse_single_enabled() {
+  const char* e = getenv("FM_FUSE_SINGLE");  // read per call: A/B runs switch it
+  return e ? atoi(e) != 0 : false;
+}
+
+// Bits for an entry's position in its row next to the sample index in ent[].x (0: no packing --
+// fusion off, or sample and position do not fit 32 bits together).
+static int entry_pos_bits(const Staged& g) {
+  if (!fuse_single_enabled() || g.N == 0) return 0;
+  const int jb = bits_for(std::max<int64_t>(g.max_len - 1, 1));
+  const int sb = bits_for(std::max<int64_t>(g.B - 1, 1));
+  return sb + jb <= 32 ? jb : 0;
 }
 
 static bool batch_fits(const fm_batch* b, const Staged& g) {
@@ -159,6 +182,8 @@ static void copy_staged(fm_ctx* ctx, const Staged& g, const Pinned& pin, fm_batc
   b->max_id = g.max_id;
   b->dev.n_rows = B;
   b->dev.nnz = N;
+  b->dev.jb = entry_pos_bits(g);
+  b->single_ok = false;
   b->dev.row_ptr.ensure(sizeof(int64_t) * (B + 1));
   b->dev.col.ensure(sizeof(uint32_t) * std::max<int64_t>(N, 4) + 16);
   b->dev.ent.ensure(sizeof(uint32_t) * 2 * std::max<int64_t>(N, 4) + 16);
@@ -175,7 +200,8 @@ static void copy_staged(fm_ctx* ctx, const Staged& g, const Pinned& pin, fm_batc
   launch_explode(reinterpret_cast<const int64_t*>(up), reinterpret_cast<const double*>(up + g.o_lab),
                  reinterpret_cast<const int32_t*>(up + g.o_xoff), reinterpret_cast<const uint32_t*>(up + g.o_col),
                  reinterpret_cast<const float*>(up + g.o_x), B, N, b->dev.row_ptr.as<int64_t>(),
-                 b->dev.label.as<double>(), b->dev.col.as<uint32_t>(), b->dev.ent.as<uint2>(), b->dev.xs.as<float>(), st);
+                 b->dev.label.as<double>(), b->dev.col.as<uint32_t>(), b->dev.ent.as<uint2>(), b->dev.xs.as<float>(), st,
+                 b->dev.jb);
 }
 
 // Synchronous upload (fm_batch_create, fm_predict, fm_loss_grad): staged in the context's
@@ -255,9 +281,13 @@ int step_impl(fm_ctx* ctx, fm_batch* b, int32_t t, double step_size, double reg_
     FM_HIP_CHECK(hipEventRecord(ctx->ev_join, ctx->side));
   }
   static const bool serial = getenv("FM_NO_OVERLAP") != nullptr;  // diagnostic: no sort/forward overlap
-  if (serial) FM_HIP_CHECK(hipStreamWaitEvent(ctx->stream, prepared ? b->ready : ctx->ev_join, 0));
+  // singleton fusion: the forward reads the prepared view's flags, so it waits for that sort
+  const bool fuse = prepared && b->single_ok && !emit && fuse_single_enabled();
+  if (serial || fuse) FM_HIP_CHECK(hipStreamWaitEvent(ctx->stream, prepared ? b->ready : ctx->ev_join, 0));
   hipEvent_t e0 = ctx->prof_begin(ctx->stream);
-  launch_forward(T, b->dev, ctx->work, p, ctx->stream, &nfwd);
+  FwdOut fx{};
+  fx.single = fuse ? b->single.as<uint8_t>() : nullptr;
+  launch_forward(T, b->dev, ctx->work, p, ctx->stream, &nfwd, nullptr, fuse ? &fx : nullptr);
   ctx->prof_end("forward", e0, ctx->stream);
   FM_HIP_CHECK(hipStreamWaitEvent(ctx->stream, prepared ? b->ready : ctx->ev_join, 0));
 #ifndef FM_SORT_GATE
@@ -271,7 +301,7 @@ int step_impl(fm_ctx* ctx, fm_batch* b, int32_t t, double step_size, double reg_
   }
   e0 = ctx->prof_begin(ctx->stream);
   double* stats = ctx->loss_hist.as<double>() + 3 * (int64_t)ctx->epoch;
-  launch_segment_update(T, b->dev, ctx->work, p, skeys, sents, nfwd, stats, ctx->stream, emit);
+  launch_segment_update(T, b->dev, ctx->work, p, skeys, sents, nfwd, stats, ctx->stream, emit, fuse);
 #ifndef FM_PREP_EAGER
 #define FM_PREP_EAGER 1
 #endif
@@ -586,6 +616,13 @@ int fm_batch_prepare(fm_ctx* ctx, fm_batch* b) {
     const uint2* sv = nullptr;
     radix_sort_pairs64(ctx->work.sort, b->dev.col.as<uint32_t>(), b->dev.ent.as<uint2>(), N, bits_for(ctx->rows - 1),
                        ctx->side, &sk, &sv, b->skeys.as<uint32_t>(), b->sents.as<uint2>());
+    b->single_ok = false;
+    if (b->dev.jb > 0 && fuse_single_enabled()) {  // which entries' rows the forward may update itself
+      b->single.ensure(N);
+      launch_single_flags(b->skeys.as<uint32_t>(), b->sents.as<uint2>(), N, b->dev.row_ptr.as<int64_t>(), b->dev.jb,
+                          b->single.as<uint8_t>(), ctx->side);
+      b->single_ok = true;
+    }
     ctx->prof_end("sort", es, ctx->side);
     FM_HIP_CHECK(hipEventRecord(b->ready, ctx->side));
     b->prepared = true;

@@ -99,6 +99,8 @@ struct fm_batch {
   DevBuf up;  // device image of the host staging (fm_capi.hip copy_staged)
   // feature-major view produced by fm_batch_prepare (consumed once by the next step)
   DevBuf skeys, sents;
+  DevBuf single;                  // [nnz] u8: the entry's feature has no other entry (BatchDev::jb > 0)
+  bool single_ok = false;         // `single` matches the prepared sorted view
   hipEvent_t ready = nullptr;     // recorded on the side stream after the prepared sort
   hipEvent_t last_use = nullptr;  // recorded on the main stream after a step read skeys/sents
   bool prepared = false;
@@ -114,6 +116,7 @@ struct fm_batch {
     if (last_use) (void)hipEventDestroy(last_use);
     skeys.release();
     sents.release();
+    single.release();
     up.release();
     dev.row_ptr.release();
     dev.col.release();

@@ -112,6 +112,9 @@ struct BatchDev {
   int64_t n_rows = 0, nnz = 0;
   DevBuf row_ptr, col, ent, label;  // int64 [B+1], uint32 [N] feature slot, uint2 [N], double [B]
   DevBuf xs;                         // fp32 [N]: x alone, the forward's stream (8 B per entry with col)
+  // jb > 0: ent[e].x = sample << jb | (e - row_ptr[sample]) (the entry's position in its row), so a
+  // sorted view can name CSR entries (singleton flags, fm_batch_prepare); 0: ent[e].x = sample
+  int jb = 0;
 };
 
 // The single-table step's per-sample record: S (kp floats) and, for kp <= 16, the sample's
@@ -165,6 +168,10 @@ struct FwdOut {
   // keyed by (fill_seed, entry index, column)
   double fill_sd = 0.0;
   uint64_t fill_seed = 0;
+  // train mode: single[e] != 0 marks an entry whose feature has no other entry in the batch; the
+  // forward applies that row's update itself (with sp) and the update kernel skips the run
+  const uint8_t* single = nullptr;
+  StepParams sp{};
 };
 constexpr int kMaxChunkSources = 64;  // sources a chunked partial pass can split
 // partial_out != nullptr: the sharded owner's partial pass (fm_shard.hip): [pairs][kp] fp32 vectors
@@ -179,12 +186,18 @@ struct SegSource {
   int64_t s_stride;
   const float2* yl;
   int64_t yl_stride;
+  int jb = 0;                // sents' sample field is sample << jb | position in row (BatchDev::jb)
+  bool skip_single = false;  // singleton runs were applied by the forward (FwdOut::single)
 };
 // emit != nullptr (replicated mode): the per-slot gradient sums go to emit[rows][kp + 4] as
 // [sum g_V (kp) | sum g_w | 1 (touched) | 0] instead of being applied to the table
 void launch_segment_update(const TableView& T, const BatchDev& b, StepWork& w, const StepParams& p,
                            const uint32_t* skeys, const uint2* sents, int64_t n_fwd_blocks,
-                           double* stats_out, hipStream_t st, float* emit = nullptr);
+                           double* stats_out, hipStream_t st, float* emit = nullptr, bool skip_single = false);
+// fm_batch_prepare on a batch with BatchDev::jb > 0: single[e] = 1 when entry e's feature has no
+// other entry in the batch (its sorted run has length 1), else 0, for every entry
+void launch_single_flags(const uint32_t* skeys, const uint2* sents, int64_t N, const int64_t* row_ptr, int jb,
+                         uint8_t* single, hipStream_t st);
 void launch_segment_update(const TableView& T, int64_t N, const SegSource& src, StepWork& w, const StepParams& p,
                            const uint32_t* skeys, const uint2* sents, int64_t n_loss_blocks, double* stats_out,
                            hipStream_t st, float* emit = nullptr);
@@ -217,6 +230,6 @@ void launch_count_present(const TableView& T, int64_t* out, hipStream_t st);
 // bits} rebuilt from row_ptr and the compact values (the explode of Model.scala:148-153)
 void launch_explode(const int64_t* row_ptr_in, const double* label_in, const int32_t* xoff, const uint32_t* col_in,
                     const float* x_in, int64_t B, int64_t N, int64_t* row_ptr, double* label, uint32_t* col, uint2* ent,
-                    float* xs, hipStream_t st);
+                    float* xs, hipStream_t st, int jb = 0);
 
 }  // namespace fmhip

@@ -108,6 +108,7 @@ __device__ __forceinline__ float gauss_draw(uint64_t seed, int64_t id, int f, do
 // squared error, deltaWi = x and deltaVi = vfxiSum * x - (v * x) * x, fp64 from the team's fp64
 // sums (a second walk over the sample's entries re-reads their rows); absent ids set the flag.
 constexpr int kTrain = 0, kPartial = 1, kPredict = 2, kLossGrad = 3;
+constexpr int kTrainFused = 4;  // kTrain + the singleton rows' updates (FM_FUSE_SINGLE=1; measured slower, off)
 #ifndef FM_FWD_U
 #define FM_FWD_U 4  // sharded partial pass: passes (entries per lane) whose rows are in flight together
 #endif
@@ -286,6 +287,79 @@ __global__ __launch_bounds__(kBlock, FM_FWD_MINW) void k_forward(TableView T, co
     }
     if (rs == 0 && qok)
       *reinterpret_cast<float4*>(S_out + s * sstr + g * 4) = make_float4((float)a0, (float)a1, (float)a2, (float)a3);
+    if (MODE == kTrainFused) {
+      // The rows whose only entry in this batch belongs to this sample: their update (SGD.scala:
+      // 145-181 over a run of one entry) is applied here, from the values the update kernel would
+      // read back -- S, r and yhat rounded to fp32 as stored, x from the batch -- with its
+      // arithmetic, so the table is bit for bit the unfused step's.  The row was read a moment ago
+      // (an L2 hit); the update kernel skips these runs (no row read, no S gather there).
+      const float r32 = (float)(yhat - label[s]), yh32 = (float)yhat;
+      const double rj = (double)r32, yh = (double)yh32;
+      const float4 Sq = make_float4((float)a0, (float)a1, (float)a2, (float)a3);
+      const StepParams& sp = xo.sp;
+      const float lamf = (float)sp.lam;
+      const int span = 4 + ((16 - ((kp + 4) & 15)) & 15);  // header + zero pad of its 64-B granule
+#ifndef FM_FUSE_ABL
+#define FM_FUSE_ABL 0  // measurement only: 1 = no stores
+#endif
+#ifndef FM_FUSE_FW
+#define FM_FUSE_FW 3  // singleton entries per lane whose rows are loaded together
+#endif
+      // the sample's singleton rows are loaded FW entries per lane at a time, all in flight, before
+      // any is computed or stored (stores in between would order every later load behind them)
+      constexpr int FW = FM_FUSE_FW;
+      for (int64_t eb = e0 + rs; eb < e1; eb += FW * RPP) {
+        bool on[FW];
+        uint32_t idv[FW];
+        float xv[FW];
+        RowHdr hv[FW];
+        float4 vv4[FW];
+#pragma unroll
+        for (int j = 0; j < FW; ++j) {
+          const int64_t e = eb + j * RPP;
+          on[j] = e < e1 && xo.single[e];
+          idv[j] = on[j] ? col[e] : 0u;
+          xv[j] = on[j] ? xs[e] : 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < FW; ++j) {
+          if (on[j]) {
+            hv[j] = *T.hdr(idv[j]);
+            vv4[j] = qok ? reinterpret_cast<const float4*>(T.v(idv[j]))[g] : make_float4(0.f, 0.f, 0.f, 0.f);
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < FW; ++j) {
+          if (!on[j]) continue;
+          const RowHdr h = hv[j];
+          const double xd = (double)xv[j];
+          const float acf = (float)(sp.cumE - h.cum);  // pending L1 of the row
+          float* rec = T.v(idv[j]);
+          const double t = xd * rj, b = (xd * xd) * rj;
+          const double gwe = (xd - 1.0) * yh + rj;  // x yhat - y (SGD.scala:145)
+          if (qok) {
+            const float4 v = shrink4f(vv4[j], acf);
+            const double g0 = fma((double)Sq.x, t, 0.0) - (double)v.x * b, g1 = fma((double)Sq.y, t, 0.0) - (double)v.y * b;
+            const double g2 = fma((double)Sq.z, t, 0.0) - (double)v.z * b, g3 = fma((double)Sq.w, t, 0.0) - (double)v.w * b;
+            const float4 u = make_float4((float)fma(g0, -sp.scale_v, (double)v.x), (float)fma(g1, -sp.scale_v, (double)v.y),
+                                         (float)fma(g2, -sp.scale_v, (double)v.z), (float)fma(g3, -sp.scale_v, (double)v.w));
+            if (FM_FUSE_ABL != 1) st_row4(rec + 4 * g, shrink4f(u, lamf));
+            else if (u.x == 12345.f) rec[0] = 0.f;  // keep the computation alive
+          }
+          for (int i = 4 * g; i < span && FM_FUSE_ABL != 1; i += 4 * GS) {
+            float4 hq = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (i == 0) {
+              RowHdr o;
+              o.w = upd_w(shrink1f(h.w, acf), 0.0 + gwe, sp);  // SGD.scala:150, :171
+              o.t = sp.epoch + 1;
+              o.cum = sp.cum_next;
+              hq = *reinterpret_cast<const float4*>(&o);
+            }
+            st_row4(rec + kp + i, hq);
+          }
+        }
+      }
+    }
     if (tl == 0) {
       const double y = label[s];
       // r = pred - label in fp64 (SGD.scala:146), rounded once: relative error 2^-24 of r itself
@@ -297,7 +371,7 @@ __global__ __launch_bounds__(kBlock, FM_FWD_MINW) void k_forward(TableView T, co
       }
     }
   }
-  if (MODE != kTrain) return;
+  if (MODE != kTrain && MODE != kTrainFused) return;
   // deterministic block reduction of the loss partials
   __shared__ double red[2][kBlock / 64];
 #pragma unroll
@@ -336,6 +410,8 @@ struct SegArgs {
   StepParams p;
   uint32_t* ucnt;  // [update blocks]
   float* emit;     // replicated mode: per-slot gradient sums [rows][kp + 4] instead of the update
+  int jb;          // sents[].x = sample << jb | position in row
+  int skip_single; // runs of one entry were applied by the forward: not loaded, not written here
 };
 
 constexpr uint32_t kFValid = 1u, kFEnd = 2u, kFStart = 4u;
@@ -474,13 +550,15 @@ __global__ __launch_bounds__(kBlock, NF == 1 ? FM_UPD_MINW : 1) void k_segment_u
       const bool st = valid && key[i] != prev;
       const bool end = valid && key[i] != next;
       ucount += (uint32_t)__popcll(__ballot(st));
+      // a run of one entry that the forward already applied stays out of phase 2 (no loads, no store)
+      const bool live = valid && !(a.skip_single && st && end);
       const int l = li(i * 64 + lane);
-      img_k[l] = make_uint2(key[i], (valid ? kFValid : 0u) | (end ? kFEnd : 0u) | (st ? kFStart : 0u));
-      img_s[l] = (int)en[i].x;
+      img_k[l] = make_uint2(key[i], (live ? kFValid : 0u) | (end ? kFEnd : 0u) | (st ? kFStart : 0u));
+      img_s[l] = (int)(en[i].x >> a.jb);
 #if FM_UPD_YL2
       img_x[l] = __uint_as_float(en[i].y);
 #else
-      yl[i] = valid ? a.yl[(int64_t)en[i].x * a.yl_stride] : make_float2(0.f, 0.f);
+      yl[i] = valid ? a.yl[(int64_t)(en[i].x >> a.jb) * a.yl_stride] : make_float2(0.f, 0.f);
 #endif
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1233,11 +1311,14 @@ void launch_fwd_t(const TableView& T, const BatchDev& b, StepWork& w, const Step
     return;
   }
   w.loss_part.ensure(sizeof(double2) * blocks);
-  hipLaunchKernelGGL((k_forward<GS, TEAM, kTrain, U>), grid, blk, 0, st, T, b.row_ptr.as<int64_t>(),
+  FwdOut tr = xo ? *xo : none;  // train mode: xo carries the singleton flags (fused updates), if any
+  if (tr.single) tr.sp = p;
+  auto kern = tr.single ? k_forward<GS, TEAM, kTrainFused, U> : k_forward<GS, TEAM, kTrain, U>;
+  hipLaunchKernelGGL(kern, grid, blk, 0, st, T, b.row_ptr.as<int64_t>(),
                      b.col.as<uint32_t>(), b.ent.as<uint2>(), b.xs.as<float>(), b.label.as<double>(), b.n_rows, p.w0, p.cumE,
                      w.S.as<float>(), s_rec_yl(T.kp) ? reinterpret_cast<float2*>(w.S.as<float>() + T.kp) : w.yl.as<float2>(),
                      (int64_t)s_rec_floats(T.kp), s_rec_yl(T.kp) ? (int64_t)s_rec_floats(T.kp) / 2 : (int64_t)1,
-                     w.loss_part.as<double2>(), none);
+                     w.loss_part.as<double2>(), tr);
 }
 
 }  // namespace
@@ -1282,10 +1363,12 @@ void launch_forward(const TableView& T, const BatchDev& b, StepWork& w, const St
 
 void launch_segment_update(const TableView& T, const BatchDev& b, StepWork& w, const StepParams& p,
                            const uint32_t* skeys, const uint2* sents, int64_t n_fwd_blocks,
-                           double* stats_out, hipStream_t st, float* emit) {
+                           double* stats_out, hipStream_t st, float* emit, bool skip_single) {
   SegSource src{w.S.as<float>(), s_rec_floats(T.kp),
                  s_rec_yl(T.kp) ? reinterpret_cast<const float2*>(w.S.as<float>() + T.kp) : w.yl.as<float2>(),
                  s_rec_yl(T.kp) ? s_rec_floats(T.kp) / 2 : 1};
+  src.jb = b.jb;
+  src.skip_single = skip_single;
   launch_segment_update(T, b.nnz, src, w, p, skeys, sents, n_fwd_blocks, stats_out, st, emit);
 }
 
@@ -1313,6 +1396,8 @@ void launch_segment_update(const TableView& T, int64_t N, const SegSource& src, 
   a.p = p;
   a.ucnt = w.ucnt.as<uint32_t>();
   a.emit = emit;
+  a.jb = src.jb;
+  a.skip_single = src.skip_single && !emit ? 1 : 0;
   if (ublocks > 0) {
     const int64_t gcap = FM_UPD_GRID > 0 && ublocks > FM_UPD_GRID ? FM_UPD_GRID : ublocks;
     const dim3 grid((unsigned)gcap), blk(kBlock);
@@ -1452,7 +1537,7 @@ __global__ __launch_bounds__(kBlock) void k_explode(const int64_t* __restrict__ 
                                                    const int32_t* __restrict__ xoff, const uint32_t* __restrict__ col_in,
                                                    const float* __restrict__ x_in, int64_t B, int64_t* __restrict__ rp,
                                                    double* __restrict__ lab, uint32_t* __restrict__ col,
-                                                   uint2* __restrict__ ent, float* __restrict__ xs) {
+                                                   uint2* __restrict__ ent, float* __restrict__ xs, int jb) {
   constexpr int T = 16;
   const int tl = threadIdx.x % T;
   const int lane = threadIdx.x & 63;
@@ -1463,7 +1548,8 @@ __global__ __launch_bounds__(kBlock) void k_explode(const int64_t* __restrict__ 
   for (int64_t i = gtid; i <= B; i += nthreads) rp[i] = rp_in[i];
   for (int64_t i = gtid; i < B; i += nthreads) lab[i] = lab_in[i];
   for (int64_t s = gtid / T; s < B; s += nthreads / T) {
-    const int64_t e1 = rp_in[s + 1];
+    const int64_t e0 = rp_in[s], e1 = rp_in[s + 1];
+    const uint32_t sj = (uint32_t)s << jb;  // jb > 0: the entry's position in its row below
     int64_t xo = xoff[s];
     for (int64_t eb = rp_in[s]; eb < e1; eb += T) {  // the team's lanes take the same trips
       const int64_t e = eb + tl;
@@ -1474,19 +1560,43 @@ __global__ __launch_bounds__(kBlock) void k_explode(const int64_t* __restrict__ 
       xo += __popcll(m & team_bits);
       if (e < e1) {
         col[e] = c & 0x7FFFFFFFu;
-        ent[e] = make_uint2((uint32_t)s, __float_as_uint(x));
+        ent[e] = make_uint2(jb ? sj | (uint32_t)(e - e0) : (uint32_t)s, __float_as_uint(x));
         xs[e] = x;
       }
     }
   }
 }
 
+// single[e] for every entry e of a sorted batch view: 1 when its run (equal feature slots) has one
+// entry, else 0; e = row_ptr[sample] + position, both from the packed sample field.
+__global__ __launch_bounds__(kBlock) void k_single_flags(const uint32_t* __restrict__ skeys,
+                                                        const uint2* __restrict__ sents, int64_t N,
+                                                        const int64_t* __restrict__ row_ptr, int jb,
+                                                        uint8_t* __restrict__ single) {
+  const uint32_t jm = (1u << jb) - 1u;
+  for (int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x; p < N; p += (int64_t)gridDim.x * kBlock) {
+    const uint32_t key = skeys[p];
+    const bool one = (p == 0 || skeys[p - 1] != key) && (p + 1 == N || skeys[p + 1] != key);
+    const uint32_t sx = sents[p].x;
+    single[row_ptr[sx >> jb] + (sx & jm)] = one ? 1 : 0;
+  }
+}
+
+void launch_single_flags(const uint32_t* skeys, const uint2* sents, int64_t N, const int64_t* row_ptr, int jb,
+                         uint8_t* single, hipStream_t st) {
+  if (N <= 0) return;
+  FM_REQUIRE(jb > 0, "singleton flags need the packed entry positions");
+  hipLaunchKernelGGL(k_single_flags, dim3(grid_for(N, kBlock, 256 * 16)), dim3(kBlock), 0, st, skeys, sents, N, row_ptr,
+                     jb, single);
+  FM_HIP_CHECK(hipGetLastError());
+}
+
 void launch_explode(const int64_t* row_ptr_in, const double* label_in, const int32_t* xoff, const uint32_t* col_in,
                     const float* x_in, int64_t B, int64_t N, int64_t* row_ptr, double* label, uint32_t* col, uint2* ent,
-                    float* xs, hipStream_t st) {
+                    float* xs, hipStream_t st, int jb) {
   (void)N;
   hipLaunchKernelGGL(k_explode, dim3(grid_for(std::max<int64_t>(B, 1) * 16, kBlock, 256 * 8)), dim3(kBlock), 0, st,
-                     row_ptr_in, label_in, xoff, col_in, x_in, B, row_ptr, label, col, ent, xs);
+                     row_ptr_in, label_in, xoff, col_in, x_in, B, row_ptr, label, col, ent, xs, jb);
   FM_HIP_CHECK(hipGetLastError());
 }
 

@@ -1,0 +1,80 @@
+"""GPU: singleton fusion (FM_FUSE_SINGLE=1, off by default) -- the forward applies the update of every row whose
+feature has one entry in the batch, and the update kernel skips those runs.
+
+The fused step must give the unfused step's table bit for bit (the forward uses the update's
+arithmetic on the same fp32-rounded S, r and yhat) and match the fp64 oracle; the flags come from
+the prepared sorted view (fm_batch_prepare), so both paths run on prepared batches here.  Widths
+cover every header-granule shape (kp = 4, 8, 12, 16, 32, 80).
+"""
+
+import numpy as np
+import pytest
+
+from oracle import fm_ref as R
+from problems import make_problem
+from test_gpu_parity import assert_tables, to_host
+
+pytestmark = pytest.mark.gpu
+
+
+def _prepared_steps(monkeypatch, fuse, csrs, F, k, ids, w, V, steps):
+    from fm_spark_amd.engine import FMContext
+
+    monkeypatch.setenv("FM_FUSE_SINGLE", "1" if fuse else "0")
+    ctx = FMContext(F, k)
+    ctx.load_tables(ids, w, V)
+    dbs = [ctx.batch(to_host(c)) for c in csrs]
+    losses = []
+    for t in range(1, steps + 1):
+        b = dbs[(t - 1) % len(dbs)]
+        b.prepare()
+        o = ctx.step_batch(b, t, 0.3, 1e-4)
+        losses.append((o.loss_sum, o.n_unique))
+    out = ctx.export_tables()
+    ctx.close()
+    return losses, out
+
+
+@pytest.mark.parametrize("k", [3, 8, 12, 16, 32, 80])
+def test_fused_singletons_bitwise_equal_unfused(monkeypatch, gpu, k):
+    F = 20000
+    csrs = [make_problem(700 + i, 1500, F, k, 12, hot=5 + i)[0] for i in range(3)]
+    _, ids, w, V = make_problem(71, 1, F, k, 1)
+    lf, tf = _prepared_steps(monkeypatch, True, csrs, F, k, ids, w, V, 4)
+    lu, tu = _prepared_steps(monkeypatch, False, csrs, F, k, ids, w, V, 4)
+    assert lf == lu
+    for a, b in zip(tf, tu):
+        assert np.array_equal(a, b)
+    # and the oracle
+    model = R.Model.empty(F, k)
+    model.load(ids, w, V)
+    for t in range(1, 5):
+        ro = R.sgd_step_fast(model, csrs[(t - 1) % 3], t, 0.3, 1e-4)
+        np.testing.assert_allclose(lf[t - 1][0], ro.loss_sum, rtol=1e-6)
+        assert lf[t - 1][1] == ro.n_unique
+    assert_tables(model, tf)
+
+
+def test_fused_absent_rows_and_l1(monkeypatch, gpu):
+    """Singleton rows absent from the model (zero rows made present by their update) and a regParam
+    whose soft-threshold zeroes values: fused and unfused agree bit for bit."""
+    F, k = 5000, 16
+    csrs = [make_problem(760 + i, 800, F, k, 10)[0] for i in range(2)]
+    _, ids, w, V = make_problem(72, 1, F, k, 1)
+    keep = ids[::3]  # two thirds of the rows absent
+    res = []
+    for fuse in (True, False):
+        from fm_spark_amd.engine import FMContext
+
+        monkeypatch.setenv("FM_FUSE_SINGLE", "1" if fuse else "0")
+        ctx = FMContext(F, k)
+        ctx.load_tables(keep, w[keep], V[keep])
+        dbs = [ctx.batch(to_host(c)) for c in csrs]
+        for t in range(1, 4):
+            b = dbs[(t - 1) % 2]
+            b.prepare()
+            ctx.step_batch(b, t, 0.5, 0.05)
+        res.append(ctx.export_tables())
+        ctx.close()
+    for a, b in zip(res[0], res[1]):
+        assert np.array_equal(a, b)
