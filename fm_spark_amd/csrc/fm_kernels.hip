@@ -108,6 +108,9 @@ __device__ __forceinline__ float gauss_draw(uint64_t seed, int64_t id, int f, do
 // squared error, deltaWi = x and deltaVi = vfxiSum * x - (v * x) * x, fp64 from the team's fp64
 // sums (a second walk over the sample's entries re-reads their rows); absent ids set the flag.
 constexpr int kTrain = 0, kPartial = 1, kPredict = 2, kLossGrad = 3;
+#ifndef FM_FUSE_MZ
+#define FM_FUSE_MZ 40  // kTrainFused, kp <= 16: entries per sample whose singleton rows are kept in LDS
+#endif
 constexpr int kTrainFused = 4;  // kTrain + the singleton rows' updates (FM_FUSE_SINGLE=1; measured slower, off)
 #ifndef FM_FWD_U
 #define FM_FWD_U 4  // sharded partial pass: passes (entries per lane) whose rows are in flight together
@@ -175,6 +178,30 @@ __global__ __launch_bounds__(kBlock, FM_FWD_MINW) void k_forward(TableView T, co
     Bl = ch_base[xo.ch_R];
   }
 
+  // kTrainFused at kp <= 16: each lane keeps, in LDS, the singleton rows of the entries it gathers
+  // (raw V quad + header + id, slot = the entry's index in its sample) -- no global re-read -- and
+  // after the sample's reduction rewrites them updated in place; their stores are issued after the
+  // next sample's first gathers (so no load waits behind them), the last sample's at the end.
+  // Every slot is read and written by the lane that gathered it: no barrier.
+  constexpr bool STASH = MODE == kTrainFused && GS <= 4 && TEAM >= 16 && FM_FUSE_MZ > 0;
+  constexpr int MZ = STASH ? FM_FUSE_MZ : 1;
+  __shared__ float4 st_v[STASH ? TPB : 1][MZ][STASH ? GS : 1];
+  __shared__ float4 st_h[STASH ? TPB : 1][MZ];
+  __shared__ uint32_t st_id[STASH ? TPB : 1][MZ];
+  const int team = tid / TEAM;
+  int pend = 0;  // slots 0 .. pend - 1 of this team may hold updated rows to store
+  const int span = 4 + ((16 - ((kp + 4) & 15)) & 15);  // header + zero pad of its 64-B granule
+  auto flush = [&]() {
+    for (int i = rs; i < pend; i += RPP) {
+      const uint32_t sid = st_id[team][i];
+      if (sid == 0xFFFFFFFFu) continue;
+      float* rec = T.v(sid);
+      if (qok) st_row4(rec + 4 * g, st_v[team][i][g]);
+      for (int c = 4 * g; c < span; c += 4 * GS) st_row4(rec + kp + c, c == 0 ? st_h[team][i] : make_float4(0.f, 0.f, 0.f, 0.f));
+    }
+    pend = 0;
+  };
+
   for (int64_t sl = (int64_t)blockIdx.x * TPB + tid / TEAM; sl < Bl; sl += (int64_t)gridDim.x * TPB) {
     int64_t s = sl;
     if (chunked) {
@@ -198,6 +225,11 @@ __global__ __launch_bounds__(kBlock, FM_FWD_MINW) void k_forward(TableView T, co
         // the batch's x stream (4 B per entry); the partial pass's entries carry x themselves
         x[j] = ok[j] ? (PARTIAL ? __uint_as_float(ld_stream(ent + e, FM_NT_CSR).y) : ld_stream(xs + e, FM_NT_CSR)) : 0.f;
       }
+      bool sg[U];
+      if (STASH) {
+#pragma unroll
+        for (int j = 0; j < U; ++j) sg[j] = ok[j] && eb + j * RPP - e0 < MZ && xo.single[eb + j * RPP] != 0;
+      }
       RowHdr h[U];
       float4 v[U];
 #pragma unroll
@@ -209,6 +241,18 @@ __global__ __launch_bounds__(kBlock, FM_FWD_MINW) void k_forward(TableView T, co
         } else {
           h[j] = RowHdr{0.f, -1, 0.0};
           v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+      }
+      if (STASH && eb == e0 + rs) flush();  // the previous sample's rows, behind this sample's first gathers
+#pragma unroll
+      for (int j = 0; j < U; ++j) {
+        if (STASH && ok[j] && eb + j * RPP - e0 < MZ) {
+          const int i = (int)(eb + j * RPP - e0);
+          if (sg[j]) {
+            st_v[team][i][g] = v[j];
+            if (g == 0) st_h[team][i] = *reinterpret_cast<const float4*>(&h[j]);
+          }
+          if (g == 0) st_id[team][i] = sg[j] ? id[j] : 0xFFFFFFFFu;
         }
       }
 #pragma unroll
@@ -298,7 +342,36 @@ __global__ __launch_bounds__(kBlock, FM_FWD_MINW) void k_forward(TableView T, co
       const float4 Sq = make_float4((float)a0, (float)a1, (float)a2, (float)a3);
       const StepParams& sp = xo.sp;
       const float lamf = (float)sp.lam;
-      const int span = 4 + ((16 - ((kp + 4) & 15)) & 15);  // header + zero pad of its 64-B granule
+      if (STASH) {
+        // the stashed rows (the sample's first MZ entries), updated in place in LDS
+        const int zc = (int)std::min<int64_t>(e1 - e0, MZ);
+        for (int i = rs; i < zc; i += RPP) {
+          const uint32_t sid = st_id[team][i];
+          if (sid == 0xFFFFFFFFu) continue;
+          const float4 hq = st_h[team][i];
+          const RowHdr h = *reinterpret_cast<const RowHdr*>(&hq);
+          const double xd = (double)xs[e0 + i];
+          const float acf = (float)(sp.cumE - h.cum);  // pending L1 of the row
+          const double t = xd * rj, b = (xd * xd) * rj;
+          const double gwe = (xd - 1.0) * yh + rj;  // x yhat - y (SGD.scala:145)
+          if (qok) {
+            const float4 v = shrink4f(st_v[team][i][g], acf);
+            const double g0 = fma((double)Sq.x, t, 0.0) - (double)v.x * b, g1 = fma((double)Sq.y, t, 0.0) - (double)v.y * b;
+            const double g2 = fma((double)Sq.z, t, 0.0) - (double)v.z * b, g3 = fma((double)Sq.w, t, 0.0) - (double)v.w * b;
+            const float4 u = make_float4((float)fma(g0, -sp.scale_v, (double)v.x), (float)fma(g1, -sp.scale_v, (double)v.y),
+                                         (float)fma(g2, -sp.scale_v, (double)v.z), (float)fma(g3, -sp.scale_v, (double)v.w));
+            st_v[team][i][g] = shrink4f(u, lamf);
+          }
+          if (g == 0) {
+            RowHdr o;
+            o.w = upd_w(shrink1f(h.w, acf), 0.0 + gwe, sp);  // SGD.scala:150, :171
+            o.t = sp.epoch + 1;
+            o.cum = sp.cum_next;
+            st_h[team][i] = *reinterpret_cast<const float4*>(&o);
+          }
+        }
+        pend = zc;
+      }
 #ifndef FM_FUSE_ABL
 #define FM_FUSE_ABL 0  // measurement only: 1 = no stores
 #endif
@@ -307,8 +380,8 @@ __global__ __launch_bounds__(kBlock, FM_FWD_MINW) void k_forward(TableView T, co
 #endif
       // the sample's singleton rows are loaded FW entries per lane at a time, all in flight, before
       // any is computed or stored (stores in between would order every later load behind them)
-      constexpr int FW = FM_FUSE_FW;
-      for (int64_t eb = e0 + rs; eb < e1; eb += FW * RPP) {
+      constexpr int FW = STASH ? 1 : FM_FUSE_FW;  // with the stash only entries beyond MZ come here
+      for (int64_t eb = e0 + (STASH ? MZ : 0) + rs; eb < e1; eb += FW * RPP) {
         bool on[FW];
         uint32_t idv[FW];
         float xv[FW];
@@ -371,6 +444,7 @@ __global__ __launch_bounds__(kBlock, FM_FWD_MINW) void k_forward(TableView T, co
       }
     }
   }
+  if (STASH) flush();  // the last sample's rows
   if (MODE != kTrain && MODE != kTrainFused) return;
   // deterministic block reduction of the loss partials
   __shared__ double red[2][kBlock / 64];
