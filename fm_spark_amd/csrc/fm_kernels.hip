@@ -212,6 +212,7 @@ __global__ __launch_bounds__(kBlock, FM_FWD_MINW) void k_forward(TableView T, co
     const int64_t e0 = row_ptr[s], e1 = row_ptr[s + 1];
     double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0, vv = 0.0, wx = 0.0;
     uint32_t npres = 0;  // kPredict: learned entries of the sample (this lane's share)
+    if (STASH && e0 + rs >= e1) flush();  // no entry of this sample for the lane: nothing to wait behind
     for (int64_t eb = e0 + rs; eb < e1; eb += U * RPP) {
       uint32_t id[U];
       float x[U];

@@ -78,3 +78,17 @@ def test_fused_absent_rows_and_l1(monkeypatch, gpu):
         ctx.close()
     for a, b in zip(res[0], res[1]):
         assert np.array_equal(a, b)
+
+
+def test_fused_short_empty_and_long_rows(monkeypatch, gpu):
+    """Rows shorter than a team's entry slots and empty rows (the stash flush for lanes without an
+    entry), and rows longer than the 40 stashed entries (the global fallback), at k = 16."""
+    F, k = 30000, 16
+    csrs = [make_problem(780 + i, 1200, F, k, 3, empty_frac=0.3)[0] for i in range(2)]
+    csrs += [make_problem(790, 300, F, k, 60)[0]]  # up to 119 entries per row
+    _, ids, w, V = make_problem(73, 1, F, k, 1)
+    lf, tf = _prepared_steps(monkeypatch, True, csrs, F, k, ids, w, V, 6)
+    lu, tu = _prepared_steps(monkeypatch, False, csrs, F, k, ids, w, V, 6)
+    assert lf == lu
+    for a, b in zip(tf, tu):
+        assert np.array_equal(a, b)
