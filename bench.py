@@ -10,9 +10,13 @@ row (Criteo-shaped synthetic data); stepSize 0.1, regParam 1e-
   python bench.py [--gpus N --steps K --warmup W]
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (one rank per GPU)
 
-N = 1 runs the fused single-table path.  N > 1 row-shards the table (owner = id mod N) and
-exchanges ids / rows / gradients with RCCL all-to-all (weak scaling: every rank steps its own
-256K-row batch each iteration).  Rank 0 prints one JSON line.
+N = 1 runs the single-table path (fused step: the forward updates the rows whose feature has one
+entry in the batch).  N > 1 row-shards the table (owner = id mod N; --parallel replicated keeps a
+whole table per GPU) and exchanges entries / partial sums / S rows with RCCL all-to-all inside
+libfm_hip (weak scaling: every rank steps its own 256K-row batch each iteration).  Without a
+launcher, --gpus N drives N GPUs from this one process through one multi-GPU fm_ctx (the Spark
+driver's path); under torch.distributed.run each process drives its own GPU.  Asking for more GPUs
+than are visible exits non-zero.  Rank 0 prints one JSON line.
 """
 
 from __future__ import annotations
@@ -58,18 +62,24 @@ def parse():
     p.add_argument("--rows", type=int, default=0, help="override rows per batch (experiments)")
     p.add_argument("--zipf", type=float, default=0.0, help="override the Zipf exponent (c5's hot rows: 1.2)")
     p.add_argument("--force-sharded", action="store_true",
-                   help="run the row-sharded RCCL path even with one rank (tests the N > 1 code path)")
+                   help="N = 1: run the multi-GPU group context (RCCL, one rank) instead of the single table")
+    p.add_argument("--parallel", default="auto", choices=["auto", "sharded", "replicated"],
+                   help="multi-GPU table layout: row-sharded by id %% R or replicated with a gradient all-reduce "
+                        "(auto: replicated for c2, else sharded); given explicitly at N = 1 it implies the group path")
     p.add_argument("--no-prefetch", action="store_true",
                    help="sort each batch inside its own step instead of during the previous step")
     p.add_argument("--host-path", action="store_true",
                    help="single table: time fm_step with the host CSR each call (PCIe-inclusive, as a JNI "
                         "caller sees it) instead of device-resident batches; reported, never the headline")
-    p.add_argument("--prefetch-depth", type=int, default=1,
-                   help="single table: how many steps ahead a batch is sorted on the side stream")
+    p.add_argument("--prefetch-depth", type=int, default=2,
+                   help="single table: how many steps ahead a batch is sorted (and split) on the side stream")
+    p.add_argument("--fuse", default="on", choices=["on", "off"],
+                   help="single table, k <= 16: the fused step (the forward updates the rows whose feature has one "
+                        "entry in the batch; fm_config.fuse_single); off = every row through the segmented update")
     p.add_argument("--trainer", default="lib", choices=["lib", "torch"],
-                   help="N > 1 / --force-sharded: 'lib' = one multi-GPU fm_ctx per process, the exchanges "
-                        "inside libfm_hip over RCCL (the C-ABI path); 'torch' = the torch.distributed test "
-                        "harness (fm_spark_amd/distributed.py) driving the fm_shard_* phases")
+                   help="N > 1: 'lib' = the multi-GPU fm_ctx, every exchange inside libfm_hip over RCCL (the "
+                        "C-ABI path); 'torch' (torch.distributed.run only) = the torch.distributed test harness "
+                        "(fm_spark_amd/distributed.py) driving the fm_shard_* phases")
     p.add_argument("--host-path-steps", type=int, default=12,
                    help="N = 1: after the timed region, time this many fm_step calls with the host CSR "
                         "(PCIe-inclusive, what a JNI caller gets) for host_path_ms_per_step; 0 = skip")
@@ -143,10 +153,11 @@ PHASE_KERNELS = {"forward": ["k_forward"], "update": ["k_segment_update", "k_seg
                  "owner_forward": ["k_forward"], "owner_update": ["k_segment_update", "k_segment_combine"]}
 
 
-def pmc_traffic(F, k, B, phase):
+def pmc_traffic(F, k, B, phase, fused=False):
     """HBM bytes per launch of `phase` from the committed rocprofv3 PMC passes of this workload
     (profiles/pmc_*.json, made by tools/pmc.sh + tools/pmc_to_json.py with the calibrated
-    FETCH_SIZE/WRITE_SIZE corrections).  None when no pass of this exact workload is committed."""
+    FETCH_SIZE/WRITE_SIZE corrections; "fused" says which step variant the passes measured).  None
+    when no pass of this exact workload and variant is committed."""
     import glob
 
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json"))):
@@ -154,7 +165,7 @@ def pmc_traffic(F, k, B, phase):
             d = json.load(open(f))
         except (OSError, ValueError):
             continue
-        if (d.get("num_features"), d.get("k"), d.get("batch_rows")) != (F, k, B):
+        if (d.get("num_features"), d.get("k"), d.get("batch_rows"), bool(d.get("fused", False))) != (F, k, B, fused):
             continue
         ks = d.get("kernels", {})
         names = PHASE_KERNELS.get(phase, [])
@@ -194,24 +205,97 @@ def cpu_baseline(cfg, batch, steps):
     }
 
 
+class PlanError(SystemExit):
+    """An impossible request: bench.py exits non-zero with this message instead of measuring
+    something other than what was asked (never a silent downgrade to fewer GPUs)."""
+
+
+def plan_run(args, env, n_visible):
+    """How this invocation runs, from the arguments, the launcher's environment and the number of
+    visible GPUs (torch.cuda.device_count(), which does not initialise the GPU):
+
+      single : one GPU, one single-table fm_ctx (N = 1, the default)
+      group  : ONE process drives N GPUs through one multi-GPU fm_ctx (fm_config.n_gpus = N,
+               RCCL inside libfm_hip: what INTEGRATION.md's createMulti gives a Spark driver); also
+               N = 1 with --force-sharded / --parallel (the group protocol on one rank)
+      procs  : torch.distributed.run started one process per GPU (WORLD_SIZE = N); each holds a
+               one-GPU group context of an N-rank job (fm_config.n_procs = N)
+
+    parallel: "sharded" (rows owned by id % R) or "replicated" (every rank the whole table,
+    gradient all-reduce); "auto" = replicated for c2 (the small-table config), else sharded."""
+    world = int(env.get("WORLD_SIZE", "1"))
+    rank = int(env.get("RANK", "0"))
+    local_rank = int(env.get("LOCAL_RANK", "0"))
+    par = args.parallel if args.parallel != "auto" else ("replicated" if args.config == "c2" else "sharded")
+    if args.gpus < 1:
+        raise PlanError("--gpus must be >= 1")
+    if world > 1:
+        if args.gpus != world:
+            raise PlanError(f"--gpus {args.gpus} under a launcher with WORLD_SIZE={world}: they must agree")
+        if n_visible < local_rank + 1:
+            raise PlanError(f"LOCAL_RANK={local_rank} but only {n_visible} GPU(s) visible")
+        return {"mode": "procs", "world": world, "rank": rank, "local_rank": local_rank, "n_local": 1,
+                "parallel": par, "devices": [local_rank]}
+    if args.gpus > 1:
+        if n_visible < args.gpus:
+            raise PlanError(f"--gpus {args.gpus} needs {args.gpus} visible GPUs in this process, {n_visible} visible; "
+                            f"nothing was measured")
+        if args.trainer != "lib":
+            raise PlanError("--trainer torch needs torch.distributed.run (one process per GPU)")
+        return {"mode": "group", "world": args.gpus, "rank": 0, "local_rank": 0, "n_local": args.gpus,
+                "parallel": par, "devices": list(range(args.gpus))}
+    if n_visible < 1:
+        raise PlanError("no GPU visible")
+    if args.force_sharded or args.parallel != "auto":
+        return {"mode": "group", "world": 1, "rank": 0, "local_rank": 0, "n_local": 1, "parallel": par,
+                "devices": [0]}
+    return {"mode": "single", "world": 1, "rank": 0, "local_rank": 0, "n_local": 1, "parallel": None,
+            "devices": [0]}
+
+
+def singleton_fraction(batches):
+    """Share of a batch's distinct feature ids that occur in exactly one entry (the rows the fused
+    step updates in its forward), averaged over the given batches."""
+    fr = {}
+    for b in batches:
+        if id(b) not in fr:
+            _, c = np.unique(b.col, return_counts=True)
+            fr[id(b)] = float(np.count_nonzero(c == 1)) / max(len(c), 1)
+    return float(np.mean([fr[id(b)] for b in batches]))
+
+
+def concat_batches(parts):
+    """Row-concatenation of CSR batches (the per-rank batches a one-process group context splits
+    back by rows, contiguously)."""
+    from fm_spark_amd.data import Batch
+
+    if len(parts) == 1:
+        return parts[0]
+    offs = np.cumsum([0] + [p.nnz for p in parts])
+    row_ptr = np.concatenate([parts[0].row_ptr[:1]] + [p.row_ptr[1:] + o for p, o in zip(parts, offs[:-1])])
+    return Batch(row_ptr=row_ptr.astype(np.int64), col=np.concatenate([p.col for p in parts]),
+                 val=np.concatenate([p.val for p in parts]), label=np.concatenate([p.label for p in parts]))
+
+
 def main():
     args = parse()
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            log(f"--gpus {args.gpus} needs torch.distributed.run (one rank per GPU); running 1 rank")
-        args.gpus = world
     import torch
-    import torch.distributed as dist
 
+    pl = plan_run(args, os.environ, torch.cuda.device_count())
+    world, rank, local_rank, mode = pl["world"], pl["rank"], pl["local_rank"], pl["mode"]
     torch.cuda.set_device(local_rank)
-    sharded = world > 1 or args.force_sharded
-    if sharded:
+    dist = None
+    if mode == "procs":
+        import torch.distributed as dist
+
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29517")
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local_rank))
+        if args.trainer == "torch":  # the test harness exchanges through torch's own RCCL
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local_rank))
+        else:
+            # libfm_hip runs every exchange over its own RCCL communicators; torch only hands the RCCL id
+            # around, and carries the barriers and the max-over-ranks time (gloo on the host)
+            dist.init_process_group("gloo", rank=rank, world_size=world)
 
     from fm_spark_amd.data import synthetic_batch
     from fm_spark_amd.engine import FMContext
@@ -227,15 +311,21 @@ def main():
     lab = {}
     if args.config == "c5":  # y = <w*, x> + N(0, 0.1) (BASELINE.md synthetic data)
         lab = dict(labels="regression", w_star=np.random.default_rng(20261015).normal(0.0, 0.1, F))
-    host_batches = [synthetic_batch(B, F, batch_index=rank * 1000 + i, zipf_s=zipf_s, **lab)
-                    for i in range(args.batches)]
-    log(f"[rank {rank}] generated {args.batches} batches in {time.perf_counter() - t0:.1f}s")
-    z = host_batches[0].nnz / B
+    # global rank g of this process's local rank l steps its own B-row batch (weak scaling); a
+    # one-process group gets the local ranks' batches concatenated and splits them back by rows
+    L = pl["n_local"]
+    granks = [rank * L + l for l in range(L)]
+    rank_batches = [[synthetic_batch(B, F, batch_index=g * 1000 + i, zipf_s=zipf_s, **lab) for i in range(args.batches)]
+                    for g in granks]
+    host_batches = [concat_batches([rb[i] for rb in rank_batches]) for i in range(args.batches)]
+    log(f"[rank {rank}] generated {args.batches} batches of {L} x {B} rows in {time.perf_counter() - t0:.1f}s")
+    z = host_batches[0].nnz / host_batches[0].n_rows
 
     median_ms = None
     host_path = None
-    if not sharded:
-        ctx = FMContext(F, k, device=local_rank, seed=20261015, init_sd=INIT_SD)
+    xg = None
+    if mode == "single":
+        ctx = FMContext(F, k, device=local_rank, seed=20261015, init_sd=INIT_SD, fuse=args.fuse == "on")
         # launch on a torch stream of our own so torch events can bracket every step on it
         main_stream = torch.cuda.Stream()
         torch.cuda.set_stream(main_stream)
@@ -288,34 +378,41 @@ def main():
         prof = ctx.profile_read() if args.profile_kernels else {}
         ctx.profile_enable(False)
         losses = ctx.loss_history()
-        assert os.environ.get("FM_ABLATE") or np.all(np.isfinite(losses)), "non-finite loss"
-        if args.host_path_steps > 0 and not args.host_path and rank == 0:
+        assert np.all(np.isfinite(losses)), "non-finite loss"
+        if args.host_path_steps > 0 and not args.host_path:
             hmed, hmean, t = host_path_leg(ctx, host_batches, t, args.host_path_steps, torch)
             host_path = {"median_ms_per_step": hmed, "mean_ms_per_step": hmean, "steps": args.host_path_steps,
                          "samples_per_s": B / (hmed * 1e-3) if hmed else None,
                          "what": "fm_step with the host CSR each call: 8 B/entry + row_ptr + fp64 labels over PCIe, "
                                  "device-side explode, then the step (two upload slots, copies overlap the previous step)"}
         U_mean = float(np.mean([uniques[i % len(dbatches)] for i in range(args.steps)]))
-        parallelism = "single table" + ((", next batch sorted during the current step" if depth == 1 else
-                                         f", batches sorted {depth} steps ahead on the side stream") if prefetch else "")
+        fused = args.fuse == "on" and (k + 3) // 4 * 4 <= 16 and prefetch
+        single_frac = singleton_fraction([host_batches[i % len(host_batches)] for i in range(args.steps)])
+        parallelism = "single table" + (", fused step (singleton rows updated by the forward)" if fused else "") + \
+            ((", next batch sorted during the current step" if depth == 1 else
+              f", batches sorted {depth} steps ahead on the side stream") if prefetch else "")
         if args.host_path:
             parallelism += ", host CSR uploaded by fm_step every step (PCIe-inclusive)"
     elif args.trainer == "lib":
         from fm_spark_amd.engine import comm_unique_id
 
-        # one fm_ctx per process (n_gpus = 1 here: torch.distributed.run starts a process per GPU);
-        # rank 0's RCCL id reaches the others over the torch group, then every exchange of the
-        # step runs inside libfm_hip (fm_group.hip)
-        idt = torch.zeros(128, dtype=torch.uint8, device="cuda")
-        if rank == 0:
-            idt.copy_(torch.tensor(list(comm_unique_id()), dtype=torch.uint8))
-        dist.broadcast(idt, src=0)
-        cid = bytes(idt.cpu().tolist())
-        ctx = FMContext(F, k, seed=20261015, init_sd=INIT_SD, parallel="sharded", n_gpus=1, devices=[local_rank],
-                        transport="rccl", n_procs=world, proc_rank=rank, comm_id=cid)
-        main_stream = torch.cuda.Stream()
-        torch.cuda.set_stream(main_stream)
-        ctx.set_stream(main_stream.cuda_stream)
+        par = pl["parallel"]
+        cid = None
+        if mode == "procs":
+            # rank 0's RCCL id reaches the others over the (gloo) torch group; then every exchange of
+            # the step runs inside libfm_hip (fm_group.hip)
+            idt = torch.zeros(128, dtype=torch.uint8)
+            if rank == 0:
+                idt.copy_(torch.tensor(list(comm_unique_id()), dtype=torch.uint8))
+            dist.broadcast(idt, src=0)
+            cid = bytes(idt.tolist())
+        ctx = FMContext(F, k, seed=20261015, init_sd=INIT_SD, parallel=par, n_gpus=L, devices=pl["devices"],
+                        transport="rccl", n_procs=world if mode == "procs" else 1, proc_rank=rank, comm_id=cid)
+        main_stream = None
+        if L == 1:  # launch on a torch stream so torch events time each step on it
+            main_stream = torch.cuda.Stream()
+            torch.cuda.set_stream(main_stream)
+            ctx.set_stream(main_stream.cuda_stream)
         ctx.init_random_range(0, F)
         dbatches = [ctx.batch(CSRHost(b.row_ptr, b.col, b.val, b.label)) for b in host_batches]
         prefetch = not args.no_prefetch
@@ -326,37 +423,54 @@ def main():
             t += 1
             uniques.append(ctx.step_batch(dbatches[i % nb], t, STEP_SIZE, REG_PARAM, sync=True).n_unique)
         ctx.sync()
-        torch.cuda.synchronize()
-        dist.barrier()
+        for d in pl["devices"]:
+            torch.cuda.synchronize(d)
+        if dist is not None:
+            dist.barrier()
         if args.profile_kernels:
             ctx.profile_reset()
             ctx.profile_enable(True)
         t_start = time.perf_counter()
-        # batch i + 1's route, entry exchange and slot sort are enqueued on the side stream behind
-        # step i (fm_batch_prepare): inside the timed region, off the critical path
-        evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+        # batch i + 1's batch-only work (sharded: route, entry exchange and slot sort; replicated: its
+        # sort) is enqueued on the side streams behind step i: inside the timed region, off the
+        # critical path
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)] if main_stream else None
         if prefetch:
             dbatches[0].prepare()
         for i in range(args.steps):
             t += 1
-            evs[i].record(main_stream)
+            if evs:
+                evs[i].record(main_stream)
             ctx.step_batch(dbatches[i % nb], t, STEP_SIZE, REG_PARAM, sync=False)
             if prefetch and i + 1 < args.steps:
                 dbatches[(i + 1) % nb].prepare()
-        evs[args.steps].record(main_stream)
+        if evs:
+            evs[args.steps].record(main_stream)
         ctx.sync()
-        torch.cuda.synchronize()
+        for d in pl["devices"]:
+            torch.cuda.synchronize(d)
         elapsed = time.perf_counter() - t_start
-        median_ms = median_step_ms(evs)
+        median_ms = median_step_ms(evs) if evs else None
         prof = ctx.profile_read() if args.profile_kernels else {}
         ctx.profile_enable(False)
         losses = ctx.loss_history()
-        assert os.environ.get("FM_ABLATE") or np.all(np.isfinite(losses)), "non-finite loss"
-        U_mean = float(np.mean(uniques)) / world  # rows one owner updates
-        xg = exchange_bytes(host_batches[0], world, rank, (k + 3) // 4 * 4)
-        parallelism = (f"row-sharded x{world}, owner-computes, one fm_ctx per process with the exchanges inside "
-                       f"libfm_hip (RCCL grouped send/recv of entries, partial sums and S rows)" +
-                       (", next batch routed, exchanged and slot-sorted during the current step" if prefetch else ""))
+        assert np.all(np.isfinite(losses)), "non-finite loss"
+        R = world
+        # rows one rank updates: sharded, the global distinct ids over the owners; replicated, every
+        # replica applies every touched row
+        U_mean = float(np.mean(uniques)) / (R if par == "sharded" else 1)
+        if par == "sharded":
+            xg = exchange_bytes(rank_batches[0][0], R, granks[0], (k + 3) // 4 * 4)
+        else:
+            gbytes = F * ((k + 3) // 4 * 4 + 4) * 4
+            xg = {"allreduce_B": gbytes, "ring_bytes_per_rank": 2 * gbytes * (R - 1) / R}
+        who = (f"one process driving {L} GPUs through one fm_ctx" if mode == "group" else
+               f"{world} processes (torch.distributed.run), one fm_ctx each")
+        parallelism = (f"row-sharded x{R}, owner-computes, {who}, exchanges inside libfm_hip over RCCL (grouped "
+                       f"send/recv of entries, partial sums and S rows)" if par == "sharded" else
+                       f"replicated x{R}, {who}, per-slot gradient sums all-reduced inside libfm_hip over RCCL")
+        if prefetch:
+            parallelism += ", next batch prepared during the current step"
     else:
         from fm_spark_amd.distributed import ShardedTrainer
 
@@ -378,8 +492,6 @@ def main():
             tr.ctx.profile_reset()
             tr.ctx.profile_enable(True)
         t_start = time.perf_counter()
-        # every timed batch's route / entry exchange / owner preparation runs inside the timed
-        # region: batch i + 1's is enqueued behind step i's update (side stream)
         evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
         for i in range(args.steps):
             t += 1
@@ -393,15 +505,17 @@ def main():
         median_ms = median_step_ms(evs)
         prof = tr.ctx.profile_read() if args.profile_kernels else {}
         losses = tr.ctx.loss_history()
-        assert os.environ.get("FM_ABLATE") or np.all(np.isfinite(losses)), "non-finite loss"
+        assert np.all(np.isfinite(losses)), "non-finite loss"
         U_mean = float(np.mean(uniques)) / world if uniques else 0.0  # rows one owner updates
         xg = exchange_bytes(host_batches[0], world, rank, (k + 3) // 4 * 4)
         parallelism = (f"row-sharded x{world}, owner-computes, torch.distributed harness (RCCL all-to-all of entries, "
-                       f"partial sums, S)" +
-                       (", next batch routed, exchanged and slot-sorted during the current step" if prefetch else ""))
+                       f"partial sums, S)" + (", next batch routed, exchanged and slot-sorted during the current step"
+                                              if prefetch else ""))
 
-    if sharded:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    if dist is not None:
+        tt = torch.tensor([elapsed], dtype=torch.float64)
+        if args.trainer == "torch":
+            tt = tt.cuda()
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
         dist.barrier()
@@ -427,20 +541,28 @@ def main():
             "data": "synthetic (Criteo-shaped, Zipf(%.2f) hashed ids, seed 20261015), random-init tables" % zipf_s,
             "config": {"workload": f"{args.config}: {desc}", "num_features": F, "k": k, "batch_rows_per_gpu": B,
                        "global_batch": B * world, "nnz_per_row": z, "rows_updated_per_gpu": U_mean,
-                       "step_size": STEP_SIZE, "reg_param": REG_PARAM, "parallelism": parallelism},
+                       "step_size": STEP_SIZE, "reg_param": REG_PARAM, "parallelism": parallelism,
+                       "launch": mode},
+            "loss_sum_all_steps": float(np.sum(losses)),
         }
         if prof:
             kern = {name: {"avg_ms": ms / max(n, 1), "launches": n} for name, (ms, n) in prof.items()}
             line["kernels"] = kern
+            if world > 1 or mode != "single":
+                line["kernels_of"] = "local rank 0 (HIP events on its streams)"
             # single table: "forward" gathers, "update" does the row read-modify-write; sharded:
             # "owner_forward" / "owner_update" do the same on the rank's own rows (per rank: the
             # entries an owner receives ~ its own batch's, the rows it updates ~ U / world)
             algo = {"forward": fwd_b, "update": upd_b, "owner_forward": fwd_b, "owner_update": upd_b}
-            # dominant kernel among those that move the path's algorithmic bytes;
-            # sort / plan / grad / serve bytes are implementation overhead, reported as times
+            fused = "tag" in kern
+            if fused:
+                # the fused forward also reads and writes the singleton rows (their 8(k+1) B each of
+                # the update's share); the segmented update keeps the rows with two or more entries
+                algo["forward"] = fwd_b + upd_b * single_frac
+                algo["update"] = upd_b * (1.0 - single_frac)
             dom = max((n for n in kern if n in algo), key=lambda n: kern[n]["avg_ms"])
             ach = algo[dom] / (kern[dom]["avg_ms"] * 1e-3) / 1e9
-            traffic, tsrc = pmc_traffic(F, k, B, dom)
+            traffic, tsrc = pmc_traffic(F, k, B, dom, fused)
             line["roofline"] = {"bound": "hbm", "kernel": dom, "achieved": ach, "peak": HBM_PEAK_GBS,
                                 "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "traffic": traffic,
                                 "algorithmic_bytes": algo[dom], "traffic_source": tsrc}
@@ -448,14 +570,18 @@ def main():
             line["step_roofline"] = {"bytes_per_step": step_bytes,
                                      "achieved_GBs": step_bytes / (ms_per_step * 1e-3) / 1e9,
                                      "frac": step_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS}
-        if sharded:
+        if xg is not None:
             step_s = (median_ms or ms_per_step) * 1e-3
-            egress = xg["entries_B"] + xg["s_rows_B"] + xg["partials_B"]
-            line["exchange"] = dict(xg, per="rank 0, per iteration, egress (ingress alike by symmetry)",
-                                    egress_B=egress, egress_GBs_at_step_time=egress / step_s / 1e9,
-                                    xgmi_peak_GBs=XGMI_LINK_GBS * max(world - 1, 0),
-                                    xgmi_frac_at_step_time=(egress / step_s / 1e9 / (XGMI_LINK_GBS * (world - 1))
-                                                            if world > 1 else None))
+            if "entries_B" in xg:
+                egress = xg["entries_B"] + xg["s_rows_B"] + xg["partials_B"]
+                line["exchange"] = dict(xg, per="rank 0, per iteration, egress (ingress alike by symmetry)",
+                                        egress_B=egress, egress_GBs_at_step_time=egress / step_s / 1e9,
+                                        xgmi_peak_GBs=XGMI_LINK_GBS * max(world - 1, 0),
+                                        xgmi_frac_at_step_time=(egress / step_s / 1e9 / (XGMI_LINK_GBS * (world - 1))
+                                                                if world > 1 else None))
+            else:
+                line["exchange"] = dict(xg, per="per iteration, the gradient all-reduce",
+                                        ring_GBs_at_step_time=xg["ring_bytes_per_rank"] / step_s / 1e9)
         if host_path:
             line["host_path_ms_per_step"] = host_path["median_ms_per_step"]
             line["host_path"] = host_path
@@ -465,7 +591,7 @@ def main():
             except Exception as e:  # reported, never silently replaced
                 line["cpu_baseline"] = {"value": None, "error": repr(e)}
         print(json.dumps(line), flush=True)
-    if sharded:
+    if dist is not None:
         dist.destroy_process_group()
 
 

@@ -19,6 +19,7 @@ FM_NOTHING_TO_DO = 1
 FM_PARALLEL_NONE, FM_PARALLEL_SHARDED, FM_PARALLEL_REPLICATED = 0, 1, 2
 FM_TRANSPORT_AUTO, FM_TRANSPORT_RCCL, FM_TRANSPORT_COPY = 0, 1, 2
 FM_MAX_LOCAL = 16
+FM_FUSE_DEFAULT, FM_FUSE_ON, FM_FUSE_OFF = 0, 1, -1
 
 
 class FMError(RuntimeError):
@@ -42,6 +43,8 @@ class fm_config(C.Structure):
         ("n_procs", C.c_int32),
         ("proc_rank", C.c_int32),
         ("comm_id", C.c_uint8 * 128),
+        ("fuse_single", C.c_int32),
+        ("xchg_chunks", C.c_int32),
     ]
 
 
@@ -137,7 +140,7 @@ def load() -> C.CDLL:
     global _lib
     if _lib is not None:
         return _lib
-    # FM_HIP_LIB: an experiment variant built by tools/variants.sh (same ABI)
+    # FM_HIP_LIB: another build of the same library (an A/B of two builds in one GPU call)
     path = Path(os.environ.get("FM_HIP_LIB") or _LIB_PATH)
     if not path.exists():
         raise FMError(f"{path} is missing: run __graft_entry__.build() (hipcc, gfx950)")

@@ -145,22 +145,10 @@ static Staged stage_csr(fm_ctx* ctx, const fm_csr* c, bool check_range, Pinned& 
   return g;
 }
 
-// Singleton fusion (FM_FUSE_SINGLE=1; off by default): prepared batches get per-entry singleton flags
-// and the forward applies those rows' updates (fm_kernels.hip k_forward<kTrainFused>,
-// k_segment_update skip_single).  Bit-exact, but measured slower: the forward's
-// extra row read and store per singleton are latency-exposed.
-static bool fuse_single_enabled() {
-  const char* e = getenv("FM_FUSE_SINGLE");  // read per call: A/B runs switch it
-  return e ? atoi(e) != 0 : false;
-}
-
-// Bits for an entry's position in its row next to the sample index in ent[].x (0: no packing --
-// fusion off, or sample and position do not fit 32 bits together).
-static int entry_pos_bits(const Staged& g) {
-  if (!fuse_single_enabled() || g.N == 0) return 0;
-  const int jb = bits_for(std::max<int64_t>(g.max_len - 1, 1));
-  const int sb = bits_for(std::max<int64_t>(g.B - 1, 1));
-  return sb + jb <= 32 ? jb : 0;
+// The fused step (fm_kernels.hip "Singleton rows") for batches this context prepares: a
+// single-table context with kp <= 16 unless fm_config.fuse_single says FM_FUSE_OFF.
+static bool fuse_on(const fm_ctx* ctx) {
+  return ctx->cfg.fuse_single != FM_FUSE_OFF && ctx->kp <= 16 && ctx->cfg.shard_count == 1;
 }
 
 static bool batch_fits(const fm_batch* b, const Staged& g) {
@@ -182,8 +170,6 @@ static void copy_staged(fm_ctx* ctx, const Staged& g, const Pinned& pin, fm_batc
   b->max_id = g.max_id;
   b->dev.n_rows = B;
   b->dev.nnz = N;
-  b->dev.jb = entry_pos_bits(g);
-  b->single_ok = false;
   b->dev.row_ptr.ensure(sizeof(int64_t) * (B + 1));
   b->dev.col.ensure(sizeof(uint32_t) * std::max<int64_t>(N, 4) + 16);
   b->dev.ent.ensure(sizeof(uint32_t) * 2 * std::max<int64_t>(N, 4) + 16);
@@ -200,8 +186,7 @@ static void copy_staged(fm_ctx* ctx, const Staged& g, const Pinned& pin, fm_batc
   launch_explode(reinterpret_cast<const int64_t*>(up), reinterpret_cast<const double*>(up + g.o_lab),
                  reinterpret_cast<const int32_t*>(up + g.o_xoff), reinterpret_cast<const uint32_t*>(up + g.o_col),
                  reinterpret_cast<const float*>(up + g.o_x), B, N, b->dev.row_ptr.as<int64_t>(),
-                 b->dev.label.as<double>(), b->dev.col.as<uint32_t>(), b->dev.ent.as<uint2>(), b->dev.xs.as<float>(), st,
-                 b->dev.jb);
+                 b->dev.label.as<double>(), b->dev.col.as<uint32_t>(), b->dev.ent.as<uint2>(), b->dev.xs.as<float>(), st);
 }
 
 // Synchronous upload (fm_batch_create, fm_predict, fm_loss_grad): staged in the context's
@@ -266,6 +251,9 @@ int step_impl(fm_ctx* ctx, fm_batch* b, int32_t t, double step_size, double reg_
   const uint32_t* skeys = nullptr;
   const uint2* sents = nullptr;
   const bool prepared = b->prepared;
+  const bool fused = prepared && b->split;  // the view holds the multi runs only (fm_batch_prepare)
+  FM_REQUIRE(!(fused && emit), "a batch prepared for the fused step cannot feed fm_repl_grad");
+  FM_REQUIRE(ctx->epoch < (1 << 29), "epoch count beyond the multi tags' range (2^29 steps)");
   if (prepared) {
     // sorted ahead of time by fm_batch_prepare on the side stream
     skeys = b->skeys.as<uint32_t>();
@@ -280,34 +268,27 @@ int step_impl(fm_ctx* ctx, fm_batch* b, int32_t t, double step_size, double reg_
     ctx->prof_end("sort", es, ctx->side);
     FM_HIP_CHECK(hipEventRecord(ctx->ev_join, ctx->side));
   }
-  static const bool serial = getenv("FM_NO_OVERLAP") != nullptr;  // diagnostic: no sort/forward overlap
-  // singleton fusion: the forward reads the prepared view's flags, so it waits for that sort
-  const bool fuse = prepared && b->single_ok && !emit && fuse_single_enabled();
-  if (serial || fuse) FM_HIP_CHECK(hipStreamWaitEvent(ctx->stream, prepared ? b->ready : ctx->ev_join, 0));
-  hipEvent_t e0 = ctx->prof_begin(ctx->stream);
+  hipEvent_t e0 = nullptr;
   FwdOut fx{};
-  fx.single = fuse ? b->single.as<uint8_t>() : nullptr;
-  launch_forward(T, b->dev, ctx->work, p, ctx->stream, &nfwd, nullptr, fuse ? &fx : nullptr);
-  ctx->prof_end("forward", e0, ctx->stream);
-  FM_HIP_CHECK(hipStreamWaitEvent(ctx->stream, prepared ? b->ready : ctx->ev_join, 0));
-#ifndef FM_SORT_GATE
-#define FM_SORT_GATE 0
-#endif
-  if (FM_SORT_GATE && prepared) {
-    // experiment: the update waits for whatever the side stream holds now (the next batch's sort,
-    // enqueued before this step), so that sort overlaps the forward and the update runs alone
-    FM_HIP_CHECK(hipEventRecord(ctx->ev_join, ctx->side));
-    FM_HIP_CHECK(hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));
+  if (fused) {
+    // the multi tags need the split of this batch (prepared a step or more ahead on the side stream)
+    FM_HIP_CHECK(hipStreamWaitEvent(ctx->stream, b->ready, 0));
+    e0 = ctx->prof_begin(ctx->stream);
+    launch_tag_multi(T, skeys, b->split_n.as<int64_t>(), N, p.epoch, ctx->stream);
+    ctx->prof_end("tag", e0, ctx->stream);
+    fx.fused = true;
   }
   e0 = ctx->prof_begin(ctx->stream);
+  launch_forward(T, b->dev, ctx->work, p, ctx->stream, &nfwd, nullptr, fused ? &fx : nullptr);
+  ctx->prof_end("forward", e0, ctx->stream);
+  if (!fused) FM_HIP_CHECK(hipStreamWaitEvent(ctx->stream, prepared ? b->ready : ctx->ev_join, 0));
+  e0 = ctx->prof_begin(ctx->stream);
   double* stats = ctx->loss_hist.as<double>() + 3 * (int64_t)ctx->epoch;
-  launch_segment_update(T, b->dev, ctx->work, p, skeys, sents, nfwd, stats, ctx->stream, emit, fuse);
-#ifndef FM_PREP_EAGER
-#define FM_PREP_EAGER 1
-#endif
+  launch_segment_update(T, b->dev, ctx->work, p, skeys, sents, nfwd, stats, ctx->stream, emit,
+                        fused ? b->split_n.as<int64_t>() : nullptr);
   // the shared sort workspace is read by the main stream only when the batch was sorted inline
   // (not prepared): only then must the next fm_batch_prepare's sort wait for this update
-  if (!prepared || !FM_PREP_EAGER) FM_HIP_CHECK(hipEventRecord(ctx->ev_upd_done, ctx->stream));
+  if (!prepared) FM_HIP_CHECK(hipEventRecord(ctx->ev_upd_done, ctx->stream));
   if (prepared) {
     FM_HIP_CHECK(hipEventRecord(b->last_use, ctx->stream));
     b->prepared = false;
@@ -344,6 +325,8 @@ int fm_create(const fm_config* cfg, fm_ctx** out) {
     FM_REQUIRE(cfg->shard_count >= 1 && cfg->shard_index >= 0 && cfg->shard_index < cfg->shard_count,
                "bad shard_index / shard_count");
     FM_REQUIRE(cfg->init_sd >= 0.0, "init_sd must be >= 0");
+    FM_REQUIRE(cfg->fuse_single == FM_FUSE_DEFAULT || cfg->fuse_single == FM_FUSE_ON || cfg->fuse_single == FM_FUSE_OFF,
+               "fuse_single must be FM_FUSE_DEFAULT, FM_FUSE_ON or FM_FUSE_OFF");
     int ndev = 0;
     FM_HIP_CHECK(hipGetDeviceCount(&ndev));
     FM_REQUIRE(cfg->device >= 0 && cfg->device < ndev, "device ordinal out of range");
@@ -354,16 +337,7 @@ int fm_create(const fm_config* cfg, fm_ctx** out) {
     c->rows = (cfg->num_features - cfg->shard_index + cfg->shard_count - 1) / cfg->shard_count;
     FM_HIP_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     c->own_stream = true;
-    // FM_SIDE_PRIO=1: the side stream (the next batch's sort) at the greatest priority, so its
-    // blocks are dispatched before the update's as CUs free up (experiment switch)
-    const char* sp = std::getenv("FM_SIDE_PRIO");
-    if (sp && std::atoi(sp) != 0) {
-      int least = 0, greatest = 0;
-      FM_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
-      FM_HIP_CHECK(hipStreamCreateWithPriority(&c->side_own, hipStreamNonBlocking, greatest));
-    } else {
-      FM_HIP_CHECK(hipStreamCreateWithFlags(&c->side_own, hipStreamNonBlocking));
-    }
+    FM_HIP_CHECK(hipStreamCreateWithFlags(&c->side_own, hipStreamNonBlocking));
     c->side = c->side_own;
     FM_HIP_CHECK(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
     FM_HIP_CHECK(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
@@ -614,14 +588,17 @@ int fm_batch_prepare(fm_ctx* ctx, fm_batch* b) {
     hipEvent_t es = ctx->prof_begin(ctx->side);
     const uint32_t* sk = nullptr;
     const uint2* sv = nullptr;
-    radix_sort_pairs64(ctx->work.sort, b->dev.col.as<uint32_t>(), b->dev.ent.as<uint2>(), N, bits_for(ctx->rows - 1),
-                       ctx->side, &sk, &sv, b->skeys.as<uint32_t>(), b->sents.as<uint2>());
-    b->single_ok = false;
-    if (b->dev.jb > 0 && fuse_single_enabled()) {  // which entries' rows the forward may update itself
-      b->single.ensure(N);
-      launch_single_flags(b->skeys.as<uint32_t>(), b->sents.as<uint2>(), N, b->dev.row_ptr.as<int64_t>(), b->dev.jb,
-                          b->single.as<uint8_t>(), ctx->side);
-      b->single_ok = true;
+    b->split = fuse_on(ctx);
+    if (b->split) {
+      // sorted in the workspace, then only the runs of two or more entries kept in the batch's view
+      radix_sort_pairs64(ctx->work.sort, b->dev.col.as<uint32_t>(), b->dev.ent.as<uint2>(), N, bits_for(ctx->rows - 1),
+                         ctx->side, &sk, &sv);
+      b->split_n.ensure(2 * sizeof(int64_t));
+      launch_split(sk, sv, N, ctx->split_work, b->skeys.as<uint32_t>(), b->sents.as<uint2>(), b->split_n.as<int64_t>(),
+                   ctx->side);
+    } else {
+      radix_sort_pairs64(ctx->work.sort, b->dev.col.as<uint32_t>(), b->dev.ent.as<uint2>(), N, bits_for(ctx->rows - 1),
+                         ctx->side, &sk, &sv, b->skeys.as<uint32_t>(), b->sents.as<uint2>());
     }
     ctx->prof_end("sort", es, ctx->side);
     FM_HIP_CHECK(hipEventRecord(b->ready, ctx->side));
@@ -754,12 +731,16 @@ int fm_init_from_batch(fm_ctx* ctx, fm_batch* b, int64_t* n_present) {
 static int loss_grad_impl(fm_ctx* ctx, const fm_csr* csr, double fill_sd, uint64_t seed, double* pred, double* loss,
                           double* dw, double* dv) {
   if (ctx && ctx->group) {
-    if (ctx->cfg.parallel == FM_PARALLEL_REPLICATED)
+    // a replicated group's replicas are identical: member 0 answers, with the group locked so that
+    // no group step is caught between a member's fm_repl_grad and fm_repl_apply
+    return guarded(ctx, [&]() -> int {
+      FM_REQUIRE(ctx->cfg.parallel == FM_PARALLEL_REPLICATED,
+                 "fm_loss_grad needs the whole table (a replicated or single-table context)");
       return loss_grad_impl(group_member0(ctx), csr, fill_sd, seed, pred, loss, dw, dv);
-    set_error("fm_loss_grad needs the whole table (a replicated or single-table context)");
-    return FM_ERR_ARG;
+    });
   }
   return guarded(ctx, [&]() -> int {
+    FM_REQUIRE(ctx->cfg.shard_count == 1, "fm_loss_grad needs the whole table (shard_count == 1)");
     FM_REQUIRE(csr != nullptr, "null argument");
     if (csr->n_rows == 0 || csr->nnz == 0) return FM_OK;
     fm_batch* b = host_batch(ctx);
@@ -803,7 +784,10 @@ int fm_calc_loss_grad(fm_ctx* ctx, const fm_csr* csr, double initial_sd, uint64_
 
 int fm_vector_sum_by_key(fm_ctx* ctx, const int32_t* keys, int64_t n, const double* vecs, int32_t k,
                          int32_t* out_keys, double* out_sums, int64_t* n_out) {
-  if (ctx && ctx->group) return fm_vector_sum_by_key(group_member0(ctx), keys, n, vecs, k, out_keys, out_sums, n_out);
+  if (ctx && ctx->group)  // on member 0's device, with the group locked
+    return guarded(ctx, [&]() -> int {
+      return fm_vector_sum_by_key(group_member0(ctx), keys, n, vecs, k, out_keys, out_sums, n_out);
+    });
   return guarded(ctx, [&]() -> int {
     FM_REQUIRE(n >= 0 && k >= 1 && n_out, "bad arguments");
     *n_out = 0;

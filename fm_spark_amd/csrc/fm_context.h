@@ -97,10 +97,12 @@ struct fm_batch {
   BatchDev dev;
   int64_t max_id = -1;
   DevBuf up;  // device image of the host staging (fm_capi.hip copy_staged)
-  // feature-major view produced by fm_batch_prepare (consumed once by the next step)
+  // feature-major view produced by fm_batch_prepare (consumed once by the next step): the whole
+  // sorted view, or -- split = true -- only the runs of two or more entries, split_n = {their
+  // count, the number of singleton runs} on the device (the fused step, fm_kernels.hip)
   DevBuf skeys, sents;
-  DevBuf single;                  // [nnz] u8: the entry's feature has no other entry (BatchDev::jb > 0)
-  bool single_ok = false;         // `single` matches the prepared sorted view
+  DevBuf split_n;
+  bool split = false;
   hipEvent_t ready = nullptr;     // recorded on the side stream after the prepared sort
   hipEvent_t last_use = nullptr;  // recorded on the main stream after a step read skeys/sents
   bool prepared = false;
@@ -116,7 +118,7 @@ struct fm_batch {
     if (last_use) (void)hipEventDestroy(last_use);
     skeys.release();
     sents.release();
-    single.release();
+    split_n.release();
     up.release();
     dev.row_ptr.release();
     dev.col.release();
@@ -167,6 +169,7 @@ struct fm_ctx {
   DevBuf sh_skey;      // [N] owner-partitioned route keys
   DevBuf sh_ent2;      // [n] uint2 {pair, x bits}: the slot sort's payload
   SortWork side_sort;  // radix sort workspace of the side stream
+  SplitWork split_work;  // fm_batch_prepare's singleton split (side stream)
   Pinned side_pinned;  // route counts (device -> host)
   // replicated step state (fm_repl_*)
   DevBuf repl_cnt;            // touched-row counter (uint64)
@@ -272,7 +275,8 @@ struct fm_ctx {
                       &work.sort.keys_a, &work.sort.keys_b, &work.sort.vals_a, &work.sort.vals_b,
                       &work.sort.counts, &work.sort.digit_tot, &side_sort.keys_a, &side_sort.keys_b,
                       &side_sort.vals_a, &side_sort.vals_b, &side_sort.counts, &side_sort.digit_tot,
-                      &sh_okey, &sh_mask, &sh_tcnt, &sh_tot, &sh_pay, &sh_skey, &sh_ent2, &repl_cnt};
+                      &sh_okey, &sh_mask, &sh_tcnt, &sh_tot, &sh_pay, &sh_skey, &sh_ent2, &repl_cnt,
+                      &split_work.cnt, &split_work.off};
     for (auto* b : bufs) b->release();
     if (own_stream && stream) (void)hipStreamDestroy(stream);
   }

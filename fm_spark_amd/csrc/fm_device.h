@@ -6,45 +6,9 @@
 
 namespace fmhip {
 
-// Cache-policy switches (experiments; 0 = plain accesses): FM_NT_ROWS nontemporal stores of the
-// update's row write-back, FM_NT_ENT nontemporal loads of the update's sorted entry stream,
-// FM_NT_SORT nontemporal stores of the sort's scatter.
-#ifndef FM_NT_ROWS
-#define FM_NT_ROWS 0
-#endif
-#ifndef FM_NT_ENT
-#define FM_NT_ENT 0
-#endif
-#ifndef FM_NT_CSR
-#define FM_NT_CSR 0  // nontemporal loads of the forward's CSR stream (col, ent)
-#endif
-#ifndef FM_NT_SORTLD
-#define FM_NT_SORTLD 0  // nontemporal loads of the sort's key / payload streams (count and scatter)
-#endif
-template <class T>
-__device__ __forceinline__ T ld_stream(const T* p, bool nt) {
-  if (nt) return __builtin_nontemporal_load(p);
-  return *p;
-}
-__device__ __forceinline__ uint4 ld_stream(const uint4* p, bool nt) {
-  if (nt) {
-    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-    const u32x4 q = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
-    return make_uint4(q.x, q.y, q.z, q.w);
-  }
-  return *p;
-}
-__device__ __forceinline__ uint2 ld_stream(const uint2* p, bool nt) {
-  if (nt) {
-    const unsigned long long q = __builtin_nontemporal_load(reinterpret_cast<const unsigned long long*>(p));
-    return make_uint2((uint32_t)q, (uint32_t)(q >> 32));
-  }
-  return *p;
-}
-#ifndef FM_NT_SORT
-#define FM_NT_SORT 0
-#endif
-typedef float fm_f4v __attribute__((ext_vector_type(4)));
+// Plain cached loads and stores throughout: nontemporal variants of the row write-back, the sorted
+// entry stream, the CSR stream and the sort's streams were measured (round 2) and
+// were neutral or slower in the step.
 
 // Block barrier that orders LDS only: the waits it implies are lgkmcnt, not vmcnt, so global
 // loads issued ahead and global stores still draining stay in flight across it (__syncthreads'
@@ -55,13 +19,7 @@ __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
-__device__ __forceinline__ void st_row4(float* p, float4 v) {
-#if FM_NT_ROWS
-  __builtin_nontemporal_store(fm_f4v{v.x, v.y, v.z, v.w}, reinterpret_cast<fm_f4v*>(p));
-#else
-  *reinterpret_cast<float4*>(p) = v;
-#endif
-}
+__device__ __forceinline__ void st_row4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
 
 __device__ __forceinline__ float shrink_f(float z, double a) {
   // signum(z) * max(0, |z| - a) (FactorizationMachinesSGD.scala:104, :179), in fp64.

@@ -73,7 +73,7 @@ struct Rank {
   fm_ctx* m = nullptr;  // the member context (owned)
   int device = 0;
   int global = 0;
-  ncclComm_t comm_main = nullptr, comm_side = nullptr;
+  ncclComm_t comm_main = nullptr, comm_side = nullptr, comm_x = nullptr;
   hipEvent_t ev_main = nullptr, ev_side = nullptr;  // COPY transport barriers
   DevBuf partials, part_in, s_send, s_recv;           // sharded wire buffers (main stream)
   DevBuf pc_out, pc_in, pred;                         // sharded predict: present counts, scores
@@ -86,7 +86,8 @@ struct Rank {
   // lanes: 0 main stream, 1 side stream (batch-only work), 2 the exchange stream
   hipStream_t stream(int lane) const { return lane == 2 ? xstream : lane ? m->side : m->stream; }
   hipEvent_t event(int lane) const { return lane == 2 ? ev_x : lane ? ev_side : ev_main; }
-  ncclComm_t comm(int lane) const { return lane == 1 ? comm_side : comm_main; }
+  // one communicator per stream, each used in the same order on every rank
+  ncclComm_t comm(int lane) const { return lane == 2 ? comm_x : lane ? comm_side : comm_main; }
 };
 constexpr int kLaneMain = 0, kLaneSide = 1, kLaneXchg = 2;
 
@@ -115,6 +116,7 @@ struct GroupBatch {
 struct Group {
   int mode = FM_PARALLEL_SHARDED;
   int L = 0, R = 0, nprocs = 1, prank = 0;
+  int xchg = 4;  // chunks of the sharded partial exchange (fm_config.xchg_chunks)
   bool rccl = false;
   std::vector<Rank> ranks;
   std::unique_ptr<fm_batch> host_b[2];  // fm_step / fm_predict uploads, used in turn
@@ -126,6 +128,7 @@ struct Group {
       if (!r.m) continue;
       (void)hipSetDevice(r.device);
       (void)hipDeviceSynchronize();
+      if (r.comm_x) (void)ncclCommDestroy(r.comm_x);
       if (r.comm_side) (void)ncclCommDestroy(r.comm_side);
       if (r.comm_main) (void)ncclCommDestroy(r.comm_main);
       for (DevBuf* d : {&r.partials, &r.part_in, &r.s_send, &r.s_recv, &r.pc_out, &r.pc_in, &r.pred, &r.grad, &r.gtmp,
@@ -476,12 +479,10 @@ void fill_out(Group& g, fm_ctx* ctx, int64_t e, int64_t global_rows, fm_step_out
 }
 
 // Chunks of the owners' partial pass whose exchange overlaps the next chunk's compute
-// (FM_XCHG_CHUNKS, default 4; 1 = one pass, then one all-to-all).  Only with R > 1.
+// (fm_config.xchg_chunks, default 4; 1 = one pass, then one all-to-all).  Only with R > 1.
 int xchg_chunks(const Group& g) {
   if (g.R <= 1 || g.R > kMaxChunkSources) return 1;
-  const char* e = std::getenv("FM_XCHG_CHUNKS");  // read per step: tests switch it
-  const int v = e ? std::atoi(e) : 4;
-  return std::max(1, std::min(v, 64));
+  return g.xchg;
 }
 
 void ensure_xchg(Group& g) {
@@ -723,6 +724,7 @@ int group_create(const fm_config* cfg, fm_ctx** out) {
   FM_REQUIRE(cfg->n_procs >= 1 && cfg->proc_rank >= 0 && cfg->proc_rank < cfg->n_procs, "bad n_procs / proc_rank");
   const int L = cfg->n_gpus, R = cfg->n_procs * cfg->n_gpus;
   FM_REQUIRE(cfg->parallel != FM_PARALLEL_SHARDED || R <= 64, "the sharded step supports at most 64 ranks");
+  FM_REQUIRE(cfg->xchg_chunks >= 0 && cfg->xchg_chunks <= 64, "xchg_chunks must be in [0, 64]");
   bool repeat = false;
   for (int a = 0; a < L; ++a)
     for (int b = a + 1; b < L; ++b) repeat = repeat || cfg->devices[a] == cfg->devices[b];
@@ -744,6 +746,7 @@ int group_create(const fm_config* cfg, fm_ctx** out) {
   g.nprocs = cfg->n_procs;
   g.prank = cfg->proc_rank;
   g.rccl = transport == FM_TRANSPORT_RCCL;
+  g.xchg = cfg->xchg_chunks > 0 ? cfg->xchg_chunks : 4;
   g.ranks.resize(L);
   for (int l = 0; l < L; ++l) {
     Rank& r = g.ranks[l];
@@ -755,6 +758,8 @@ int group_create(const fm_config* cfg, fm_ctx** out) {
     mc.device = r.device;
     mc.shard_index = g.sharded() ? r.global : 0;
     mc.shard_count = g.sharded() ? R : 1;
+    // a replica's batches feed fm_repl_grad, which needs the whole sorted view (no singleton split)
+    if (!g.sharded()) mc.fuse_single = FM_FUSE_OFF;
     mcheck(fm_create(&mc, &r.m), "fm_create (member)");
     FM_HIP_CHECK(hipSetDevice(r.device));
     FM_HIP_CHECK(hipEventCreateWithFlags(&r.ev_main, hipEventDisableTiming));
@@ -778,12 +783,14 @@ int group_create(const fm_config* cfg, fm_ctx** out) {
       FM_RCCL_CHECK(ncclCommInitRank(&r.comm_main, R, id, r.global));
     }
     FM_RCCL_CHECK(ncclGroupEnd());
-    FM_RCCL_CHECK(ncclGroupStart());
-    for (auto& r : g.ranks) {
-      FM_HIP_CHECK(hipSetDevice(r.device));
-      FM_RCCL_CHECK(ncclCommSplit(r.comm_main, 0, r.global, &r.comm_side, nullptr));
+    for (ncclComm_t Rank::*dst : {&Rank::comm_side, &Rank::comm_x}) {
+      FM_RCCL_CHECK(ncclGroupStart());
+      for (auto& r : g.ranks) {
+        FM_HIP_CHECK(hipSetDevice(r.device));
+        FM_RCCL_CHECK(ncclCommSplit(r.comm_main, 0, r.global, &(r.*dst), nullptr));
+      }
+      FM_RCCL_CHECK(ncclGroupEnd());
     }
-    FM_RCCL_CHECK(ncclGroupEnd());
   }
   *out = c.release();
   return FM_OK;

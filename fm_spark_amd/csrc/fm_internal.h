@@ -83,7 +83,7 @@ struct DevBuf {
 
 // ------------------------------------------------------------------- radix sort
 struct SortWork {
-  DevBuf keys_a, keys_b, vals_a, vals_b, counts, digit_tot, scratch;
+  DevBuf keys_a, keys_b, vals_a, vals_b, counts, digit_tot;
   int64_t cap = 0;
   void ensure(int64_t n);
 };
@@ -112,18 +112,12 @@ struct BatchDev {
   int64_t n_rows = 0, nnz = 0;
   DevBuf row_ptr, col, ent, label;  // int64 [B+1], uint32 [N] feature slot, uint2 [N], double [B]
   DevBuf xs;                         // fp32 [N]: x alone, the forward's stream (8 B per entry with col)
-  // jb > 0: ent[e].x = sample << jb | (e - row_ptr[sample]) (the entry's position in its row), so a
-  // sorted view can name CSR entries (singleton flags, fm_batch_prepare); 0: ent[e].x = sample
-  int jb = 0;
 };
 
 // The single-table step's per-sample record: S (kp floats) and, for kp <= 16, the sample's
 // {r, yhat} in the same 64-B (kp <= 12) or 128-B (kp = 16) record, so the update's S gather and
-// {r, yhat} load hit one line (FM_S_REC); wider rows keep {r, yhat} in StepWork::yl.
-#ifndef FM_S_REC
-#define FM_S_REC 1
-#endif
-inline bool s_rec_yl(int kp) { return FM_S_REC && kp <= 16; }
+// {r, yhat} load hit one line; wider rows keep {r, yhat} in StepWork::yl.
+inline bool s_rec_yl(int kp) { return kp <= 16; }
 inline int s_rec_floats(int kp) { return s_rec_yl(kp) ? (kp + 2 <= 16 ? 16 : 32) : kp; }
 
 struct StepWork {
@@ -168,9 +162,9 @@ struct FwdOut {
   // keyed by (fill_seed, entry index, column)
   double fill_sd = 0.0;
   uint64_t fill_seed = 0;
-  // train mode: single[e] != 0 marks an entry whose feature has no other entry in the batch; the
-  // forward applies that row's update itself (with sp) and the update kernel skips the run
-  const uint8_t* single = nullptr;
+  // train mode: the forward applies the update of every row whose header carries no multi tag of
+  // this epoch (a singleton; fm_kernels.hip "Singleton rows"), with sp; kp <= 16
+  bool fused = false;
   StepParams sp{};
 };
 constexpr int kMaxChunkSources = 64;  // sources a chunked partial pass can split
@@ -186,18 +180,26 @@ struct SegSource {
   int64_t s_stride;
   const float2* yl;
   int64_t yl_stride;
-  int jb = 0;                // sents' sample field is sample << jb | position in row (BatchDev::jb)
-  bool skip_single = false;  // singleton runs were applied by the forward (FwdOut::single)
+  // non-null: the entry count is n_dev[0] (device) <= N, and n_dev[1] singleton rows were updated
+  // by the fused forward (added to the distinct count)
+  const int64_t* n_dev = nullptr;
 };
 // emit != nullptr (replicated mode): the per-slot gradient sums go to emit[rows][kp + 4] as
 // [sum g_V (kp) | sum g_w | 1 (touched) | 0] instead of being applied to the table
 void launch_segment_update(const TableView& T, const BatchDev& b, StepWork& w, const StepParams& p,
                            const uint32_t* skeys, const uint2* sents, int64_t n_fwd_blocks,
-                           double* stats_out, hipStream_t st, float* emit = nullptr, bool skip_single = false);
-// fm_batch_prepare on a batch with BatchDev::jb > 0: single[e] = 1 when entry e's feature has no
-// other entry in the batch (its sorted run has length 1), else 0, for every entry
-void launch_single_flags(const uint32_t* skeys, const uint2* sents, int64_t N, const int64_t* row_ptr, int jb,
-                         uint8_t* single, hipStream_t st);
+                           double* stats_out, hipStream_t st, float* emit = nullptr, const int64_t* n_dev = nullptr);
+// fm_batch_prepare's singleton split of a sorted view (fm_kernels.hip "Singleton rows"): the entries
+// of runs of two or more, in order, into mkeys / ments (capacity N); n_out[0] = their count,
+// n_out[1] = the number of singleton runs (device)
+struct SplitWork {
+  DevBuf cnt, off;
+};
+void launch_split(const uint32_t* skeys, const uint2* sents, int64_t N, SplitWork& sw, uint32_t* mkeys, uint2* ments,
+                  int64_t* n_out, hipStream_t st);
+// the step's multi tags: every row starting a run of mkeys[0 .. n_dev[0]) (n_max: host bound)
+void launch_tag_multi(const TableView& T, const uint32_t* mkeys, const int64_t* n_dev, int64_t n_max, int32_t epoch,
+                      hipStream_t st);
 void launch_segment_update(const TableView& T, int64_t N, const SegSource& src, StepWork& w, const StepParams& p,
                            const uint32_t* skeys, const uint2* sents, int64_t n_loss_blocks, double* stats_out,
                            hipStream_t st, float* emit = nullptr);
@@ -230,6 +232,6 @@ void launch_count_present(const TableView& T, int64_t* out, hipStream_t st);
 // bits} rebuilt from row_ptr and the compact values (the explode of Model.scala:148-153)
 void launch_explode(const int64_t* row_ptr_in, const double* label_in, const int32_t* xoff, const uint32_t* col_in,
                     const float* x_in, int64_t B, int64_t N, int64_t* row_ptr, double* label, uint32_t* col, uint2* ent,
-                    float* xs, hipStream_t st, int jb = 0);
+                    float* xs, hipStream_t st);
 
 }  // namespace fmhip

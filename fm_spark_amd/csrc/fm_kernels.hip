@@ -37,30 +37,10 @@ namespace {
 
 constexpr int kBlock = 256;
 constexpr int kWaveEnt = 256;  // sorted entries per update wave
-#ifndef FM_UPD_D
-#define FM_UPD_D 2
-#endif
-constexpr int kUpdD = FM_UPD_D;  // entries whose rows a lane group loads per step
-#ifndef FM_UPD_D4
-#define FM_UPD_D4 1  // k = 13..16 (4 lanes per entry, paired row stores): one entry ahead keeps the kernel
-#endif               // at 116 VGPRs; two spill under the 4-wave cap (A/B: step 1.11 vs 1.14 ms)
-constexpr int kUpdD4 = FM_UPD_D4;
-#ifndef FM_UPD_D2
-#define FM_UPD_D2 1  // k = 5..8 (2 lanes per entry, paired row stores): two ahead spill under the 4-wave cap
-#endif
-constexpr int kUpdD2 = FM_UPD_D2;
-
-// experiment switches (tools/variants.sh; all 0 in the product build): drop the update's
-// per-sample record loads (S row and {r, yhat}), row loads or row stores to measure what each costs
-#ifndef FM_ABL_NOS
-#define FM_ABL_NOS 0
-#endif
-#ifndef FM_ABL_NOROW
-#define FM_ABL_NOROW 0
-#endif
-#ifndef FM_ABL_NOWR
-#define FM_ABL_NOWR 0
-#endif
+constexpr int kUpdD = 2;   // entries whose rows a lane group loads per step
+constexpr int kUpdD4 = 1;  // k = 13..16 (4 lanes per entry, paired row stores): one entry ahead keeps the
+                           // kernel within the 5-wave register budget
+constexpr int kUpdD2 = 1;  // k = 5..8 (2 lanes per entry, paired row stores)
 
 // The row header and one V quad brought current (absent rows read as zero).
 __device__ __forceinline__ void current_row(const RowHdr& h, float4& v, float& w, double cumE) {
@@ -107,31 +87,40 @@ __device__ __forceinline__ float gauss_draw(uint64_t seed, int64_t id, int f, do
 // MODE kLossGrad: calcLossGrad's per-entry columns (Model.scala:225-233): the sample's yhat, its
 // squared error, deltaWi = x and deltaVi = vfxiSum * x - (v * x) * x, fp64 from the team's fp64
 // sums (a second walk over the sample's entries re-reads their rows); absent ids set the flag.
-constexpr int kTrain = 0, kPartial = 1, kPredict = 2, kLossGrad = 3;
-#ifndef FM_FUSE_MZ
-#define FM_FUSE_MZ 40  // kTrainFused, kp <= 16: entries per sample whose singleton rows are kept in LDS
-#endif
-constexpr int kTrainFused = 4;  // kTrain + the singleton rows' updates (FM_FUSE_SINGLE=1; measured slower, off)
-#ifndef FM_FWD_U
-#define FM_FWD_U 4  // sharded partial pass: passes (entries per lane) whose rows are in flight together
-#endif
-#ifndef FM_FWD_MINW
-#define FM_FWD_MINW 1  // waves per SIMD the register allocation must allow
-#endif
+// MODE kTrainFused: kTrain, and every row whose feature has exactly one entry in the batch (a
+// singleton: 92 % of a c3 batch's distinct rows) is updated here, by the sample that holds that
+// entry, instead of by the segmented update (see "Singleton rows" below).
+constexpr int kTrain = 0, kPartial = 1, kPredict = 2, kLossGrad = 3, kTrainFused = 4;
+constexpr int kFuseMZ = 40;   // kTrainFused: entries per sample whose singleton rows wait in LDS
+constexpr int kPartialU = 4;  // sharded partial pass: passes (entries per lane) whose rows are in flight together
 // The step's forward (and predict / loss-grad): 32 lanes per sample, 2 passes in flight -- the
 // same 16 rows in flight per sample at k = 16 as 16 lanes x 4 passes, with fewer registers per
 // lane (measured 1.196 against 1.213 ms per c3 step, 5 runs each on two boxes)
-#ifndef FM_FWD_TEAM
-#define FM_FWD_TEAM 32
-#endif
-#ifndef FM_FWD_TU
-#define FM_FWD_TU 2
-#endif
-#ifndef FM_FWD_GRID
-#define FM_FWD_GRID 2048  // forward blocks at most (grid-stride over samples beyond)
-#endif
+constexpr int kFwdTeam = 32, kFwdU = 2;
+constexpr int kFwdGrid = 2048;  // forward blocks at most (grid-stride over samples beyond)
+
+// Singleton rows.  fm_batch_prepare splits the batch's sorted view into the runs of two or more
+// entries (the only ones that need a per-feature reduction; k_split_*) and the singletons.  At the
+// start of the step k_tag_multi marks every row with two or more entries in the row header's t
+// field, the word that otherwise only says present (t >= 0) or absent (t = -1):
+//   present, multi at epoch E : t = kTagPresent + (E & kTagMask)   (>= 2^30; normal t < 2^30)
+//   absent,  multi at epoch E : t = -2 - (E & kTagMask)            (<= -2: still "absent")
+// so every reader that asks t >= 0 is unchanged, and the fused forward, which loads the header of
+// every entry's row anyway, knows which rows it may update in place: nobody else reads them in
+// this step.  The segmented update then walks the multi runs only and rewrites their headers
+// (t = E + 1), clearing the tags.
+constexpr int32_t kTagPresent = 1 << 30;
+constexpr int32_t kTagMask = (1 << 29) - 1;
+__device__ __forceinline__ int32_t multi_tag(int32_t epoch, bool present) {
+  return present ? kTagPresent + (epoch & kTagMask) : -2 - (epoch & kTagMask);
+}
+__device__ __forceinline__ bool is_multi(int32_t t, int32_t epoch) {
+  const int32_t e = epoch & kTagMask;
+  return t >= kTagPresent ? t - kTagPresent == e : (t <= -2 && -2 - t == e);
+}
+
 template <int GS, int TEAM, int MODE, int U>
-__global__ __launch_bounds__(kBlock, FM_FWD_MINW) void k_forward(TableView T, const int64_t* __restrict__ row_ptr,
+__global__ __launch_bounds__(kBlock) void k_forward(TableView T, const int64_t* __restrict__ row_ptr,
                                                     const uint32_t* __restrict__ col,
                                                     const uint2* __restrict__ ent, const float* __restrict__ xs,
                                                     const double* __restrict__ label, int64_t B,
@@ -178,13 +167,14 @@ __global__ __launch_bounds__(kBlock, FM_FWD_MINW) void k_forward(TableView T, co
     Bl = ch_base[xo.ch_R];
   }
 
-  // kTrainFused at kp <= 16: each lane keeps, in LDS, the singleton rows of the entries it gathers
+  // kTrainFused (kp <= 16): each lane keeps, in LDS, the singleton rows of the entries it gathers
   // (raw V quad + header + id, slot = the entry's index in its sample) -- no global re-read -- and
   // after the sample's reduction rewrites them updated in place; their stores are issued after the
   // next sample's first gathers (so no load waits behind them), the last sample's at the end.
   // Every slot is read and written by the lane that gathered it: no barrier.
-  constexpr bool STASH = MODE == kTrainFused && GS <= 4 && TEAM >= 16 && FM_FUSE_MZ > 0;
-  constexpr int MZ = STASH ? FM_FUSE_MZ : 1;
+  constexpr bool STASH = MODE == kTrainFused;
+  static_assert(!STASH || (GS <= 4 && TEAM >= 16), "the fused forward serves kp <= 16");
+  constexpr int MZ = STASH ? kFuseMZ : 1;
   __shared__ float4 st_v[STASH ? TPB : 1][MZ][STASH ? GS : 1];
   __shared__ float4 st_h[STASH ? TPB : 1][MZ];
   __shared__ uint32_t st_id[STASH ? TPB : 1][MZ];
@@ -221,15 +211,10 @@ __global__ __launch_bounds__(kBlock, FM_FWD_MINW) void k_forward(TableView T, co
       for (int j = 0; j < U; ++j) {
         const int64_t e = eb + j * RPP;
         ok[j] = e < e1;
-        id[j] = ok[j] ? ld_stream(col + e, FM_NT_CSR) : 0u;
+        id[j] = ok[j] ? col[e] : 0u;
         if (MODE == kPredict) ok[j] = ok[j] && id[j] < (uint64_t)T.rows;
         // the batch's x stream (4 B per entry); the partial pass's entries carry x themselves
-        x[j] = ok[j] ? (PARTIAL ? __uint_as_float(ld_stream(ent + e, FM_NT_CSR).y) : ld_stream(xs + e, FM_NT_CSR)) : 0.f;
-      }
-      bool sg[U];
-      if (STASH) {
-#pragma unroll
-        for (int j = 0; j < U; ++j) sg[j] = ok[j] && eb + j * RPP - e0 < MZ && xo.single[eb + j * RPP] != 0;
+        x[j] = ok[j] ? (PARTIAL ? __uint_as_float(ent[e].y) : xs[e]) : 0.f;
       }
       RowHdr h[U];
       float4 v[U];
@@ -245,6 +230,9 @@ __global__ __launch_bounds__(kBlock, FM_FWD_MINW) void k_forward(TableView T, co
         }
       }
       if (STASH && eb == e0 + rs) flush();  // the previous sample's rows, behind this sample's first gathers
+      bool sg[U];  // singleton rows (untagged), updated by this sample after its reduction
+#pragma unroll
+      for (int j = 0; j < U; ++j) sg[j] = STASH && ok[j] && !is_multi(h[j].t, xo.sp.epoch);
 #pragma unroll
       for (int j = 0; j < U; ++j) {
         if (STASH && ok[j] && eb + j * RPP - e0 < MZ) {
@@ -373,64 +361,36 @@ __global__ __launch_bounds__(kBlock, FM_FWD_MINW) void k_forward(TableView T, co
         }
         pend = zc;
       }
-#ifndef FM_FUSE_ABL
-#define FM_FUSE_ABL 0  // measurement only: 1 = no stores
-#endif
-#ifndef FM_FUSE_FW
-#define FM_FUSE_FW 3  // singleton entries per lane whose rows are loaded together
-#endif
-      // the sample's singleton rows are loaded FW entries per lane at a time, all in flight, before
-      // any is computed or stored (stores in between would order every later load behind them)
-      constexpr int FW = STASH ? 1 : FM_FUSE_FW;  // with the stash only entries beyond MZ come here
-      for (int64_t eb = e0 + (STASH ? MZ : 0) + rs; eb < e1; eb += FW * RPP) {
-        bool on[FW];
-        uint32_t idv[FW];
-        float xv[FW];
-        RowHdr hv[FW];
-        float4 vv4[FW];
-#pragma unroll
-        for (int j = 0; j < FW; ++j) {
-          const int64_t e = eb + j * RPP;
-          on[j] = e < e1 && xo.single[e];
-          idv[j] = on[j] ? col[e] : 0u;
-          xv[j] = on[j] ? xs[e] : 0.f;
+      // entries beyond the stash (samples longer than MZ): the row is read again (nobody else
+      // reads or writes a singleton row in this step) and updated straight away
+      for (int64_t e = e0 + MZ + rs; STASH && e < e1; e += RPP) {
+        const uint32_t id = col[e];
+        const RowHdr h = *T.hdr(id);
+        const float4 vq = qok ? reinterpret_cast<const float4*>(T.v(id))[g] : make_float4(0.f, 0.f, 0.f, 0.f);
+        if (is_multi(h.t, sp.epoch)) continue;
+        const double xd = (double)xs[e];
+        const float acf = (float)(sp.cumE - h.cum);  // pending L1 of the row
+        float* rec = T.v(id);
+        const double t = xd * rj, b = (xd * xd) * rj;
+        const double gwe = (xd - 1.0) * yh + rj;  // x yhat - y (SGD.scala:145)
+        if (qok) {
+          const float4 v = shrink4f(vq, acf);
+          const double g0 = fma((double)Sq.x, t, 0.0) - (double)v.x * b, g1 = fma((double)Sq.y, t, 0.0) - (double)v.y * b;
+          const double g2 = fma((double)Sq.z, t, 0.0) - (double)v.z * b, g3 = fma((double)Sq.w, t, 0.0) - (double)v.w * b;
+          const float4 u = make_float4((float)fma(g0, -sp.scale_v, (double)v.x), (float)fma(g1, -sp.scale_v, (double)v.y),
+                                       (float)fma(g2, -sp.scale_v, (double)v.z), (float)fma(g3, -sp.scale_v, (double)v.w));
+          st_row4(rec + 4 * g, shrink4f(u, lamf));
         }
-#pragma unroll
-        for (int j = 0; j < FW; ++j) {
-          if (on[j]) {
-            hv[j] = *T.hdr(idv[j]);
-            vv4[j] = qok ? reinterpret_cast<const float4*>(T.v(idv[j]))[g] : make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int i = 4 * g; i < span; i += 4 * GS) {  // the header and the zero pad of its granule
+          float4 hq = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (i == 0) {
+            RowHdr o;
+            o.w = upd_w(shrink1f(h.w, acf), 0.0 + gwe, sp);  // SGD.scala:150, :171
+            o.t = sp.epoch + 1;
+            o.cum = sp.cum_next;
+            hq = *reinterpret_cast<const float4*>(&o);
           }
-        }
-#pragma unroll
-        for (int j = 0; j < FW; ++j) {
-          if (!on[j]) continue;
-          const RowHdr h = hv[j];
-          const double xd = (double)xv[j];
-          const float acf = (float)(sp.cumE - h.cum);  // pending L1 of the row
-          float* rec = T.v(idv[j]);
-          const double t = xd * rj, b = (xd * xd) * rj;
-          const double gwe = (xd - 1.0) * yh + rj;  // x yhat - y (SGD.scala:145)
-          if (qok) {
-            const float4 v = shrink4f(vv4[j], acf);
-            const double g0 = fma((double)Sq.x, t, 0.0) - (double)v.x * b, g1 = fma((double)Sq.y, t, 0.0) - (double)v.y * b;
-            const double g2 = fma((double)Sq.z, t, 0.0) - (double)v.z * b, g3 = fma((double)Sq.w, t, 0.0) - (double)v.w * b;
-            const float4 u = make_float4((float)fma(g0, -sp.scale_v, (double)v.x), (float)fma(g1, -sp.scale_v, (double)v.y),
-                                         (float)fma(g2, -sp.scale_v, (double)v.z), (float)fma(g3, -sp.scale_v, (double)v.w));
-            if (FM_FUSE_ABL != 1) st_row4(rec + 4 * g, shrink4f(u, lamf));
-            else if (u.x == 12345.f) rec[0] = 0.f;  // keep the computation alive
-          }
-          for (int i = 4 * g; i < span && FM_FUSE_ABL != 1; i += 4 * GS) {
-            float4 hq = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (i == 0) {
-              RowHdr o;
-              o.w = upd_w(shrink1f(h.w, acf), 0.0 + gwe, sp);  // SGD.scala:150, :171
-              o.t = sp.epoch + 1;
-              o.cum = sp.cum_next;
-              hq = *reinterpret_cast<const float4*>(&o);
-            }
-            st_row4(rec + kp + i, hq);
-          }
+          st_row4(rec + kp + i, hq);
         }
       }
     }
@@ -485,21 +445,13 @@ struct SegArgs {
   StepParams p;
   uint32_t* ucnt;  // [update blocks]
   float* emit;     // replicated mode: per-slot gradient sums [rows][kp + 4] instead of the update
-  int jb;          // sents[].x = sample << jb | position in row
-  int skip_single; // runs of one entry were applied by the forward: not loaded, not written here
+  // non-null: the entry count is n_dev[0] <= N (a prepared batch's multi runs, counted on the
+  // device by k_split_*), and n_dev[1] distinct singleton rows were updated by the forward
+  const int64_t* n_dev;
 };
 
 constexpr uint32_t kFValid = 1u, kFEnd = 2u, kFStart = 4u;
 
-#ifndef FM_UPD_GRID
-#define FM_UPD_GRID 0  // update blocks at most (0: one per 1024 sorted entries); a cap leaves CU room for the side stream
-#endif
-#ifndef FM_UPD_LEAN
-#define FM_UPD_LEAN 1  // single-buffered loads + head pieces in LDS: 90 VGPRs, 5 waves/SIMD at k = 16 (step -3.5 %)
-#endif
-#ifndef FM_UPD_YL2
-#define FM_UPD_YL2 1  // the sample's {r, yhat} loaded in phase 2 with its S row (same 64/128-B record
-#endif                // in the single-table layout) instead of one lane per entry in phase 1
 
 // Lane-group geometry: Q lanes per entry, NF float4 column quads per lane (columns
 // 4 (q + Q n) .. + 3), NG = 64 / Q groups per wave, RL = 256 / NG entries per group.
@@ -513,13 +465,12 @@ struct UpdGeom {
                                           // row against bank conflicts (no pad column: at k = 32 the
                                           // pad cost the fourth block per CU)
   static __device__ __forceinline__ int at(int row, int g) { return row * NG + (g ^ (row & (NG - 1))); }
-  // FM_UPD_YL2: {slot, flags} | sample | x (16 B); else {t, b} f64x2 | g_w f64 | {slot, flags} | sample
-  static constexpr int IMG = IMG_N * (FM_UPD_YL2 ? 16 : 36);
-  static constexpr int PIECES = 2 * NG * PIECE * 8;
-  // FM_UPD_LEAN: the groups' head pieces go to their own region after the image as they close
-  // (one slot per group) instead of living in registers until phase 3
+  // image entry: {slot, flags} | sample | x (16 B)
+  static constexpr int IMG = IMG_N * 16;
+  // the groups' head pieces go to their own region after the image as they close (one slot per
+  // group) instead of living in registers until phase 3
   static constexpr int HEADS = NG * PIECE * 8;
-  static constexpr int BYTES = FM_UPD_LEAN ? IMG + HEADS : (IMG > PIECES ? IMG : PIECES);
+  static constexpr int BYTES = IMG + HEADS;
 };
 
 // The interaction gradient of one entry (Model.scala:201-204, SGD.scala:146) is
@@ -542,20 +493,11 @@ struct UpdGeom {
 //    it closes inside the wave; the wave's first piece (run begun in an earlier wave) and a run
 //    still open at the wave's end leave fp64 partials (slot 0 / slot 1), summed in wave order by
 //    k_segment_combine.  Every sum runs in a fixed order: the step is bitwise reproducible.
-#ifndef FM_UPD_PAIRST
-#define FM_UPD_PAIRST 1  // k = 13..16: each updated row written by one 8-lane 128-B store (see flush_pair)
-#endif
-#ifndef FM_UPD_PAIR8
-#define FM_UPD_PAIR8 0  // k = 29..32 too (8 lanes V + 4 lanes header granule in one instruction)
-#endif
-#ifndef FM_UPD_MINW
-#define FM_UPD_MINW 4  // k <= 64 (NF = 1): waves per SIMD the register allocation must allow (4 blocks/CU:
-                       // the LDS limit); without it the compiler took 130 VGPRs at k = 16 (3 waves/SIMD):
-                       // update -8.6 %, step -1.7 % (A/B 3 x 40 steps).  A 29-B LDS image + 5 waves
-                       // spills: slower.
-#endif
+// k <= 64 (NF = 1): waves per SIMD the register allocation must allow (4 blocks/CU); without it the
+// compiler took 130 VGPRs at k = 16 (3 waves/SIMD): update -8.6 %, step -1.7 % (A/B 3 x 40 steps)
+constexpr int kUpdMinW = 4;
 template <int Q, int NF, int D0>
-__global__ __launch_bounds__(kBlock, NF == 1 ? FM_UPD_MINW : 1) void k_segment_update(SegArgs a) {
+__global__ __launch_bounds__(kBlock, NF == 1 ? kUpdMinW : 1) void k_segment_update(SegArgs a) {
   using Geo = UpdGeom<Q, NF>;
   constexpr int NG = Geo::NG, RL = Geo::RL, PIECE = Geo::PIECE, NP = kWaveEnt / 64, C = 4 * NF;
   constexpr int D = D0 < RL ? D0 : RL;  // entries loaded ahead (divides RL)
@@ -565,54 +507,35 @@ __global__ __launch_bounds__(kBlock, NF == 1 ? FM_UPD_MINW : 1) void k_segment_u
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   unsigned char* smem = smem_all[wave];
   constexpr int IN = Geo::IMG_N;
-#if FM_UPD_YL2
-  uint2* img_k = reinterpret_cast<uint2*>(smem);                 // {slot, flags}
-  int* img_s = reinterpret_cast<int*>(smem + IN * 8);            // sample
-  float* img_x = reinterpret_cast<float*>(smem + IN * 12);       // x
-#else
-  double2* img_d = reinterpret_cast<double2*>(smem);            // {x r, x^2 r}
-  double* img_w = reinterpret_cast<double*>(smem + IN * 16);     // x yhat - y
-  uint2* img_k = reinterpret_cast<uint2*>(smem + IN * 24);       // {slot, flags}
-  int* img_s = reinterpret_cast<int*>(smem + IN * 32);           // sample
-#endif
+  uint2* img_k = reinterpret_cast<uint2*>(smem);            // {slot, flags}
+  int* img_s = reinterpret_cast<int*>(smem + IN * 8);       // sample
+  float* img_x = reinterpret_cast<float*>(smem + IN * 12);  // x
   int* pflag = pflag_all[wave];
   const TableView& T = a.T;
   const int kp = T.kp;
   const uint32_t kNone = 0xFFFFFFFFu;
   auto li = [](int e) { return Geo::at(e % RL, e / RL); };
-  // logical blocks of 4 waves x 256 entries; a capped grid (FM_UPD_GRID) walks them in turn
-  const int64_t nlblk = (a.N + (int64_t)kWaveEnt * (kBlock / 64) - 1) / ((int64_t)kWaveEnt * (kBlock / 64));
+  const int64_t N = a.n_dev ? a.n_dev[0] : a.N;
+  // logical blocks of 4 waves x 256 entries (one per block of the grid; blocks beyond a device count exit)
+  const int64_t nlblk = (N + (int64_t)kWaveEnt * (kBlock / 64) - 1) / ((int64_t)kWaveEnt * (kBlock / 64));
   for (int64_t lblk = blockIdx.x; lblk < nlblk; lblk += gridDim.x) {
   const int64_t wid = lblk * (kBlock / 64) + wave;
   const int64_t base = wid * kWaveEnt;
   uint32_t ucount = 0;
 
-  if (base < a.N) {  // wave-uniform
+  if (base < N) {  // wave-uniform
     // ---------------- phase 1: one lane per entry
     uint32_t key[NP];
     uint2 en[NP];
 #pragma unroll
     for (int i = 0; i < NP; ++i) {
       const int64_t p = base + i * 64 + lane;
-      const bool v = p < a.N;
-#if FM_NT_ENT
-      key[i] = v ? __builtin_nontemporal_load(a.skeys + p) : kNone;
-      if (v) {
-        const unsigned long long q = __builtin_nontemporal_load(reinterpret_cast<const unsigned long long*>(a.sents) + p);
-        en[i] = make_uint2((uint32_t)q, (uint32_t)(q >> 32));
-      } else {
-        en[i] = make_uint2(0u, 0u);
-      }
-#else
+      const bool v = p < N;
       key[i] = v ? a.skeys[p] : kNone;
       en[i] = v ? a.sents[p] : make_uint2(0u, 0u);
-#endif
     }
     const uint32_t before = base > 0 ? a.skeys[base - 1] : kNone;
-    const uint32_t after = base + kWaveEnt < a.N ? a.skeys[base + kWaveEnt] : kNone;
-#if !FM_UPD_YL2
-    float2 yl[NP];
-#endif
+    const uint32_t after = base + kWaveEnt < N ? a.skeys[base + kWaveEnt] : kNone;
 #pragma unroll
     for (int i = 0; i < NP; ++i) {
       const uint32_t up = __shfl_up(key[i], 1);
@@ -625,16 +548,10 @@ __global__ __launch_bounds__(kBlock, NF == 1 ? FM_UPD_MINW : 1) void k_segment_u
       const bool st = valid && key[i] != prev;
       const bool end = valid && key[i] != next;
       ucount += (uint32_t)__popcll(__ballot(st));
-      // a run of one entry that the forward already applied stays out of phase 2 (no loads, no store)
-      const bool live = valid && !(a.skip_single && st && end);
       const int l = li(i * 64 + lane);
-      img_k[l] = make_uint2(key[i], (live ? kFValid : 0u) | (end ? kFEnd : 0u) | (st ? kFStart : 0u));
-      img_s[l] = (int)(en[i].x >> a.jb);
-#if FM_UPD_YL2
+      img_k[l] = make_uint2(key[i], (valid ? kFValid : 0u) | (end ? kFEnd : 0u) | (st ? kFStart : 0u));
+      img_s[l] = (int)en[i].x;
       img_x[l] = __uint_as_float(en[i].y);
-#else
-      yl[i] = valid ? a.yl[(int64_t)(en[i].x >> a.jb) * a.yl_stride] : make_float2(0.f, 0.f);
-#endif
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -642,9 +559,9 @@ __global__ __launch_bounds__(kBlock, NF == 1 ? FM_UPD_MINW : 1) void k_segment_u
 
     // ---------------- phase 2: group g, lane q of the group
     const int g = lane / Q, q = lane % Q;
-    // two buffers of D entries: the rows of the next step are in flight while a step is consumed
-    float4 Sp0[D][NF], Vp0[D][NF], Hp0[D], Sp1[D][NF], Vp1[D][NF], Hp1[D];
-    float2 Yp0[D], Yp1[D];  // FM_UPD_YL2: the samples' {r, yhat}
+    // D entries loaded ahead (one buffer: the next step's loads are issued after a step is consumed)
+    float4 Sp0[D][NF], Vp0[D][NF], Hp0[D];
+    float2 Yp0[D];  // the samples' {r, yhat}
     auto prefetch = [&](int b0, float4 (&Sp)[D][NF], float4 (&Vp)[D][NF], float4 (&Hp)[D], float2 (&Yp)[D]) {
 #pragma unroll
       for (int u = 0; u < D; ++u) {
@@ -655,39 +572,24 @@ __global__ __launch_bounds__(kBlock, NF == 1 ? FM_UPD_MINW : 1) void k_segment_u
 #pragma unroll
         for (int n = 0; n < NF; ++n) {
           const int c = 4 * (q + Q * n);
-          const bool cv = valid && c < kp && !FM_ABL_NOS;
+          const bool cv = valid && c < kp;
           Sp[u][n] = cv ? *reinterpret_cast<const float4*>(a.S + (int64_t)s * a.s_stride + c)
                         : make_float4(0.f, 0.f, 0.f, 0.f);
-          Vp[u][n] = (valid && c < kp && end && !FM_ABL_NOROW) ? *reinterpret_cast<const float4*>(T.v(kf.x) + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+          Vp[u][n] = (valid && c < kp && end) ? *reinterpret_cast<const float4*>(T.v(kf.x) + c) : make_float4(0.f, 0.f, 0.f, 0.f);
         }
-        Hp[u] = (valid && end && !FM_ABL_NOROW) ? *reinterpret_cast<const float4*>(T.hdr(kf.x))
-                               : make_float4(0.f, __int_as_float(-1), 0.f, 0.f);
-        if (FM_UPD_YL2) Yp[u] = valid && !FM_ABL_NOS ? a.yl[(int64_t)s * a.yl_stride] : make_float2(0.f, 0.f);
+        Hp[u] = (valid && end) ? *reinterpret_cast<const float4*>(T.hdr(kf.x)) : make_float4(0.f, __int_as_float(-1), 0.f, 0.f);
+        Yp[u] = valid ? a.yl[(int64_t)s * a.yl_stride] : make_float2(0.f, 0.f);
       }
     };
-    prefetch(0, Sp0, Vp0, Hp0, Yp0);  // in flight together with phase 1's {yhat, y} reads
-#if !FM_UPD_YL2
-#pragma unroll
-    for (int i = 0; i < NP; ++i) {
-      const int l = li(i * 64 + lane);
-      const double xd = (double)__uint_as_float(en[i].y);
-      const double rj = (double)yl[i].x, yh = (double)yl[i].y;
-      img_d[l] = make_double2(xd * rj, (xd * xd) * rj);
-      // g_w = deltaWi * pred - label = x yhat - (yhat - r) (SGD.scala:145)
-      img_w[l] = (xd - 1.0) * yh + rj;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#endif
+    prefetch(0, Sp0, Vp0, Hp0, Yp0);
 
     // Paired row stores (kp = 4Q, Q = 2 or 4: records of V (16Q B) + a header granule of the same
     // size, i.e. k = 5..8 in 64 B and k = 13..16 in 128 B): the new row of a run closed in phase 2
     // is kept in registers and written at the end of the entry step by 2Q lanes, the group's Q (V)
     // and its neighbour group's Q (header + zero pad), so every row leaves in ONE store
     // instruction covering its whole record instead of two half-record ones.
-    constexpr bool kPairCfg = FM_UPD_PAIRST && (Q == 2 || Q == 4 || (Q == 8 && FM_UPD_PAIR8)) && NF == 1;
-    const bool paired = kPairCfg && kp == 4 * Q && !a.emit && !FM_ABL_NOWR;  // wave-uniform
+    constexpr bool kPairCfg = (Q == 2 || Q == 4) && NF == 1;
+    const bool paired = kPairCfg && kp == 4 * Q && !a.emit;  // wave-uniform
     float4 pend_v = make_float4(0.f, 0.f, 0.f, 0.f);
     float pend_w = 0.f;             // the row's new w (its header is {w, epoch + 1, cum_next})
     uint32_t pend_slot = kNone;     // kNone: nothing pending
@@ -700,7 +602,6 @@ __global__ __launch_bounds__(kBlock, NF == 1 ? FM_UPD_MINW : 1) void k_segment_u
       const float acf = (float)(a.p.cumE - h.cum);  // pending L1 of the row
       const float lamf = (float)a.p.lam;
       float* rec = T.v(slot);
-      if (FM_ABL_NOWR) return;
       if (kPairCfg && defer) {  // this lane's V quad and (lane q = 0) the header, written by flush_pair
         const float4 v = shrink4f(vq[0], acf);
         const double g0 = A[0] - (double)v.x * b, g1 = A[1] - (double)v.y * b;
@@ -767,13 +668,12 @@ __global__ __launch_bounds__(kBlock, NF == 1 ? FM_UPD_MINW : 1) void k_segment_u
       for (int pass = 0; pass < 2; ++pass) {
         const bool writer = (g & 1) == pass;
         const uint32_t slot = writer ? pend_slot : p_slot;
-        // the header granule is 4 + pad floats: 4Q of them at kp = 4Q <= 16, 16 at kp = 32
+        // the header granule is 4 + pad floats: 4Q of them at kp = 4Q <= 16
         if (slot != kNone && (writer || 4 * q < pair_span)) st_row4(T.v(slot) + (writer ? 4 * q : kp + 4 * q), writer ? pend_v : p_h);
       }
       pend_slot = kNone;
     };
 
-#if FM_UPD_LEAN
     double* heads = reinterpret_cast<double*>(smem + Geo::IMG);  // [NG][PIECE]
     auto put_head = [&](const double (&A)[C], double b, double gw) {
       double* ph = heads + g * PIECE;
@@ -790,12 +690,6 @@ __global__ __launch_bounds__(kBlock, NF == 1 ? FM_UPD_MINW : 1) void k_segment_u
 #pragma unroll
     for (int j = 0; j < C; ++j) acc[j] = 0.0;
     double accb = 0.0, accw = 0.0;
-#else
-    double acc[C], hacc[C];
-#pragma unroll
-    for (int j = 0; j < C; ++j) acc[j] = hacc[j] = 0.0;
-    double accb = 0.0, accw = 0.0, hb = 0.0, hw = 0.0;
-#endif
     int hst = 0;  // the group's head piece: 0 none, 1 open through the group's end, 2 closed
     bool started = false, open = false;
     uint32_t lastkey = kNone;
@@ -806,17 +700,11 @@ __global__ __launch_bounds__(kBlock, NF == 1 ? FM_UPD_MINW : 1) void k_segment_u
         const int l = Geo::at(b0 + u, g);
         const uint2 kf = img_k[l];
         if (kf.y & kFValid) {
-#if FM_UPD_YL2
         // t = x r, x^2 r and g_w = deltaWi * pred - label = x yhat - (yhat - r) (SGD.scala:145)
         const double xd = (double)img_x[l], rj = (double)Yp[u].x, yh = (double)Yp[u].y;
         const double t = xd * rj;
         const double2 tb = make_double2(t, (xd * xd) * rj);
         const double gwe = (xd - 1.0) * yh + rj;
-#else
-        const double2 tb = img_d[l];
-        const double t = tb.x;
-        const double gwe = img_w[l];
-#endif
         if (kf.y & kFStart) started = true;
         open = true;
         lastkey = kf.x;
@@ -833,14 +721,7 @@ __global__ __launch_bounds__(kBlock, NF == 1 ? FM_UPD_MINW : 1) void k_segment_u
           if (started) {
             close_run(kf.x, Vp[u], Hp[u], acc, accb, accw, paired);
           } else {  // the head piece closes
-#if FM_UPD_LEAN
             put_head(acc, accb, accw);
-#else
-#pragma unroll
-            for (int j = 0; j < C; ++j) hacc[j] = acc[j];
-            hb = accb;
-            hw = accw;
-#endif
             hst = 2;
           }
 #pragma unroll
@@ -854,33 +735,14 @@ __global__ __launch_bounds__(kBlock, NF == 1 ? FM_UPD_MINW : 1) void k_segment_u
         if (kPairCfg && paired) flush_pair();  // converged: every lane of the wave
       }
     };
-#if FM_UPD_LEAN
 #pragma unroll 1
     for (int b0 = D; b0 <= RL; b0 += D) {  // the first step's loads are in flight already
       consume(b0 - D, Sp0, Vp0, Hp0, Yp0);
       if (b0 < RL) prefetch(b0, Sp0, Vp0, Hp0, Yp0);
     }
-#else
-#pragma unroll 1
-    for (int b0 = 0; b0 < RL; b0 += 2 * D) {
-      if (b0 + D < RL) prefetch(b0 + D, Sp1, Vp1, Hp1, Yp1);
-      consume(b0, Sp0, Vp0, Hp0, Yp0);
-      if (b0 + D < RL) {
-        if (b0 + 2 * D < RL) prefetch(b0 + 2 * D, Sp0, Vp0, Hp0, Yp0);
-        consume(b0 + D, Sp1, Vp1, Hp1, Yp1);
-      }
-    }
-#endif
     const bool tail = open && started;  // the open piece began in this group
     if (open && !started) {             // the head piece runs through the group's end
-#if FM_UPD_LEAN
       put_head(acc, accb, accw);
-#else
-#pragma unroll
-      for (int j = 0; j < C; ++j) hacc[j] = acc[j];
-      hb = accb;
-      hw = accw;
-#endif
       hst = 1;
     }
 
@@ -888,24 +750,7 @@ __global__ __launch_bounds__(kBlock, NF == 1 ? FM_UPD_MINW : 1) void k_segment_u
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#if FM_UPD_LEAN
     double* pc = heads;  // head piece of group g at pc + g * PIECE, written in phase 2
-    constexpr int PS = 1;
-#else
-    double* pc = reinterpret_cast<double*>(smem);
-    constexpr int PS = 2;
-    if (hst) {
-      double* ph = pc + (2 * g) * PIECE;
-#pragma unroll
-      for (int n = 0; n < NF; ++n)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) ph[1 + 4 * (q + Q * n) + j] = hacc[4 * n + j];
-      if (q == 0) {
-        ph[0] = hw;
-        ph[PIECE - 1] = hb;
-      }
-    }
-#endif
     if (q == 0) pflag[2 * g] = hst;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -915,7 +760,7 @@ __global__ __launch_bounds__(kBlock, NF == 1 ? FM_UPD_MINW : 1) void k_segment_u
       for (int g2 = from; g2 < NG; ++g2) {
         const int f2 = pflag[2 * g2];
         if (f2 == 0) return false;  // unreachable: an open piece always continues into a head piece
-        const double* ph = pc + (PS * g2) * PIECE;
+        const double* ph = pc + g2 * PIECE;
 #pragma unroll
         for (int n = 0; n < NF; ++n)
 #pragma unroll
@@ -945,13 +790,11 @@ __global__ __launch_bounds__(kBlock, NF == 1 ? FM_UPD_MINW : 1) void k_segment_u
       }
     };
     if (g == 0 && hst) {  // the wave's first piece: its run began in an earlier wave
-#if FM_UPD_LEAN
       double hacc[C], hb = pc[PIECE - 1], hw = pc[0];
 #pragma unroll
       for (int n = 0; n < NF; ++n)
 #pragma unroll
         for (int j = 0; j < 4; ++j) hacc[4 * n + j] = pc[1 + 4 * (q + Q * n) + j];
-#endif
       if (hst == 1) extend(hacc, hb, hw, 1);
       write_part(0, hacc, hb, hw);
     }
@@ -1035,6 +878,8 @@ __global__ __launch_bounds__(kBlock) void k_segment_combine(SegArgs a, const dou
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int kp = a.T.kp;
   const int64_t W = kp + 2;
+  const int64_t N = a.n_dev ? a.n_dev[0] : a.N;
+  const int64_t nranges = (N + a.L - 1) / a.L;
   __shared__ double run_sum[kBlock / 64][258];  // one long run's summed piece per wave (kp <= 256)
   if (blockIdx.x == 0) {
     __shared__ double rl[kBlock], rc[kBlock], ru[kBlock];
@@ -1043,7 +888,11 @@ __global__ __launch_bounds__(kBlock) void k_segment_combine(SegArgs a, const dou
       l += loss_part[i].x;
       c += loss_part[i].y;
     }
-    for (int64_t i = tid; i < n_ucnt; i += kBlock) u += (double)a.ucnt[i];
+    // update blocks that held entries (a device count leaves the grid's tail without any)
+    const int64_t per_blk = (int64_t)kWaveEnt * (kBlock / 64);
+    const int64_t nu = a.n_dev ? min(n_ucnt, (N + per_blk - 1) / per_blk) : n_ucnt;
+    for (int64_t i = tid; i < nu; i += kBlock) u += (double)a.ucnt[i];
+    if (a.n_dev && tid == 0) u += (double)a.n_dev[1];  // the singleton rows the forward updated
     rl[tid] = l;
     rc[tid] = c;
     ru[tid] = u;
@@ -1068,10 +917,10 @@ __global__ __launch_bounds__(kBlock) void k_segment_combine(SegArgs a, const dou
   const int64_t L = a.L;
   bool owner = false;
   uint32_t key = 0;
-  if (chunk < a.nranges) {
+  if (chunk < nranges) {
     const int64_t p0 = chunk * L;
-    const int64_t p1 = p0 + L < a.N ? p0 + L : a.N;
-    if (p1 < a.N) {
+    const int64_t p1 = p0 + L < N ? p0 + L : N;
+    if (p1 < N) {
       key = a.skeys[p1 - 1];
       // the range's last run continues into the next range and starts inside this range
       owner = a.skeys[p1] == key && !(a.skeys[p0] == key && p0 > 0 && a.skeys[p0 - 1] == key);
@@ -1081,7 +930,7 @@ __global__ __launch_bounds__(kBlock) void k_segment_combine(SegArgs a, const dou
   bool two = false;
   if (owner) {
     const int64_t c2 = chunk + 2;
-    two = !(c2 < a.nranges && a.skeys[c2 * L] == key);
+    two = !(c2 < nranges && a.skeys[c2 * L] == key);
   }
   if (owner && two) {
     const double* pt = a.part + (chunk * 2 + 1) * W;
@@ -1105,7 +954,7 @@ __global__ __launch_bounds__(kBlock) void k_segment_combine(SegArgs a, const dou
     int64_t cend = c0 + 1;
     for (;;) {
       const int64_t c = cend + lane;
-      const bool cont = c < a.nranges && a.skeys[c * L] == k0;
+      const bool cont = c < nranges && a.skeys[c * L] == k0;
       const uint64_t m = __ballot(cont);
       if (m == ~0ull) {
         cend += 64;
@@ -1361,7 +1210,7 @@ void launch_fwd_t(const TableView& T, const BatchDev& b, StepWork& w, const Step
                   int64_t* nblk, float* partial_out, const FwdOut* xo) {
   constexpr int TPB = kBlock / TEAM;
   int64_t blocks = (b.n_rows + TPB - 1) / TPB;
-  if (blocks > FM_FWD_GRID) blocks = FM_FWD_GRID;
+  if (blocks > kFwdGrid) blocks = kFwdGrid;
   if (blocks < 1) blocks = 1;
   *nblk = blocks;
   const dim3 grid((unsigned)blocks), blk(kBlock);
@@ -1386,9 +1235,16 @@ void launch_fwd_t(const TableView& T, const BatchDev& b, StepWork& w, const Step
     return;
   }
   w.loss_part.ensure(sizeof(double2) * blocks);
-  FwdOut tr = xo ? *xo : none;  // train mode: xo carries the singleton flags (fused updates), if any
-  if (tr.single) tr.sp = p;
-  auto kern = tr.single ? k_forward<GS, TEAM, kTrainFused, U> : k_forward<GS, TEAM, kTrain, U>;
+  FwdOut tr = xo ? *xo : none;  // train mode: xo->fused = the singleton rows' updates in the forward
+  auto kern = k_forward<GS, TEAM, kTrain, U>;
+  if constexpr (GS <= 4 && TEAM >= 16) {
+    if (tr.fused) {
+      tr.sp = p;
+      kern = k_forward<GS, TEAM, kTrainFused, U>;
+    }
+  } else {
+    FM_REQUIRE(!tr.fused, "the fused forward serves kp <= 16");
+  }
   hipLaunchKernelGGL(kern, grid, blk, 0, st, T, b.row_ptr.as<int64_t>(),
                      b.col.as<uint32_t>(), b.ent.as<uint2>(), b.xs.as<float>(), b.label.as<double>(), b.n_rows, p.w0, p.cumE,
                      w.S.as<float>(), s_rec_yl(T.kp) ? reinterpret_cast<float2*>(w.S.as<float>() + T.kp) : w.yl.as<float2>(),
@@ -1404,9 +1260,9 @@ template <int GS>
 void launch_partial_t(const TableView& T, const BatchDev& b, StepWork& w, const StepParams& p, hipStream_t st,
                       int64_t* nblk, float* partial_out, const FwdOut* xo) {
   const double avg = b.n_rows > 0 ? (double)b.nnz / (double)b.n_rows : 0.0;
-  if (GS <= 16 && avg <= 4.0) launch_fwd_t<GS, GS, FM_FWD_U>(T, b, w, p, st, nblk, partial_out, xo);
-  else if (GS <= 16 && avg <= 8.0) launch_fwd_t<GS, (2 * GS > 16 ? 16 : 2 * GS), FM_FWD_U>(T, b, w, p, st, nblk, partial_out, xo);
-  else launch_fwd_t<GS, (GS > 16 ? GS : 16), FM_FWD_U>(T, b, w, p, st, nblk, partial_out, xo);
+  if (GS <= 16 && avg <= 4.0) launch_fwd_t<GS, GS, kPartialU>(T, b, w, p, st, nblk, partial_out, xo);
+  else if (GS <= 16 && avg <= 8.0) launch_fwd_t<GS, (2 * GS > 16 ? 16 : 2 * GS), kPartialU>(T, b, w, p, st, nblk, partial_out, xo);
+  else launch_fwd_t<GS, (GS > 16 ? GS : 16), kPartialU>(T, b, w, p, st, nblk, partial_out, xo);
 }
 
 void launch_forward(const TableView& T, const BatchDev& b, StepWork& w, const StepParams& p, hipStream_t st,
@@ -1418,32 +1274,31 @@ void launch_forward(const TableView& T, const BatchDev& b, StepWork& w, const St
     else if (nq <= 4) launch_partial_t<4>(T, b, w, p, st, nblk, partial_out, pred);
     else if (nq <= 8) launch_partial_t<8>(T, b, w, p, st, nblk, partial_out, pred);
     else if (nq <= 16) launch_partial_t<16>(T, b, w, p, st, nblk, partial_out, pred);
-    else if (nq <= 32) launch_fwd_t<32, 32, FM_FWD_U>(T, b, w, p, st, nblk, partial_out, pred);
-    else if (nq <= 64) launch_fwd_t<64, 64, FM_FWD_U>(T, b, w, p, st, nblk, partial_out, pred);
+    else if (nq <= 32) launch_fwd_t<32, 32, kPartialU>(T, b, w, p, st, nblk, partial_out, pred);
+    else if (nq <= 64) launch_fwd_t<64, 64, kPartialU>(T, b, w, p, st, nblk, partial_out, pred);
     else FM_REQUIRE(false, "dimFactorization > 256 is not supported");
     FM_HIP_CHECK(hipGetLastError());
     return;
   }
-  constexpr int TM = FM_FWD_TEAM, TU = FM_FWD_TU;
+  constexpr int TM = kFwdTeam, TU = kFwdU;
   if (nq <= 1) launch_fwd_t<1, TM, TU>(T, b, w, p, st, nblk, partial_out, pred);
   else if (nq <= 2) launch_fwd_t<2, TM, TU>(T, b, w, p, st, nblk, partial_out, pred);
   else if (nq <= 4) launch_fwd_t<4, (TM < 4 ? 4 : TM), TU>(T, b, w, p, st, nblk, partial_out, pred);
   else if (nq <= 8) launch_fwd_t<8, (TM < 8 ? 8 : TM), TU>(T, b, w, p, st, nblk, partial_out, pred);
   else if (nq <= 16) launch_fwd_t<16, (TM < 16 ? 16 : TM), TU>(T, b, w, p, st, nblk, partial_out, pred);
-  else if (nq <= 32) launch_fwd_t<32, 32, FM_FWD_U>(T, b, w, p, st, nblk, partial_out, pred);
-  else if (nq <= 64) launch_fwd_t<64, 64, FM_FWD_U>(T, b, w, p, st, nblk, partial_out, pred);
+  else if (nq <= 32) launch_fwd_t<32, 32, kPartialU>(T, b, w, p, st, nblk, partial_out, pred);
+  else if (nq <= 64) launch_fwd_t<64, 64, kPartialU>(T, b, w, p, st, nblk, partial_out, pred);
   else FM_REQUIRE(false, "dimFactorization > 256 is not supported");
   FM_HIP_CHECK(hipGetLastError());
 }
 
 void launch_segment_update(const TableView& T, const BatchDev& b, StepWork& w, const StepParams& p,
                            const uint32_t* skeys, const uint2* sents, int64_t n_fwd_blocks,
-                           double* stats_out, hipStream_t st, float* emit, bool skip_single) {
+                           double* stats_out, hipStream_t st, float* emit, const int64_t* n_dev) {
   SegSource src{w.S.as<float>(), s_rec_floats(T.kp),
                  s_rec_yl(T.kp) ? reinterpret_cast<const float2*>(w.S.as<float>() + T.kp) : w.yl.as<float2>(),
                  s_rec_yl(T.kp) ? s_rec_floats(T.kp) / 2 : 1};
-  src.jb = b.jb;
-  src.skip_single = skip_single;
+  src.n_dev = n_dev;
   launch_segment_update(T, b.nnz, src, w, p, skeys, sents, n_fwd_blocks, stats_out, st, emit);
 }
 
@@ -1471,11 +1326,9 @@ void launch_segment_update(const TableView& T, int64_t N, const SegSource& src, 
   a.p = p;
   a.ucnt = w.ucnt.as<uint32_t>();
   a.emit = emit;
-  a.jb = src.jb;
-  a.skip_single = src.skip_single && !emit ? 1 : 0;
+  a.n_dev = src.n_dev;
   if (ublocks > 0) {
-    const int64_t gcap = FM_UPD_GRID > 0 && ublocks > FM_UPD_GRID ? FM_UPD_GRID : ublocks;
-    const dim3 grid((unsigned)gcap), blk(kBlock);
+    const dim3 grid((unsigned)ublocks), blk(kBlock);
     const int nq = T.kp / 4;  // column quads
     if (nq <= 1) hipLaunchKernelGGL((k_segment_update<1, 1, kUpdD>), grid, blk, 0, st, a);
     else if (nq <= 2) hipLaunchKernelGGL((k_segment_update<2, 1, kUpdD2>), grid, blk, 0, st, a);
@@ -1612,7 +1465,7 @@ __global__ __launch_bounds__(kBlock) void k_explode(const int64_t* __restrict__ 
                                                    const int32_t* __restrict__ xoff, const uint32_t* __restrict__ col_in,
                                                    const float* __restrict__ x_in, int64_t B, int64_t* __restrict__ rp,
                                                    double* __restrict__ lab, uint32_t* __restrict__ col,
-                                                   uint2* __restrict__ ent, float* __restrict__ xs, int jb) {
+                                                   uint2* __restrict__ ent, float* __restrict__ xs) {
   constexpr int T = 16;
   const int tl = threadIdx.x % T;
   const int lane = threadIdx.x & 63;
@@ -1624,7 +1477,6 @@ __global__ __launch_bounds__(kBlock) void k_explode(const int64_t* __restrict__ 
   for (int64_t i = gtid; i < B; i += nthreads) lab[i] = lab_in[i];
   for (int64_t s = gtid / T; s < B; s += nthreads / T) {
     const int64_t e0 = rp_in[s], e1 = rp_in[s + 1];
-    const uint32_t sj = (uint32_t)s << jb;  // jb > 0: the entry's position in its row below
     int64_t xo = xoff[s];
     for (int64_t eb = rp_in[s]; eb < e1; eb += T) {  // the team's lanes take the same trips
       const int64_t e = eb + tl;
@@ -1635,43 +1487,150 @@ __global__ __launch_bounds__(kBlock) void k_explode(const int64_t* __restrict__ 
       xo += __popcll(m & team_bits);
       if (e < e1) {
         col[e] = c & 0x7FFFFFFFu;
-        ent[e] = make_uint2(jb ? sj | (uint32_t)(e - e0) : (uint32_t)s, __float_as_uint(x));
+        ent[e] = make_uint2((uint32_t)s, __float_as_uint(x));
         xs[e] = x;
       }
     }
   }
 }
 
-// single[e] for every entry e of a sorted batch view: 1 when its run (equal feature slots) has one
-// entry, else 0; e = row_ptr[sample] + position, both from the packed sample field.
-__global__ __launch_bounds__(kBlock) void k_single_flags(const uint32_t* __restrict__ skeys,
-                                                        const uint2* __restrict__ sents, int64_t N,
-                                                        const int64_t* __restrict__ row_ptr, int jb,
-                                                        uint8_t* __restrict__ single) {
-  const uint32_t jm = (1u << jb) - 1u;
-  for (int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x; p < N; p += (int64_t)gridDim.x * kBlock) {
-    const uint32_t key = skeys[p];
-    const bool one = (p == 0 || skeys[p - 1] != key) && (p + 1 == N || skeys[p + 1] != key);
-    const uint32_t sx = sents[p].x;
-    single[row_ptr[sx >> jb] + (sx & jm)] = one ? 1 : 0;
+// ------------------------------------------------------- singleton split (fm_batch_prepare)
+// The sorted view of a batch -> the entries of its runs of two or more (stable: the order the
+// segmented update needs) and the number of singleton runs.  One wave per chunk of 1024 sorted
+// entries: count, one-block scan of the chunk counts, then each wave writes its multi entries at
+// its offset in order (ballot ranks).  Integer work only: deterministic.
+constexpr int kSplitChunk = 1024;
+
+__device__ __forceinline__ bool split_multi(const uint32_t* __restrict__ skeys, int64_t N, int64_t p, uint32_t key,
+                                            int lane) {
+  uint32_t prev = __shfl_up(key, 1), next = __shfl_down(key, 1);
+  if (lane == 0) prev = p > 0 && p <= N ? skeys[p - 1] : 0xFFFFFFFFu;
+  if (lane == 63) next = p + 1 < N ? skeys[p + 1] : 0xFFFFFFFFu;
+  if (p == 0) prev = 0xFFFFFFFFu;      // (lane 0 only)
+  if (p + 1 >= N) next = 0xFFFFFFFFu;  // the last entry has no successor
+  return p < N && (prev == key || next == key);
+}
+
+__global__ __launch_bounds__(kBlock) void k_split_count(const uint32_t* __restrict__ skeys, int64_t N,
+                                                        uint2* __restrict__ cnt, int64_t nchunks) {
+  const int lane = threadIdx.x & 63;
+  const int64_t c = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+  if (c >= nchunks) return;  // wave-uniform
+  uint32_t nm = 0, ns = 0;
+  for (int r = 0; r < kSplitChunk / 64; ++r) {
+    const int64_t p = c * kSplitChunk + r * 64 + lane;
+    const uint32_t key = p < N ? skeys[p] : 0xFFFFFFFEu;
+    const bool m = split_multi(skeys, N, p, key, lane);
+    nm += (uint32_t)__popcll(__ballot(m));
+    ns += (uint32_t)__popcll(__ballot(p < N && !m));
+  }
+  if (lane == 0) cnt[c] = make_uint2(nm, ns);
+}
+
+// one block: exclusive scan of the chunks' multi counts -> off[c]; totals -> n_out[0] (multi
+// entries), n_out[1] (singleton runs)
+__global__ __launch_bounds__(1024) void k_split_scan(const uint2* __restrict__ cnt, int64_t nchunks,
+                                                     int64_t* __restrict__ off, int64_t* __restrict__ n_out) {
+  __shared__ int64_t wsum[16], ssum[16];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int64_t carry = 0, singles = 0;
+  for (int64_t b = 0; b < nchunks; b += 1024) {
+    const int64_t i = b + threadIdx.x;
+    const uint2 v = i < nchunks ? cnt[i] : make_uint2(0u, 0u);
+    int64_t incl = v.x, sg = v.y;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int64_t t = __shfl_up(incl, o);
+      if (lane >= o) incl += t;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) sg += __shfl_xor(sg, o);
+    if (lane == 63) wsum[wave] = incl;
+    if (lane == 0) ssum[wave] = sg;
+    __syncthreads();
+    int64_t wpre = 0, tot = 0, stot = 0;
+    for (int w = 0; w < 16; ++w) {
+      wpre += w < wave ? wsum[w] : 0;
+      tot += wsum[w];
+      stot += ssum[w];
+    }
+    if (i < nchunks) off[i] = carry + wpre + incl - (int64_t)v.x;
+    carry += tot;
+    singles += stot;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    n_out[0] = carry;
+    n_out[1] = singles;
   }
 }
 
-void launch_single_flags(const uint32_t* skeys, const uint2* sents, int64_t N, const int64_t* row_ptr, int jb,
-                         uint8_t* single, hipStream_t st) {
-  if (N <= 0) return;
-  FM_REQUIRE(jb > 0, "singleton flags need the packed entry positions");
-  hipLaunchKernelGGL(k_single_flags, dim3(grid_for(N, kBlock, 256 * 16)), dim3(kBlock), 0, st, skeys, sents, N, row_ptr,
-                     jb, single);
+__global__ __launch_bounds__(kBlock) void k_split_scatter(const uint32_t* __restrict__ skeys,
+                                                          const uint2* __restrict__ sents, int64_t N,
+                                                          const int64_t* __restrict__ off, int64_t nchunks,
+                                                          uint32_t* __restrict__ mkeys, uint2* __restrict__ ments) {
+  const int lane = threadIdx.x & 63;
+  const int64_t c = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+  if (c >= nchunks) return;  // wave-uniform
+  const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+  int64_t o = off[c];
+  for (int r = 0; r < kSplitChunk / 64; ++r) {
+    const int64_t p = c * kSplitChunk + r * 64 + lane;
+    const uint32_t key = p < N ? skeys[p] : 0xFFFFFFFEu;
+    const bool m = split_multi(skeys, N, p, key, lane);
+    const uint64_t bm = __ballot(m);
+    if (m) {
+      const int64_t d = o + __popcll(bm & lt);
+      mkeys[d] = key;
+      ments[d] = sents[p];
+    }
+    o += __popcll(bm);
+  }
+}
+
+// At the step's start (main stream, after the previous step's writes): the header of every row
+// with two or more entries gets the epoch's multi tag (the t word only; see "Singleton rows").
+__global__ __launch_bounds__(kBlock) void k_tag_multi(TableView T, const uint32_t* __restrict__ mkeys,
+                                                      const int64_t* __restrict__ n_dev, int32_t epoch) {
+  const int64_t n = n_dev[0];
+  for (int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x; p < n; p += (int64_t)gridDim.x * kBlock) {
+    const uint32_t key = mkeys[p];
+    if (p > 0 && mkeys[p - 1] == key) continue;
+    int32_t* t = &T.hdr(key)->t;
+    *t = multi_tag(epoch, *t >= 0);
+  }
+}
+
+void launch_split(const uint32_t* skeys, const uint2* sents, int64_t N, SplitWork& sw, uint32_t* mkeys, uint2* ments,
+                  int64_t* n_out, hipStream_t st) {
+  const int64_t nchunks = (N + kSplitChunk - 1) / kSplitChunk;
+  sw.cnt.ensure(sizeof(uint2) * (size_t)std::max<int64_t>(nchunks, 1));
+  sw.off.ensure(sizeof(int64_t) * (size_t)std::max<int64_t>(nchunks, 1));
+  if (N <= 0) {
+    FM_HIP_CHECK(hipMemsetAsync(n_out, 0, 2 * sizeof(int64_t), st));
+    return;
+  }
+  const unsigned blocks = (unsigned)((nchunks + kBlock / 64 - 1) / (kBlock / 64));
+  hipLaunchKernelGGL(k_split_count, dim3(blocks), dim3(kBlock), 0, st, skeys, N, sw.cnt.as<uint2>(), nchunks);
+  hipLaunchKernelGGL(k_split_scan, dim3(1), dim3(1024), 0, st, sw.cnt.as<uint2>(), nchunks, sw.off.as<int64_t>(), n_out);
+  hipLaunchKernelGGL(k_split_scatter, dim3(blocks), dim3(kBlock), 0, st, skeys, sents, N, sw.off.as<int64_t>(), nchunks,
+                     mkeys, ments);
+  FM_HIP_CHECK(hipGetLastError());
+}
+
+void launch_tag_multi(const TableView& T, const uint32_t* mkeys, const int64_t* n_dev, int64_t n_max, int32_t epoch,
+                      hipStream_t st) {
+  if (n_max <= 0) return;
+  hipLaunchKernelGGL(k_tag_multi, dim3(grid_for(n_max, kBlock, 256 * 8)), dim3(kBlock), 0, st, T, mkeys, n_dev, epoch);
   FM_HIP_CHECK(hipGetLastError());
 }
 
 void launch_explode(const int64_t* row_ptr_in, const double* label_in, const int32_t* xoff, const uint32_t* col_in,
                     const float* x_in, int64_t B, int64_t N, int64_t* row_ptr, double* label, uint32_t* col, uint2* ent,
-                    float* xs, hipStream_t st, int jb) {
+                    float* xs, hipStream_t st) {
   (void)N;
   hipLaunchKernelGGL(k_explode, dim3(grid_for(std::max<int64_t>(B, 1) * 16, kBlock, 256 * 8)), dim3(kBlock), 0, st,
-                     row_ptr_in, label_in, xoff, col_in, x_in, B, row_ptr, label, col, ent, xs, jb);
+                     row_ptr_in, label_in, xoff, col_in, x_in, B, row_ptr, label, col, ent, xs);
   FM_HIP_CHECK(hipGetLastError());
 }
 

@@ -273,6 +273,9 @@ class FactorizationMachinesSGD:
         "dimFactorization": 10, "featuresCol": "features", "labelCol": "label", "predictionCol": "prediction",
         "sampleIdCol": "sampleId", "maxIter": 10, "miniBatchFraction": 0.1, "regParam": 0.1, "stepSize": 1.0,
         "minLabel": 0.0, "maxLabel": 1.0, "initialSd": 0.01,
+        # HasFitIntercept, mixed into the estimator's params (FactorizationMachines.scala:18), Spark's
+        # default true; the reference never reads it (w0 stays 0.0, SGD.scala:246), nor does fit here
+        "fitIntercept": True,
         # not in the reference: the init draw is unseeded there; device / seed here
         "seed": 0, "device": 0, "numFeatures": None,
         # not in the reference: the table over several GPUs of this process (include/fm_hip.h
@@ -324,13 +327,17 @@ class FactorizationMachinesSGD:
     def getMinLabel(self): return self._params["minLabel"]
     def getMaxLabel(self): return self._params["maxLabel"]
     def getInitialSd(self): return self._params["initialSd"]
+    def getFitIntercept(self): return self._params["fitIntercept"]
 
     def copy(self, extra: dict | None = None) -> "FactorizationMachinesSGD":
         """defaultCopy (SGD.scala:254): same uid, params overridden by extra (keyed by name or Param)."""
         c = FactorizationMachinesSGD(self.uid)
         c._params = dict(self._params)
         for key, value in (extra or {}).items():
-            c._params[key.name if isinstance(key, Param) else key] = value
+            name = key.name if isinstance(key, Param) else key
+            if name == "fitIntercept" and not isinstance(value, (bool, np.bool_)):
+                raise TypeError("fitIntercept is a BooleanParam")  # Spark's BooleanParam rejects non-booleans
+            c._params[name] = value
         return c
 
     def transformSchema(self, schema):
@@ -399,6 +406,6 @@ class FactorizationMachinesSGD:
 
 # fm.regParam, fm.dimFactorization, ...: the Param handles spark.ml tuning keys grids by
 for _name in ("dimFactorization", "featuresCol", "labelCol", "predictionCol", "maxIter", "miniBatchFraction",
-              "regParam", "stepSize", "minLabel", "maxLabel", "initialSd", "seed"):
+              "regParam", "stepSize", "minLabel", "maxLabel", "initialSd", "seed", "fitIntercept"):
     setattr(FactorizationMachinesSGD, _name, property(lambda self, _n=_name: Param(self.uid, _n)))
 del _name

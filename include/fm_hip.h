@@ -47,6 +47,9 @@ extern "C" {
 #define FM_TRANSPORT_RCCL 1      /* RCCL send/recv and all-reduce over xGMI */
 #define FM_TRANSPORT_COPY 2      /* one process only: device-to-device copies between the ranks */
 #define FM_MAX_LOCAL 16
+#define FM_FUSE_DEFAULT 0 /* fm_config.fuse_single: the library's choice (on) */
+#define FM_FUSE_ON 1
+#define FM_FUSE_OFF (-1)
 
 typedef struct fm_ctx fm_ctx;
 typedef struct fm_batch fm_batch;
@@ -69,7 +72,17 @@ typedef struct fm_batch fm_batch;
  *                S1/S2/S5/S6 of SURVEY §2b (Model.scala:155-164, SGD.scala:148-166).
  * transport    : how the ranks exchange (FM_TRANSPORT_*).  n_procs > 1 needs RCCL and comm_id:
  *                process 0 calls fm_comm_unique_id and hands the 128 bytes to the others by any
- *                channel (Spark broadcast, torch.distributed, a file). */
+ *                channel (Spark broadcast, torch.distributed, a file).
+ *                RCCL with R > 1 ranks has not run on hardware yet (every test box had one
+ *                MI355X): the R > 1 protocol is verified through the COPY transport only.
+ * fuse_single  : FM_FUSE_DEFAULT (0) / FM_FUSE_ON: a batch prepared by fm_batch_prepare on a
+ *                single-table context with k <= 16 takes the fused step -- the forward updates every
+ *                row whose feature has one entry in the batch, the segmented update only the rest
+ *                (bit for bit the same table as the unfused step); FM_FUSE_OFF: never.
+ * xchg_chunks  : sharded step with R > 1: the owners' partial pass runs in this many chunks, each
+ *                sent while the next is computed (0 = the default, 4; 1 = one pass then one
+ *                all-to-all; at most 64).  Every process of a job must pass the same value.
+ * Zero-initialise the struct: every field's 0 is its default. */
 typedef struct fm_config {
   int64_t num_features;
   int32_t k;
@@ -86,6 +99,8 @@ typedef struct fm_config {
   int32_t n_procs;
   int32_t proc_rank;
   uint8_t comm_id[128];
+  int32_t fuse_single;
+  int32_t xchg_chunks;
 } fm_config;
 
 /* One mini-batch in CSR form: the result of explode(udfVecToMap(features))

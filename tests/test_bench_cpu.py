@@ -1,0 +1,90 @@
+"""CPU: bench.py's run planning -- how --gpus N, the launcher's environment and the visible GPUs map
+onto the single-table path, one process driving N GPUs through one multi-GPU fm_ctx, or one process
+per GPU -- and that an impossible request exits non-zero instead of measuring fewer GPUs."""
+
+import argparse
+
+import numpy as np
+import pytest
+
+import bench
+
+
+def _args(**kw):
+    base = dict(gpus=1, config="c3", parallel="auto", force_sharded=False, trainer="lib")
+    base.update(kw)
+    return argparse.Namespace(**base)
+
+
+def test_default_is_the_single_table():
+    pl = bench.plan_run(_args(), {}, 1)
+    assert pl["mode"] == "single" and pl["world"] == 1 and pl["devices"] == [0]
+
+
+def test_more_gpus_than_visible_fails_loudly():
+    with pytest.raises(SystemExit) as ei:
+        bench.plan_run(_args(gpus=2), {}, 1)
+    assert "needs 2 visible GPUs" in str(ei.value) and ei.value.code != 0
+    with pytest.raises(SystemExit):
+        bench.plan_run(_args(gpus=8), {}, 4)
+
+
+def test_one_process_drives_n_gpus():
+    pl = bench.plan_run(_args(gpus=8), {}, 8)
+    assert pl["mode"] == "group" and pl["world"] == 8 and pl["n_local"] == 8
+    assert pl["devices"] == list(range(8)) and pl["parallel"] == "sharded"
+    pl = bench.plan_run(_args(gpus=2, config="c2"), {}, 8)
+    assert pl["parallel"] == "replicated"  # c2: the replicated-table config
+    pl = bench.plan_run(_args(gpus=2, parallel="sharded", config="c2"), {}, 2)
+    assert pl["parallel"] == "sharded"
+
+
+def test_launcher_one_process_per_gpu():
+    env = {"WORLD_SIZE": "4", "RANK": "2", "LOCAL_RANK": "2"}
+    pl = bench.plan_run(_args(gpus=4), env, 4)
+    assert pl["mode"] == "procs" and pl["world"] == 4 and pl["rank"] == 2 and pl["devices"] == [2]
+    assert pl["n_local"] == 1
+    with pytest.raises(SystemExit):  # --gpus disagrees with the launcher
+        bench.plan_run(_args(gpus=2), env, 4)
+    with pytest.raises(SystemExit):  # the local rank's GPU is not visible
+        bench.plan_run(_args(gpus=4), env, 2)
+
+
+def test_group_path_on_one_gpu():
+    pl = bench.plan_run(_args(force_sharded=True), {}, 1)
+    assert pl["mode"] == "group" and pl["n_local"] == 1 and pl["parallel"] == "sharded"
+    pl = bench.plan_run(_args(parallel="replicated"), {}, 1)
+    assert pl["mode"] == "group" and pl["parallel"] == "replicated"
+
+
+def test_torch_harness_needs_the_launcher():
+    with pytest.raises(SystemExit):
+        bench.plan_run(_args(gpus=2, trainer="torch"), {}, 2)
+
+
+def test_no_gpu_fails_loudly():
+    with pytest.raises(SystemExit):
+        bench.plan_run(_args(), {}, 0)
+
+
+def test_concat_batches_splits_back_by_rows():
+    from fm_spark_amd.data import synthetic_batch
+
+    parts = [synthetic_batch(100 + 7 * i, 5000, batch_index=i) for i in range(3)]
+    cat = bench.concat_batches(parts)
+    assert cat.n_rows == sum(p.n_rows for p in parts) and cat.nnz == sum(p.nnz for p in parts)
+    r0 = 0
+    for p in parts:  # the library's contiguous row split of the concatenation gives each part back
+        e0, e1 = cat.row_ptr[r0], cat.row_ptr[r0 + p.n_rows]
+        np.testing.assert_array_equal(cat.row_ptr[r0:r0 + p.n_rows + 1] - e0, p.row_ptr)
+        np.testing.assert_array_equal(cat.col[e0:e1], p.col)
+        np.testing.assert_array_equal(cat.val[e0:e1], p.val)
+        np.testing.assert_array_equal(cat.label[r0:r0 + p.n_rows], p.label)
+        r0 += p.n_rows
+
+
+def test_singleton_fraction():
+    from fm_spark_amd.data import Batch
+
+    b = Batch(row_ptr=np.array([0, 3, 5]), col=np.array([1, 2, 3, 3, 4], np.int32), val=np.ones(5), label=np.zeros(2))
+    assert bench.singleton_fraction([b, b]) == pytest.approx(3 / 4)

@@ -1,10 +1,16 @@
-"""GPU: singleton fusion (FM_FUSE_SINGLE=1, off by default) -- the forward applies the update of every row whose
-feature has one entry in the batch, and the update kernel skips those runs.
+"""GPU: the fused step (fm_config.fuse_single, on by default for prepared single-table batches with
+k <= 16).
 
-The fused step must give the unfused step's table bit for bit (the forward uses the update's
-arithmetic on the same fp32-rounded S, r and yhat) and match the fp64 oracle; the flags come from
-the prepared sorted view (fm_batch_prepare), so both paths run on prepared batches here.  Widths
-cover every header-granule shape (kp = 4, 8, 12, 16, 32, 80).
+fm_batch_prepare sorts the batch and keeps only the runs of two or more entries (k_split_*); the
+step tags those rows' headers (k_tag_multi), the forward updates every untagged row -- a feature
+with one entry in the batch -- in place, and the segmented update walks the multi runs only.  The
+forward uses the update's arithmetic on the same fp32-rounded S, r and yhat, so the fused step must
+give the unfused step's table bit for bit, the same loss and the same distinct count, and match the
+fp64 oracle.  Cases: every kp the fused forward serves (4, 8, 12, 16) and one it does not (32, where
+the switch changes nothing); rows absent from the model and an L1 that zeroes values; empty, short
+and long rows (beyond the 40 entries a sample keeps in LDS: the re-read path); a feature in every
+row; split chunks of 1024 sorted entries crossed by long runs; a batch that is not prepared (the
+unfused path) between prepared ones.
 """
 
 import numpy as np
@@ -17,78 +23,108 @@ from test_gpu_parity import assert_tables, to_host
 pytestmark = pytest.mark.gpu
 
 
-def _prepared_steps(monkeypatch, fuse, csrs, F, k, ids, w, V, steps):
+def _steps(fuse, csrs, F, k, ids, w, V, steps, step_size=0.3, reg=1e-4, prepare=lambda t: True):
     from fm_spark_amd.engine import FMContext
 
-    monkeypatch.setenv("FM_FUSE_SINGLE", "1" if fuse else "0")
-    ctx = FMContext(F, k)
+    ctx = FMContext(F, k, fuse=fuse)
     ctx.load_tables(ids, w, V)
     dbs = [ctx.batch(to_host(c)) for c in csrs]
     losses = []
     for t in range(1, steps + 1):
         b = dbs[(t - 1) % len(dbs)]
-        b.prepare()
-        o = ctx.step_batch(b, t, 0.3, 1e-4)
-        losses.append((o.loss_sum, o.n_unique))
+        if prepare(t):
+            b.prepare()
+        o = ctx.step_batch(b, t, step_size, reg)
+        losses.append((o.loss_sum, o.n_unique, o.n_loss_rows))
     out = ctx.export_tables()
     ctx.close()
     return losses, out
 
 
-@pytest.mark.parametrize("k", [3, 8, 12, 16, 32, 80])
-def test_fused_singletons_bitwise_equal_unfused(monkeypatch, gpu, k):
+def _assert_same(a, b):
+    (la, ta), (lb, tb) = a, b
+    assert la == lb
+    for x, y in zip(ta, tb):
+        assert np.array_equal(x, y)
+
+
+@pytest.mark.parametrize("k", [3, 8, 12, 16, 32])
+def test_fused_bitwise_equal_unfused_and_oracle(gpu, k):
     F = 20000
     csrs = [make_problem(700 + i, 1500, F, k, 12, hot=5 + i)[0] for i in range(3)]
     _, ids, w, V = make_problem(71, 1, F, k, 1)
-    lf, tf = _prepared_steps(monkeypatch, True, csrs, F, k, ids, w, V, 4)
-    lu, tu = _prepared_steps(monkeypatch, False, csrs, F, k, ids, w, V, 4)
-    assert lf == lu
-    for a, b in zip(tf, tu):
-        assert np.array_equal(a, b)
-    # and the oracle
+    fused = _steps(True, csrs, F, k, ids, w, V, 4)
+    unfused = _steps(False, csrs, F, k, ids, w, V, 4)
+    _assert_same(fused, unfused)
     model = R.Model.empty(F, k)
     model.load(ids, w, V)
     for t in range(1, 5):
         ro = R.sgd_step_fast(model, csrs[(t - 1) % 3], t, 0.3, 1e-4)
-        np.testing.assert_allclose(lf[t - 1][0], ro.loss_sum, rtol=1e-6)
-        assert lf[t - 1][1] == ro.n_unique
-    assert_tables(model, tf)
+        np.testing.assert_allclose(fused[0][t - 1][0], ro.loss_sum, rtol=1e-6)
+        assert fused[0][t - 1][1] == ro.n_unique
+    assert_tables(model, fused[1])
 
 
-def test_fused_absent_rows_and_l1(monkeypatch, gpu):
-    """Singleton rows absent from the model (zero rows made present by their update) and a regParam
-    whose soft-threshold zeroes values: fused and unfused agree bit for bit."""
+def test_fused_absent_rows_and_l1(gpu):
+    """Rows absent from the model (singletons and multi rows made present by their update) and a
+    regParam whose soft-threshold zeroes values: fused and unfused agree bit for bit."""
     F, k = 5000, 16
     csrs = [make_problem(760 + i, 800, F, k, 10)[0] for i in range(2)]
     _, ids, w, V = make_problem(72, 1, F, k, 1)
     keep = ids[::3]  # two thirds of the rows absent
-    res = []
-    for fuse in (True, False):
-        from fm_spark_amd.engine import FMContext
-
-        monkeypatch.setenv("FM_FUSE_SINGLE", "1" if fuse else "0")
-        ctx = FMContext(F, k)
-        ctx.load_tables(keep, w[keep], V[keep])
-        dbs = [ctx.batch(to_host(c)) for c in csrs]
-        for t in range(1, 4):
-            b = dbs[(t - 1) % 2]
-            b.prepare()
-            ctx.step_batch(b, t, 0.5, 0.05)
-        res.append(ctx.export_tables())
-        ctx.close()
-    for a, b in zip(res[0], res[1]):
-        assert np.array_equal(a, b)
+    res = [_steps(f, csrs, F, k, keep, w[keep], V[keep], 3, step_size=0.5, reg=0.05) for f in (True, False)]
+    _assert_same(res[0], res[1])
 
 
-def test_fused_short_empty_and_long_rows(monkeypatch, gpu):
-    """Rows shorter than a team's entry slots and empty rows (the stash flush for lanes without an
-    entry), and rows longer than the 40 stashed entries (the global fallback), at k = 16."""
+def test_fused_short_empty_long_rows_and_unprepared(gpu):
+    """Rows shorter than a team's entry slots, empty rows, rows longer than the 40 entries a sample
+    keeps in LDS (119 at most: the re-read path), and every third step on a batch that is not
+    prepared (the unfused path, sorted inside its step) between fused ones."""
     F, k = 30000, 16
     csrs = [make_problem(780 + i, 1200, F, k, 3, empty_frac=0.3)[0] for i in range(2)]
-    csrs += [make_problem(790, 300, F, k, 60)[0]]  # up to 119 entries per row
+    csrs += [make_problem(790, 300, F, k, 60)[0]]
     _, ids, w, V = make_problem(73, 1, F, k, 1)
-    lf, tf = _prepared_steps(monkeypatch, True, csrs, F, k, ids, w, V, 6)
-    lu, tu = _prepared_steps(monkeypatch, False, csrs, F, k, ids, w, V, 6)
-    assert lf == lu
-    for a, b in zip(tf, tu):
-        assert np.array_equal(a, b)
+    prep = lambda t: t % 3 != 0  # noqa: E731
+    fused = _steps(True, csrs, F, k, ids, w, V, 7, prepare=prep)
+    unfused = _steps(False, csrs, F, k, ids, w, V, 7, prepare=prep)
+    _assert_same(fused, unfused)
+
+
+def test_fused_feature_in_every_row_and_long_runs(gpu):
+    """A feature present in every row (one run of n_rows entries) and hot features whose runs cross
+    many 1024-entry split chunks and 256-entry update waves; the split keeps them whole and in order."""
+    F, k = 200000, 8
+    csrs = []
+    for i in range(2):
+        c, _, _, _ = make_problem(800 + i, 6000, F - 8, k, 20, hot=17 + i, empty_frac=0.0)
+        col = c.col + 8
+        col[c.row_ptr[:-1]] = 3  # each row's first (smallest) id becomes id 3: rows stay sorted and distinct
+        csrs.append(R.CSR(c.row_ptr, col.astype(np.int32), c.val, c.label))
+    _, ids, w, V = make_problem(74, 1, F, k, 1)
+    fused = _steps(True, csrs, F, k, ids, w, V, 4)
+    unfused = _steps(False, csrs, F, k, ids, w, V, 4)
+    _assert_same(fused, unfused)
+    model = R.Model.empty(F, k)
+    model.load(ids, w, V)
+    for t in range(1, 5):
+        ro = R.sgd_step_fast(model, csrs[(t - 1) % 2], t, 0.3, 1e-4)
+        assert fused[0][t - 1][1] == ro.n_unique
+    assert_tables(model, fused[1])
+
+
+def test_fused_all_singletons_and_all_multi(gpu):
+    """Batches whose features are all singletons (nothing left for the segmented update) and all
+    repeated (nothing for the fused forward)."""
+    F, k = 100000, 16
+    rng = np.random.default_rng(5)
+    B, z = 500, 8
+    ids_all = rng.permutation(F)[: B * z].astype(np.int32)
+    rp = np.arange(0, B * z + 1, z, dtype=np.int64)
+    single = R.CSR(rp, np.sort(ids_all.reshape(B, z), axis=1).ravel(), rng.normal(size=B * z), rng.random(B))
+    pool = rng.permutation(F)[:40].astype(np.int32)
+    cols = np.concatenate([np.sort(rng.choice(pool, size=z, replace=False)) for _ in range(B)]).astype(np.int32)
+    multi = R.CSR(rp, cols, rng.normal(size=B * z), rng.random(B))
+    _, ids, w, V = make_problem(75, 1, F, k, 1)
+    fused = _steps(True, [single, multi], F, k, ids, w, V, 4)
+    unfused = _steps(False, [single, multi], F, k, ids, w, V, 4)
+    _assert_same(fused, unfused)

@@ -79,14 +79,13 @@ def test_group_sharded_step_matches_oracle(gpu, R, k, F, hot, transport):
     ctx.close()
 
 
-@pytest.mark.parametrize("chunks", ["1", "3", "16"])
-def test_group_sharded_exchange_chunks(gpu, chunks, monkeypatch):
+@pytest.mark.parametrize("chunks", [1, 3, 16])
+def test_group_sharded_exchange_chunks(gpu, chunks):
     """The owners' partial pass in C chunks whose exchange overlaps the next chunk's compute
-    (FM_XCHG_CHUNKS; default 4): any C gives the oracle step, including chunks with no pairs."""
-    monkeypatch.setenv("FM_XCHG_CHUNKS", chunks)
+    (fm_config.xchg_chunks; default 4): any C gives the oracle step, including chunks with no pairs."""
     F, k, R = 257, 8, 4
     _, ids, w, V = make_problem(21, 1, F, k, 1)
-    ctx = _ctx(F, k, R)
+    ctx = _ctx(F, k, R, xchg_chunks=chunks)
     ctx.load_tables(ids, w, V)
     model = R_.Model.empty(F, k)
     model.load(ids, w, V)

@@ -38,3 +38,16 @@ def test_from_rows_partitions_and_sample_ids():
     assert df.partition_sizes == [2, 3, 2, 3]  # ParallelCollectionRDD slicing
     sid = FactorizationMachinesModel.addSampleId(df)["sampleId"]
     assert sid[:3] == [0, 1, 1 << 33] and sid[-1] == (3 << 33) + 2
+
+
+def test_fit_intercept_param_survives_copy_and_param_maps():
+    """HasFitIntercept (FactorizationMachines.scala:18): Spark's default true, settable through a
+    ParamMap / copy(extra) by name or by the Param handle, as CrossValidator does; a BooleanParam."""
+    fm = FactorizationMachinesSGD("fm_y")
+    assert fm.getFitIntercept() is True
+    assert fm.fitIntercept.name == "fitIntercept" and fm.fitIntercept.parent == "fm_y"
+    c = fm.copy({fm.fitIntercept: False})
+    assert c.getFitIntercept() is False and fm.getFitIntercept() is True
+    assert fm.copy({"fitIntercept": False}).getFitIntercept() is False
+    with pytest.raises(TypeError):
+        fm.copy({"fitIntercept": 1.5})
