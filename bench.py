@@ -323,6 +323,7 @@ def main():
 
     median_ms = None
     host_path = None
+    host_trace = None
     xg = None
     if mode == "single":
         ctx = FMContext(F, k, device=local_rank, seed=20261015, init_sd=INIT_SD, fuse=args.fuse == "on")
@@ -435,15 +436,20 @@ def main():
         # sort) is enqueued on the side streams behind step i: inside the timed region, off the
         # critical path
         evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)] if main_stream else None
+        h_step, h_prep = [], []  # host time in each call: the GPU never waits on the host if their sum < the step
         if prefetch:
             dbatches[0].prepare()
         for i in range(args.steps):
             t += 1
             if evs:
                 evs[i].record(main_stream)
+            h0 = time.perf_counter()
             ctx.step_batch(dbatches[i % nb], t, STEP_SIZE, REG_PARAM, sync=False)
+            h1 = time.perf_counter()
             if prefetch and i + 1 < args.steps:
                 dbatches[(i + 1) % nb].prepare()
+                h_prep.append(time.perf_counter() - h1)
+            h_step.append(h1 - h0)
         if evs:
             evs[args.steps].record(main_stream)
         ctx.sync()
@@ -471,6 +477,10 @@ def main():
                        f"replicated x{R}, {who}, per-slot gradient sums all-reduced inside libfm_hip over RCCL")
         if prefetch:
             parallelism += ", next batch prepared during the current step"
+        host_trace = {"step_enqueue_ms_median": 1e3 * float(np.median(h_step)),
+                      "prepare_ms_median": 1e3 * float(np.median(h_prep)) if h_prep else None,
+                      "what": "host time inside fm_step_batch (out = NULL: enqueue only) and fm_batch_prepare of the "
+                              "next batch, per iteration; below the step time the GPU never waits on the host"}
     else:
         from fm_spark_amd.distributed import ShardedTrainer
 
@@ -582,6 +592,8 @@ def main():
             else:
                 line["exchange"] = dict(xg, per="per iteration, the gradient all-reduce",
                                         ring_GBs_at_step_time=xg["ring_bytes_per_rank"] / step_s / 1e9)
+        if host_trace:
+            line["host_trace"] = host_trace
         if host_path:
             line["host_path_ms_per_step"] = host_path["median_ms_per_step"]
             line["host_path"] = host_path

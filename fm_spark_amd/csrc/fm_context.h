@@ -347,6 +347,10 @@ inline int bits_for(int64_t max_value) {
 void upload_batch(fm_ctx* ctx, const fm_csr* c, fm_batch* b, bool check_range);
 void reserve_work(fm_ctx* ctx, int64_t B, int64_t N);
 
+// the sharded route (fm_shard_route) in two halves, for fm_group.hip: enqueue (counts stay in
+// ctx->sh_tot on the device), then digest the host copy of those counts ([R] pairs, [R] entries)
+void shard_route_launch(fm_ctx* ctx, fm_batch* b, void* send_slot, void* send_ent);
+void shard_route_finish(fm_ctx* ctx, fm_batch* b, const unsigned long long* hc, int64_t* counts);
 // sharded predict building blocks (fm_shard.hip), called by fm_group.hip with the member locked:
 // the owner partial pass with the per-pair count of present rows (Model.scala:103-112 inner
 // joins: absent ids contribute nothing), and the requester's predict epilogue

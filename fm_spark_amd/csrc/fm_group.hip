@@ -370,9 +370,44 @@ void sync_group_batch_view(fm_batch* b) {  // fm_batch_rows / fm_batch_nnz of th
   b->dev.nnz = b->grp->nnz;
 }
 
+// Every rank's route counts (device, ctx->sh_tot: [R] pairs, [R] entries) -> the host, rank-major
+// [R][2R] in that layout: RCCL all-gathers them on the side streams and one copy comes back; COPY
+// reads each rank's.  One host wait for the whole job, after every rank's route was enqueued.
+std::vector<unsigned long long> gather_route_counts(Group& g) {
+  const int R = g.R;
+  const size_t row = sizeof(unsigned long long) * 2 * R;
+  Rank& r0 = g.ranks[0];
+  r0.xg_pin.ensure(row * R);
+  if (g.rccl) {
+    for (auto& r : g.ranks) ensure_on(r.device, r.xg_recv, row * R);
+    FM_RCCL_CHECK(ncclGroupStart());
+    for (auto& r : g.ranks) {
+      FM_HIP_CHECK(hipSetDevice(r.device));
+      FM_RCCL_CHECK(ncclAllGather(r.m->sh_tot.p, r.xg_recv.p, 2 * R, ncclUint64, r.comm_side, r.m->side));
+    }
+    FM_RCCL_CHECK(ncclGroupEnd());
+    FM_HIP_CHECK(hipSetDevice(r0.device));
+    FM_HIP_CHECK(hipMemcpyAsync(r0.xg_pin.p, r0.xg_recv.p, row * R, hipMemcpyDeviceToHost, r0.m->side));
+    FM_HIP_CHECK(hipStreamSynchronize(r0.m->side));
+  } else {
+    for (auto& r : g.ranks) {
+      FM_HIP_CHECK(hipSetDevice(r.device));
+      FM_HIP_CHECK(hipMemcpyAsync(reinterpret_cast<char*>(r0.xg_pin.p) + row * r.global, r.m->sh_tot.p, row,
+                                  hipMemcpyDeviceToHost, r.m->side));
+    }
+    for (auto& r : g.ranks) {
+      FM_HIP_CHECK(hipSetDevice(r.device));
+      FM_HIP_CHECK(hipStreamSynchronize(r.m->side));
+    }
+  }
+  const unsigned long long* h = reinterpret_cast<const unsigned long long*>(r0.xg_pin.p);
+  return std::vector<unsigned long long>(h, h + (size_t)2 * R * R);
+}
+
 // The batch-only phases of a sharded iteration (fm_shard.hip phases 1 and 1b): route every part,
 // exchange the counts and the entries, build the owners' pair tables and slot orders.  Side
-// streams; the host waits for the routes' counts only (they size the exchange).
+// streams; the host waits once, for the job's route counts (they size the exchange), after every
+// local rank's route is enqueued.
 void prefetch(Group& g, GroupBatch& gb) {
   if (gb.prefetched) return;
   const int R = g.R, L = g.L;
@@ -382,9 +417,19 @@ void prefetch(Group& g, GroupBatch& gb) {
     GPart& p = gb.parts[l];
     ensure_on(r.device, p.send_slot, sizeof(uint32_t) * p.nnz);
     ensure_on(r.device, p.send_ent, sizeof(uint2) * p.nnz);
-    mcheck(fm_shard_route(r.m, p.b, p.send_slot.p, p.send_ent.p, counts[l].data()), "fm_shard_route");
+    on(r, [&] { shard_route_launch(r.m, p.b, p.send_slot.p, p.send_ent.p); });
   }
-  const std::vector<int64_t> all = allgather(g, counts, 2 * R);  // [source][2R]
+  const std::vector<unsigned long long> rc = gather_route_counts(g);  // [source][pairs R | entries R]
+  std::vector<int64_t> all((size_t)R * 2 * R);                         // [source][entries R | pairs R]
+  for (int s = 0; s < R; ++s)
+    for (int o = 0; o < R; ++o) {
+      all[(size_t)s * 2 * R + o] = (int64_t)rc[(size_t)s * 2 * R + R + o];
+      all[(size_t)s * 2 * R + R + o] = (int64_t)rc[(size_t)s * 2 * R + o];
+    }
+  for (int l = 0; l < L; ++l) {
+    Rank& r = g.ranks[l];
+    on(r, [&] { shard_route_finish(r.m, gb.parts[l].b, rc.data() + (size_t)r.global * 2 * R, counts[l].data()); });
+  }
   std::vector<const char*> ss(L), se(L);
   std::vector<char*> rs(L), re(L);
   std::vector<const int64_t*> out(L), in(L);

@@ -124,6 +124,28 @@ __global__ __launch_bounds__(kBlock) void k_route_keys(const int64_t* __restrict
   }
 }
 
+// The owner's received S rows, wire layout [P][kp] vectors then [P] {r, yhat} -> the single-table
+// step's per-sample records [P][rec] = [S (kp) | {r, yhat} | 0 pad] (kp <= 16: 64- or 128-B
+// records), so the segmented update gathers one line per entry instead of two (the S row and its
+// scalars).  Streaming, float4 per lane.
+__global__ __launch_bounds__(kBlock) void k_pack_srec(const float* __restrict__ vec, const float2* __restrict__ sc,
+                                                      int64_t P, int kp, int rec, float* __restrict__ out) {
+  const int q = rec / 4;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < P * q; i += (int64_t)gridDim.x * kBlock) {
+    const int64_t pr = i / q;
+    const int j = (int)(i - pr * q) * 4;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (j < kp) {
+      v = *reinterpret_cast<const float4*>(vec + pr * kp + j);
+    } else if (j == kp) {
+      const float2 s2 = sc[pr];
+      v.x = s2.x;
+      v.y = s2.y;
+    }
+    *reinterpret_cast<float4*>(out + pr * rec + j) = v;
+  }
+}
+
 __global__ void k_key_slots(const uint32_t* __restrict__ key, int64_t n, uint32_t slot_mask,
                             uint32_t* __restrict__ slot) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
@@ -427,6 +449,26 @@ extern "C" {
 int fm_shard_route(fm_ctx* ctx, fm_batch* b, void* send_slot, void* send_ent, int64_t* counts) {
   return guarded(ctx, [&]() -> int {
     FM_REQUIRE(counts != nullptr, "bad arguments");
+    shard_route_launch(ctx, b, send_slot, send_ent);
+    const int R = ctx->cfg.shard_count;
+    ctx->side_pinned.ensure(sizeof(unsigned long long) * 2 * R);
+    FM_HIP_CHECK(hipMemcpyAsync(ctx->side_pinned.p, ctx->sh_tot.p, sizeof(unsigned long long) * 2 * R,
+                                hipMemcpyDeviceToHost, ctx->side));
+    FM_HIP_CHECK(hipStreamSynchronize(ctx->side));  // the side stream only: the main stream keeps running
+    shard_route_finish(ctx, b, reinterpret_cast<const unsigned long long*>(ctx->side_pinned.p), counts);
+    return FM_OK;
+  });
+}
+
+}  // extern "C"
+
+namespace fmhip {
+
+// Phase 1 enqueued on the side stream, its counts left on the device in ctx->sh_tot ([R] pairs,
+// then [R] entries per owner, uint64): a multi-GPU context gathers every rank's counts on the
+// device and reads them back once for the whole job (fm_group.hip prefetch).
+void shard_route_launch(fm_ctx* ctx, fm_batch* b, void* send_slot, void* send_ent) {
+  {
     ShardBatchState& S = shard_state(ctx, b);
     const int R = ctx->cfg.shard_count;
     FM_REQUIRE(R <= kMaxR, "the owner-computes sharded step supports at most 64 ranks");
@@ -487,10 +529,18 @@ int fm_shard_route(fm_ctx* ctx, fm_batch* b, void* send_slot, void* send_ent, in
     }
     FM_HIP_CHECK(hipGetLastError());
     ctx->prof_end("route", e0, st);
-    ctx->side_pinned.ensure(sizeof(unsigned long long) * 2 * R);
-    FM_HIP_CHECK(hipMemcpyAsync(ctx->side_pinned.p, tot, sizeof(unsigned long long) * 2 * R, hipMemcpyDeviceToHost, st));
-    FM_HIP_CHECK(hipStreamSynchronize(st));  // the side stream only: the main stream keeps running
-    const unsigned long long* hc = reinterpret_cast<const unsigned long long*>(ctx->side_pinned.p);
+    S.route_nnz = -1;  // until shard_route_finish has the counts
+  }
+}
+
+// The host's copy of the route counts hc ([R] pairs, [R] entries) -> counts[0..R) entries and
+// counts[R..2R) pairs per owner, and the batch's requester state.
+void shard_route_finish(fm_ctx* ctx, fm_batch* b, const unsigned long long* hc, int64_t* counts) {
+  {
+    ShardBatchState& S = shard_state(ctx, b);
+    const int R = ctx->cfg.shard_count;
+    const int64_t N = b->dev.nnz;
+    const bool drop = b->max_id >= (int64_t)ctx->cfg.num_features;
     S.pairs_out.assign(R, 0);
     int64_t ne = 0;
     for (int o = 0; o < R; ++o) {
@@ -502,9 +552,12 @@ int fm_shard_route(fm_ctx* ctx, fm_batch* b, void* send_slot, void* send_ent, in
     FM_REQUIRE(drop ? ne <= N : ne == N, "route: inconsistent entry count");
     S.route_nnz = N;
     S.combined = false;
-    return FM_OK;
-  });
+  }
 }
+
+}  // namespace fmhip
+
+extern "C" {
 
 int fm_shard_owner_prepare(fm_ctx* ctx, fm_batch* b, const void* recv_slot, const void* recv_ent, int64_t n,
                            const int64_t* src_entries, const int64_t* src_pairs) {
@@ -714,8 +767,19 @@ int fm_shard_owner_update(fm_ctx* ctx, fm_batch* b, const void* s_recv, int32_t 
     double* stats = ctx->loss_hist.as<double>() + 3 * (int64_t)ctx->epoch;
     FM_HIP_CHECK(hipStreamWaitEvent(st, S.ready_upd, 0));
     hipEvent_t e0 = ctx->prof_begin(st);
-    const float* Srow = reinterpret_cast<const float*>(s_recv);  // [P][kp] S, then [P] {yhat, y}
-    SegSource src{Srow, ctx->kp, reinterpret_cast<const float2*>(Srow ? Srow + S.P * ctx->kp : nullptr), 1};
+    const float* Srow = reinterpret_cast<const float*>(s_recv);  // [P][kp] S, then [P] {r, yhat}
+    const int kp = ctx->kp;
+    SegSource src{Srow, kp, reinterpret_cast<const float2*>(Srow ? Srow + S.P * kp : nullptr), 1};
+    if (s_rec_yl(kp) && S.P > 0) {
+      // one record per pair (S and {r, yhat} in one line), as the single-table step's
+      const int rec = s_rec_floats(kp);
+      ctx->work.S.ensure(sizeof(float) * (size_t)S.P * rec);
+      const int64_t nq = S.P * (rec / 4);
+      hipLaunchKernelGGL(k_pack_srec, dim3(blocks_for(nq)), dim3(kBlock), 0, st, Srow, src.yl, S.P, kp, rec,
+                         ctx->work.S.as<float>());
+      FM_HIP_CHECK(hipGetLastError());
+      src = SegSource{ctx->work.S.as<float>(), rec, reinterpret_cast<const float2*>(ctx->work.S.as<float>() + kp), rec / 2};
+    }
     launch_segment_update(ctx->view(), n, src, ctx->work, p, S.skeys.as<uint32_t>(), S.sents.as<uint2>(),
                           S.loss_blocks, stats, st);
     ctx->prof_end("owner_update", e0, st);

@@ -91,6 +91,29 @@ void oracle_init_random(oracle_model* m, uint64_t seed, double sd, int64_t b, in
   }
 }
 
+/* Marks [b, e) present with the device's createInitialModel draw (fm_kernels.hip gauss_draw:
+ * N(0, sd^2) keyed by (seed, id, factor; -1 = w), Box-Muller in fp64, rounded to fp32 as the
+ * device table holds it), so a whole-table comparison starts from the same table. */
+static inline double device_gauss(uint64_t seed, int64_t id, int f, double sd) {
+  const uint64_t c = ((uint64_t)id << 10) ^ (uint64_t)(f + 1);
+  const uint64_t h1 = splitmix64(seed ^ splitmix64(c));
+  const uint64_t h2 = splitmix64(h1 ^ 0x632BE59BD9B4E019ull);
+  const double u1 = (double)((h1 >> 11) + 1) * 0x1.0p-53;
+  const double u2 = (double)(h2 >> 11) * 0x1.0p-53;
+  const double g = sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2);
+  return (double)(float)(g * sd);
+}
+
+void oracle_init_device_draw(oracle_model* m, uint64_t seed, double sd, int64_t b, int64_t e) {
+  const int32_t k = m->k;
+#pragma omp parallel for schedule(static)
+  for (int64_t id = b; id < e; ++id) {
+    m->w[id] = device_gauss(seed, id, -1, sd);
+    for (int32_t f = 0; f < k; ++f) m->V[id * k + f] = device_gauss(seed, id, f, sd);
+    m->present[id] = 1;
+  }
+}
+
 static void ensure_rows(oracle_model* m, int64_t B) {
   if (B <= m->cap_rows) return;
   free(m->S); free(m->yhat);

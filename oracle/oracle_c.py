@@ -33,6 +33,7 @@ def load():
     lib.oracle_destroy.argtypes = [P]
     lib.oracle_load.argtypes = [P, C.POINTER(C.c_int32), C.c_int64, C.POINTER(C.c_double), C.POINTER(C.c_double)]
     lib.oracle_init_random.argtypes = [P, C.c_uint64, C.c_double, C.c_int64, C.c_int64]
+    lib.oracle_init_device_draw.argtypes = [P, C.c_uint64, C.c_double, C.c_int64, C.c_int64]
     lib.oracle_step.argtypes = [P, C.POINTER(C.c_int64), C.POINTER(C.c_int32), C.POINTER(C.c_double),
                                 C.POINTER(C.c_double), C.c_int64, C.c_int32, C.c_double, C.c_double,
                                 C.POINTER(C.c_double), C.POINTER(C.c_int64), C.POINTER(C.c_int64)]

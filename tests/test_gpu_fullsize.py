@@ -192,3 +192,50 @@ def test_c2_full_size_table_parity(gpu):
     np.testing.assert_array_equal(gi, np.arange(F))
     np.testing.assert_allclose(gw, model.w, rtol=RTOL, atol=ATOL)
     np.testing.assert_allclose(gV, model.V, rtol=RTOL, atol=ATOL)
+
+
+def test_c3_whole_table_parity_against_c_oracle(gpu):
+    """c3 at full size, every row: the whole 100M x k = 16 table, initialised with the device's
+    seeded draw on both sides (oracle_init_device_draw replicates it), stepped twice -- the device
+    through prepared batches (the fused step: singleton rows updated by the forward, the rest by the
+    segmented update, lazy L1 for the untouched rows) and the fp64 C oracle (oracle/fm_oracle.c,
+    eager L1 over every row as SGD.scala:157-181) -- then every row compared in id-range chunks
+    through fm_export_rows at rtol 1e-5 (atol 1e-8 for values the L1 leaves next to zero)."""
+    from fm_spark_amd.data import synthetic_batch
+    from fm_spark_amd.engine import FMContext
+    from oracle import oracle_c
+
+    F, k, B, seed, sd = 100_000_000, 16, 262144, 20261015, 0.01
+    hb = [synthetic_batch(B, F, batch_index=40 + i) for i in range(2)]
+    lib = oracle_c.load()
+    m = oracle_c.create(lib, F, k)
+    try:
+        lib.oracle_init_device_draw(m, seed, sd, 0, F)
+        ctx = FMContext(F, k, seed=seed, init_sd=sd)
+        ctx.init_random_range(0, F)
+        dbs = [ctx.batch(_host(b)) for b in hb]
+        for t, (b, db) in enumerate(zip(hb, dbs), start=1):
+            db.prepare()
+            go = ctx.step_batch(db, t, STEP, REG, sync=True)
+            rc, loss, nl, nu = oracle_c.step(lib, m, b, t, STEP, REG)
+            assert rc == 0
+            assert (go.n_loss_rows, go.n_unique) == (nl, nu)
+            assert go.loss_sum == pytest.approx(loss, rel=1e-9)
+        ow, oV, opres = (np.ctypeslib.as_array(lib.oracle_w(m), shape=(F,)),
+                         np.ctypeslib.as_array(lib.oracle_V(m), shape=(F * k,)).reshape(F, k),
+                         np.ctypeslib.as_array(lib.oracle_present(m), shape=(F,)))
+        worst = 0.0
+        chunk = 1 << 23
+        for a in range(0, F, chunk):
+            ids = np.arange(a, min(F, a + chunk), dtype=np.int32)
+            w, V, pres = ctx.export_rows(ids)
+            assert pres.all() and opres[a:a + len(ids)].all()
+            np.testing.assert_allclose(w, ow[a:a + len(ids)], rtol=RTOL, atol=ATOL)
+            np.testing.assert_allclose(V, oV[a:a + len(ids)], rtol=RTOL, atol=ATOL)
+            ref = oV[a:a + len(ids)]
+            big = np.abs(ref) >= 1e-6
+            worst = max(worst, float(np.max(np.abs(V[big] - ref[big]) / np.abs(ref[big]))))
+        print(f"c3 whole table: {F} rows x {k} compared after 2 steps, max relative error {worst:.3e}")
+        ctx.close()
+    finally:
+        lib.oracle_destroy(m)

@@ -4,9 +4,12 @@ k <= 16).
 fm_batch_prepare sorts the batch and keeps only the runs of two or more entries (k_split_*); the
 step tags those rows' headers (k_tag_multi), the forward updates every untagged row -- a feature
 with one entry in the batch -- in place, and the segmented update walks the multi runs only.  The
-forward uses the update's arithmetic on the same fp32-rounded S, r and yhat, so the fused step must
-give the unfused step's table bit for bit, the same loss and the same distinct count, and match the
-fp64 oracle.  Cases: every kp the fused forward serves (4, 8, 12, 16) and one it does not (32, where
+forward uses the update's arithmetic on the same fp32-rounded S, r and yhat; the multi runs are
+summed in the same entry order, but their pieces meet at other wave boundaries of the compacted
+view, so the fp64 run sums may differ in the last bits: the fused step must give the unfused step's
+counts exactly, its loss to 1e-9 and its table within the north_star tolerance (rtol 1e-5,
+atol 1e-8 where a strong L1 leaves values next to zero), match the fp64
+oracle, and be bitwise reproducible run to run.  Cases: every kp the fused forward serves (4, 8, 12, 16) and one it does not (32, where
 the switch changes nothing); rows absent from the model and an L1 that zeroes values; empty, short
 and long rows (beyond the 40 entries a sample keeps in LDS: the re-read path); a feature in every
 row; split chunks of 1024 sorted entries crossed by long runs; a batch that is not prepared (the
@@ -43,6 +46,16 @@ def _steps(fuse, csrs, F, k, ids, w, V, steps, step_size=0.3, reg=1e-4, prepare=
 
 def _assert_same(a, b):
     (la, ta), (lb, tb) = a, b
+    for (l1, u1, n1), (l2, u2, n2) in zip(la, lb):
+        assert (u1, n1) == (u2, n2)
+        assert l1 == pytest.approx(l2, rel=1e-9)
+    np.testing.assert_array_equal(ta[0], tb[0])
+    np.testing.assert_allclose(ta[1], tb[1], rtol=1e-5, atol=1e-8)
+    np.testing.assert_allclose(ta[2], tb[2], rtol=1e-5, atol=1e-8)
+
+
+def _assert_bitwise(a, b):
+    (la, ta), (lb, tb) = a, b
     assert la == lb
     for x, y in zip(ta, tb):
         assert np.array_equal(x, y)
@@ -56,6 +69,7 @@ def test_fused_bitwise_equal_unfused_and_oracle(gpu, k):
     fused = _steps(True, csrs, F, k, ids, w, V, 4)
     unfused = _steps(False, csrs, F, k, ids, w, V, 4)
     _assert_same(fused, unfused)
+    _assert_bitwise(fused, _steps(True, csrs, F, k, ids, w, V, 4))  # reproducible
     model = R.Model.empty(F, k)
     model.load(ids, w, V)
     for t in range(1, 5):
@@ -67,7 +81,7 @@ def test_fused_bitwise_equal_unfused_and_oracle(gpu, k):
 
 def test_fused_absent_rows_and_l1(gpu):
     """Rows absent from the model (singletons and multi rows made present by their update) and a
-    regParam whose soft-threshold zeroes values: fused and unfused agree bit for bit."""
+    regParam whose soft-threshold zeroes values: fused and unfused agree."""
     F, k = 5000, 16
     csrs = [make_problem(760 + i, 800, F, k, 10)[0] for i in range(2)]
     _, ids, w, V = make_problem(72, 1, F, k, 1)

@@ -1,11 +1,10 @@
 #!/bin/bash
-# GPU box: GPU tests (stop at first failure), then the serial kernel profile and a default bench.
+# GPU box: GPU tests (stop at first failure), then a default bench.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -rf --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
 rc=$?; tail -15 gpurun_out/pytest_gpu.log >&2; [ $rc -ne 0 ] && exit $rc
-bash tools/serial_prof.sh || exit $?
 timeout -k 10 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/bench.log 2>&1 || exit $?
 tail -1 gpurun_out/bench.log >&2
 exit 0

@@ -5,7 +5,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 out=gpurun_out/${1:-ab}; reps=${2:-2}
 mkdir -p $out
-timeout -k 10 600 python -u -m pytest tests/test_gpu_fuse.py tests/test_gpu_parity.py -x -q --timeout 120 \
+timeout -k 10 900 python -u -m pytest tests/test_gpu_fuse.py tests/test_gpu_parity.py tests/test_gpu_group.py tests/test_gpu_bench.py -x -q --timeout 120 \
     --timeout-method thread > $out/pytest.log 2>&1
 rc=$?; tail -3 $out/pytest.log >&2; [ $rc -ne 0 ] && exit $rc
 for rep in $(seq 1 $reps); do
