@@ -91,7 +91,7 @@ __device__ __forceinline__ float gauss_draw(uint64_t seed, int64_t id, int f, do
 // singleton: 92 % of a c3 batch's distinct rows) is updated here, by the sample that holds that
 // entry, instead of by the segmented update (see "Singleton rows" below).
 constexpr int kTrain = 0, kPartial = 1, kPredict = 2, kLossGrad = 3, kTrainFused = 4;
-constexpr int kFuseMZ = 40;   // kTrainFused: entries per sample whose singleton rows wait in LDS
+constexpr int kFuseNS = 5;    // kTrainFused: singleton rows per lane group and sample that wait in LDS
 constexpr int kPartialU = 4;  // sharded partial pass: passes (entries per lane) whose rows are in flight together
 // The step's forward (and predict / loss-grad): 32 lanes per sample, 2 passes in flight -- the
 // same 16 rows in flight per sample at k = 16 as 16 lanes x 4 passes, with fewer registers per
@@ -167,27 +167,51 @@ __global__ __launch_bounds__(kBlock) void k_forward(TableView T, const int64_t* 
     Bl = ch_base[xo.ch_R];
   }
 
-  // kTrainFused (kp <= 16): each lane keeps, in LDS, the singleton rows of the entries it gathers
-  // (raw V quad + header + id, slot = the entry's index in its sample) -- no global re-read -- and
-  // after the sample's reduction rewrites them updated in place; their stores are issued after the
-  // next sample's first gathers (so no load waits behind them), the last sample's at the end.
-  // Every slot is read and written by the lane that gathered it: no barrier.
+  // kTrainFused (kp <= 16): each lane group keeps, in LDS, the singleton rows among the entries it
+  // gathers (raw V quads + header with x + id; slot rs + j RPP for its j-th singleton, at most NS
+  // per sample) -- no global re-read -- and after the sample's reduction rewrites them updated in
+  // place.  Their stores go out during the next sample, once its first ids are in and before its
+  // first row gathers, so no gather is queued behind them; the last sample's at the end.  Every
+  // slot is read and written by the lanes of the group that gathered it: no barrier.
   constexpr bool STASH = MODE == kTrainFused;
   static_assert(!STASH || (GS <= 4 && TEAM >= 16), "the fused forward serves kp <= 16");
-  constexpr int MZ = STASH ? kFuseMZ : 1;
+  constexpr int NS = STASH ? kFuseNS : 1;  // singleton rows a lane group keeps per sample
+  constexpr int MZ = STASH ? NS * RPP : 1;
   __shared__ float4 st_v[STASH ? TPB : 1][MZ][STASH ? GS : 1];
   __shared__ float4 st_h[STASH ? TPB : 1][MZ];
   __shared__ uint32_t st_id[STASH ? TPB : 1][MZ];
   const int team = tid / TEAM;
-  int pend = 0;  // slots 0 .. pend - 1 of this team may hold updated rows to store
+  int nst = 0;          // singletons of the current sample met by this lane group
+  int pend = 0;         // updated rows of the previous sample waiting in slots rs + j RPP, j < pend
   const int span = 4 + ((16 - ((kp + 4) & 15)) & 15);  // header + zero pad of its 64-B granule
   auto flush = [&]() {
-    for (int i = rs; i < pend; i += RPP) {
-      const uint32_t sid = st_id[team][i];
-      if (sid == 0xFFFFFFFFu) continue;
-      float* rec = T.v(sid);
-      if (qok) st_row4(rec + 4 * g, st_v[team][i][g]);
-      for (int c = 4 * g; c < span; c += 4 * GS) st_row4(rec + kp + c, c == 0 ? st_h[team][i] : make_float4(0.f, 0.f, 0.f, 0.f));
+    if constexpr (GS >= 2) {
+      // paired: each updated record leaves in ONE store instruction of 2 GS lanes -- the group
+      // writes its row's V, the neighbour group (rs ^ 1) that row's header granule (span <= 4 GS)
+      // -- first the even groups' rows, then the odd groups' (a record written by two half-record
+      // instructions costs more: DESIGN.md §5, paired row stores)
+      const int pp = __shfl_xor(pend, GS);  // the neighbour group's count
+      const bool even = (rs & 1) == 0;
+      const int n = pend > pp ? pend : pp;
+      for (int j = 0; j < n; ++j) {
+#pragma unroll
+        for (int pass = 0; pass < 2; ++pass) {
+          const bool writer = even == (pass == 0);  // this lane writes V of its own group's row
+          const int slot = (writer ? rs : rs ^ 1) + j * RPP;
+          const bool live = j < (writer ? pend : pp);
+          const uint32_t sid = live ? st_id[team][slot] : 0u;
+          float* rec = T.v(sid);
+          const float4 val = writer ? st_v[team][slot][g] : (g == 0 ? st_h[team][slot] : make_float4(0.f, 0.f, 0.f, 0.f));
+          if (live && (writer ? qok : 4 * g < span)) st_row4(writer ? rec + 4 * g : rec + kp + 4 * g, val);
+        }
+      }
+    } else {
+      for (int j = 0; j < pend; ++j) {
+        const int i = rs + j * RPP;
+        float* rec = T.v(st_id[team][i]);
+        if (qok) st_row4(rec + 4 * g, st_v[team][i][g]);
+        for (int c = 4 * g; c < span; c += 4 * GS) st_row4(rec + kp + c, c == 0 ? st_h[team][i] : make_float4(0.f, 0.f, 0.f, 0.f));
+      }
     }
     pend = 0;
   };
@@ -200,9 +224,15 @@ __global__ __launch_bounds__(kBlock) void k_forward(TableView T, const int64_t* 
       s = ch_start[r] + (sl - ch_base[r]);
     }
     const int64_t e0 = row_ptr[s], e1 = row_ptr[s + 1];
+    // the fused update needs the label in every lane after the reduction: its load is issued now,
+    // with the sample's first loads, not behind the reduction
+    const double ys = MODE == kTrainFused ? label[s] : 0.0;
     double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0, vv = 0.0, wx = 0.0;
     uint32_t npres = 0;  // kPredict: learned entries of the sample (this lane's share)
-    if (STASH && e0 + rs >= e1) flush();  // no entry of this sample for the lane: nothing to wait behind
+    if (STASH) {
+      nst = 0;
+      if (e0 + rs >= e1) flush();  // no entry of this sample for the lane group: nothing to wait behind
+    }
     for (int64_t eb = e0 + rs; eb < e1; eb += U * RPP) {
       uint32_t id[U];
       float x[U];
@@ -216,6 +246,7 @@ __global__ __launch_bounds__(kBlock) void k_forward(TableView T, const int64_t* 
         // the batch's x stream (4 B per entry); the partial pass's entries carry x themselves
         x[j] = ok[j] ? (PARTIAL ? __uint_as_float(ent[e].y) : xs[e]) : 0.f;
       }
+      if (STASH && eb == e0 + rs) flush();  // the previous sample's rows: ids in, gathers not yet issued
       RowHdr h[U];
       float4 v[U];
 #pragma unroll
@@ -229,19 +260,22 @@ __global__ __launch_bounds__(kBlock) void k_forward(TableView T, const int64_t* 
           v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
         }
       }
-      if (STASH && eb == e0 + rs) flush();  // the previous sample's rows, behind this sample's first gathers
-      bool sg[U];  // singleton rows (untagged), updated by this sample after its reduction
-#pragma unroll
-      for (int j = 0; j < U; ++j) sg[j] = STASH && ok[j] && !is_multi(h[j].t, xo.sp.epoch);
 #pragma unroll
       for (int j = 0; j < U; ++j) {
-        if (STASH && ok[j] && eb + j * RPP - e0 < MZ) {
-          const int i = (int)(eb + j * RPP - e0);
-          if (sg[j]) {
+        // a singleton row (untagged), updated by this sample after its reduction; the group's
+        // lanes see the same entry, so nst stays uniform across them
+        if (STASH && ok[j] && !is_multi(h[j].t, xo.sp.epoch)) {
+          if (nst < NS) {
+            const int i = rs + nst * RPP;
             st_v[team][i][g] = v[j];
-            if (g == 0) st_h[team][i] = *reinterpret_cast<const float4*>(&h[j]);
+            if (g == 0) {  // the header with the entry's x in place of t (the update rewrites t)
+              RowHdr hx = h[j];
+              hx.t = __float_as_int(x[j]);
+              st_h[team][i] = *reinterpret_cast<const float4*>(&hx);
+              st_id[team][i] = id[j];
+            }
           }
-          if (g == 0) st_id[team][i] = sg[j] ? id[j] : 0xFFFFFFFFu;
+          ++nst;
         }
       }
 #pragma unroll
@@ -326,20 +360,19 @@ __global__ __launch_bounds__(kBlock) void k_forward(TableView T, const int64_t* 
       // read back -- S, r and yhat rounded to fp32 as stored, x from the batch -- with its
       // arithmetic, so the table is bit for bit the unfused step's.  The row was read a moment ago
       // (an L2 hit); the update kernel skips these runs (no row read, no S gather there).
-      const float r32 = (float)(yhat - label[s]), yh32 = (float)yhat;
+      const float r32 = (float)(yhat - ys), yh32 = (float)yhat;
       const double rj = (double)r32, yh = (double)yh32;
       const float4 Sq = make_float4((float)a0, (float)a1, (float)a2, (float)a3);
       const StepParams& sp = xo.sp;
       const float lamf = (float)sp.lam;
       if (STASH) {
-        // the stashed rows (the sample's first MZ entries), updated in place in LDS
-        const int zc = (int)std::min<int64_t>(e1 - e0, MZ);
-        for (int i = rs; i < zc; i += RPP) {
-          const uint32_t sid = st_id[team][i];
-          if (sid == 0xFFFFFFFFu) continue;
+        // the stashed rows (the group's first NS singletons), updated in place in LDS
+        const int zc = nst < NS ? nst : NS;
+        for (int jj = 0; jj < zc; ++jj) {
+          const int i = rs + jj * RPP;
           const float4 hq = st_h[team][i];
           const RowHdr h = *reinterpret_cast<const RowHdr*>(&hq);
-          const double xd = (double)xs[e0 + i];
+          const double xd = (double)__int_as_float(h.t);  // the stash keeps x in the t word
           const float acf = (float)(sp.cumE - h.cum);  // pending L1 of the row
           const double t = xd * rj, b = (xd * xd) * rj;
           const double gwe = (xd - 1.0) * yh + rj;  // x yhat - y (SGD.scala:145)
@@ -361,13 +394,16 @@ __global__ __launch_bounds__(kBlock) void k_forward(TableView T, const int64_t* 
         }
         pend = zc;
       }
-      // entries beyond the stash (samples longer than MZ): the row is read again (nobody else
-      // reads or writes a singleton row in this step) and updated straight away
-      for (int64_t e = e0 + MZ + rs; STASH && e < e1; e += RPP) {
+      // singletons beyond the group's NS (long samples): the group walks its entries again, and
+      // rows past the first NS singletons are read again (nobody else reads or writes a singleton
+      // row in this step) and updated straight away
+      int seen = 0;
+      for (int64_t e = e0 + rs; STASH && nst > NS && e < e1; e += RPP) {
         const uint32_t id = col[e];
         const RowHdr h = *T.hdr(id);
-        const float4 vq = qok ? reinterpret_cast<const float4*>(T.v(id))[g] : make_float4(0.f, 0.f, 0.f, 0.f);
         if (is_multi(h.t, sp.epoch)) continue;
+        if (++seen <= NS) continue;  // stashed
+        const float4 vq = qok ? reinterpret_cast<const float4*>(T.v(id))[g] : make_float4(0.f, 0.f, 0.f, 0.f);
         const double xd = (double)xs[e];
         const float acf = (float)(sp.cumE - h.cum);  // pending L1 of the row
         float* rec = T.v(id);
