@@ -73,9 +73,10 @@ def parse():
                         "caller sees it) instead of device-resident batches; reported, never the headline")
     p.add_argument("--prefetch-depth", type=int, default=2,
                    help="single table: how many steps ahead a batch is sorted (and split) on the side stream")
-    p.add_argument("--fuse", default="on", choices=["on", "off"],
+    p.add_argument("--fuse", default="auto", choices=["auto", "on", "off"],
                    help="single table, k <= 16: the fused step (the forward updates the rows whose feature has one "
-                        "entry in the batch; fm_config.fuse_single); off = every row through the segmented update")
+                        "entry in the batch; fm_config.fuse_single): auto = the library's default (tables larger "
+                        "than the 256-MB Infinity Cache), on, off")
     p.add_argument("--trainer", default="lib", choices=["lib", "torch"],
                    help="N > 1: 'lib' = the multi-GPU fm_ctx, every exchange inside libfm_hip over RCCL (the "
                         "C-ABI path); 'torch' (torch.distributed.run only) = the torch.distributed test harness "
@@ -326,7 +327,8 @@ def main():
     host_trace = None
     xg = None
     if mode == "single":
-        ctx = FMContext(F, k, device=local_rank, seed=20261015, init_sd=INIT_SD, fuse=args.fuse == "on")
+        ctx = FMContext(F, k, device=local_rank, seed=20261015, init_sd=INIT_SD,
+                        fuse={"auto": None, "on": True, "off": False}[args.fuse])
         # launch on a torch stream of our own so torch events can bracket every step on it
         main_stream = torch.cuda.Stream()
         torch.cuda.set_stream(main_stream)
@@ -387,7 +389,7 @@ def main():
                          "what": "fm_step with the host CSR each call: 8 B/entry + row_ptr + fp64 labels over PCIe, "
                                  "device-side explode, then the step (two upload slots, copies overlap the previous step)"}
         U_mean = float(np.mean([uniques[i % len(dbatches)] for i in range(args.steps)]))
-        fused = args.fuse == "on" and (k + 3) // 4 * 4 <= 16 and prefetch
+        fused = "tag" in prof
         single_frac = singleton_fraction([host_batches[i % len(host_batches)] for i in range(args.steps)])
         parallelism = "single table" + (", fused step (singleton rows updated by the forward)" if fused else "") + \
             ((", next batch sorted during the current step" if depth == 1 else

@@ -146,9 +146,14 @@ static Staged stage_csr(fm_ctx* ctx, const fm_csr* c, bool check_range, Pinned& 
 }
 
 // The fused step (fm_kernels.hip "Singleton rows") for batches this context prepares: a
-// single-table context with kp <= 16 unless fm_config.fuse_single says FM_FUSE_OFF.
+// single-table context with kp <= 16; by default (FM_FUSE_DEFAULT) only for a table larger than
+// the 256-MB Infinity Cache, where the update's re-read of the singleton rows goes to HBM -- a
+// cache-resident table re-reads them on-die, and the split and tags would cost more than they save
+// (c2 / c5: 0.245 / 0.273 ms per step fused against 0.184 / 0.208 unfused, profiles/r03_v1).
 static bool fuse_on(const fm_ctx* ctx) {
-  return ctx->cfg.fuse_single != FM_FUSE_OFF && ctx->kp <= 16 && ctx->cfg.shard_count == 1;
+  if (ctx->cfg.fuse_single == FM_FUSE_OFF || ctx->kp > 16 || ctx->cfg.shard_count != 1) return false;
+  const double table_bytes = (double)ctx->rows * ctx->stride * sizeof(float);
+  return ctx->cfg.fuse_single == FM_FUSE_ON || table_bytes > 256.0 * 1024 * 1024;
 }
 
 static bool batch_fits(const fm_batch* b, const Staged& g) {
@@ -219,8 +224,6 @@ void reserve_work(fm_ctx* ctx, int64_t B, int64_t N) {
 }  // namespace fmhip
 
 namespace {
-
-__global__ void k_store_count(const unsigned long long* c, double* dst) { *dst = (double)*c; }
 
 // One fused step.  emit != nullptr (replicated mode, fm_repl_grad): the per-slot gradient sums
 // are written to emit[rows][kp + 4] instead of being applied, and the epoch does not advance.
@@ -906,14 +909,11 @@ int fm_repl_apply(fm_ctx* ctx, const void* grad, int32_t t, double step_size, do
     p.cum_next = p.cumE + p.lam;
     p.w0 = ctx->cfg.w0;
     ctx->ensure_hist(ctx->epoch + 1);
-    ctx->repl_cnt.ensure(sizeof(unsigned long long));
+    ctx->repl_cnt.ensure(sizeof(uint32_t) * kReplApplyBlocks);
     hipEvent_t e0 = ctx->prof_begin(ctx->stream);
-    launch_repl_apply(ctx->view(), reinterpret_cast<const float*>(grad), p, ctx->repl_cnt.as<unsigned long long>(),
-                      ctx->stream);
     double* stats = ctx->loss_hist.as<double>() + 3 * (int64_t)ctx->epoch;
-    hipLaunchKernelGGL(k_store_count, dim3(1), dim3(1), 0, ctx->stream, ctx->repl_cnt.as<unsigned long long>(),
-                       stats + 2);
-    FM_HIP_CHECK(hipGetLastError());
+    launch_repl_apply(ctx->view(), reinterpret_cast<const float*>(grad), p, ctx->repl_cnt.as<uint32_t>(), stats + 2,
+                      ctx->stream);
     ctx->prof_end("apply", e0, ctx->stream);
     ctx->epoch += 1;
     ctx->cum_host.push_back(p.cum_next);

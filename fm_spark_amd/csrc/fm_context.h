@@ -169,10 +169,11 @@ struct fm_ctx {
   DevBuf sh_skey;      // [N] owner-partitioned route keys
   DevBuf sh_ent2;      // [n] uint2 {pair, x bits}: the slot sort's payload
   SortWork side_sort;  // radix sort workspace of the side stream
+  SortWork route_sort;  // the route's owner partition (fm_shard_route; the group's route stream)
   SplitWork split_work;  // fm_batch_prepare's singleton split (side stream)
   Pinned side_pinned;  // route counts (device -> host)
   // replicated step state (fm_repl_*)
-  DevBuf repl_cnt;            // touched-row counter (uint64)
+  DevBuf repl_cnt;            // touched-row counts per apply block (uint32)
   bool repl_pending = false;  // fm_repl_grad ran, fm_repl_apply not yet
 
   TableView view() const {
@@ -275,6 +276,8 @@ struct fm_ctx {
                       &work.sort.keys_a, &work.sort.keys_b, &work.sort.vals_a, &work.sort.vals_b,
                       &work.sort.counts, &work.sort.digit_tot, &side_sort.keys_a, &side_sort.keys_b,
                       &side_sort.vals_a, &side_sort.vals_b, &side_sort.counts, &side_sort.digit_tot,
+                      &route_sort.keys_a, &route_sort.keys_b, &route_sort.vals_a, &route_sort.vals_b,
+                      &route_sort.counts, &route_sort.digit_tot,
                       &sh_okey, &sh_mask, &sh_tcnt, &sh_tot, &sh_pay, &sh_skey, &sh_ent2, &repl_cnt,
                       &split_work.cnt, &split_work.off};
     for (auto* b : bufs) b->release();
@@ -349,7 +352,9 @@ void reserve_work(fm_ctx* ctx, int64_t B, int64_t N);
 
 // the sharded route (fm_shard_route) in two halves, for fm_group.hip: enqueue (counts stay in
 // ctx->sh_tot on the device), then digest the host copy of those counts ([R] pairs, [R] entries)
-void shard_route_launch(fm_ctx* ctx, fm_batch* b, void* send_slot, void* send_ent);
+// (on stream st: the group routes on a stream of its own, so the route does not queue behind the
+// previous batch's owner preparation on the side stream)
+void shard_route_launch(fm_ctx* ctx, fm_batch* b, void* send_slot, void* send_ent, hipStream_t st);
 void shard_route_finish(fm_ctx* ctx, fm_batch* b, const unsigned long long* hc, int64_t* counts);
 // sharded predict building blocks (fm_shard.hip), called by fm_group.hip with the member locked:
 // the owner partial pass with the per-pair count of present rows (Model.scala:103-112 inner

@@ -73,23 +73,28 @@ struct Rank {
   fm_ctx* m = nullptr;  // the member context (owned)
   int device = 0;
   int global = 0;
-  ncclComm_t comm_main = nullptr, comm_side = nullptr, comm_x = nullptr;
+  ncclComm_t comm_main = nullptr, comm_side = nullptr, comm_x = nullptr, comm_route = nullptr;
   hipEvent_t ev_main = nullptr, ev_side = nullptr;  // COPY transport barriers
   DevBuf partials, part_in, s_send, s_recv;           // sharded wire buffers (main stream)
   DevBuf pc_out, pc_in, pred;                         // sharded predict: present counts, scores
   DevBuf grad, gtmp;                                  // replicated gradient buffer
   DevBuf xg_send, xg_recv;                            // counts all-gather (RCCL)
   Pinned xg_pin;
-  // chunked partial exchange of the sharded step (R > 1): its own stream, on the main communicator
+  // chunked partial exchange of the sharded step (R > 1): its own stream and communicator
   hipStream_t xstream = nullptr;
   hipEvent_t ev_x = nullptr, ev_fwd = nullptr, ev_xdone = nullptr;
-  // lanes: 0 main stream, 1 side stream (batch-only work), 2 the exchange stream
-  hipStream_t stream(int lane) const { return lane == 2 ? xstream : lane ? m->side : m->stream; }
-  hipEvent_t event(int lane) const { return lane == 2 ? ev_x : lane ? ev_side : ev_main; }
+  // the sharded route and its counts (batch-only, ahead of the step): a stream of their own
+  hipStream_t rstream = nullptr;
+  hipEvent_t ev_route = nullptr;
+  // lanes: 0 main stream, 1 side stream (batch-only work), 2 the exchange stream, 3 the route stream
+  hipStream_t stream(int lane) const { return lane == 3 ? rstream : lane == 2 ? xstream : lane ? m->side : m->stream; }
+  hipEvent_t event(int lane) const { return lane == 3 ? ev_route : lane == 2 ? ev_x : lane ? ev_side : ev_main; }
   // one communicator per stream, each used in the same order on every rank
-  ncclComm_t comm(int lane) const { return lane == 2 ? comm_x : lane ? comm_side : comm_main; }
+  ncclComm_t comm(int lane) const {
+    return lane == 3 ? comm_route : lane == 2 ? comm_x : lane ? comm_side : comm_main;
+  }
 };
-constexpr int kLaneMain = 0, kLaneSide = 1, kLaneXchg = 2;
+constexpr int kLaneMain = 0, kLaneSide = 1, kLaneXchg = 2, kLaneRoute = 3;
 
 struct GPart {
   fm_batch* b = nullptr;  // the member's batch (owned)
@@ -128,6 +133,7 @@ struct Group {
       if (!r.m) continue;
       (void)hipSetDevice(r.device);
       (void)hipDeviceSynchronize();
+      if (r.comm_route) (void)ncclCommDestroy(r.comm_route);
       if (r.comm_x) (void)ncclCommDestroy(r.comm_x);
       if (r.comm_side) (void)ncclCommDestroy(r.comm_side);
       if (r.comm_main) (void)ncclCommDestroy(r.comm_main);
@@ -136,9 +142,10 @@ struct Group {
         d->release();
       if (r.ev_main) (void)hipEventDestroy(r.ev_main);
       if (r.ev_side) (void)hipEventDestroy(r.ev_side);
-      for (hipEvent_t e : {r.ev_x, r.ev_fwd, r.ev_xdone})
+      for (hipEvent_t e : {r.ev_x, r.ev_fwd, r.ev_xdone, r.ev_route})
         if (e) (void)hipEventDestroy(e);
       if (r.xstream) (void)hipStreamDestroy(r.xstream);
+      if (r.rstream) (void)hipStreamDestroy(r.rstream);
     }
     for (auto& r : ranks)
       if (r.m) fm_destroy(r.m);
@@ -383,21 +390,21 @@ std::vector<unsigned long long> gather_route_counts(Group& g) {
     FM_RCCL_CHECK(ncclGroupStart());
     for (auto& r : g.ranks) {
       FM_HIP_CHECK(hipSetDevice(r.device));
-      FM_RCCL_CHECK(ncclAllGather(r.m->sh_tot.p, r.xg_recv.p, 2 * R, ncclUint64, r.comm_side, r.m->side));
+      FM_RCCL_CHECK(ncclAllGather(r.m->sh_tot.p, r.xg_recv.p, 2 * R, ncclUint64, r.comm_route, r.rstream));
     }
     FM_RCCL_CHECK(ncclGroupEnd());
     FM_HIP_CHECK(hipSetDevice(r0.device));
-    FM_HIP_CHECK(hipMemcpyAsync(r0.xg_pin.p, r0.xg_recv.p, row * R, hipMemcpyDeviceToHost, r0.m->side));
-    FM_HIP_CHECK(hipStreamSynchronize(r0.m->side));
+    FM_HIP_CHECK(hipMemcpyAsync(r0.xg_pin.p, r0.xg_recv.p, row * R, hipMemcpyDeviceToHost, r0.rstream));
+    FM_HIP_CHECK(hipStreamSynchronize(r0.rstream));
   } else {
     for (auto& r : g.ranks) {
       FM_HIP_CHECK(hipSetDevice(r.device));
       FM_HIP_CHECK(hipMemcpyAsync(reinterpret_cast<char*>(r0.xg_pin.p) + row * r.global, r.m->sh_tot.p, row,
-                                  hipMemcpyDeviceToHost, r.m->side));
+                                  hipMemcpyDeviceToHost, r.rstream));
     }
     for (auto& r : g.ranks) {
       FM_HIP_CHECK(hipSetDevice(r.device));
-      FM_HIP_CHECK(hipStreamSynchronize(r.m->side));
+      FM_HIP_CHECK(hipStreamSynchronize(r.rstream));
     }
   }
   const unsigned long long* h = reinterpret_cast<const unsigned long long*>(r0.xg_pin.p);
@@ -417,7 +424,7 @@ void prefetch(Group& g, GroupBatch& gb) {
     GPart& p = gb.parts[l];
     ensure_on(r.device, p.send_slot, sizeof(uint32_t) * p.nnz);
     ensure_on(r.device, p.send_ent, sizeof(uint2) * p.nnz);
-    on(r, [&] { shard_route_launch(r.m, p.b, p.send_slot.p, p.send_ent.p); });
+    on(r, [&] { shard_route_launch(r.m, p.b, p.send_slot.p, p.send_ent.p, r.rstream); });
   }
   const std::vector<unsigned long long> rc = gather_route_counts(g);  // [source][pairs R | entries R]
   std::vector<int64_t> all((size_t)R * 2 * R);                         // [source][entries R | pairs R]
@@ -428,7 +435,12 @@ void prefetch(Group& g, GroupBatch& gb) {
     }
   for (int l = 0; l < L; ++l) {
     Rank& r = g.ranks[l];
-    on(r, [&] { shard_route_finish(r.m, gb.parts[l].b, rc.data() + (size_t)r.global * 2 * R, counts[l].data()); });
+    on(r, [&] {
+      shard_route_finish(r.m, gb.parts[l].b, rc.data() + (size_t)r.global * 2 * R, counts[l].data());
+      // the entry exchange and the owner preparation (side stream) read what the route wrote
+      FM_HIP_CHECK(hipEventRecord(r.ev_route, r.rstream));
+      FM_HIP_CHECK(hipStreamWaitEvent(r.m->side, r.ev_route, 0));
+    });
   }
   std::vector<const char*> ss(L), se(L);
   std::vector<char*> rs(L), re(L);
@@ -809,6 +821,8 @@ int group_create(const fm_config* cfg, fm_ctx** out) {
     FM_HIP_CHECK(hipSetDevice(r.device));
     FM_HIP_CHECK(hipEventCreateWithFlags(&r.ev_main, hipEventDisableTiming));
     FM_HIP_CHECK(hipEventCreateWithFlags(&r.ev_side, hipEventDisableTiming));
+    FM_HIP_CHECK(hipEventCreateWithFlags(&r.ev_route, hipEventDisableTiming));
+    FM_HIP_CHECK(hipStreamCreateWithFlags(&r.rstream, hipStreamNonBlocking));
   }
   for (auto& a : g.ranks)  // peer access between the distinct devices (copies, RCCL's P2P)
     for (auto& b : g.ranks)
@@ -828,7 +842,7 @@ int group_create(const fm_config* cfg, fm_ctx** out) {
       FM_RCCL_CHECK(ncclCommInitRank(&r.comm_main, R, id, r.global));
     }
     FM_RCCL_CHECK(ncclGroupEnd());
-    for (ncclComm_t Rank::*dst : {&Rank::comm_side, &Rank::comm_x}) {
+    for (ncclComm_t Rank::*dst : {&Rank::comm_side, &Rank::comm_x, &Rank::comm_route}) {
       FM_RCCL_CHECK(ncclGroupStart());
       for (auto& r : g.ranks) {
         FM_HIP_CHECK(hipSetDevice(r.device));

@@ -204,9 +204,11 @@ void launch_segment_update(const TableView& T, int64_t N, const SegSource& src, 
                            const uint32_t* skeys, const uint2* sents, int64_t n_loss_blocks, double* stats_out,
                            hipStream_t st, float* emit = nullptr);
 // replicated mode: apply the all-reduced gradient sums grad[rows][kp + 4] to every touched row;
-// the number of touched rows -> *n_touched (device)
-void launch_repl_apply(const TableView& T, const float* grad, const StepParams& p, unsigned long long* n_touched,
-                       hipStream_t st);
+// the number of touched rows -> *n_touched (device, fp64 stats slot), through per-block counts in
+// blk_touched[kReplApplyBlocks]
+constexpr int kReplApplyBlocks = 256 * 16;
+void launch_repl_apply(const TableView& T, const float* grad, const StepParams& p, uint32_t* blk_touched,
+                       double* n_touched, hipStream_t st);
 
 void launch_init_random(const TableView& T, const int32_t* ids, int64_t n, int64_t id_begin,
                         uint64_t seed, double sd, int32_t epoch, double cumE, hipStream_t st);

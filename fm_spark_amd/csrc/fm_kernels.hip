@@ -1045,7 +1045,7 @@ __global__ __launch_bounds__(kBlock) void k_segment_combine(SegArgs a, const dou
 // of SGD.scala:150-181 on touched rows (untouched rows take their L1 lazily, as always).
 template <int G>
 __global__ __launch_bounds__(kBlock) void k_repl_apply(TableView T, const float* __restrict__ grad, StepParams p,
-                                                       unsigned long long* __restrict__ n_touched) {
+                                                       uint32_t* __restrict__ blk_touched) {
   const int g = threadIdx.x % G;
   const int kp = T.kp, nq = kp >> 2, W = kp + 4;
   uint32_t touched = 0;
@@ -1075,10 +1075,33 @@ __global__ __launch_bounds__(kBlock) void k_repl_apply(TableView T, const float*
       store_hdr(T, i, o);
     }
   }
-  // integer count: deterministic
+  // the block's count (one word per block: a same-address atomic per wave serialises ~16K waves)
+  __shared__ uint32_t wt[kBlock / 64];
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) touched += __shfl_xor(touched, o);
-  if ((threadIdx.x & 63) == 0 && touched) atomicAdd(n_touched, (unsigned long long)touched);
+  if ((threadIdx.x & 63) == 0) wt[threadIdx.x >> 6] = touched;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+    for (int w = 0; w < kBlock / 64; ++w) t += wt[w];
+    blk_touched[blockIdx.x] = t;
+  }
+}
+
+// the blocks' counts summed into one fp64 stats slot (one block, fixed order)
+__global__ __launch_bounds__(kBlock) void k_sum_counts(const uint32_t* __restrict__ c, int64_t n, double* __restrict__ out) {
+  __shared__ uint64_t ws[kBlock / 64];
+  uint64_t t = 0;
+  for (int64_t i = threadIdx.x; i < n; i += kBlock) t += c[i];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o);
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = t;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t a = 0;
+    for (int w = 0; w < kBlock / 64; ++w) a += ws[w];
+    *out = (double)a;
+  }
 }
 
 // ---------------------------------------------------------------- table utilities
@@ -1425,20 +1448,23 @@ void launch_table_reset(const TableView& T, hipStream_t st) {
   FM_HIP_CHECK(hipGetLastError());
 }
 
-void launch_repl_apply(const TableView& T, const float* grad, const StepParams& p, unsigned long long* n_touched,
-                       hipStream_t st) {
-  FM_HIP_CHECK(hipMemsetAsync(n_touched, 0, sizeof(unsigned long long), st));
-  if (T.rows <= 0) return;
+void launch_repl_apply(const TableView& T, const float* grad, const StepParams& p, uint32_t* blk_touched,
+                       double* n_touched, hipStream_t st) {
+  if (T.rows <= 0) {
+    FM_HIP_CHECK(hipMemsetAsync(n_touched, 0, sizeof(double), st));
+    return;
+  }
   const int nq = T.kp / 4;
   const int G = nq <= 1 ? 1 : nq <= 2 ? 2 : nq <= 4 ? 4 : nq <= 8 ? 8 : 16;
-  const unsigned grid = grid_for(T.rows * G, kBlock);
+  const unsigned grid = grid_for(T.rows * G, kBlock);  // <= kReplApplyBlocks
   switch (G) {
-    case 1: hipLaunchKernelGGL(k_repl_apply<1>, dim3(grid), dim3(kBlock), 0, st, T, grad, p, n_touched); break;
-    case 2: hipLaunchKernelGGL(k_repl_apply<2>, dim3(grid), dim3(kBlock), 0, st, T, grad, p, n_touched); break;
-    case 4: hipLaunchKernelGGL(k_repl_apply<4>, dim3(grid), dim3(kBlock), 0, st, T, grad, p, n_touched); break;
-    case 8: hipLaunchKernelGGL(k_repl_apply<8>, dim3(grid), dim3(kBlock), 0, st, T, grad, p, n_touched); break;
-    default: hipLaunchKernelGGL(k_repl_apply<16>, dim3(grid), dim3(kBlock), 0, st, T, grad, p, n_touched); break;
+    case 1: hipLaunchKernelGGL(k_repl_apply<1>, dim3(grid), dim3(kBlock), 0, st, T, grad, p, blk_touched); break;
+    case 2: hipLaunchKernelGGL(k_repl_apply<2>, dim3(grid), dim3(kBlock), 0, st, T, grad, p, blk_touched); break;
+    case 4: hipLaunchKernelGGL(k_repl_apply<4>, dim3(grid), dim3(kBlock), 0, st, T, grad, p, blk_touched); break;
+    case 8: hipLaunchKernelGGL(k_repl_apply<8>, dim3(grid), dim3(kBlock), 0, st, T, grad, p, blk_touched); break;
+    default: hipLaunchKernelGGL(k_repl_apply<16>, dim3(grid), dim3(kBlock), 0, st, T, grad, p, blk_touched); break;
   }
+  hipLaunchKernelGGL(k_sum_counts, dim3(1), dim3(kBlock), 0, st, blk_touched, (int64_t)grid, n_touched);
   FM_HIP_CHECK(hipGetLastError());
 }
 

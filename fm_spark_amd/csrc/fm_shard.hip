@@ -449,7 +449,7 @@ extern "C" {
 int fm_shard_route(fm_ctx* ctx, fm_batch* b, void* send_slot, void* send_ent, int64_t* counts) {
   return guarded(ctx, [&]() -> int {
     FM_REQUIRE(counts != nullptr, "bad arguments");
-    shard_route_launch(ctx, b, send_slot, send_ent);
+    shard_route_launch(ctx, b, send_slot, send_ent, ctx->side);
     const int R = ctx->cfg.shard_count;
     ctx->side_pinned.ensure(sizeof(unsigned long long) * 2 * R);
     FM_HIP_CHECK(hipMemcpyAsync(ctx->side_pinned.p, ctx->sh_tot.p, sizeof(unsigned long long) * 2 * R,
@@ -467,14 +467,14 @@ namespace fmhip {
 // Phase 1 enqueued on the side stream, its counts left on the device in ctx->sh_tot ([R] pairs,
 // then [R] entries per owner, uint64): a multi-GPU context gathers every rank's counts on the
 // device and reads them back once for the whole job (fm_group.hip prefetch).
-void shard_route_launch(fm_ctx* ctx, fm_batch* b, void* send_slot, void* send_ent) {
+void shard_route_launch(fm_ctx* ctx, fm_batch* b, void* send_slot, void* send_ent, hipStream_t st) {
   {
     ShardBatchState& S = shard_state(ctx, b);
     const int R = ctx->cfg.shard_count;
     FM_REQUIRE(R <= kMaxR, "the owner-computes sharded step supports at most 64 ranks");
     const int64_t B = b->dev.n_rows, N = b->dev.nnz;
     FM_REQUIRE(N == 0 || (send_slot && send_ent), "null send buffer");
-    hipStream_t st = ctx->side;
+    if (!st) st = ctx->side;
     // the batch's previous iteration may still read its requester state on the main stream
     FM_HIP_CHECK(hipStreamWaitEvent(st, S.last_use, 0));
     hipEvent_t e0 = ctx->prof_begin(st);
@@ -521,7 +521,7 @@ void shard_route_launch(fm_ctx* ctx, fm_batch* b, void* send_slot, void* send_en
                            b->dev.row_ptr.as<int64_t>(), b->dev.col.as<uint32_t>(), b->dev.ent.as<uint2>(), B,
                            (uint32_t)R, sb, F, S.pairidx.as<int32_t>(), ctx->sh_okey.as<uint32_t>(),
                            ctx->sh_pay.as<uint2>());
-        radix_sort_pairs64_bits(ctx->side_sort, ctx->sh_okey.as<uint32_t>(), ctx->sh_pay.as<uint2>(), N, sb, sb + ob, st,
+        radix_sort_pairs64_bits(ctx->route_sort, ctx->sh_okey.as<uint32_t>(), ctx->sh_pay.as<uint2>(), N, sb, sb + ob, st,
                                 ctx->sh_skey.as<uint32_t>(), reinterpret_cast<uint2*>(send_ent));
         hipLaunchKernelGGL(k_key_slots, dim3(blocks_for(N)), dim3(kBlock), 0, st, ctx->sh_skey.as<uint32_t>(), N,
                            (uint32_t)((sb >= 32) ? 0xFFFFFFFFu : ((1u << sb) - 1u)), reinterpret_cast<uint32_t*>(send_slot));

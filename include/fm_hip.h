@@ -47,7 +47,7 @@ extern "C" {
 #define FM_TRANSPORT_RCCL 1      /* RCCL send/recv and all-reduce over xGMI */
 #define FM_TRANSPORT_COPY 2      /* one process only: device-to-device copies between the ranks */
 #define FM_MAX_LOCAL 16
-#define FM_FUSE_DEFAULT 0 /* fm_config.fuse_single: the library's choice (on) */
+#define FM_FUSE_DEFAULT 0 /* fm_config.fuse_single: the library's choice (tables above 256 MB) */
 #define FM_FUSE_ON 1
 #define FM_FUSE_OFF (-1)
 
@@ -75,10 +75,11 @@ typedef struct fm_batch fm_batch;
  *                channel (Spark broadcast, torch.distributed, a file).
  *                RCCL with R > 1 ranks has not run on hardware yet (every test box had one
  *                MI355X): the R > 1 protocol is verified through the COPY transport only.
- * fuse_single  : FM_FUSE_DEFAULT (0) / FM_FUSE_ON: a batch prepared by fm_batch_prepare on a
- *                single-table context with k <= 16 takes the fused step -- the forward updates every
- *                row whose feature has one entry in the batch, the segmented update only the rest
- *                (bit for bit the same table as the unfused step); FM_FUSE_OFF: never.
+ * fuse_single  : FM_FUSE_ON: a batch prepared by fm_batch_prepare on a single-table context with
+ *                k <= 16 takes the fused step -- the forward updates every row whose feature has one
+ *                entry in the batch, the segmented update only the rest (the same table as the
+ *                unfused step within fp64 summation order); FM_FUSE_DEFAULT (0): the same, for tables
+ *                larger than the 256-MB Infinity Cache; FM_FUSE_OFF: never.
  * xchg_chunks  : sharded step with R > 1: the owners' partial pass runs in this many chunks, each
  *                sent while the next is computed (0 = the default, 4; 1 = one pass then one
  *                all-to-all; at most 64).  Every process of a job must pass the same value.

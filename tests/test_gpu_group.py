@@ -197,3 +197,39 @@ def test_group_c3_r8_matches_single_table(gpu):
     np.testing.assert_allclose(pg, pr, rtol=1e-5, atol=1e-7)
     ref.close()
     grp.close()
+
+
+@pytest.mark.parametrize("mode", ["sharded", "replicated"])
+def test_rccl_two_devices_matches_copy(gpu, mode):
+    """The first lease with two GPUs checks RCCL with R > 1 -- grouped ncclSend / ncclRecv on
+    three communicators, the device-side all-gather of the route counts, the chunked partial
+    exchange, the in-place stats all-reduce -- against the COPY transport and the oracle on the
+    same job.  Skipped on a one-GPU box (every box of rounds 1-3 had one MI355X)."""
+    import torch
+
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs two GPUs: RCCL refuses two ranks on one device")
+    F, k = 513, 8
+    _, ids, w, V = make_problem(31, 1, F, k, 1)
+    model = R_.Model.empty(F, k)
+    model.load(ids, w, V)
+    from fm_spark_amd.engine import FMContext
+
+    ctxs = {"rccl": FMContext(F, k, parallel=mode, n_gpus=2, devices=[0, 1], transport="rccl"),
+            "copy": FMContext(F, k, parallel=mode, n_gpus=2, devices=[0, 0], transport="copy")}
+    for c in ctxs.values():
+        c.load_tables(ids, w, V)
+    for t in range(1, 4):
+        p = make_problem(500 + t, 300, F, k, 9, hot=4)[0]
+        outs = {tr: c.step(_host(p), t, 0.3, 1e-4) for tr, c in ctxs.items()}
+        ref = R_.sgd_step_fast(model, p, t, 0.3, 1e-4)
+        for o in outs.values():
+            assert o.loss_sum == pytest.approx(ref.loss_sum, rel=1e-5)
+            assert (o.n_loss_rows, o.n_unique) == (ref.n_loss_rows, ref.n_unique)
+        assert outs["rccl"].loss_sum == pytest.approx(outs["copy"].loss_sum, rel=1e-12)
+    tabs = {tr: c.export_tables() for tr, c in ctxs.items()}
+    for a, b in zip(tabs["rccl"], tabs["copy"]):
+        assert np.array_equal(a, b)  # the same ranks, the same fixed orders: bitwise
+    _check_tables(ctxs["rccl"], model)
+    for c in ctxs.values():
+        c.close()

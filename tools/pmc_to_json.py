@@ -9,9 +9,9 @@ coalesced streams) is tallied at half its bytes (rd80 and stream: exactly 1/2), 
 in full (rd64: 1.03x).  The step kernels' reads are line requests except the update's S-row
 gathers (64 B), so  traffic = 2 * FETCH + WRITE  is exact for k_forward and an upper bound
 for k_segment_update (its S gathers are double counted).  With a 4th argument (a directory of
-the update's ablation passes, tools/abl_pmc.sh: base-FETCH_SIZE.csv and nos-FETCH_SIZE.csv, the
-build with and without the S-row loads) the S gathers' FETCH share is measured and counted once:
-traffic = 2 * (FETCH - S) + S + WRITE for k_segment_update."""
+the update's ablation passes: base-FETCH_SIZE.csv and nos-FETCH_SIZE.csv, a build with and
+without the S-row loads, as round 2 made them) the S gathers' FETCH share is measured and counted
+once: traffic = 2 * (FETCH - S) + S + WRITE for k_segment_update."""
 import csv
 import glob
 import json
