@@ -72,7 +72,8 @@ def parse():
                    help="single table: time fm_step with the host CSR each call (PCIe-inclusive, as a JNI "
                         "caller sees it) instead of device-resident batches; reported, never the headline")
     p.add_argument("--prefetch-depth", type=int, default=2,
-                   help="single table: how many steps ahead a batch is sorted (and split) on the side stream")
+                   help="how many steps ahead a batch is prepared: sorted (and split) on the side stream, or "
+                        "sharded, routed on the route stream")
     p.add_argument("--fuse", default="auto", choices=["auto", "on", "off"],
                    help="single table, k <= 16: the fused step (the forward updates the rows whose feature has one "
                         "entry in the batch; fm_config.fuse_single): auto = the library's default (tables larger "
@@ -439,8 +440,13 @@ def main():
         # critical path
         evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)] if main_stream else None
         h_step, h_prep = [], []  # host time in each call: the GPU never waits on the host if their sum < the step
+        # sharded, fm_batch_prepare is two-phase: it enqueues the batch's route and count gather, and
+        # reads the counts of the batch prepared before it (exchange + owner slot sort on the side
+        # streams); depth 2 gives each route a whole step to finish before the host reads its counts
+        depth = max(1, min(args.prefetch_depth, nb - 1))
         if prefetch:
-            dbatches[0].prepare()
+            for j in range(min(depth, args.steps)):
+                dbatches[j % nb].prepare()
         for i in range(args.steps):
             t += 1
             if evs:
@@ -448,8 +454,8 @@ def main():
             h0 = time.perf_counter()
             ctx.step_batch(dbatches[i % nb], t, STEP_SIZE, REG_PARAM, sync=False)
             h1 = time.perf_counter()
-            if prefetch and i + 1 < args.steps:
-                dbatches[(i + 1) % nb].prepare()
+            if prefetch and i + depth < args.steps:
+                dbatches[(i + depth) % nb].prepare()
                 h_prep.append(time.perf_counter() - h1)
             h_step.append(h1 - h0)
         if evs:
@@ -478,7 +484,7 @@ def main():
                        f"send/recv of entries, partial sums and S rows)" if par == "sharded" else
                        f"replicated x{R}, {who}, per-slot gradient sums all-reduced inside libfm_hip over RCCL")
         if prefetch:
-            parallelism += ", next batch prepared during the current step"
+            parallelism += f", batches prepared {depth} step{'s' if depth > 1 else ''} ahead (route beside the steps)"
         host_trace = {"step_enqueue_ms_median": 1e3 * float(np.median(h_step)),
                       "prepare_ms_median": 1e3 * float(np.median(h_prep)) if h_prep else None,
                       "what": "host time inside fm_step_batch (out = NULL: enqueue only) and fm_batch_prepare of the "

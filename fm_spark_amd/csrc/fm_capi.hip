@@ -593,12 +593,15 @@ int fm_batch_prepare(fm_ctx* ctx, fm_batch* b) {
     const uint2* sv = nullptr;
     b->split = fuse_on(ctx);
     if (b->split) {
-      // sorted in the workspace, then only the runs of two or more entries kept in the batch's view
-      radix_sort_pairs64(ctx->work.sort, b->dev.col.as<uint32_t>(), b->dev.ent.as<uint2>(), N, bits_for(ctx->rows - 1),
-                         ctx->side, &sk, &sv);
+      // only the entries of slots that occur two or more times are sorted into the batch's view
+      SplitWork& sw = ctx->split_work;
+      sw.keys.ensure(sizeof(uint32_t) * N);
+      sw.ents.ensure(sizeof(uint2) * N);
       b->split_n.ensure(2 * sizeof(int64_t));
-      launch_split(sk, sv, N, ctx->split_work, b->skeys.as<uint32_t>(), b->sents.as<uint2>(), b->split_n.as<int64_t>(),
-                   ctx->side);
+      launch_split(b->dev.col.as<uint32_t>(), b->dev.ent.as<uint2>(), N, ctx->rows, sw, sw.keys.as<uint32_t>(),
+                   sw.ents.as<uint2>(), b->split_n.as<int64_t>(), ctx->side);
+      radix_sort_pairs64_dev(ctx->work.sort, sw.keys.as<uint32_t>(), sw.ents.as<uint2>(), N, b->split_n.as<int64_t>(),
+                             bits_for(ctx->rows - 1), ctx->side, b->skeys.as<uint32_t>(), b->sents.as<uint2>());
     } else {
       radix_sort_pairs64(ctx->work.sort, b->dev.col.as<uint32_t>(), b->dev.ent.as<uint2>(), N, bits_for(ctx->rows - 1),
                          ctx->side, &sk, &sv, b->skeys.as<uint32_t>(), b->sents.as<uint2>());

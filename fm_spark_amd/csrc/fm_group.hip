@@ -108,18 +108,19 @@ struct GroupBatch {
   std::vector<GPart> parts;
   int64_t rows = 0, nnz = 0, global_rows = 0;
   bool prefetched = false;  // routed, exchanged and slot-sorted for its next step
-  ~GroupBatch() {
-    for (auto& p : parts) {
-      (void)hipSetDevice(p.device);
-      for (DevBuf* d : {&p.send_slot, &p.send_ent, &p.recv_slot, &p.recv_ent}) d->release();
-      if (p.b) fm_batch_destroy(p.b);
-      p.b = nullptr;
-    }
-  }
+  // sharded prepare, phase 1 done: routes and their count gather enqueued (route streams), the
+  // counts on their way to cnt_pin; phase 2 (the host reads them, exchange, owner preparation)
+  // runs at the context's next fm_batch_prepare or at this batch's step
+  bool routed = false;
+  Pinned cnt_pin;
+  std::vector<hipEvent_t> ev_cnt;  // per local rank: its route-stream work of phase 1 is done
+  Group* g = nullptr;              // the group while this batch is its pending phase 2
+  ~GroupBatch();
 };
 
 struct Group {
   int mode = FM_PARALLEL_SHARDED;
+  GroupBatch* pending = nullptr;  // the batch whose sharded prepare waits for its phase 2
   int L = 0, R = 0, nprocs = 1, prank = 0;
   int xchg = 4;  // chunks of the sharded partial exchange (fm_config.xchg_chunks)
   bool rccl = false;
@@ -128,6 +129,7 @@ struct Group {
   int hnext = 0;
   bool sharded() const { return mode == FM_PARALLEL_SHARDED; }
   ~Group() {
+    if (pending) pending->g = nullptr;
     for (auto& h : host_b) h.reset();
     for (auto& r : ranks) {
       if (!r.m) continue;
@@ -151,6 +153,21 @@ struct Group {
       if (r.m) fm_destroy(r.m);
   }
 };
+
+GroupBatch::~GroupBatch() {
+  if (g && g->pending == this) g->pending = nullptr;
+  for (size_t l = 0; l < ev_cnt.size(); ++l) {
+    (void)hipSetDevice(parts[l].device);
+    (void)hipEventSynchronize(ev_cnt[l]);
+    (void)hipEventDestroy(ev_cnt[l]);
+  }
+  for (auto& p : parts) {
+    (void)hipSetDevice(p.device);
+    for (DevBuf* d : {&p.send_slot, &p.send_ent, &p.recv_slot, &p.recv_ent}) d->release();
+    if (p.b) fm_batch_destroy(p.b);
+    p.b = nullptr;
+  }
+}
 
 void GroupDeleter::operator()(Group* g) const { delete g; }
 void GroupBatchDeleter::operator()(GroupBatch* g) const { delete g; }
@@ -319,6 +336,8 @@ std::vector<int64_t> allgather(Group& g, const std::vector<std::vector<int64_t>>
   return all;
 }
 
+void drop_route(Group& g, GroupBatch& gb);
+
 // Split a host CSR by rows over the local ranks and upload each part into its member batch.
 void upload_parts(Group& g, const fm_csr* c, GroupBatch& gb, bool check_range) {
   FM_REQUIRE(c != nullptr, "null fm_csr");
@@ -331,6 +350,7 @@ void upload_parts(Group& g, const fm_csr* c, GroupBatch& gb, bool check_range) {
   } else {
     FM_REQUIRE(c->nnz == 0, "nnz > 0 with n_rows == 0");
   }
+  drop_route(g, gb);  // a routed plan of the old contents is dropped before its buffers are reused
   gb.parts.resize(g.L);
   gb.rows = B;
   gb.nnz = c->nnz;
@@ -377,14 +397,28 @@ void sync_group_batch_view(fm_batch* b) {  // fm_batch_rows / fm_batch_nnz of th
   b->dev.nnz = b->grp->nnz;
 }
 
-// Every rank's route counts (device, ctx->sh_tot: [R] pairs, [R] entries) -> the host, rank-major
-// [R][2R] in that layout: RCCL all-gathers them on the side streams and one copy comes back; COPY
-// reads each rank's.  One host wait for the whole job, after every rank's route was enqueued.
-std::vector<unsigned long long> gather_route_counts(Group& g) {
-  const int R = g.R;
+// Sharded prepare, phase 1: every local rank's route (fm_shard.hip phase 1) on its route stream,
+// then the job's route counts (ctx->sh_tot: [R] pairs, [R] entries per rank) gathered and copied
+// to the batch's pinned buffer, rank-major [R][2R]: RCCL all-gathers them on the route streams and
+// local rank 0 copies them back, COPY copies each rank's.  Nothing waits on the host.
+void launch_routes(Group& g, GroupBatch& gb) {
+  const int R = g.R, L = g.L;
   const size_t row = sizeof(unsigned long long) * 2 * R;
-  Rank& r0 = g.ranks[0];
-  r0.xg_pin.ensure(row * R);
+  for (int l = 0; l < L; ++l) {
+    Rank& r = g.ranks[l];
+    GPart& p = gb.parts[l];
+    ensure_on(r.device, p.send_slot, sizeof(uint32_t) * p.nnz);
+    ensure_on(r.device, p.send_ent, sizeof(uint2) * p.nnz);
+    on(r, [&] { shard_route_launch(r.m, p.b, p.send_slot.p, p.send_ent.p, r.rstream); });
+  }
+  gb.cnt_pin.ensure(row * R);
+  if ((int)gb.ev_cnt.size() != L) {
+    gb.ev_cnt.assign(L, nullptr);
+    for (int l = 0; l < L; ++l) {
+      FM_HIP_CHECK(hipSetDevice(g.ranks[l].device));
+      FM_HIP_CHECK(hipEventCreateWithFlags(&gb.ev_cnt[l], hipEventDisableTiming));
+    }
+  }
   if (g.rccl) {
     for (auto& r : g.ranks) ensure_on(r.device, r.xg_recv, row * R);
     FM_RCCL_CHECK(ncclGroupStart());
@@ -393,41 +427,49 @@ std::vector<unsigned long long> gather_route_counts(Group& g) {
       FM_RCCL_CHECK(ncclAllGather(r.m->sh_tot.p, r.xg_recv.p, 2 * R, ncclUint64, r.comm_route, r.rstream));
     }
     FM_RCCL_CHECK(ncclGroupEnd());
+    Rank& r0 = g.ranks[0];
     FM_HIP_CHECK(hipSetDevice(r0.device));
-    FM_HIP_CHECK(hipMemcpyAsync(r0.xg_pin.p, r0.xg_recv.p, row * R, hipMemcpyDeviceToHost, r0.rstream));
-    FM_HIP_CHECK(hipStreamSynchronize(r0.rstream));
+    FM_HIP_CHECK(hipMemcpyAsync(gb.cnt_pin.p, r0.xg_recv.p, row * R, hipMemcpyDeviceToHost, r0.rstream));
   } else {
     for (auto& r : g.ranks) {
       FM_HIP_CHECK(hipSetDevice(r.device));
-      FM_HIP_CHECK(hipMemcpyAsync(reinterpret_cast<char*>(r0.xg_pin.p) + row * r.global, r.m->sh_tot.p, row,
+      FM_HIP_CHECK(hipMemcpyAsync(reinterpret_cast<char*>(gb.cnt_pin.p) + row * r.global, r.m->sh_tot.p, row,
                                   hipMemcpyDeviceToHost, r.rstream));
     }
-    for (auto& r : g.ranks) {
-      FM_HIP_CHECK(hipSetDevice(r.device));
-      FM_HIP_CHECK(hipStreamSynchronize(r.rstream));
-    }
   }
-  const unsigned long long* h = reinterpret_cast<const unsigned long long*>(r0.xg_pin.p);
-  return std::vector<unsigned long long>(h, h + (size_t)2 * R * R);
+  for (int l = 0; l < L; ++l) {
+    FM_HIP_CHECK(hipSetDevice(g.ranks[l].device));
+    FM_HIP_CHECK(hipEventRecord(gb.ev_cnt[l], g.ranks[l].rstream));
+  }
+  gb.routed = true;
 }
 
-// The batch-only phases of a sharded iteration (fm_shard.hip phases 1 and 1b): route every part,
-// exchange the counts and the entries, build the owners' pair tables and slot orders.  Side
-// streams; the host waits once, for the job's route counts (they size the exchange), after every
-// local rank's route is enqueued.
-void prefetch(Group& g, GroupBatch& gb) {
-  if (gb.prefetched) return;
-  const int R = g.R, L = g.L;
-  std::vector<std::vector<int64_t>> counts(L, std::vector<int64_t>(2 * R, 0));
-  for (int l = 0; l < L; ++l) {
-    Rank& r = g.ranks[l];
-    GPart& p = gb.parts[l];
-    ensure_on(r.device, p.send_slot, sizeof(uint32_t) * p.nnz);
-    ensure_on(r.device, p.send_ent, sizeof(uint2) * p.nnz);
-    on(r, [&] { shard_route_launch(r.m, p.b, p.send_slot.p, p.send_ent.p, r.rstream); });
+// A routed batch whose plan is dropped (re-uploaded, or routed again for a transform): its route
+// work must be done before its buffers are reused.
+void drop_route(Group& g, GroupBatch& gb) {
+  if (!gb.routed) return;
+  for (size_t l = 0; l < gb.ev_cnt.size(); ++l) {
+    FM_HIP_CHECK(hipSetDevice(g.ranks[l].device));
+    FM_HIP_CHECK(hipEventSynchronize(gb.ev_cnt[l]));
   }
-  const std::vector<unsigned long long> rc = gather_route_counts(g);  // [source][pairs R | entries R]
-  std::vector<int64_t> all((size_t)R * 2 * R);                         // [source][entries R | pairs R]
+  gb.routed = false;
+  if (g.pending == &gb) g.pending = nullptr;
+}
+
+// Sharded prepare, phase 2 (fm_shard.hip phase 1b): the host reads the job's counts (the one host
+// wait, for route work enqueued an iteration earlier), then on the side streams the entry exchange
+// and every owner's pair table and slot order.
+void finish_routes(Group& g, GroupBatch& gb) {
+  const int R = g.R, L = g.L;
+  for (int l = 0; l < L; ++l) {
+    FM_HIP_CHECK(hipSetDevice(g.ranks[l].device));
+    FM_HIP_CHECK(hipEventSynchronize(gb.ev_cnt[l]));
+  }
+  if (g.pending == &gb) g.pending = nullptr;
+  gb.routed = false;
+  const unsigned long long* rc = reinterpret_cast<const unsigned long long*>(gb.cnt_pin.p);  // [source][pairs | entries]
+  std::vector<std::vector<int64_t>> counts(L, std::vector<int64_t>(2 * R, 0));
+  std::vector<int64_t> all((size_t)R * 2 * R);  // [source][entries R | pairs R]
   for (int s = 0; s < R; ++s)
     for (int o = 0; o < R; ++o) {
       all[(size_t)s * 2 * R + o] = (int64_t)rc[(size_t)s * 2 * R + R + o];
@@ -436,7 +478,7 @@ void prefetch(Group& g, GroupBatch& gb) {
   for (int l = 0; l < L; ++l) {
     Rank& r = g.ranks[l];
     on(r, [&] {
-      shard_route_finish(r.m, gb.parts[l].b, rc.data() + (size_t)r.global * 2 * R, counts[l].data());
+      shard_route_finish(r.m, gb.parts[l].b, rc + (size_t)r.global * 2 * R, counts[l].data());
       // the entry exchange and the owner preparation (side stream) read what the route wrote
       FM_HIP_CHECK(hipEventRecord(r.ev_route, r.rstream));
       FM_HIP_CHECK(hipStreamWaitEvent(r.m->side, r.ev_route, 0));
@@ -476,6 +518,14 @@ void prefetch(Group& g, GroupBatch& gb) {
            "fm_shard_owner_prepare");
   }
   gb.prefetched = true;
+}
+
+// The batch-only phases of a sharded iteration, both halves (what the step needs if the caller
+// did not prepare the batch).
+void prefetch(Group& g, GroupBatch& gb) {
+  if (gb.prefetched) return;
+  if (!gb.routed) launch_routes(g, gb);
+  finish_routes(g, gb);
 }
 
 // the pair buffers of one direction in the wire layout: [P][kp] fp32 vectors, then [P][2] fp32
@@ -870,7 +920,14 @@ int group_batch_prepare(fm_ctx* ctx, fm_batch* b) {
   Group& g = grp(ctx);
   GroupBatch& gb = gbatch(ctx, b);
   if (g.sharded()) {
-    prefetch(g, gb);
+    // phase 2 of the batch prepared before this one (its routes ran beside the steps enqueued
+    // since), then phase 1 of this one: the host waits only for route work an iteration old
+    if (g.pending && g.pending != &gb) finish_routes(g, *g.pending);
+    if (!gb.prefetched && !gb.routed) {
+      launch_routes(g, gb);
+      gb.g = &g;
+      g.pending = &gb;
+    }
   } else {
     for (int l = 0; l < g.L; ++l) mcheck(fm_batch_prepare(g.ranks[l].m, gb.parts[l].b), "fm_batch_prepare");
   }

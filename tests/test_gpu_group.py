@@ -79,6 +79,42 @@ def test_group_sharded_step_matches_oracle(gpu, R, k, F, hot, transport):
     ctx.close()
 
 
+@pytest.mark.parametrize("R,transport", [(3, "copy"), (1, "rccl")])
+def test_group_sharded_prepare_two_ahead(gpu, R, transport):
+    """fm_batch_prepare on a sharded group is two-phase: it enqueues the batch's route and count
+    gather, and completes the batch prepared before it.  Batches prepared two steps ahead, a batch
+    prepared twice, a pending batch predicted (its plan completed, then re-routed for the transform)
+    and a pending batch destroyed before its step all leave the oracle steps."""
+    F, k = 600, 8
+    _, ids, w, V = make_problem(5, 1, F, k, 1)
+    ctx = _ctx(F, k, R, transport=transport)
+    ctx.load_tables(ids, w, V)
+    model = R_.Model.empty(F, k)
+    model.load(ids, w, V)
+    probs = [make_problem(90 + i, 120 + 17 * i, F, k, 8, hot=13)[0] for i in range(3)]
+    bs = [ctx.batch(_host(p)) for p in probs]
+    gone = ctx.batch(_host(probs[0]))
+    gone.prepare()
+    gone.close()  # pending when destroyed
+    bs[0].prepare()
+    bs[1].prepare()  # completes bs[0]'s plan, routes bs[1]
+    bs[1].prepare()  # already routed: nothing new
+    refs = []
+    for i in range(6):
+        t = i + 1
+        ctx.step_batch(bs[i % 3], t, 0.3, 1e-4, sync=False)
+        refs.append(R_.sgd_step_fast(model, probs[i % 3], t, 0.3, 1e-4).loss_sum)
+        if i == 3:  # bs[1] is pending here (routed after step 3): a transform completes and redoes it
+            got = ctx.predict_batch(bs[1], 0.0, 1.0)
+            np.testing.assert_allclose(got, R_.predict(model, probs[1], 0.0, 1.0, num_features=F), rtol=1e-5, atol=1e-7)
+        if i + 2 < 6:
+            bs[(i + 2) % 3].prepare()
+    ctx.sync()
+    np.testing.assert_allclose(ctx.loss_history(), refs, rtol=1e-5)
+    _check_tables(ctx, model)
+    ctx.close()
+
+
 @pytest.mark.parametrize("chunks", [1, 3, 16])
 def test_group_sharded_exchange_chunks(gpu, chunks):
     """The owners' partial pass in C chunks whose exchange overlaps the next chunk's compute
