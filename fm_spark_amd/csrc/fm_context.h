@@ -346,6 +346,14 @@ inline int bits_for(int64_t max_value) {
   return b;
 }
 
+// fm_config.sort_filter: group a batch of N entries by the singleton filter (fm_kernels.hip) -- by
+// default when the table has 4 or more rows per entry, where most of a batch's features occur once
+// (c3: 92 % of the distinct rows); a dense batch (c2: 1M rows, 2.5M entries) sorts everything
+inline bool filter_on(const fm_ctx* ctx, int64_t N) {
+  if (ctx->cfg.sort_filter == FM_FILTER_OFF) return false;
+  return ctx->cfg.sort_filter == FM_FILTER_ON || ctx->rows >= 4 * N;
+}
+
 // shared host helpers (fm_capi.hip)
 void upload_batch(fm_ctx* ctx, const fm_csr* c, fm_batch* b, bool check_range);
 void reserve_work(fm_ctx* ctx, int64_t B, int64_t N);

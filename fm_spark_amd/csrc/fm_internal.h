@@ -193,16 +193,19 @@ struct SegSource {
 void launch_segment_update(const TableView& T, const BatchDev& b, StepWork& w, const StepParams& p,
                            const uint32_t* skeys, const uint2* sents, int64_t n_fwd_blocks,
                            double* stats_out, hipStream_t st, float* emit = nullptr, const int64_t* n_dev = nullptr);
-// fm_batch_prepare's singleton filter (fm_kernels.hip "singleton filter"): the entries (CSR order)
-// whose slot occurs two or more times in the batch, in order, into mkeys / ments (capacity N);
-// n_out[0] = their count, n_out[1] = the number of singleton entries (device).  rows: the table's
-// slot count (bitmap size)
+// A batch's grouped view for the segmented update (fm_kernels.hip "singleton filter"): the entries
+// (keys = slots < rows, key_bits wide, CSR order) whose slot occurs two or more times, sorted stably by slot, then
+// -- singles -- the singleton entries in CSR order, into out_keys / out_ents (capacity N).
+// split_n[0] = the multi entries, split_n[1] = the singletons (device; nullptr: the work's own).
+// Without singles (the fused step) the view holds the multi runs only.
 struct SplitWork {
   DevBuf cnt, off, bits;  // bits: [rows / 32] seen, then [rows / 32] seen again
-  DevBuf keys, ents;      // the compacted multi entries, sorted into the batch's view
+  DevBuf keys, ents;      // the compacted multi entries (the sort's input)
+  DevBuf n;               // split_n when the caller keeps none
+  DevBuf vkeys, vents;    // a step's own view when its batch was not prepared
 };
-void launch_split(const uint32_t* keys, const uint2* ents, int64_t N, int64_t rows, SplitWork& sw, uint32_t* mkeys,
-                  uint2* ments, int64_t* n_out, hipStream_t st);
+void grouped_view(SortWork& sort, SplitWork& sw, const uint32_t* keys, const uint2* ents, int64_t N, int64_t rows,
+                  int key_bits, bool singles, uint32_t* out_keys, uint2* out_ents, int64_t* split_n, hipStream_t st);
 // the step's multi tags: every row starting a run of mkeys[0 .. n_dev[0]) (n_max: host bound)
 void launch_tag_multi(const TableView& T, const uint32_t* mkeys, const int64_t* n_dev, int64_t n_max, int32_t epoch,
                       hipStream_t st);

@@ -1564,7 +1564,10 @@ __global__ __launch_bounds__(kBlock) void k_explode(const int64_t* __restrict__ 
 // second bitmap are compacted in CSR order (stable) and only they are sorted.  Compaction: one
 // wave per chunk of 1024 entries counts, one block scans the chunk counts, each wave writes its
 // entries at its offset in order (ballot ranks).  Sorting the compacted list stably gives exactly
-// the multi runs of the full sort.  Integer work only: deterministic.
+// the multi runs of the full sort.  Without the fused forward the singleton entries follow them in
+// CSR order: [multi, sorted | singletons] keeps equal slots contiguous and in CSR order, all the
+// segmented update asks of its view (a singleton is a run of one; no singleton slot equals a multi
+// one).  Integer work only: deterministic.
 constexpr int kSplitChunk = 1024;
 
 __global__ __launch_bounds__(kBlock) void k_mark_repeats(const uint32_t* __restrict__ keys, int64_t N,
@@ -1637,28 +1640,39 @@ __global__ __launch_bounds__(1024) void k_split_scan(const uint2* __restrict__ c
   }
 }
 
+// multi entries -> mkeys / ments[off ..]; singletons (skeys != nullptr) -> skeys / sents[n_out[0] + ..]
 __global__ __launch_bounds__(kBlock) void k_split_scatter(const uint32_t* __restrict__ keys,
                                                           const uint2* __restrict__ ents, int64_t N,
                                                           const uint32_t* __restrict__ multi,
-                                                          const int64_t* __restrict__ off, int64_t nchunks,
-                                                          uint32_t* __restrict__ mkeys, uint2* __restrict__ ments) {
+                                                          const int64_t* __restrict__ off,
+                                                          const int64_t* __restrict__ n_out, int64_t nchunks,
+                                                          uint32_t* __restrict__ mkeys, uint2* __restrict__ ments,
+                                                          uint32_t* __restrict__ skeys, uint2* __restrict__ sents) {
   const int lane = threadIdx.x & 63;
   const int64_t c = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
   if (c >= nchunks) return;  // wave-uniform
   const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
   int64_t o = off[c];
+  int64_t so = skeys ? n_out[0] + c * kSplitChunk - o : 0;  // the singletons before this chunk follow the multi
 #pragma unroll 4
   for (int r = 0; r < kSplitChunk / 64; ++r) {
     const int64_t p = c * kSplitChunk + r * 64 + lane;
-    const uint32_t key = p < N ? keys[p] : 0u;
-    const bool m = p < N && is_repeat(multi, key);
+    const bool in = p < N;
+    const uint32_t key = in ? keys[p] : 0u;
+    const bool m = in && is_repeat(multi, key);
     const uint64_t bm = __ballot(m);
+    const uint64_t bs = __ballot(in && !m);
     if (m) {
       const int64_t d = o + __popcll(bm & lt);
       mkeys[d] = key;
       ments[d] = ents[p];
+    } else if (in && skeys) {
+      const int64_t d = so + __popcll(bs & lt);
+      skeys[d] = key;
+      sents[d] = ents[p];
     }
     o += __popcll(bm);
+    so += __popcll(bs);
   }
 }
 
@@ -1675,8 +1689,8 @@ __global__ __launch_bounds__(kBlock) void k_tag_multi(TableView T, const uint32_
   }
 }
 
-void launch_split(const uint32_t* keys, const uint2* ents, int64_t N, int64_t rows, SplitWork& sw, uint32_t* mkeys,
-                  uint2* ments, int64_t* n_out, hipStream_t st) {
+static void launch_split(const uint32_t* keys, const uint2* ents, int64_t N, int64_t rows, SplitWork& sw,
+                         uint32_t* mkeys, uint2* ments, int64_t* n_out, uint32_t* skeys, uint2* sents, hipStream_t st) {
   const int64_t nchunks = (N + kSplitChunk - 1) / kSplitChunk;
   sw.cnt.ensure(sizeof(uint2) * (size_t)std::max<int64_t>(nchunks, 1));
   sw.off.ensure(sizeof(int64_t) * (size_t)std::max<int64_t>(nchunks, 1));
@@ -1694,8 +1708,26 @@ void launch_split(const uint32_t* keys, const uint2* ents, int64_t N, int64_t ro
   hipLaunchKernelGGL(k_split_count, dim3(blocks), dim3(kBlock), 0, st, keys, N, multi, sw.cnt.as<uint2>(), nchunks);
   hipLaunchKernelGGL(k_split_scan, dim3(1), dim3(1024), 0, st, sw.cnt.as<uint2>(), nchunks, sw.off.as<int64_t>(), n_out);
   hipLaunchKernelGGL(k_split_scatter, dim3(blocks), dim3(kBlock), 0, st, keys, ents, N, multi, sw.off.as<int64_t>(),
-                     nchunks, mkeys, ments);
+                     n_out, nchunks, mkeys, ments, skeys, sents);
   FM_HIP_CHECK(hipGetLastError());
+}
+
+void grouped_view(SortWork& sort, SplitWork& sw, const uint32_t* keys, const uint2* ents, int64_t N, int64_t rows,
+                  int key_bits, bool singles, uint32_t* out_keys, uint2* out_ents, int64_t* split_n, hipStream_t st) {
+  if (!split_n) {
+    sw.n.ensure(2 * sizeof(int64_t));
+    split_n = sw.n.as<int64_t>();
+  }
+  if (N <= 0) {
+    FM_HIP_CHECK(hipMemsetAsync(split_n, 0, 2 * sizeof(int64_t), st));
+    return;
+  }
+  sw.keys.ensure(sizeof(uint32_t) * N);
+  sw.ents.ensure(sizeof(uint2) * N);
+  launch_split(keys, ents, N, rows, sw, sw.keys.as<uint32_t>(), sw.ents.as<uint2>(), split_n,
+               singles ? out_keys : nullptr, singles ? out_ents : nullptr, st);
+  radix_sort_pairs64_dev(sort, sw.keys.as<uint32_t>(), sw.ents.as<uint2>(), N, split_n, key_bits, st, out_keys,
+                         out_ents);
 }
 
 void launch_tag_multi(const TableView& T, const uint32_t* mkeys, const int64_t* n_dev, int64_t n_max, int32_t epoch,
