@@ -74,8 +74,6 @@ def parse():
     p.add_argument("--prefetch-depth", type=int, default=2,
                    help="how many steps ahead a batch is prepared: sorted (and split) on the side stream, or "
                         "sharded, routed on the route stream")
-    p.add_argument("--sort-filter", default="auto", choices=["auto", "on", "off"],
-                   help="fm_config.sort_filter: sort only the repeated features (auto: the library's choice)")
     p.add_argument("--fuse", default="auto", choices=["auto", "on", "off"],
                    help="single table, k <= 16: the fused step (the forward updates the rows whose feature has one "
                         "entry in the batch; fm_config.fuse_single): auto = the library's default (tables larger "
@@ -331,8 +329,7 @@ def main():
     xg = None
     if mode == "single":
         ctx = FMContext(F, k, device=local_rank, seed=20261015, init_sd=INIT_SD,
-                        fuse={"auto": None, "on": True, "off": False}[args.fuse],
-                        sort_filter={"auto": None, "on": True, "off": False}[args.sort_filter])
+                        fuse={"auto": None, "on": True, "off": False}[args.fuse])
         # launch on a torch stream of our own so torch events can bracket every step on it
         main_stream = torch.cuda.Stream()
         torch.cuda.set_stream(main_stream)
@@ -414,8 +411,7 @@ def main():
             dist.broadcast(idt, src=0)
             cid = bytes(idt.tolist())
         ctx = FMContext(F, k, seed=20261015, init_sd=INIT_SD, parallel=par, n_gpus=L, devices=pl["devices"],
-                        transport="rccl", n_procs=world if mode == "procs" else 1, proc_rank=rank, comm_id=cid,
-                        sort_filter={"auto": None, "on": True, "off": False}[args.sort_filter])
+                        transport="rccl", n_procs=world if mode == "procs" else 1, proc_rank=rank, comm_id=cid)
         main_stream = None
         if L == 1:  # launch on a torch stream so torch events time each step on it
             main_stream = torch.cuda.Stream()

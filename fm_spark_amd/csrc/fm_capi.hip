@@ -266,18 +266,8 @@ int step_impl(fm_ctx* ctx, fm_batch* b, int32_t t, double step_size, double reg_
     FM_HIP_CHECK(hipEventRecord(ctx->ev_fork, ctx->stream));
     FM_HIP_CHECK(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
     hipEvent_t es = ctx->prof_begin(ctx->side);
-    if (filter_on(ctx, N)) {
-      SplitWork& sw = ctx->split_work;
-      sw.vkeys.ensure(sizeof(uint32_t) * N);
-      sw.vents.ensure(sizeof(uint2) * N);
-      grouped_view(ctx->work.sort, sw, b->dev.col.as<uint32_t>(), b->dev.ent.as<uint2>(), N, ctx->rows,
-                   bits_for(ctx->rows - 1), true, sw.vkeys.as<uint32_t>(), sw.vents.as<uint2>(), nullptr, ctx->side);
-      skeys = sw.vkeys.as<uint32_t>();
-      sents = sw.vents.as<uint2>();
-    } else {
-      radix_sort_pairs64(ctx->work.sort, b->dev.col.as<uint32_t>(), b->dev.ent.as<uint2>(), N,
-                         bits_for(ctx->rows - 1), ctx->side, &skeys, &sents);
-    }
+    radix_sort_pairs64(ctx->work.sort, b->dev.col.as<uint32_t>(), b->dev.ent.as<uint2>(), N,
+                       bits_for(ctx->rows - 1), ctx->side, &skeys, &sents);
     ctx->prof_end("sort", es, ctx->side);
     FM_HIP_CHECK(hipEventRecord(ctx->ev_join, ctx->side));
   }
@@ -340,9 +330,6 @@ int fm_create(const fm_config* cfg, fm_ctx** out) {
     FM_REQUIRE(cfg->init_sd >= 0.0, "init_sd must be >= 0");
     FM_REQUIRE(cfg->fuse_single == FM_FUSE_DEFAULT || cfg->fuse_single == FM_FUSE_ON || cfg->fuse_single == FM_FUSE_OFF,
                "fuse_single must be FM_FUSE_DEFAULT, FM_FUSE_ON or FM_FUSE_OFF");
-    FM_REQUIRE(cfg->sort_filter == FM_FILTER_DEFAULT || cfg->sort_filter == FM_FILTER_ON ||
-                   cfg->sort_filter == FM_FILTER_OFF,
-               "sort_filter must be FM_FILTER_DEFAULT, FM_FILTER_ON or FM_FILTER_OFF");
     int ndev = 0;
     FM_HIP_CHECK(hipGetDeviceCount(&ndev));
     FM_REQUIRE(cfg->device >= 0 && cfg->device < ndev, "device ordinal out of range");
@@ -605,13 +592,13 @@ int fm_batch_prepare(fm_ctx* ctx, fm_batch* b) {
     const uint32_t* sk = nullptr;
     const uint2* sv = nullptr;
     b->split = fuse_on(ctx);
-    if (b->split || filter_on(ctx, N)) {
-      // only the entries of slots that occur two or more times are sorted; the view holds them and
-      // then (unless fused: the forward updates those rows) the singleton entries in CSR order
-      if (b->split) b->split_n.ensure(2 * sizeof(int64_t));
-      grouped_view(ctx->work.sort, ctx->split_work, b->dev.col.as<uint32_t>(), b->dev.ent.as<uint2>(), N, ctx->rows,
-                   bits_for(ctx->rows - 1), !b->split, b->skeys.as<uint32_t>(), b->sents.as<uint2>(),
-                   b->split ? b->split_n.as<int64_t>() : nullptr, ctx->side);
+    if (b->split) {
+      // sorted in the workspace, then only the runs of two or more entries kept in the batch's view
+      radix_sort_pairs64(ctx->work.sort, b->dev.col.as<uint32_t>(), b->dev.ent.as<uint2>(), N, bits_for(ctx->rows - 1),
+                         ctx->side, &sk, &sv);
+      b->split_n.ensure(2 * sizeof(int64_t));
+      launch_split(sk, sv, N, ctx->split_work, b->skeys.as<uint32_t>(), b->sents.as<uint2>(), b->split_n.as<int64_t>(),
+                   ctx->side);
     } else {
       radix_sort_pairs64(ctx->work.sort, b->dev.col.as<uint32_t>(), b->dev.ent.as<uint2>(), N, bits_for(ctx->rows - 1),
                          ctx->side, &sk, &sv, b->skeys.as<uint32_t>(), b->sents.as<uint2>());

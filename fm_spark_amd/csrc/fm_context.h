@@ -170,7 +170,7 @@ struct fm_ctx {
   DevBuf sh_ent2;      // [n] uint2 {pair, x bits}: the slot sort's payload
   SortWork side_sort;  // radix sort workspace of the side stream
   SortWork route_sort;  // the route's owner partition (fm_shard_route; the group's route stream)
-  SplitWork split_work;  // fm_batch_prepare's singleton filter (side stream)
+  SplitWork split_work;  // fm_batch_prepare's singleton split (side stream)
   Pinned side_pinned;  // route counts (device -> host)
   // replicated step state (fm_repl_*)
   DevBuf repl_cnt;            // touched-row counts per apply block (uint32)
@@ -279,7 +279,7 @@ struct fm_ctx {
                       &route_sort.keys_a, &route_sort.keys_b, &route_sort.vals_a, &route_sort.vals_b,
                       &route_sort.counts, &route_sort.digit_tot,
                       &sh_okey, &sh_mask, &sh_tcnt, &sh_tot, &sh_pay, &sh_skey, &sh_ent2, &repl_cnt,
-                      &split_work.cnt, &split_work.off, &split_work.bits, &split_work.keys, &split_work.ents};
+                      &split_work.cnt, &split_work.off};
     for (auto* b : bufs) b->release();
     if (own_stream && stream) (void)hipStreamDestroy(stream);
   }
@@ -344,14 +344,6 @@ inline int bits_for(int64_t max_value) {
   int b = 1;
   while (b < 63 && (int64_t(1) << b) <= max_value) ++b;
   return b;
-}
-
-// fm_config.sort_filter: group a batch of N entries by the singleton filter (fm_kernels.hip) -- by
-// default when the table has 4 or more rows per entry, where most of a batch's features occur once
-// (c3: 92 % of the distinct rows); a dense batch (c2: 1M rows, 2.5M entries) sorts everything
-inline bool filter_on(const fm_ctx* ctx, int64_t N) {
-  if (ctx->cfg.sort_filter == FM_FILTER_OFF) return false;
-  return ctx->cfg.sort_filter == FM_FILTER_ON || ctx->rows >= 4 * N;
 }
 
 // shared host helpers (fm_capi.hip)

@@ -104,10 +104,6 @@ void radix_sort_pairs64(SortWork& w, const uint32_t* keys_in, const uint2* vals_
 // final_keys / final_vals.
 void radix_sort_pairs64_bits(SortWork& w, const uint32_t* keys_in, const uint2* vals_in, int64_t n, int lo_bit,
                              int hi_bit, hipStream_t st, uint32_t* final_keys, uint2* final_vals);
-// Same, the key count on the device: n_dev[0] <= n_max keys (the grids are sized for n_max)
-void radix_sort_pairs64_dev(SortWork& w, const uint32_t* keys_in, const uint2* vals_in, int64_t n_max,
-                            const int64_t* n_dev, int key_bits, hipStream_t st, uint32_t* final_keys,
-                            uint2* final_vals);
 
 // ---------------------------------------------------------------- step kernels
 // A device-resident mini-batch: the exploded (sampleId, featureId, featureValue) rows of
@@ -193,19 +189,14 @@ struct SegSource {
 void launch_segment_update(const TableView& T, const BatchDev& b, StepWork& w, const StepParams& p,
                            const uint32_t* skeys, const uint2* sents, int64_t n_fwd_blocks,
                            double* stats_out, hipStream_t st, float* emit = nullptr, const int64_t* n_dev = nullptr);
-// A batch's grouped view for the segmented update (fm_kernels.hip "singleton filter"): the entries
-// (keys = slots < rows, key_bits wide, CSR order) whose slot occurs two or more times, sorted stably by slot, then
-// -- singles -- the singleton entries in CSR order, into out_keys / out_ents (capacity N).
-// split_n[0] = the multi entries, split_n[1] = the singletons (device; nullptr: the work's own).
-// Without singles (the fused step) the view holds the multi runs only.
+// fm_batch_prepare's singleton split of a sorted view (fm_kernels.hip "Singleton rows"): the entries
+// of runs of two or more, in order, into mkeys / ments (capacity N); n_out[0] = their count,
+// n_out[1] = the number of singleton runs (device)
 struct SplitWork {
-  DevBuf cnt, off, bits;  // bits: [rows / 32] seen, then [rows / 32] seen again
-  DevBuf keys, ents;      // the compacted multi entries (the sort's input)
-  DevBuf n;               // split_n when the caller keeps none
-  DevBuf vkeys, vents;    // a step's own view when its batch was not prepared
+  DevBuf cnt, off;
 };
-void grouped_view(SortWork& sort, SplitWork& sw, const uint32_t* keys, const uint2* ents, int64_t N, int64_t rows,
-                  int key_bits, bool singles, uint32_t* out_keys, uint2* out_ents, int64_t* split_n, hipStream_t st);
+void launch_split(const uint32_t* skeys, const uint2* sents, int64_t N, SplitWork& sw, uint32_t* mkeys, uint2* ments,
+                  int64_t* n_out, hipStream_t st);
 // the step's multi tags: every row starting a run of mkeys[0 .. n_dev[0]) (n_max: host bound)
 void launch_tag_multi(const TableView& T, const uint32_t* mkeys, const int64_t* n_dev, int64_t n_max, int32_t epoch,
                       hipStream_t st);

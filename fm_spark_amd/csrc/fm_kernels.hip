@@ -99,9 +99,8 @@ constexpr int kPartialU = 4;  // sharded partial pass: passes (entries per lane)
 constexpr int kFwdTeam = 32, kFwdU = 2;
 constexpr int kFwdGrid = 2048;  // forward blocks at most (grid-stride over samples beyond)
 
-// Singleton rows.  fm_batch_prepare keeps only the entries of slots that occur two or more times
-// (the only ones that need a per-feature reduction; "singleton filter": k_mark_repeats, k_split_*)
-// and sorts just those into the batch's view; the singletons are counted.  At the
+// Singleton rows.  fm_batch_prepare splits the batch's sorted view into the runs of two or more
+// entries (the only ones that need a per-feature reduction; k_split_*) and the singletons.  At the
 // start of the step k_tag_multi marks every row with two or more entries in the row header's t
 // field, the word that otherwise only says present (t >= 0) or absent (t = -1):
 //   present, multi at epoch E : t = kTagPresent + (E & kTagMask)   (>= 2^30; normal t < 2^30)
@@ -483,7 +482,7 @@ struct SegArgs {
   uint32_t* ucnt;  // [update blocks]
   float* emit;     // replicated mode: per-slot gradient sums [rows][kp + 4] instead of the update
   // non-null: the entry count is n_dev[0] <= N (a prepared batch's multi runs, counted on the
-  // device by the singleton filter), and n_dev[1] distinct singleton rows were updated by the forward
+  // device by k_split_*), and n_dev[1] distinct singleton rows were updated by the forward
   const int64_t* n_dev;
 };
 
@@ -1557,53 +1556,41 @@ __global__ __launch_bounds__(kBlock) void k_explode(const int64_t* __restrict__ 
   }
 }
 
-// ------------------------------------------------------- singleton filter (fm_batch_prepare)
-// Before the sort: one pass over the batch's slots marks every slot seen in a bitmap and every slot
-// seen again in a second one (one returning atomic OR per entry, a second only for a repeat; the
-// bitmaps, F / 8 bytes each, stay in the Infinity Cache), then the entries whose slot is in the
-// second bitmap are compacted in CSR order (stable) and only they are sorted.  Compaction: one
-// wave per chunk of 1024 entries counts, one block scans the chunk counts, each wave writes its
-// entries at its offset in order (ballot ranks).  Sorting the compacted list stably gives exactly
-// the multi runs of the full sort.  Without the fused forward the singleton entries follow them in
-// CSR order: [multi, sorted | singletons] keeps equal slots contiguous and in CSR order, all the
-// segmented update asks of its view (a singleton is a run of one; no singleton slot equals a multi
-// one).  Integer work only: deterministic.
+// ------------------------------------------------------- singleton split (fm_batch_prepare)
+// The sorted view of a batch -> the entries of its runs of two or more (stable: the order the
+// segmented update needs) and the number of singleton runs.  One wave per chunk of 1024 sorted
+// entries: count, one-block scan of the chunk counts, then each wave writes its multi entries at
+// its offset in order (ballot ranks).  Integer work only: deterministic.
 constexpr int kSplitChunk = 1024;
 
-__global__ __launch_bounds__(kBlock) void k_mark_repeats(const uint32_t* __restrict__ keys, int64_t N,
-                                                         uint32_t* __restrict__ seen, uint32_t* __restrict__ multi) {
-  for (int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x; p < N; p += (int64_t)gridDim.x * kBlock) {
-    const uint32_t s = keys[p];
-    const uint32_t bit = 1u << (s & 31u);
-    const uint32_t old = atomicOr(&seen[s >> 5], bit);
-    if (old & bit) atomicOr(&multi[s >> 5], bit);
-  }
+__device__ __forceinline__ bool split_multi(const uint32_t* __restrict__ skeys, int64_t N, int64_t p, uint32_t key,
+                                            int lane) {
+  uint32_t prev = __shfl_up(key, 1), next = __shfl_down(key, 1);
+  if (lane == 0) prev = p > 0 && p <= N ? skeys[p - 1] : 0xFFFFFFFFu;
+  if (lane == 63) next = p + 1 < N ? skeys[p + 1] : 0xFFFFFFFFu;
+  if (p == 0) prev = 0xFFFFFFFFu;      // (lane 0 only)
+  if (p + 1 >= N) next = 0xFFFFFFFFu;  // the last entry has no successor
+  return p < N && (prev == key || next == key);
 }
 
-__device__ __forceinline__ bool is_repeat(const uint32_t* __restrict__ multi, uint32_t s) {
-  return (multi[s >> 5] >> (s & 31u)) & 1u;
-}
-
-__global__ __launch_bounds__(kBlock) void k_split_count(const uint32_t* __restrict__ keys, int64_t N,
-                                                        const uint32_t* __restrict__ multi, uint2* __restrict__ cnt,
-                                                        int64_t nchunks) {
+__global__ __launch_bounds__(kBlock) void k_split_count(const uint32_t* __restrict__ skeys, int64_t N,
+                                                        uint2* __restrict__ cnt, int64_t nchunks) {
   const int lane = threadIdx.x & 63;
   const int64_t c = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
   if (c >= nchunks) return;  // wave-uniform
   uint32_t nm = 0, ns = 0;
-#pragma unroll 4
   for (int r = 0; r < kSplitChunk / 64; ++r) {
     const int64_t p = c * kSplitChunk + r * 64 + lane;
-    const bool in = p < N;
-    const bool m = in && is_repeat(multi, keys[p]);
+    const uint32_t key = p < N ? skeys[p] : 0xFFFFFFFEu;
+    const bool m = split_multi(skeys, N, p, key, lane);
     nm += (uint32_t)__popcll(__ballot(m));
-    ns += (uint32_t)__popcll(__ballot(in && !m));
+    ns += (uint32_t)__popcll(__ballot(p < N && !m));
   }
   if (lane == 0) cnt[c] = make_uint2(nm, ns);
 }
 
 // one block: exclusive scan of the chunks' multi counts -> off[c]; totals -> n_out[0] (multi
-// entries), n_out[1] (singleton entries = singleton rows)
+// entries), n_out[1] (singleton runs)
 __global__ __launch_bounds__(1024) void k_split_scan(const uint2* __restrict__ cnt, int64_t nchunks,
                                                      int64_t* __restrict__ off, int64_t* __restrict__ n_out) {
   __shared__ int64_t wsum[16], ssum[16];
@@ -1640,39 +1627,26 @@ __global__ __launch_bounds__(1024) void k_split_scan(const uint2* __restrict__ c
   }
 }
 
-// multi entries -> mkeys / ments[off ..]; singletons (skeys != nullptr) -> skeys / sents[n_out[0] + ..]
-__global__ __launch_bounds__(kBlock) void k_split_scatter(const uint32_t* __restrict__ keys,
-                                                          const uint2* __restrict__ ents, int64_t N,
-                                                          const uint32_t* __restrict__ multi,
-                                                          const int64_t* __restrict__ off,
-                                                          const int64_t* __restrict__ n_out, int64_t nchunks,
-                                                          uint32_t* __restrict__ mkeys, uint2* __restrict__ ments,
-                                                          uint32_t* __restrict__ skeys, uint2* __restrict__ sents) {
+__global__ __launch_bounds__(kBlock) void k_split_scatter(const uint32_t* __restrict__ skeys,
+                                                          const uint2* __restrict__ sents, int64_t N,
+                                                          const int64_t* __restrict__ off, int64_t nchunks,
+                                                          uint32_t* __restrict__ mkeys, uint2* __restrict__ ments) {
   const int lane = threadIdx.x & 63;
   const int64_t c = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
   if (c >= nchunks) return;  // wave-uniform
   const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
   int64_t o = off[c];
-  int64_t so = skeys ? n_out[0] + c * kSplitChunk - o : 0;  // the singletons before this chunk follow the multi
-#pragma unroll 4
   for (int r = 0; r < kSplitChunk / 64; ++r) {
     const int64_t p = c * kSplitChunk + r * 64 + lane;
-    const bool in = p < N;
-    const uint32_t key = in ? keys[p] : 0u;
-    const bool m = in && is_repeat(multi, key);
+    const uint32_t key = p < N ? skeys[p] : 0xFFFFFFFEu;
+    const bool m = split_multi(skeys, N, p, key, lane);
     const uint64_t bm = __ballot(m);
-    const uint64_t bs = __ballot(in && !m);
     if (m) {
       const int64_t d = o + __popcll(bm & lt);
       mkeys[d] = key;
-      ments[d] = ents[p];
-    } else if (in && skeys) {
-      const int64_t d = so + __popcll(bs & lt);
-      skeys[d] = key;
-      sents[d] = ents[p];
+      ments[d] = sents[p];
     }
     o += __popcll(bm);
-    so += __popcll(bs);
   }
 }
 
@@ -1689,8 +1663,8 @@ __global__ __launch_bounds__(kBlock) void k_tag_multi(TableView T, const uint32_
   }
 }
 
-static void launch_split(const uint32_t* keys, const uint2* ents, int64_t N, int64_t rows, SplitWork& sw,
-                         uint32_t* mkeys, uint2* ments, int64_t* n_out, uint32_t* skeys, uint2* sents, hipStream_t st) {
+void launch_split(const uint32_t* skeys, const uint2* sents, int64_t N, SplitWork& sw, uint32_t* mkeys, uint2* ments,
+                  int64_t* n_out, hipStream_t st) {
   const int64_t nchunks = (N + kSplitChunk - 1) / kSplitChunk;
   sw.cnt.ensure(sizeof(uint2) * (size_t)std::max<int64_t>(nchunks, 1));
   sw.off.ensure(sizeof(int64_t) * (size_t)std::max<int64_t>(nchunks, 1));
@@ -1698,36 +1672,12 @@ static void launch_split(const uint32_t* keys, const uint2* ents, int64_t N, int
     FM_HIP_CHECK(hipMemsetAsync(n_out, 0, 2 * sizeof(int64_t), st));
     return;
   }
-  const int64_t words = (rows + 31) / 32;
-  sw.bits.ensure(sizeof(uint32_t) * 2 * (size_t)words);
-  uint32_t* seen = sw.bits.as<uint32_t>();
-  uint32_t* multi = seen + words;
-  FM_HIP_CHECK(hipMemsetAsync(seen, 0, sizeof(uint32_t) * 2 * (size_t)words, st));
-  hipLaunchKernelGGL(k_mark_repeats, dim3(grid_for(N, kBlock, 256 * 16)), dim3(kBlock), 0, st, keys, N, seen, multi);
   const unsigned blocks = (unsigned)((nchunks + kBlock / 64 - 1) / (kBlock / 64));
-  hipLaunchKernelGGL(k_split_count, dim3(blocks), dim3(kBlock), 0, st, keys, N, multi, sw.cnt.as<uint2>(), nchunks);
+  hipLaunchKernelGGL(k_split_count, dim3(blocks), dim3(kBlock), 0, st, skeys, N, sw.cnt.as<uint2>(), nchunks);
   hipLaunchKernelGGL(k_split_scan, dim3(1), dim3(1024), 0, st, sw.cnt.as<uint2>(), nchunks, sw.off.as<int64_t>(), n_out);
-  hipLaunchKernelGGL(k_split_scatter, dim3(blocks), dim3(kBlock), 0, st, keys, ents, N, multi, sw.off.as<int64_t>(),
-                     n_out, nchunks, mkeys, ments, skeys, sents);
+  hipLaunchKernelGGL(k_split_scatter, dim3(blocks), dim3(kBlock), 0, st, skeys, sents, N, sw.off.as<int64_t>(), nchunks,
+                     mkeys, ments);
   FM_HIP_CHECK(hipGetLastError());
-}
-
-void grouped_view(SortWork& sort, SplitWork& sw, const uint32_t* keys, const uint2* ents, int64_t N, int64_t rows,
-                  int key_bits, bool singles, uint32_t* out_keys, uint2* out_ents, int64_t* split_n, hipStream_t st) {
-  if (!split_n) {
-    sw.n.ensure(2 * sizeof(int64_t));
-    split_n = sw.n.as<int64_t>();
-  }
-  if (N <= 0) {
-    FM_HIP_CHECK(hipMemsetAsync(split_n, 0, 2 * sizeof(int64_t), st));
-    return;
-  }
-  sw.keys.ensure(sizeof(uint32_t) * N);
-  sw.ents.ensure(sizeof(uint2) * N);
-  launch_split(keys, ents, N, rows, sw, sw.keys.as<uint32_t>(), sw.ents.as<uint2>(), split_n,
-               singles ? out_keys : nullptr, singles ? out_ents : nullptr, st);
-  radix_sort_pairs64_dev(sort, sw.keys.as<uint32_t>(), sw.ents.as<uint2>(), N, split_n, key_bits, st, out_keys,
-                         out_ents);
 }
 
 void launch_tag_multi(const TableView& T, const uint32_t* mkeys, const int64_t* n_dev, int64_t n_max, int32_t epoch,

@@ -599,20 +599,14 @@ int fm_shard_owner_prepare(fm_ctx* ctx, fm_batch* b, const void* recv_slot, cons
     }
     FM_HIP_CHECK(hipEventRecord(S.ready_fwd, st));
     if (n > 0) {
-      // the update's grouping: received entries grouped by slot (stable: source rank, then CSR order)
+      // the update's grouping: received entries sorted by slot (stable: source rank, then CSR order)
       S.skeys.ensure(sizeof(uint32_t) * n);
       S.sents.ensure(sizeof(uint2) * n);
       const uint32_t* sk = nullptr;
       const uint2* sv = nullptr;
-      const int kb = bits_for(std::max<int64_t>(ctx->rows - 1, 1));
-      if (filter_on(ctx, n)) {  // [repeated slots sorted | singleton slots in arrival order]
-        grouped_view(ctx->side_sort, ctx->split_work, reinterpret_cast<const uint32_t*>(recv_slot),
-                     ctx->sh_ent2.as<uint2>(), n, ctx->rows, kb, true, S.skeys.as<uint32_t>(), S.sents.as<uint2>(),
-                     nullptr, st);
-      } else {
-        radix_sort_pairs64(ctx->side_sort, reinterpret_cast<const uint32_t*>(recv_slot), ctx->sh_ent2.as<uint2>(), n,
-                           kb, st, &sk, &sv, S.skeys.as<uint32_t>(), S.sents.as<uint2>());
-      }
+      radix_sort_pairs64(ctx->side_sort, reinterpret_cast<const uint32_t*>(recv_slot), ctx->sh_ent2.as<uint2>(), n,
+                         bits_for(std::max<int64_t>(ctx->rows - 1, 1)), st, &sk, &sv, S.skeys.as<uint32_t>(),
+                         S.sents.as<uint2>());
     }
     FM_HIP_CHECK(hipEventRecord(S.ready_upd, st));
     ctx->prof_end("owner_prepare", e0, st);

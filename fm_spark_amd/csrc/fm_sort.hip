@@ -34,18 +34,10 @@ constexpr int kMaxRadix = 1 << kMaxRB;
 // contiguous, so a digit's runs written by neighbouring tiles meet in the same L2 and leave it as
 // whole 64-B granules (a partly written granule costs a read-modify-write in HBM;
 // tools/traffic_cal.hip), and a digit row's line of per-tile counts is written by one L2.
-// A grid sized for more tiles than the pass has (a device-side count, below) leaves the blocks
-// past an XCD's group idle: tile -1.
 __device__ __forceinline__ int64_t tile_of_block(int64_t ntiles) {
   const int64_t per = (ntiles + 7) / 8;
-  const int64_t j = blockIdx.x / 8;
-  return j < per ? (int64_t)(blockIdx.x % 8) * per + j : -1;
+  return (int64_t)(blockIdx.x % 8) * per + blockIdx.x / 8;
 }
-
-// The pass's key count: the host's n, or n_dev[0] <= n when the count is known on the device only
-// (fm_batch_prepare's multi entries); every kernel derives the same tile count from it.
-__device__ __forceinline__ int64_t pass_n(int64_t n, const int64_t* n_dev) { return n_dev ? n_dev[0] : n; }
-inline int64_t tiles_of(int64_t n) { return (n + kTile - 1) / kTile; }
 
 inline int64_t blocks_for_tiles(int64_t ntiles) { return (ntiles + 7) / 8 * 8; }
 
@@ -53,14 +45,12 @@ static_assert(kTile % (4 * kBlock) == 0, "count block must divide the tile into 
 
 template <int RB>
 __global__ __launch_bounds__(kBlock) void k_radix_count(const uint32_t* __restrict__ keys, int64_t n, int shift,
-                                                        uint32_t* __restrict__ counts, const int64_t* n_dev) {
+                                                        uint32_t* __restrict__ counts, int64_t ntiles) {
   constexpr int R = 1 << RB;
   constexpr uint32_t M = R - 1;
   __shared__ uint32_t hist[R];
-  n = pass_n(n, n_dev);
-  const int64_t ntiles = (n + kTile - 1) / kTile;
   const int64_t tile = tile_of_block(ntiles);
-  if (tile < 0 || tile >= ntiles) return;  // block-uniform
+  if (tile >= ntiles) return;  // block-uniform
   for (int d = threadIdx.x; d < R; d += kBlock) hist[d] = 0;
   lds_barrier();
   const int64_t base = tile * kTile;
@@ -94,12 +84,9 @@ __device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v, int lane) {
 }
 
 // Exclusive scan of each digit's row counts[d][0..ntiles), row totals -> digit_tot[d].
-__global__ __launch_bounds__(kBlock) void k_radix_scan_rows(uint32_t* __restrict__ counts, int64_t n,
-                                                            const int64_t* __restrict__ n_dev,
+__global__ __launch_bounds__(kBlock) void k_radix_scan_rows(uint32_t* __restrict__ counts, int64_t ntiles,
                                                             uint32_t* __restrict__ digit_tot) {
   __shared__ uint32_t wsum[kWaves];
-  n = pass_n(n, n_dev);
-  const int64_t ntiles = (n + kTile - 1) / kTile;
   uint32_t* row = counts + (int64_t)blockIdx.x * ntiles;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   uint32_t carry = 0;
@@ -161,7 +148,7 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint32_t* __rest
                                                           P* __restrict__ vals_out, int64_t n,
                                                           int shift, const uint32_t* __restrict__ counts,
                                                           const uint32_t* __restrict__ digit_tot,
-                                                          const int64_t* __restrict__ n_dev) {
+                                                          int64_t ntiles) {
   constexpr int R = 1 << RB;
   constexpr uint32_t M = R - 1;
   constexpr int D = R / kBlock;  // digits per thread in the block scans
@@ -176,10 +163,8 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint32_t* __rest
   __shared__ uint32_t glob_off[R];
   __shared__ uint32_t wsum[kWaves];
 
-  n = pass_n(n, n_dev);
-  const int64_t ntiles = (n + kTile - 1) / kTile;
   const int64_t tile = tile_of_block(ntiles);
-  if (tile < 0 || tile >= ntiles) return;  // block-uniform
+  if (tile >= ntiles) return;  // block-uniform
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   const int64_t tile_base = tile * kTile;
@@ -295,25 +280,23 @@ void SortWork::ensure(int64_t n) {
   cap = c;
 }
 
-// n: the host's key count, or (n_dev) its upper bound that sizes the grids
 template <class P, int RB>
-static void radix_pass_impl(const uint32_t* kin, const P* vin, uint32_t* ko, P* vo, int64_t n, const int64_t* n_dev,
-                            int shift, SortWork& w, hipStream_t st) {
-  const unsigned blocks = (unsigned)blocks_for_tiles(tiles_of(n));
-  hipLaunchKernelGGL(k_radix_count<RB>, dim3(blocks), dim3(kBlock), 0, st, kin, n, shift, w.counts.as<uint32_t>(),
-                     n_dev);
-  hipLaunchKernelGGL(k_radix_scan_rows, dim3(1u << RB), dim3(kBlock), 0, st, w.counts.as<uint32_t>(), n, n_dev,
-                     w.digit_tot.as<uint32_t>());
-  hipLaunchKernelGGL((k_radix_scatter<P, RB>), dim3(blocks), dim3(kBlock), 0, st, kin, vin, ko, vo, n, shift,
-                     w.counts.as<uint32_t>(), w.digit_tot.as<uint32_t>(), n_dev);
+static void radix_pass_impl(const uint32_t* kin, const P* vin, uint32_t* ko, P* vo, int64_t n, int shift,
+                       SortWork& w, int64_t ntiles, hipStream_t st) {
+  hipLaunchKernelGGL(k_radix_count<RB>, dim3((unsigned)blocks_for_tiles(ntiles)), dim3(kBlock), 0, st, kin, n, shift,
+                     w.counts.as<uint32_t>(), ntiles);
+  hipLaunchKernelGGL(k_radix_scan_rows, dim3(1u << RB), dim3(kBlock), 0, st, w.counts.as<uint32_t>(), ntiles,
+                       w.digit_tot.as<uint32_t>());
+  hipLaunchKernelGGL((k_radix_scatter<P, RB>), dim3((unsigned)blocks_for_tiles(ntiles)), dim3(kBlock), 0, st, kin,
+                     vin, ko, vo, n, shift, w.counts.as<uint32_t>(), w.digit_tot.as<uint32_t>(), ntiles);
   FM_HIP_CHECK(hipGetLastError());
 }
 
 template <class P, int RB>
-static void radix_pass(const uint32_t* kin, const P* vin, uint32_t* ko, P* vo, int64_t n, const int64_t* n_dev,
-                       int shift, SortWork& w, hipStream_t st) {
+static void radix_pass(const uint32_t* kin, const P* vin, uint32_t* ko, P* vo, int64_t n, int shift,
+                       SortWork& w, int64_t ntiles, hipStream_t st) {
   if constexpr ((1 << RB) >= kBlock) {
-    radix_pass_impl<P, RB>(kin, vin, ko, vo, n, n_dev, shift, w, st);
+    radix_pass_impl<P, RB>(kin, vin, ko, vo, n, shift, w, ntiles, st);
   } else {
     FM_REQUIRE(false, "sort digit narrower than the block");
   }
@@ -334,8 +317,7 @@ inline int digit_bits(int key_bits, int* passes) {
 template <class P>
 static void radix_sort_impl(SortWork& w, const uint32_t* keys_in, const P* vals_in, int64_t n, int key_bits,
                             hipStream_t st, const uint32_t** keys_out, const P** vals_out,
-                            uint32_t* final_keys = nullptr, P* final_vals = nullptr, int lo_bit = 0,
-                            const int64_t* n_dev = nullptr) {
+                            uint32_t* final_keys = nullptr, P* final_vals = nullptr, int lo_bit = 0) {
   FM_REQUIRE(n >= 0 && n < (int64_t(1) << 32) - 1, "sort size out of range");
   w.ensure(n > 0 ? n : 1);
   if (n == 0) {
@@ -345,7 +327,8 @@ static void radix_sort_impl(SortWork& w, const uint32_t* keys_in, const P* vals_
   }
   int passes = 0;
   const int rb = digit_bits(key_bits, &passes);
-  FM_REQUIRE(tiles_of(n) < (int64_t(1) << 31), "too many sort tiles");
+  const int64_t ntiles = (n + kTile - 1) / kTile;
+  FM_REQUIRE(ntiles < (int64_t(1) << 31), "too many sort tiles");
   const uint32_t* kin = keys_in;
   const P* vin = vals_in;
   uint32_t* kbuf[2] = {w.keys_a.as<uint32_t>(), w.keys_b.as<uint32_t>()};
@@ -363,8 +346,8 @@ static void radix_sort_impl(SortWork& w, const uint32_t* keys_in, const P* vals_
     uint32_t* ko = last ? final_keys : kbuf[which];
     P* vo = last ? final_vals : vbuf[which];
     switch (rb) {
-      case 9: radix_pass<P, 9>(kin, vin, ko, vo, n, n_dev, shift, w, st); break;
-      default: radix_pass<P, 10>(kin, vin, ko, vo, n, n_dev, shift, w, st); break;
+      case 9: radix_pass<P, 9>(kin, vin, ko, vo, n, shift, w, ntiles, st); break;
+      default: radix_pass<P, 10>(kin, vin, ko, vo, n, shift, w, ntiles, st); break;
     }
     kin = ko;
     vin = vo;
@@ -391,15 +374,6 @@ void radix_sort_pairs64(SortWork& w, const uint32_t* keys_in, const uint2* vals_
                         hipStream_t st, const uint32_t** keys_out, const uint2** vals_out, uint32_t* final_keys,
                         uint2* final_vals) {
   radix_sort_impl<uint2>(w, keys_in, vals_in, n, key_bits, st, keys_out, vals_out, final_keys, final_vals);
-}
-
-void radix_sort_pairs64_dev(SortWork& w, const uint32_t* keys_in, const uint2* vals_in, int64_t n_max,
-                            const int64_t* n_dev, int key_bits, hipStream_t st, uint32_t* final_keys,
-                            uint2* final_vals) {
-  FM_REQUIRE(n_dev && final_keys && final_vals, "device-counted sort needs its count and outputs");
-  const uint32_t* ko = nullptr;
-  const uint2* vo = nullptr;
-  radix_sort_impl<uint2>(w, keys_in, vals_in, n_max, key_bits, st, &ko, &vo, final_keys, final_vals, 0, n_dev);
 }
 
 }  // namespace fmhip

@@ -50,9 +50,6 @@ extern "C" {
 #define FM_FUSE_DEFAULT 0 /* fm_config.fuse_single: the library's choice (tables above 256 MB) */
 #define FM_FUSE_ON 1
 #define FM_FUSE_OFF (-1)
-#define FM_FILTER_DEFAULT 0 /* fm_config.sort_filter: the library's choice (4 or more table rows per entry) */
-#define FM_FILTER_ON 1
-#define FM_FILTER_OFF (-1)
 
 typedef struct fm_ctx fm_ctx;
 typedef struct fm_batch fm_batch;
@@ -86,13 +83,6 @@ typedef struct fm_batch fm_batch;
  * xchg_chunks  : sharded step with R > 1: the owners' partial pass runs in this many chunks, each
  *                sent while the next is computed (0 = the default, 4; 1 = one pass then one
  *                all-to-all; at most 64).  Every process of a job must pass the same value.
- * sort_filter  : how a batch is grouped by feature for the segmented update.  FM_FILTER_ON: only the
- *                entries of features that occur two or more times in the batch are sorted (bitmaps
- *                of the features seen once / again, then a stable compaction), the singleton entries
- *                follow in CSR order; FM_FILTER_OFF: every entry is sorted; FM_FILTER_DEFAULT (0):
- *                the filter when the table has at least 4 rows per entry of the batch (a sparse
- *                batch: most features once).  The same table within fp64 summation order.  The fused
- *                step (fuse_single) always filters.
  * Zero-initialise the struct: every field's 0 is its default. */
 typedef struct fm_config {
   int64_t num_features;
@@ -112,7 +102,6 @@ typedef struct fm_config {
   uint8_t comm_id[128];
   int32_t fuse_single;
   int32_t xchg_chunks;
-  int32_t sort_filter;
 } fm_config;
 
 /* One mini-batch in CSR form: the result of explode(udfVecToMap(features))

@@ -69,15 +69,14 @@ def test_config_layout_matches_header(tmp_path):
     src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "fm_hip.h"\n'
                    'int main(void){printf("%zu %zu %zu %zu %zu\\n", sizeof(fm_config), offsetof(fm_config, parallel),'
                    ' offsetof(fm_config, devices), offsetof(fm_config, proc_rank), offsetof(fm_config, comm_id));'
-                   'printf("%zu %zu %zu\\n", offsetof(fm_config, fuse_single), offsetof(fm_config, xchg_chunks),'
-                   ' offsetof(fm_config, sort_filter));'
+                   'printf("%zu %zu\\n", offsetof(fm_config, fuse_single), offsetof(fm_config, xchg_chunks));'
                    'return 0;}\n')
     exe = tmp_path / "sz"
     subprocess.run(["gcc", f"-I{HEADER.parent}", str(src), "-o", str(exe)], check=True)
     got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
     F = N.fm_config
     assert got == [C.sizeof(F), F.parallel.offset, F.devices.offset, F.proc_rank.offset, F.comm_id.offset,
-                   F.fuse_single.offset, F.xchg_chunks.offset, F.sort_filter.offset]
+                   F.fuse_single.offset, F.xchg_chunks.offset]
 
 
 def test_multi_gpu_context_without_gpu_fails_loudly():

@@ -14,10 +14,6 @@ the switch changes nothing); rows absent from the model and an L1 that zeroes va
 and long rows (beyond the 40 entries a sample keeps in LDS: the re-read path); a feature in every
 row; split chunks of 1024 sorted entries crossed by long runs; a batch that is not prepared (the
 unfused path) between prepared ones.
-
-The singleton filter without fusion (fm_config.sort_filter): the grouped view [repeated features
-sorted | singletons in CSR order] gives the full sort's step within the same tolerance, the same
-view whether the batch is prepared or sorted inside its step (bitwise), and the oracle's step.
 """
 
 import numpy as np
@@ -30,10 +26,10 @@ from test_gpu_parity import assert_tables, to_host
 pytestmark = pytest.mark.gpu
 
 
-def _steps(fuse, csrs, F, k, ids, w, V, steps, step_size=0.3, reg=1e-4, prepare=lambda t: True, sort_filter=None):
+def _steps(fuse, csrs, F, k, ids, w, V, steps, step_size=0.3, reg=1e-4, prepare=lambda t: True):
     from fm_spark_amd.engine import FMContext
 
-    ctx = FMContext(F, k, fuse=fuse, sort_filter=sort_filter)
+    ctx = FMContext(F, k, fuse=fuse)
     ctx.load_tables(ids, w, V)
     dbs = [ctx.batch(to_host(c)) for c in csrs]
     losses = []
@@ -146,39 +142,3 @@ def test_fused_all_singletons_and_all_multi(gpu):
     fused = _steps(True, [single, multi], F, k, ids, w, V, 4)
     unfused = _steps(False, [single, multi], F, k, ids, w, V, 4)
     _assert_same(fused, unfused)
-
-
-@pytest.mark.parametrize("k", [4, 16, 32])
-def test_sort_filter_matches_full_sort(gpu, k):
-    F = 40000
-    csrs = [make_problem(820 + i, 1500, F, k, 10, hot=7 + i)[0] for i in range(3)]
-    _, ids, w, V = make_problem(76, 1, F, k, 1)
-    full = _steps(False, csrs, F, k, ids, w, V, 4, sort_filter=False)
-    filt = _steps(False, csrs, F, k, ids, w, V, 4, sort_filter=True)
-    _assert_same(filt, full)
-    # a prepared batch and one sorted inside its step get the same grouped view
-    _assert_bitwise(filt, _steps(False, csrs, F, k, ids, w, V, 4, sort_filter=True, prepare=lambda t: t % 2 == 0))
-    model = R.Model.empty(F, k)
-    model.load(ids, w, V)
-    for t in range(1, 5):
-        ro = R.sgd_step_fast(model, csrs[(t - 1) % 3], t, 0.3, 1e-4)
-        np.testing.assert_allclose(filt[0][t - 1][0], ro.loss_sum, rtol=1e-6)
-        assert filt[0][t - 1][1] == ro.n_unique
-    assert_tables(model, filt[1])
-
-
-def test_sort_filter_all_singletons_all_repeated_and_empty(gpu):
-    """The filter with nothing repeated (no sort at all), nothing single, and an empty batch."""
-    F, k = 100000, 8
-    rng = np.random.default_rng(6)
-    B, z = 400, 8
-    rp = np.arange(0, B * z + 1, z, dtype=np.int64)
-    ids_all = rng.permutation(F)[: B * z].astype(np.int32)
-    single = R.CSR(rp, np.sort(ids_all.reshape(B, z), axis=1).ravel(), rng.normal(size=B * z), rng.random(B))
-    pool = rng.permutation(F)[:30].astype(np.int32)
-    cols = np.concatenate([np.sort(rng.choice(pool, size=z, replace=False)) for _ in range(B)]).astype(np.int32)
-    multi = R.CSR(rp, cols, rng.normal(size=B * z), rng.random(B))
-    empty_rows = R.CSR(np.zeros(11, np.int64), np.zeros(0, np.int32), np.zeros(0), rng.random(10))
-    _, ids, w, V = make_problem(77, 1, F, k, 1)
-    res = [_steps(False, [single, multi, empty_rows], F, k, ids, w, V, 6, sort_filter=f) for f in (True, False)]
-    _assert_same(res[0], res[1])

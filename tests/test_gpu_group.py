@@ -115,26 +115,6 @@ def test_group_sharded_prepare_two_ahead(gpu, R, transport):
     ctx.close()
 
 
-@pytest.mark.parametrize("mode,R,transport", [("sharded", 3, "copy"), ("sharded", 1, "rccl"), ("replicated", 2, "copy")])
-def test_group_sort_filter_matches_oracle(gpu, mode, R, transport):
-    """fm_config.sort_filter on the owners' grouping (sharded: [repeated slots sorted | singletons in
-    arrival order]) and on the replicas' batches: the oracle step."""
-    F, k = 50000, 8
-    _, ids, w, V = make_problem(6, 1, F, k, 1)
-    ctx = _ctx(F, k, R, mode=mode, transport=transport, sort_filter=True)
-    ctx.load_tables(ids, w, V)
-    model = R_.Model.empty(F, k)
-    model.load(ids, w, V)
-    for t in range(1, 4):
-        p = make_problem(500 + t, 300, F, k, 9, hot=5)[0]
-        o = ctx.step(_host(p), t, 0.3, 1e-4)
-        ref = R_.sgd_step_fast(model, p, t, 0.3, 1e-4)
-        assert o.loss_sum == pytest.approx(ref.loss_sum, rel=1e-5)
-        assert (o.n_rows, o.n_loss_rows, o.n_unique) == (ref.n_rows, ref.n_loss_rows, ref.n_unique)
-    _check_tables(ctx, model)
-    ctx.close()
-
-
 @pytest.mark.parametrize("chunks", [1, 3, 16])
 def test_group_sharded_exchange_chunks(gpu, chunks):
     """The owners' partial pass in C chunks whose exchange overlaps the next chunk's compute
