@@ -28,6 +28,12 @@ import os
 import sys
 import time
 
+# HIP maps a process's streams round-robin onto GPU_MAX_HW_QUEUES hardware queues (4 by default);
+# two streams on one queue run in submission order, so the library's main, side and exchange streams
+# must not share one with each other or with torch's ("Hardware queues").  Set before
+# anything initialises HIP.
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+
 import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))

@@ -169,7 +169,7 @@ struct fm_ctx {
   DevBuf sh_skey;      // [N] owner-partitioned route keys
   DevBuf sh_ent2;      // [n] uint2 {pair, x bits}: the slot sort's payload
   SortWork side_sort;  // radix sort workspace of the side stream
-  SortWork route_sort;  // the route's owner partition (fm_shard_route; the group's route stream)
+  SortWork route_sort;  // the route's owner partition (fm_shard_route)
   SplitWork split_work;  // fm_batch_prepare's singleton split (side stream)
   Pinned side_pinned;  // route counts (device -> host)
   // replicated step state (fm_repl_*)

@@ -73,7 +73,7 @@ struct Rank {
   fm_ctx* m = nullptr;  // the member context (owned)
   int device = 0;
   int global = 0;
-  ncclComm_t comm_main = nullptr, comm_side = nullptr, comm_x = nullptr, comm_route = nullptr;
+  ncclComm_t comm_main = nullptr, comm_side = nullptr, comm_x = nullptr;
   hipEvent_t ev_main = nullptr, ev_side = nullptr;  // COPY transport barriers
   DevBuf partials, part_in, s_send, s_recv;           // sharded wire buffers (main stream)
   DevBuf pc_out, pc_in, pred;                         // sharded predict: present counts, scores
@@ -83,18 +83,17 @@ struct Rank {
   // chunked partial exchange of the sharded step (R > 1): its own stream and communicator
   hipStream_t xstream = nullptr;
   hipEvent_t ev_x = nullptr, ev_fwd = nullptr, ev_xdone = nullptr;
-  // the sharded route and its counts (batch-only, ahead of the step): a stream of their own
-  hipStream_t rstream = nullptr;
-  hipEvent_t ev_route = nullptr;
-  // lanes: 0 main stream, 1 side stream (batch-only work), 2 the exchange stream, 3 the route stream
-  hipStream_t stream(int lane) const { return lane == 3 ? rstream : lane == 2 ? xstream : lane ? m->side : m->stream; }
-  hipEvent_t event(int lane) const { return lane == 3 ? ev_route : lane == 2 ? ev_x : lane ? ev_side : ev_main; }
+  // lanes: 0 main stream, 1 side stream (batch-only work: route, entry exchange, owner preparation),
+  // 2 the exchange stream.  Few streams on purpose: HIP maps a process's streams round-robin onto
+  // GPU_MAX_HW_QUEUES hardware queues (4 by default), and two streams on one queue run in submission
+  // order -- a route on a stream of its own shared the main stream's queue (profiles/r03_v3 kernel
+  // trace: queue 4 for both) and waited behind the step
+  hipStream_t stream(int lane) const { return lane == 2 ? xstream : lane ? m->side : m->stream; }
+  hipEvent_t event(int lane) const { return lane == 2 ? ev_x : lane ? ev_side : ev_main; }
   // one communicator per stream, each used in the same order on every rank
-  ncclComm_t comm(int lane) const {
-    return lane == 3 ? comm_route : lane == 2 ? comm_x : lane ? comm_side : comm_main;
-  }
+  ncclComm_t comm(int lane) const { return lane == 2 ? comm_x : lane ? comm_side : comm_main; }
 };
-constexpr int kLaneMain = 0, kLaneSide = 1, kLaneXchg = 2, kLaneRoute = 3;
+constexpr int kLaneMain = 0, kLaneSide = 1, kLaneXchg = 2;
 
 struct GPart {
   fm_batch* b = nullptr;  // the member's batch (owned)
@@ -108,12 +107,12 @@ struct GroupBatch {
   std::vector<GPart> parts;
   int64_t rows = 0, nnz = 0, global_rows = 0;
   bool prefetched = false;  // routed, exchanged and slot-sorted for its next step
-  // sharded prepare, phase 1 done: routes and their count gather enqueued (route streams), the
+  // sharded prepare, phase 1 done: routes and their count gather enqueued (side streams), the
   // counts on their way to cnt_pin; phase 2 (the host reads them, exchange, owner preparation)
   // runs at the context's next fm_batch_prepare or at this batch's step
   bool routed = false;
   Pinned cnt_pin;
-  std::vector<hipEvent_t> ev_cnt;  // per local rank: its route-stream work of phase 1 is done
+  std::vector<hipEvent_t> ev_cnt;  // per local rank: its side-stream work of phase 1 is done
   Group* g = nullptr;              // the group while this batch is its pending phase 2
   ~GroupBatch();
 };
@@ -135,7 +134,6 @@ struct Group {
       if (!r.m) continue;
       (void)hipSetDevice(r.device);
       (void)hipDeviceSynchronize();
-      if (r.comm_route) (void)ncclCommDestroy(r.comm_route);
       if (r.comm_x) (void)ncclCommDestroy(r.comm_x);
       if (r.comm_side) (void)ncclCommDestroy(r.comm_side);
       if (r.comm_main) (void)ncclCommDestroy(r.comm_main);
@@ -144,10 +142,9 @@ struct Group {
         d->release();
       if (r.ev_main) (void)hipEventDestroy(r.ev_main);
       if (r.ev_side) (void)hipEventDestroy(r.ev_side);
-      for (hipEvent_t e : {r.ev_x, r.ev_fwd, r.ev_xdone, r.ev_route})
+      for (hipEvent_t e : {r.ev_x, r.ev_fwd, r.ev_xdone})
         if (e) (void)hipEventDestroy(e);
       if (r.xstream) (void)hipStreamDestroy(r.xstream);
-      if (r.rstream) (void)hipStreamDestroy(r.rstream);
     }
     for (auto& r : ranks)
       if (r.m) fm_destroy(r.m);
@@ -397,9 +394,9 @@ void sync_group_batch_view(fm_batch* b) {  // fm_batch_rows / fm_batch_nnz of th
   b->dev.nnz = b->grp->nnz;
 }
 
-// Sharded prepare, phase 1: every local rank's route (fm_shard.hip phase 1) on its route stream,
+// Sharded prepare, phase 1: every local rank's route (fm_shard.hip phase 1) on its side stream,
 // then the job's route counts (ctx->sh_tot: [R] pairs, [R] entries per rank) gathered and copied
-// to the batch's pinned buffer, rank-major [R][2R]: RCCL all-gathers them on the route streams and
+// to the batch's pinned buffer, rank-major [R][2R]: RCCL all-gathers them on the side streams and
 // local rank 0 copies them back, COPY copies each rank's.  Nothing waits on the host.
 void launch_routes(Group& g, GroupBatch& gb) {
   const int R = g.R, L = g.L;
@@ -409,7 +406,7 @@ void launch_routes(Group& g, GroupBatch& gb) {
     GPart& p = gb.parts[l];
     ensure_on(r.device, p.send_slot, sizeof(uint32_t) * p.nnz);
     ensure_on(r.device, p.send_ent, sizeof(uint2) * p.nnz);
-    on(r, [&] { shard_route_launch(r.m, p.b, p.send_slot.p, p.send_ent.p, r.rstream); });
+    on(r, [&] { shard_route_launch(r.m, p.b, p.send_slot.p, p.send_ent.p, r.m->side); });
   }
   gb.cnt_pin.ensure(row * R);
   if ((int)gb.ev_cnt.size() != L) {
@@ -424,22 +421,22 @@ void launch_routes(Group& g, GroupBatch& gb) {
     FM_RCCL_CHECK(ncclGroupStart());
     for (auto& r : g.ranks) {
       FM_HIP_CHECK(hipSetDevice(r.device));
-      FM_RCCL_CHECK(ncclAllGather(r.m->sh_tot.p, r.xg_recv.p, 2 * R, ncclUint64, r.comm_route, r.rstream));
+      FM_RCCL_CHECK(ncclAllGather(r.m->sh_tot.p, r.xg_recv.p, 2 * R, ncclUint64, r.comm_side, r.m->side));
     }
     FM_RCCL_CHECK(ncclGroupEnd());
     Rank& r0 = g.ranks[0];
     FM_HIP_CHECK(hipSetDevice(r0.device));
-    FM_HIP_CHECK(hipMemcpyAsync(gb.cnt_pin.p, r0.xg_recv.p, row * R, hipMemcpyDeviceToHost, r0.rstream));
+    FM_HIP_CHECK(hipMemcpyAsync(gb.cnt_pin.p, r0.xg_recv.p, row * R, hipMemcpyDeviceToHost, r0.m->side));
   } else {
     for (auto& r : g.ranks) {
       FM_HIP_CHECK(hipSetDevice(r.device));
       FM_HIP_CHECK(hipMemcpyAsync(reinterpret_cast<char*>(gb.cnt_pin.p) + row * r.global, r.m->sh_tot.p, row,
-                                  hipMemcpyDeviceToHost, r.rstream));
+                                  hipMemcpyDeviceToHost, r.m->side));
     }
   }
   for (int l = 0; l < L; ++l) {
     FM_HIP_CHECK(hipSetDevice(g.ranks[l].device));
-    FM_HIP_CHECK(hipEventRecord(gb.ev_cnt[l], g.ranks[l].rstream));
+    FM_HIP_CHECK(hipEventRecord(gb.ev_cnt[l], g.ranks[l].m->side));
   }
   gb.routed = true;
 }
@@ -477,12 +474,7 @@ void finish_routes(Group& g, GroupBatch& gb) {
     }
   for (int l = 0; l < L; ++l) {
     Rank& r = g.ranks[l];
-    on(r, [&] {
-      shard_route_finish(r.m, gb.parts[l].b, rc + (size_t)r.global * 2 * R, counts[l].data());
-      // the entry exchange and the owner preparation (side stream) read what the route wrote
-      FM_HIP_CHECK(hipEventRecord(r.ev_route, r.rstream));
-      FM_HIP_CHECK(hipStreamWaitEvent(r.m->side, r.ev_route, 0));
-    });
+    on(r, [&] { shard_route_finish(r.m, gb.parts[l].b, rc + (size_t)r.global * 2 * R, counts[l].data()); });
   }
   std::vector<const char*> ss(L), se(L);
   std::vector<char*> rs(L), re(L);
@@ -871,8 +863,6 @@ int group_create(const fm_config* cfg, fm_ctx** out) {
     FM_HIP_CHECK(hipSetDevice(r.device));
     FM_HIP_CHECK(hipEventCreateWithFlags(&r.ev_main, hipEventDisableTiming));
     FM_HIP_CHECK(hipEventCreateWithFlags(&r.ev_side, hipEventDisableTiming));
-    FM_HIP_CHECK(hipEventCreateWithFlags(&r.ev_route, hipEventDisableTiming));
-    FM_HIP_CHECK(hipStreamCreateWithFlags(&r.rstream, hipStreamNonBlocking));
   }
   for (auto& a : g.ranks)  // peer access between the distinct devices (copies, RCCL's P2P)
     for (auto& b : g.ranks)
@@ -892,7 +882,7 @@ int group_create(const fm_config* cfg, fm_ctx** out) {
       FM_RCCL_CHECK(ncclCommInitRank(&r.comm_main, R, id, r.global));
     }
     FM_RCCL_CHECK(ncclGroupEnd());
-    for (ncclComm_t Rank::*dst : {&Rank::comm_side, &Rank::comm_x, &Rank::comm_route}) {
+    for (ncclComm_t Rank::*dst : {&Rank::comm_side, &Rank::comm_x}) {
       FM_RCCL_CHECK(ncclGroupStart());
       for (auto& r : g.ranks) {
         FM_HIP_CHECK(hipSetDevice(r.device));
