@@ -100,6 +100,9 @@ struct GPart {
   int device = 0;
   int64_t rows = 0, row0 = 0, nnz = 0;
   DevBuf send_slot, send_ent, recv_slot, recv_ent;
+  // what the owner reads: recv_*, or for a one-rank job its own send buffers (nothing to exchange)
+  void* in_slot = nullptr;
+  void* in_ent = nullptr;
   std::vector<int64_t> ent_out, pair_out, ent_in, pair_in;  // per global peer
 };
 
@@ -479,7 +482,6 @@ void finish_routes(Group& g, GroupBatch& gb) {
   std::vector<const char*> ss(L), se(L);
   std::vector<char*> rs(L), re(L);
   std::vector<const int64_t*> out(L), in(L);
-  std::vector<std::vector<int64_t>> out2(L), in2(L);
   for (int l = 0; l < L; ++l) {
     GPart& p = gb.parts[l];
     const int gl = g.ranks[l].global;
@@ -492,8 +494,12 @@ void finish_routes(Group& g, GroupBatch& gb) {
       p.pair_in[s] = all[(size_t)s * 2 * R + R + gl];
     }
     const int64_t n_in = std::accumulate(p.ent_in.begin(), p.ent_in.end(), int64_t(0));
-    ensure_on(g.ranks[l].device, p.recv_slot, sizeof(uint32_t) * n_in);
-    ensure_on(g.ranks[l].device, p.recv_ent, sizeof(uint2) * n_in);
+    if (R > 1) {
+      ensure_on(g.ranks[l].device, p.recv_slot, sizeof(uint32_t) * n_in);
+      ensure_on(g.ranks[l].device, p.recv_ent, sizeof(uint2) * n_in);
+    }
+    p.in_slot = R > 1 ? p.recv_slot.p : p.send_slot.p;  // R = 1: the owner block is the send buffers' head
+    p.in_ent = R > 1 ? p.recv_ent.p : p.send_ent.p;
     ss[l] = p.send_slot.as<char>();
     se[l] = p.send_ent.as<char>();
     rs[l] = p.recv_slot.as<char>();
@@ -501,12 +507,12 @@ void finish_routes(Group& g, GroupBatch& gb) {
     out[l] = p.ent_out.data();
     in[l] = p.ent_in.data();
   }
-  a2a_multi(g, true, {A2ASeg{ss, rs, sizeof(uint32_t)}, A2ASeg{se, re, sizeof(uint2)}}, out, in);
+  if (R > 1) a2a_multi(g, true, {A2ASeg{ss, rs, sizeof(uint32_t)}, A2ASeg{se, re, sizeof(uint2)}}, out, in);
   for (int l = 0; l < L; ++l) {
     Rank& r = g.ranks[l];
     GPart& p = gb.parts[l];
     const int64_t n_in = std::accumulate(p.ent_in.begin(), p.ent_in.end(), int64_t(0));
-    mcheck(fm_shard_owner_prepare(r.m, p.b, p.recv_slot.p, p.recv_ent.p, n_in, p.ent_in.data(), p.pair_in.data()),
+    mcheck(fm_shard_owner_prepare(r.m, p.b, p.in_slot, p.in_ent, n_in, p.ent_in.data(), p.pair_in.data()),
            "fm_shard_owner_prepare");
   }
   gb.prefetched = true;
@@ -977,8 +983,9 @@ int group_init_from_batch(fm_ctx* ctx, fm_batch* b, int64_t* n_present) {
         FM_HIP_CHECK(hipStreamSynchronize(r.m->side));
         DevBuf ids;
         ids.ensure(sizeof(uint32_t) * n_in);
-        hipLaunchKernelGGL(k_slots_to_ids, dim3(grid_of(n_in)), dim3(kBlock), 0, r.m->stream, p.recv_slot.as<uint32_t>(),
-                           n_in, (uint32_t)g.R, (uint32_t)r.global, ids.as<uint32_t>());
+        hipLaunchKernelGGL(k_slots_to_ids, dim3(grid_of(n_in)), dim3(kBlock), 0, r.m->stream,
+                           static_cast<const uint32_t*>(p.in_slot), n_in, (uint32_t)g.R, (uint32_t)r.global,
+                           ids.as<uint32_t>());
         launch_init_entries(r.m->view(), ids.as<uint32_t>(), n_in, r.m->cfg.seed, r.m->cfg.init_sd, r.m->epoch,
                             r.m->cum_host.back(), r.m->stream);
         FM_HIP_CHECK(hipStreamSynchronize(r.m->stream));

@@ -235,7 +235,10 @@ class FactorizationMachinesModel:
         """Model.scala:135-234: one row per active entry with columns label, sampleId,
         featureId, prediction, loss, deltaWi, deltaVi (deltaVi before the (pred - label) factor).
         Ids the model lacks get per-entry N(0, initialSd^2) draws (:144-146, 170-171); the
-        reference's draws are unseeded, here they are keyed by `seed` and the entry."""
+        reference's draws are unseeded, here they are keyed by `seed` and the entry.  A model whose
+        table is row-sharded over several GPUs (setParallel("sharded")) refuses it with FMError:
+        the per-entry rows would need every owner's rows on one device (fm_loss_grad, include/fm_hip.h);
+        a replicated or single-GPU model answers it."""
         if not initialSd > 0.0:
             raise ValueError("requirement failed: initSd (initial Standard Deviation) must be > 0.0")
         fcol, lcol = self._params["featuresCol"], self._params["labelCol"]

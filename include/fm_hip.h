@@ -129,7 +129,9 @@ typedef struct fm_step_out {
 /* Replaces: new FactorizationMachinesModel(uid, k, globalBias, ...) (Model.scala:43-48).
  * A multi-GPU context (parallel != FM_PARALLEL_NONE) accepts every entry point below except the
  * manual fm_shard_* / fm_repl_* phases, fm_set_stream / fm_set_side_stream (unless n_gpus == 1)
- * and fm_loss_grad on a sharded table; the table entry points act on the rows this process's ranks
+ * and fm_loss_grad / fm_calc_loss_grad on a sharded table (FM_ERR_ARG: the per-entry outputs
+ * need every owner's rows on one device; replicated contexts answer them); the table entry points
+ * act on the rows this process's ranks
  * hold (all rows when n_procs == 1). */
 int fm_create(const fm_config* cfg, fm_ctx** out);
 /* RCCL unique id for a job of several processes (ncclGetUniqueId), 128 bytes into id. */
@@ -228,7 +230,8 @@ int fm_loss_grad(fm_ctx* ctx, const fm_csr* csr, double* pred, double* loss, dou
  * (Model.scala:144-146, 170-171: coalesce(strength, randn() * initialSd) and udfInitVec() per
  * joined row): every entry whose id is absent (or >= num_features) gets its own w and v drawn
  * from N(0, initial_sd^2) -- keyed by (seed, entry index in CSR order, column), so a call is
- * reproducible where the reference's draws are unseeded.  initial_sd must be > 0 (:136). */
+ * reproducible where the reference's draws are unseeded.  initial_sd must be > 0 (:136).
+ * Refused on a row-sharded multi-GPU context (see fm_create). */
 int fm_calc_loss_grad(fm_ctx* ctx, const fm_csr* csr, double initial_sd, uint64_t seed, double* pred,
                       double* loss, double* delta_w, double* delta_v);
 /* VectorSum UDAF + groupBy (FactorizationMachines.scala:45-81): for every distinct key,

@@ -269,3 +269,28 @@ def test_rccl_two_devices_matches_copy(gpu, mode):
     _check_tables(ctxs["rccl"], model)
     for c in ctxs.values():
         c.close()
+
+
+def test_group_loss_grad_refused_when_sharded_answered_when_replicated(gpu):
+    """calcLossGrad's per-entry rows need the whole table: a sharded group refuses it (FM_ERR_ARG,
+    include/fm_hip.h fm_create), a replicated group answers it as a single-table context does."""
+    from fm_spark_amd._native import FMError
+    from fm_spark_amd.engine import FMContext
+
+    F, k = 300, 4
+    _, ids, w, V = make_problem(14, 1, F, k, 1)
+    p = make_problem(15, 40, F, k, 6)[0]
+    sh = _ctx(F, k, 2)
+    sh.load_tables(ids, w, V)
+    with pytest.raises(FMError, match="whole table"):
+        sh.loss_grad(_host(p))
+    sh.close()
+    rep = _ctx(F, k, 2, mode="replicated")
+    one = FMContext(F, k)
+    for c in (rep, one):
+        c.load_tables(ids, w, V)
+    got, ref = rep.loss_grad(_host(p)), one.loss_grad(_host(p))
+    for a, b in zip(got, ref):
+        np.testing.assert_array_equal(a, b)
+    rep.close()
+    one.close()
