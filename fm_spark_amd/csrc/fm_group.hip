@@ -31,6 +31,7 @@
 #include <numeric>
 
 #include "fm_context.h"
+#include "fm_plan.h"
 #include "fm_device.h"
 
 namespace fmhip {
@@ -217,6 +218,12 @@ struct A2ASeg {
 // receive rc[l][p] from p into recv[l] + ro[l][p].
 struct A2APlan {
   std::vector<std::vector<int64_t>> so, sc, ro, rc;
+  void add(plan::Plan&& p) {  // the next local rank's plan (fm_plan.h)
+    so.push_back(std::move(p.so));
+    sc.push_back(std::move(p.sc));
+    ro.push_back(std::move(p.ro));
+    rc.push_back(std::move(p.rc));
+  }
 };
 
 // All-to-all-v of one or more segments with the same plan between the job's ranks, on `lane`;
@@ -277,18 +284,7 @@ void a2a_plan(Group& g, int lane, const std::vector<A2ASeg>& segs, const A2APlan
 // The plan of a packed all-to-all-v: blocks peer-major in both buffers, out[l][p] / in[l][p] elements.
 A2APlan packed_plan(Group& g, const std::vector<const int64_t*>& out, const std::vector<const int64_t*>& in) {
   A2APlan pl;
-  for (auto* v : {&pl.so, &pl.sc, &pl.ro, &pl.rc}) v->assign(g.L, std::vector<int64_t>(g.R, 0));
-  for (int l = 0; l < g.L; ++l) {
-    int64_t so = 0, ro = 0;
-    for (int p = 0; p < g.R; ++p) {
-      pl.so[l][p] = so;
-      pl.sc[l][p] = out[l][p];
-      pl.ro[l][p] = ro;
-      pl.rc[l][p] = in[l][p];
-      so += out[l][p];
-      ro += in[l][p];
-    }
-  }
+  for (int l = 0; l < g.L; ++l) pl.add(plan::packed(out[l], in[l], g.R));
   return pl;
 }
 
@@ -468,31 +464,19 @@ void finish_routes(Group& g, GroupBatch& gb) {
   if (g.pending == &gb) g.pending = nullptr;
   gb.routed = false;
   const unsigned long long* rc = reinterpret_cast<const unsigned long long*>(gb.cnt_pin.p);  // [source][pairs | entries]
-  std::vector<std::vector<int64_t>> counts(L, std::vector<int64_t>(2 * R, 0));
-  std::vector<int64_t> all((size_t)R * 2 * R);  // [source][entries R | pairs R]
-  for (int s = 0; s < R; ++s)
-    for (int o = 0; o < R; ++o) {
-      all[(size_t)s * 2 * R + o] = (int64_t)rc[(size_t)s * 2 * R + R + o];
-      all[(size_t)s * 2 * R + R + o] = (int64_t)rc[(size_t)s * 2 * R + o];
-    }
-  for (int l = 0; l < L; ++l) {
-    Rank& r = g.ranks[l];
-    on(r, [&] { shard_route_finish(r.m, gb.parts[l].b, rc + (size_t)r.global * 2 * R, counts[l].data()); });
-  }
+  std::vector<int64_t> counts(2 * R);
   std::vector<const char*> ss(L), se(L);
   std::vector<char*> rs(L), re(L);
   std::vector<const int64_t*> out(L), in(L);
   for (int l = 0; l < L; ++l) {
+    Rank& r = g.ranks[l];
     GPart& p = gb.parts[l];
-    const int gl = g.ranks[l].global;
-    p.ent_out.assign(counts[l].begin(), counts[l].begin() + R);
-    p.pair_out.assign(counts[l].begin() + R, counts[l].end());
-    p.ent_in.resize(R);
-    p.pair_in.resize(R);
-    for (int s = 0; s < R; ++s) {
-      p.ent_in[s] = all[(size_t)s * 2 * R + gl];
-      p.pair_in[s] = all[(size_t)s * 2 * R + R + gl];
-    }
+    on(r, [&] { shard_route_finish(r.m, p.b, rc + (size_t)r.global * 2 * R, counts.data()); });
+    plan::RouteCounts c = plan::route_counts(rc, R, r.global);
+    p.ent_out = std::move(c.ent_out);
+    p.pair_out = std::move(c.pair_out);
+    p.ent_in = std::move(c.ent_in);
+    p.pair_in = std::move(c.pair_in);
     const int64_t n_in = std::accumulate(p.ent_in.begin(), p.ent_in.end(), int64_t(0));
     if (R > 1) {
       ensure_on(g.ranks[l].device, p.recv_slot, sizeof(uint32_t) * n_in);
@@ -608,22 +592,15 @@ void forward_exchange_chunked(Group& g, GroupBatch& gb, int kp, int C, const std
   ensure_xchg(g);
   std::vector<const char*> sv(L), sc(L);
   std::vector<char*> rv(L), rc(L);
-  std::vector<std::vector<int64_t>> ioff(L, std::vector<int64_t>(R + 1, 0)), ooff(L, std::vector<int64_t>(R + 1, 0));
   for (int l = 0; l < L; ++l) {
     Rank& r = g.ranks[l];
-    GPart& p = gb.parts[l];
     sv[l] = r.partials.as<char>();
     sc[l] = r.partials.as<char>() + sizeof(float) * Pin[l] * kp;
     rv[l] = r.part_in.as<char>();
     rc[l] = r.part_in.as<char>() + sizeof(float) * Pout[l] * kp;
-    for (int q = 0; q < R; ++q) {
-      ioff[l][q + 1] = ioff[l][q] + p.pair_in[q];
-      ooff[l][q + 1] = ooff[l][q] + p.pair_out[q];
-    }
   }
-  A2APlan pl;
-  for (auto* v : {&pl.so, &pl.sc, &pl.ro, &pl.rc}) v->assign(L, std::vector<int64_t>(R, 0));
   for (int c = 0; c < C; ++c) {
+    A2APlan pl;
     for (int l = 0; l < L; ++l) {
       Rank& r = g.ranks[l];
       on(r, [&] {
@@ -631,14 +608,7 @@ void forward_exchange_chunked(Group& g, GroupBatch& gb, int kp, int C, const std
         FM_HIP_CHECK(hipEventRecord(r.ev_fwd, r.m->stream));
         FM_HIP_CHECK(hipStreamWaitEvent(r.xstream, r.ev_fwd, 0));
       });
-      const GPart& p = gb.parts[l];
-      for (int q = 0; q < R; ++q) {
-        const int64_t Pi = p.pair_in[q], Po = p.pair_out[q];
-        pl.so[l][q] = ioff[l][q] + Pi * c / C;
-        pl.sc[l][q] = Pi * (c + 1) / C - Pi * c / C;
-        pl.ro[l][q] = ooff[l][q] + Po * c / C;
-        pl.rc[l][q] = Po * (c + 1) / C - Po * c / C;
-      }
+      pl.add(plan::chunk(gb.parts[l].pair_in.data(), gb.parts[l].pair_out.data(), R, c, C));
     }
     a2a_plan(g, kLaneXchg, {A2ASeg{sv, rv, sizeof(float) * kp}, A2ASeg{sc, rc, sizeof(float) * 2}}, pl);
   }
