@@ -63,6 +63,9 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-steps", type=int, default=2)
     p.add_argument("--profile-kernels", type=int, default=1, help="HIP-event timing of each kernel phase")
+    p.add_argument("--profile-every", type=int, default=4,
+                   help="time the kernel phases of every n-th timed step (HIP events cost ~2 %% of a c3 step, "
+                        "~12 %% of a c5 step when every step carries them)")
     p.add_argument("--features", type=int, default=0, help="override num_features (experiments)")
     p.add_argument("--k", type=int, default=0, help="override k (experiments)")
     p.add_argument("--rows", type=int, default=0, help="override rows per batch (experiments)")
@@ -161,11 +164,12 @@ PHASE_KERNELS = {"forward": ["k_forward"], "update": ["k_segment_update", "k_seg
                  "owner_forward": ["k_forward"], "owner_update": ["k_segment_update", "k_segment_combine"]}
 
 
-def pmc_traffic(F, k, B, phase, fused=False):
+def pmc_traffic(F, k, B, phase, fused=False, world=1):
     """HBM bytes per launch of `phase` from the committed rocprofv3 PMC passes of this workload
     (profiles/pmc_*.json, made by tools/pmc.sh + tools/pmc_to_json.py with the calibrated
-    FETCH_SIZE/WRITE_SIZE corrections; "fused" says which step variant the passes measured).  None
-    when no pass of this exact workload and variant is committed."""
+    FETCH_SIZE/WRITE_SIZE corrections; "fused" says which step variant the passes measured, "mode"
+    whether the single-table step or the sharded owner phases).  None when no pass of this exact
+    workload and variant is committed."""
     import glob
 
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json"))):
@@ -173,7 +177,9 @@ def pmc_traffic(F, k, B, phase, fused=False):
             d = json.load(open(f))
         except (OSError, ValueError):
             continue
-        if (d.get("num_features"), d.get("k"), d.get("batch_rows"), bool(d.get("fused", False))) != (F, k, B, fused):
+        mode = "sharded" if phase.startswith("owner_") else "single"
+        if (d.get("num_features"), d.get("k"), d.get("batch_rows"), bool(d.get("fused", False)),
+                d.get("mode", "single"), d.get("world", 1)) != (F, k, B, fused, mode, world):
             continue
         ks = d.get("kernels", {})
         names = PHASE_KERNELS.get(phase, [])
@@ -285,6 +291,27 @@ def concat_batches(parts):
                  val=np.concatenate([p.val for p in parts]), label=np.concatenate([p.label for p in parts]))
 
 
+class ProfileSampler:
+    """Per-phase HIP-event timing (fm_profile_*) on every n-th timed step only: each phase's start
+    and stop events sit on its launch stream inside the timed region, and the kernels' average
+    durations come from the sampled launches (batches cycle, so every batch is sampled)."""
+
+    def __init__(self, ctx, args):
+        self.ctx, self.on = ctx, False
+        self.every = max(1, args.profile_every) if args.profile_kernels else 0
+
+    def __call__(self, i):
+        want = self.every > 0 and i % self.every == 0
+        if want != self.on:
+            self.ctx.profile_enable(want)
+            self.on = want
+
+    def off(self):
+        if self.on:
+            self.ctx.profile_enable(False)
+            self.on = False
+
+
 def main():
     args = parse()
     import torch
@@ -357,7 +384,7 @@ def main():
         ctx.sync()
         if args.profile_kernels:
             ctx.profile_reset()
-            ctx.profile_enable(True)
+        prof_on = ProfileSampler(ctx, args)
         prefetch = not args.no_prefetch
         depth = max(1, min(args.prefetch_depth, len(dbatches) - 1))
         if args.host_path:
@@ -375,6 +402,7 @@ def main():
         evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
         for i in range(0 if args.host_path else args.steps):
             t += 1
+            prof_on(i)
             evs[i].record(main_stream)
             if prefetch and i + depth < args.steps:
                 dbatches[(i + depth) % len(dbatches)].prepare()  # sorted on the side stream during step i
@@ -386,7 +414,7 @@ def main():
         if not args.host_path:
             median_ms = median_step_ms(evs)
         prof = ctx.profile_read() if args.profile_kernels else {}
-        ctx.profile_enable(False)
+        prof_on.off()
         losses = ctx.loss_history()
         assert np.all(np.isfinite(losses)), "non-finite loss"
         if args.host_path_steps > 0 and not args.host_path:
@@ -439,7 +467,7 @@ def main():
             dist.barrier()
         if args.profile_kernels:
             ctx.profile_reset()
-            ctx.profile_enable(True)
+        prof_on = ProfileSampler(ctx, args)
         t_start = time.perf_counter()
         # batch i + 1's batch-only work (sharded: route, entry exchange and slot sort; replicated: its
         # sort) is enqueued on the side streams behind step i: inside the timed region, off the
@@ -455,6 +483,7 @@ def main():
                 dbatches[j % nb].prepare()
         for i in range(args.steps):
             t += 1
+            prof_on(i)
             if evs:
                 evs[i].record(main_stream)
             h0 = time.perf_counter()
@@ -472,7 +501,7 @@ def main():
         elapsed = time.perf_counter() - t_start
         median_ms = median_step_ms(evs) if evs else None
         prof = ctx.profile_read() if args.profile_kernels else {}
-        ctx.profile_enable(False)
+        prof_on.off()
         losses = ctx.loss_history()
         assert np.all(np.isfinite(losses)), "non-finite loss"
         R = world
@@ -572,6 +601,8 @@ def main():
         if prof:
             kern = {name: {"avg_ms": ms / max(n, 1), "launches": n} for name, (ms, n) in prof.items()}
             line["kernels"] = kern
+            if args.trainer == "lib" and not args.host_path:
+                line["kernels_sampled"] = f"HIP events on every {max(1, args.profile_every)}. timed step (launch streams)"
             if world > 1 or mode != "single":
                 line["kernels_of"] = "local rank 0 (HIP events on its streams)"
             # single table: "forward" gathers, "update" does the row read-modify-write; sharded:
@@ -586,7 +617,7 @@ def main():
                 algo["update"] = upd_b * (1.0 - single_frac)
             dom = max((n for n in kern if n in algo), key=lambda n: kern[n]["avg_ms"])
             ach = algo[dom] / (kern[dom]["avg_ms"] * 1e-3) / 1e9
-            traffic, tsrc = pmc_traffic(F, k, B, dom, fused)
+            traffic, tsrc = pmc_traffic(F, k, B, dom, fused, world)
             line["roofline"] = {"bound": "hbm", "kernel": dom, "achieved": ach, "peak": HBM_PEAK_GBS,
                                 "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "traffic": traffic,
                                 "algorithmic_bytes": algo[dom], "traffic_source": tsrc}

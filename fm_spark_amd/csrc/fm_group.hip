@@ -632,9 +632,11 @@ int step_sharded(fm_ctx* ctx, Group& g, GroupBatch& gb, int32_t t, double step_s
     Pin[l] = std::accumulate(p.pair_in.begin(), p.pair_in.end(), int64_t(0));
     Pout[l] = std::accumulate(p.pair_out.begin(), p.pair_out.end(), int64_t(0));
     ensure_on(r.device, r.partials, sizeof(float) * Pin[l] * W);
-    ensure_on(r.device, r.s_recv, sizeof(float) * Pin[l] * W);
-    ensure_on(r.device, r.part_in, sizeof(float) * Pout[l] * W);
     ensure_on(r.device, r.s_send, sizeof(float) * Pout[l] * W);
+    if (g.R > 1) {  // a one-rank job keeps its pairs where they were written (below)
+      ensure_on(r.device, r.s_recv, sizeof(float) * Pin[l] * W);
+      ensure_on(r.device, r.part_in, sizeof(float) * Pout[l] * W);
+    }
     parts[l] = &r.partials;
     part_in[l] = &r.part_in;
     s_send[l] = &r.s_send;
@@ -642,6 +644,11 @@ int step_sharded(fm_ctx* ctx, Group& g, GroupBatch& gb, int32_t t, double step_s
     pin[l] = p.pair_in.data();
     pout[l] = p.pair_out.data();
   }
+  // R = 1: the owner's pairs are its own batch's, in the same order (Pin = Pout), so the combine
+  // reads the partials where the owner pass wrote them and the update the S rows where the combine
+  // wrote them -- no self copy (as the entries, finish_routes)
+  const bool self = g.R == 1;
+  for (int l = 0; self && l < L; ++l) FM_REQUIRE(Pin[l] == Pout[l], "one-rank job: pair counts differ");
   const int C = xchg_chunks(g);
   if (C > 1) {
     forward_exchange_chunked(g, gb, kp, C, Pin, Pout);
@@ -650,16 +657,20 @@ int step_sharded(fm_ctx* ctx, Group& g, GroupBatch& gb, int32_t t, double step_s
     for (int l = 0; l < L; ++l)
       mcheck(fm_shard_owner_forward(g.ranks[l].m, gb.parts[l].b, g.ranks[l].partials.p), "fm_shard_owner_forward");
     // back to the requesters (owner l -> requester p: the pair_in[l][p] pairs it got from p)
-    a2a_pairs(g, kp, parts, Pin, part_in, Pout, pin, pout);
+    if (!self) a2a_pairs(g, kp, parts, Pin, part_in, Pout, pin, pout);
   }
-  for (int l = 0; l < L; ++l)
-    mcheck(fm_shard_combine(g.ranks[l].m, gb.parts[l].b, g.ranks[l].part_in.p, g.ranks[l].s_send.p), "fm_shard_combine");
+  for (int l = 0; l < L; ++l) {
+    Rank& r = g.ranks[l];
+    mcheck(fm_shard_combine(r.m, gb.parts[l].b, (self ? r.partials : r.part_in).p, r.s_send.p), "fm_shard_combine");
+  }
   // S rows to the owners
-  a2a_pairs(g, kp, s_send, Pout, s_recv, Pin, pout, pin);
-  for (int l = 0; l < L; ++l)
-    mcheck(fm_shard_owner_update(g.ranks[l].m, gb.parts[l].b, g.ranks[l].s_recv.p, t, step_size, reg_param,
+  if (!self) a2a_pairs(g, kp, s_send, Pout, s_recv, Pin, pout, pin);
+  for (int l = 0; l < L; ++l) {
+    Rank& r = g.ranks[l];
+    mcheck(fm_shard_owner_update(r.m, gb.parts[l].b, (self ? r.s_send : r.s_recv).p, t, step_size, reg_param,
                                  gb.global_rows),
            "fm_shard_owner_update");
+  }
   gb.prefetched = false;
   const int64_t e = g.ranks[0].m->epoch - 1;
   reduce_stats(g, e);

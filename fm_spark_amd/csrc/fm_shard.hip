@@ -101,26 +101,24 @@ __global__ __launch_bounds__(kBlock) void k_sample_mask(const int64_t* __restric
 
 // per entry, in CSR order: key = owner << sb | slot and the wire payload {pair index of (sample,
 // owner) within the owner's block, x bits}, so one stable pass over the owner bits lays out the
-// send buffers.  Ids >= F get owner R: they sort after every owner's block and are not sent.
-__global__ __launch_bounds__(kBlock) void k_route_keys(const int64_t* __restrict__ row_ptr,
-                                                       const uint32_t* __restrict__ col,
-                                                       const uint2* __restrict__ ent, int64_t B, uint32_t R, int sb,
-                                                       uint64_t F, const int32_t* __restrict__ pairidx,
-                                                       uint32_t* __restrict__ key, uint2* __restrict__ pay) {
-  constexpr int TPB = kBlock / kTeamR;
-  const int tl = threadIdx.x % kTeamR;
-  for (int64_t s = (int64_t)blockIdx.x * TPB + threadIdx.x / kTeamR; s < B; s += (int64_t)gridDim.x * TPB) {
-    for (int64_t e = row_ptr[s] + tl; e < row_ptr[s + 1]; e += kTeamR) {
-      const uint32_t id = col[e];
-      if (id >= F) {
-        key[e] = R << sb;
-        pay[e] = make_uint2(0u, ent[e].y);
-        continue;
-      }
-      const uint32_t o = id % R;
-      key[e] = (o << sb) | (id / R);
-      pay[e] = make_uint2((uint32_t)pairidx[s * R + o], ent[e].y);
+// send buffers.  Ids >= F get owner R: they sort after every owner's block and are not sent.  One
+// lane per entry: the exploded entry {sample, x} names its sample, so the pass streams the id and
+// entry arrays without the CSR row walk (neighbouring lanes share a sample's pair indices).
+__global__ __launch_bounds__(kBlock) void k_route_keys(const uint32_t* __restrict__ col, const uint2* __restrict__ ent,
+                                                       int64_t N, uint32_t R, int sb, uint64_t F,
+                                                       const int32_t* __restrict__ pairidx, uint32_t* __restrict__ key,
+                                                       uint2* __restrict__ pay) {
+  for (int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x; e < N; e += (int64_t)gridDim.x * kBlock) {
+    const uint32_t id = col[e];
+    const uint2 en = ent[e];
+    if (id >= F) {
+      key[e] = R << sb;
+      pay[e] = make_uint2(0u, en.y);
+      continue;
     }
+    const uint32_t o = id % R;
+    key[e] = (o << sb) | (id / R);
+    pay[e] = make_uint2((uint32_t)pairidx[(int64_t)en.x * R + o], en.y);
   }
 }
 
@@ -510,17 +508,15 @@ void shard_route_launch(fm_ctx* ctx, fm_batch* b, void* send_slot, void* send_en
       if (R == 1 && !drop) {
         // one owner: CSR order is already the owner order and the key is the slot -- the keys and
         // payloads go straight to the send buffers, no partition pass
-        hipLaunchKernelGGL(k_route_keys, dim3(blocks_for(B * kTeamR)), dim3(kBlock), 0, st,
-                           b->dev.row_ptr.as<int64_t>(), b->dev.col.as<uint32_t>(), b->dev.ent.as<uint2>(), B,
-                           (uint32_t)R, sb, F, S.pairidx.as<int32_t>(), reinterpret_cast<uint32_t*>(send_slot),
-                           reinterpret_cast<uint2*>(send_ent));
+        hipLaunchKernelGGL(k_route_keys, dim3(blocks_for(N)), dim3(kBlock), 0, st, b->dev.col.as<uint32_t>(),
+                           b->dev.ent.as<uint2>(), N, (uint32_t)R, sb, F, S.pairidx.as<int32_t>(),
+                           reinterpret_cast<uint32_t*>(send_slot), reinterpret_cast<uint2*>(send_ent));
       } else {
         ctx->sh_pay.ensure(sizeof(uint2) * std::max<int64_t>(N, 4) + 16);
         ctx->sh_skey.ensure(sizeof(uint32_t) * std::max<int64_t>(N, 4) + 16);
-        hipLaunchKernelGGL(k_route_keys, dim3(blocks_for(B * kTeamR)), dim3(kBlock), 0, st,
-                           b->dev.row_ptr.as<int64_t>(), b->dev.col.as<uint32_t>(), b->dev.ent.as<uint2>(), B,
-                           (uint32_t)R, sb, F, S.pairidx.as<int32_t>(), ctx->sh_okey.as<uint32_t>(),
-                           ctx->sh_pay.as<uint2>());
+        hipLaunchKernelGGL(k_route_keys, dim3(blocks_for(N)), dim3(kBlock), 0, st, b->dev.col.as<uint32_t>(),
+                           b->dev.ent.as<uint2>(), N, (uint32_t)R, sb, F, S.pairidx.as<int32_t>(),
+                           ctx->sh_okey.as<uint32_t>(), ctx->sh_pay.as<uint2>());
         radix_sort_pairs64_bits(ctx->route_sort, ctx->sh_okey.as<uint32_t>(), ctx->sh_pay.as<uint2>(), N, sb, sb + ob, st,
                                 ctx->sh_skey.as<uint32_t>(), reinterpret_cast<uint2*>(send_ent));
         hipLaunchKernelGGL(k_key_slots, dim3(blocks_for(N)), dim3(kBlock), 0, st, ctx->sh_skey.as<uint32_t>(), N,

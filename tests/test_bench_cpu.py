@@ -88,3 +88,36 @@ def test_singleton_fraction():
 
     b = Batch(row_ptr=np.array([0, 3, 5]), col=np.array([1, 2, 3, 3, 4], np.int32), val=np.ones(5), label=np.zeros(2))
     assert bench.singleton_fraction([b, b]) == pytest.approx(3 / 4)
+
+
+def test_pmc_traffic_matches_workload_variant_and_mode():
+    # the committed passes: c3 unfused and fused single-table steps, c2 and c5 (profiles/pmc_*.json)
+    t_unf, src_unf = bench.pmc_traffic(100_000_000, 16, 262144, "update", fused=False)
+    t_fus, src_fus = bench.pmc_traffic(100_000_000, 16, 262144, "forward", fused=True)
+    assert t_unf and t_fus and src_unf != src_fus
+    assert bench.pmc_traffic(1_000_000, 16, 65536, "update")[0]  # c5
+    assert bench.pmc_traffic(1_000_000, 8, 65536, "update")[0]  # c2
+    # a sharded owner phase or another world size never borrows the single-table counters
+    assert bench.pmc_traffic(100_000_000, 16, 262144, "owner_update", fused=False, world=8)[0] is None
+    assert bench.pmc_traffic(100_000_000, 16, 262144, "update", fused=False, world=2)[0] is None
+    assert bench.pmc_traffic(123, 16, 262144, "update")[0] is None
+
+
+def test_profile_sampler_toggles_every_nth_step():
+    calls = []
+
+    class Ctx:
+        def profile_enable(self, on):
+            calls.append(on)
+
+    s = bench.ProfileSampler(Ctx(), argparse.Namespace(profile_kernels=1, profile_every=4))
+    for i in range(9):
+        s(i)
+    s.off()
+    assert calls == [True, False, True, False, True, False]
+    calls.clear()
+    s = bench.ProfileSampler(Ctx(), argparse.Namespace(profile_kernels=0, profile_every=4))
+    for i in range(5):
+        s(i)
+    s.off()
+    assert calls == []

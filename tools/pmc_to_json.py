@@ -22,11 +22,22 @@ from collections import defaultdict
 src = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
 out = sys.argv[2] if len(sys.argv) > 2 else None
 meta = json.loads(sys.argv[3]) if len(sys.argv) > 3 else {}
+# meta "timed_steps": N keeps only the last N launches of the once-per-step kernels of the main
+# stream (bench.py's warmup and U-count steps run unprepared batches, i.e. the unfused variant)
+timed = int(meta.get("timed_steps", 0))
+PER_STEP = ("k_forward", "k_segment_update", "k_segment_combine", "k_tag_multi")
 acc = defaultdict(lambda: defaultdict(list))
 for f in sorted(glob.glob(os.path.join(src, "p*", "run_counter_collection.csv")) +
                 glob.glob(os.path.join(src, "p*_counters.csv"))):
+    per = defaultdict(list)
     for r in csv.DictReader(open(f)):
-        acc[r["Kernel_Name"].split("(")[0]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        per[(r["Kernel_Name"].split("(")[0], r["Counter_Name"])].append((int(r.get("Dispatch_Id") or 0),
+                                                                         float(r["Counter_Value"])))
+    for (kn, cn), vals in per.items():
+        vals.sort()
+        if timed and kn in PER_STEP:
+            vals = vals[-timed:]
+        acc[kn][cn] += [v for _, v in vals]
 res = {"source": src, "units": "bytes per launch", **meta, "kernels": {}}
 for k, d in acc.items():
     m = {c: sum(v) / len(v) for c, v in d.items()}
