@@ -98,6 +98,12 @@ constexpr int kPartialU = 4;  // sharded partial pass: passes (entries per lane)
 // lane (measured 1.196 against 1.213 ms per c3 step, 5 runs each on two boxes)
 constexpr int kFwdTeam = 32, kFwdU = 2;
 constexpr int kFwdGrid = 2048;  // forward blocks at most (grid-stride over samples beyond)
+#ifndef FM_XP_FUSE_GRID
+#define FM_XP_FUSE_GRID 2048
+#endif
+#ifndef FM_XP_FUSE_U
+#define FM_XP_FUSE_U 2
+#endif
 
 // Singleton rows.  fm_batch_prepare splits the batch's sorted view into the runs of two or more
 // entries (the only ones that need a per-feature reduction; k_split_*) and the singletons.  At the
@@ -1296,15 +1302,22 @@ void launch_fwd_t(const TableView& T, const BatchDev& b, StepWork& w, const Step
   w.loss_part.ensure(sizeof(double2) * blocks);
   FwdOut tr = xo ? *xo : none;  // train mode: xo->fused = the singleton rows' updates in the forward
   auto kern = k_forward<GS, TEAM, kTrain, U>;
+  dim3 g2 = grid;
   if constexpr (GS <= 4 && TEAM >= 16) {
     if (tr.fused) {
       tr.sp = p;
-      kern = k_forward<GS, TEAM, kTrainFused, U>;
+      kern = k_forward<GS, TEAM, kTrainFused, FM_XP_FUSE_U>;
+      int64_t fb = (b.n_rows + TPB - 1) / TPB;
+      if (fb > FM_XP_FUSE_GRID) fb = FM_XP_FUSE_GRID;
+      if (fb < 1) fb = 1;
+      g2 = dim3((unsigned)fb);
+      *nblk = fb;
+      w.loss_part.ensure(sizeof(double2) * fb);
     }
   } else {
     FM_REQUIRE(!tr.fused, "the fused forward serves kp <= 16");
   }
-  hipLaunchKernelGGL(kern, grid, blk, 0, st, T, b.row_ptr.as<int64_t>(),
+  hipLaunchKernelGGL(kern, g2, blk, 0, st, T, b.row_ptr.as<int64_t>(),
                      b.col.as<uint32_t>(), b.ent.as<uint2>(), b.xs.as<float>(), b.label.as<double>(), b.n_rows, p.w0, p.cumE,
                      w.S.as<float>(), s_rec_yl(T.kp) ? reinterpret_cast<float2*>(w.S.as<float>() + T.kp) : w.yl.as<float2>(),
                      (int64_t)s_rec_floats(T.kp), s_rec_yl(T.kp) ? (int64_t)s_rec_floats(T.kp) / 2 : (int64_t)1,
