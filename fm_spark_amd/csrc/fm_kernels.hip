@@ -102,7 +102,7 @@ constexpr int kFwdGrid = 2048;  // forward blocks at most (grid-stride over samp
 #define FM_XP_FUSE_GRID 2048
 #endif
 #ifndef FM_XP_FUSE_U
-#define FM_XP_FUSE_U 2
+#define FM_XP_FUSE_U 3
 #endif
 
 // Singleton rows.  fm_batch_prepare splits the batch's sorted view into the runs of two or more

@@ -68,11 +68,22 @@ def main():
     # updates, 8 (k + 1) B; the owner forward reads each received entry (slot 4 B + {pair, x} 8 B) and
     # gathers its row 4 (k + 1) B, and writes a partial row per pair ((kp + 4) 4-B words)
     algo = {"owner_update": 8 * (k + 1) * n_upd, "owner_forward": n_in * (12 + 4 * (k + 1)) + P * (kp + 4) * 4}
+    # counted HBM traffic per launch from the committed PMC passes of this command (profiles/pmc_c4.json,
+    # tools/r03_pmc.sh + tools/pmc_to_json.py), when present
+    pmc = {}
+    try:
+        pmc = json.load(open(os.path.join(ROOT, "profiles", "pmc_c4.json"))).get("kernels", {})
+    except (OSError, ValueError):
+        pass
+    kern_of = {"owner_update": ["k_segment_update", "k_segment_combine"], "owner_forward": ["k_forward"]}
     roof = {}
     for name, bytes_ in algo.items():
         if name in phases:
             ach = bytes_ / (phases[name]["avg_ms"] * 1e-3) / 1e9
             roof[name] = {"algorithmic_bytes": bytes_, "achieved_GBs": ach, "frac": ach / HBM_PEAK_GBS}
+            if all("traffic_bytes" in pmc.get(kn, {}) for kn in kern_of[name]):
+                roof[name]["traffic"] = sum(pmc[kn]["traffic_bytes"] for kn in kern_of[name])
+                roof[name]["traffic_source"] = "profiles/pmc_c4.json"
     crit = sum(phases[n]["avg_ms"] for n in ("owner_forward", "combine", "owner_update") if n in phases)
     line = {
         "workload": "c4 per rank: F = 2^31 - 1, k = 32, rank 0 of 8 (268,435,456 rows x 256 B resident), "
