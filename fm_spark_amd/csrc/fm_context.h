@@ -101,6 +101,7 @@ struct fm_batch {
   // sorted view, or -- split = true -- only the runs of two or more entries, split_n = {their
   // count, the number of singleton runs} on the device (the fused step, fm_kernels.hip)
   DevBuf skeys, sents;
+  DevBuf fkeys, fents;  // split on the main stream: the whole sorted view, split by the step
   DevBuf split_n;
   bool split = false;
   hipEvent_t ready = nullptr;     // recorded on the side stream after the prepared sort
@@ -118,6 +119,8 @@ struct fm_batch {
     if (last_use) (void)hipEventDestroy(last_use);
     skeys.release();
     sents.release();
+    fkeys.release();
+    fents.release();
     split_n.release();
     up.release();
     dev.row_ptr.release();

@@ -222,6 +222,7 @@ __global__ __launch_bounds__(kBlock) void k_pair_index(const uint64_t* __restric
 // The received entries are source-major, each source's in its CSR order, carrying their pair's
 // index within that source's block: ent2 = {pair = pbase[source] + local, x}, and the first
 // entry of every pair opens it in pair_ptr (one pass, no scan).
+// ent2 == nullptr (one source: its pairs start at 0, so ent2 would equal ent): the pair table only.
 __global__ void k_pair_table(const uint2* __restrict__ ent, int64_t n, const int64_t* __restrict__ src_off,
                              const int64_t* __restrict__ pbase, int R, int64_t* __restrict__ pair_ptr,
                              uint2* __restrict__ ent2) {
@@ -230,7 +231,7 @@ __global__ void k_pair_table(const uint2* __restrict__ ent, int64_t n, const int
     while (r + 1 < R && src_off[r + 1] <= i) ++r;
     const uint2 e = ent[i];
     const uint32_t pair = (uint32_t)pbase[r] + e.x;
-    ent2[i] = make_uint2(pair, e.y);
+    if (ent2) ent2[i] = make_uint2(pair, e.y);
     if (i == src_off[r] || ent[i - 1].x != e.x) pair_ptr[pair] = i;
   }
 }
@@ -586,11 +587,17 @@ int fm_shard_owner_prepare(fm_ctx* ctx, fm_batch* b, const void* recv_slot, cons
     int64_t* pair_ptr = S.pair_ptr.as<int64_t>();
     // the pair table closes with n (pair_ptr[P])
     FM_HIP_CHECK(hipMemcpyAsync(pair_ptr + P, S.src_off.as<int64_t>() + R, sizeof(int64_t), hipMemcpyDeviceToDevice, st));
+    // the slot sort's payload: {pair index at this owner, x}; one source numbers its pairs from 0,
+    // so the received entries already are that (no copy)
+    const uint2* ent2 = reinterpret_cast<const uint2*>(recv_ent);
     if (n > 0) {
-      ctx->sh_ent2.ensure(sizeof(uint2) * n);
+      if (R > 1) {
+        ctx->sh_ent2.ensure(sizeof(uint2) * n);
+        ent2 = ctx->sh_ent2.as<uint2>();
+      }
       hipLaunchKernelGGL(k_pair_table, dim3(blocks_for(n)), dim3(kBlock), 0, st, reinterpret_cast<const uint2*>(recv_ent),
                          n, S.src_off.as<int64_t>(), S.src_off.as<int64_t>() + (R + 1), R, pair_ptr,
-                         ctx->sh_ent2.as<uint2>());
+                         R > 1 ? ctx->sh_ent2.as<uint2>() : nullptr);
       FM_HIP_CHECK(hipGetLastError());
     }
     FM_HIP_CHECK(hipEventRecord(S.ready_fwd, st));
@@ -600,7 +607,7 @@ int fm_shard_owner_prepare(fm_ctx* ctx, fm_batch* b, const void* recv_slot, cons
       S.sents.ensure(sizeof(uint2) * n);
       const uint32_t* sk = nullptr;
       const uint2* sv = nullptr;
-      radix_sort_pairs64(ctx->side_sort, reinterpret_cast<const uint32_t*>(recv_slot), ctx->sh_ent2.as<uint2>(), n,
+      radix_sort_pairs64(ctx->side_sort, reinterpret_cast<const uint32_t*>(recv_slot), ent2, n,
                          bits_for(std::max<int64_t>(ctx->rows - 1, 1)), st, &sk, &sv, S.skeys.as<uint32_t>(),
                          S.sents.as<uint2>());
     }
