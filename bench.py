@@ -424,7 +424,7 @@ def main():
                          "what": "fm_step with the host CSR each call: 8 B/entry + row_ptr + fp64 labels over PCIe, "
                                  "device-side explode, then the step (two upload slots, copies overlap the previous step)"}
         U_mean = float(np.mean([uniques[i % len(dbatches)] for i in range(args.steps)]))
-        fused = "tag" in prof
+        fused = "split" in prof
         single_frac = singleton_fraction([host_batches[i % len(host_batches)] for i in range(args.steps)])
         parallelism = "single table" + (", fused step (singleton rows updated by the forward)" if fused else "") + \
             ((", next batch sorted during the current step" if depth == 1 else
@@ -609,7 +609,7 @@ def main():
             # "owner_forward" / "owner_update" do the same on the rank's own rows (per rank: the
             # entries an owner receives ~ its own batch's, the rows it updates ~ U / world)
             algo = {"forward": fwd_b, "update": upd_b, "owner_forward": fwd_b, "owner_update": upd_b}
-            fused = "tag" in kern
+            fused = "split" in kern
             if fused:
                 # the fused forward also reads and writes the singleton rows (their 8(k+1) B each of
                 # the update's share); the segmented update keeps the rows with two or more entries

@@ -150,9 +150,6 @@ static Staged stage_csr(fm_ctx* ctx, const fm_csr* c, bool check_range, Pinned& 
 // the 256-MB Infinity Cache, where the update's re-read of the singleton rows goes to HBM -- a
 // cache-resident table re-reads them on-die, and the split and tags would cost more than they save
 // (c2 / c5: 0.245 / 0.273 ms per step fused against 0.184 / 0.208 unfused, profiles/r03_v1).
-#ifndef FM_XP_SPLIT_MAIN
-#define FM_XP_SPLIT_MAIN 0
-#endif
 static bool fuse_on(const fm_ctx* ctx) {
   if (ctx->cfg.fuse_single == FM_FUSE_OFF || ctx->kp > 16 || ctx->cfg.shard_count != 1) return false;
   const double table_bytes = (double)ctx->rows * ctx->stride * sizeof(float);
@@ -279,15 +276,13 @@ int step_impl(fm_ctx* ctx, fm_batch* b, int32_t t, double step_size, double reg_
   if (fused) {
     // the multi tags need the split of this batch (prepared a step or more ahead on the side stream)
     FM_HIP_CHECK(hipStreamWaitEvent(ctx->stream, b->ready, 0));
-    if (FM_XP_SPLIT_MAIN) {
-      e0 = ctx->prof_begin(ctx->stream);
-      launch_split(b->fkeys.as<uint32_t>(), b->fents.as<uint2>(), N, ctx->split_work, b->skeys.as<uint32_t>(),
-                   b->sents.as<uint2>(), b->split_n.as<int64_t>(), ctx->stream);
-      ctx->prof_end("split", e0, ctx->stream);
-    }
+    // the split of the sorted view into its multi runs, each multi row tagged as its run is found;
+    // on the main stream (the side queue is the busier one: it carries every batch's sort), and
+    // at the step because the tags name this step's epoch
     e0 = ctx->prof_begin(ctx->stream);
-    launch_tag_multi(T, skeys, b->split_n.as<int64_t>(), N, p.epoch, ctx->stream);
-    ctx->prof_end("tag", e0, ctx->stream);
+    launch_split(b->fkeys.as<uint32_t>(), b->fents.as<uint2>(), N, ctx->split_work, b->skeys.as<uint32_t>(),
+                 b->sents.as<uint2>(), b->split_n.as<int64_t>(), ctx->stream, &T, p.epoch);
+    ctx->prof_end("split", e0, ctx->stream);
     fx.fused = true;
   }
   e0 = ctx->prof_begin(ctx->stream);
@@ -601,20 +596,13 @@ int fm_batch_prepare(fm_ctx* ctx, fm_batch* b) {
     const uint32_t* sk = nullptr;
     const uint2* sv = nullptr;
     b->split = fuse_on(ctx);
-    if (b->split && FM_XP_SPLIT_MAIN) {
-      // sorted into the batch's own buffers; the step splits them on the main stream
+    if (b->split) {
+      // sorted into the batch's own buffers; the step splits them into the multi runs (skeys / sents)
       b->fkeys.ensure(sizeof(uint32_t) * N);
       b->fents.ensure(sizeof(uint2) * N);
       b->split_n.ensure(2 * sizeof(int64_t));
       radix_sort_pairs64(ctx->work.sort, b->dev.col.as<uint32_t>(), b->dev.ent.as<uint2>(), N, bits_for(ctx->rows - 1),
                          ctx->side, &sk, &sv, b->fkeys.as<uint32_t>(), b->fents.as<uint2>());
-    } else if (b->split) {
-      // sorted in the workspace, then only the runs of two or more entries kept in the batch's view
-      radix_sort_pairs64(ctx->work.sort, b->dev.col.as<uint32_t>(), b->dev.ent.as<uint2>(), N, bits_for(ctx->rows - 1),
-                         ctx->side, &sk, &sv);
-      b->split_n.ensure(2 * sizeof(int64_t));
-      launch_split(sk, sv, N, ctx->split_work, b->skeys.as<uint32_t>(), b->sents.as<uint2>(), b->split_n.as<int64_t>(),
-                   ctx->side);
     } else {
       radix_sort_pairs64(ctx->work.sort, b->dev.col.as<uint32_t>(), b->dev.ent.as<uint2>(), N, bits_for(ctx->rows - 1),
                          ctx->side, &sk, &sv, b->skeys.as<uint32_t>(), b->sents.as<uint2>());

@@ -173,7 +173,7 @@ struct fm_ctx {
   DevBuf sh_ent2;      // [n] uint2 {pair, x bits}: the slot sort's payload
   SortWork side_sort;  // radix sort workspace of the side stream
   SortWork route_sort;  // the route's owner partition (fm_shard_route)
-  SplitWork split_work;  // fm_batch_prepare's singleton split (side stream)
+  SplitWork split_work;  // the fused step's split of its batch's sorted view (main stream)
   Pinned side_pinned;  // route counts (device -> host)
   // replicated step state (fm_repl_*)
   DevBuf repl_cnt;            // touched-row counts per apply block (uint32)

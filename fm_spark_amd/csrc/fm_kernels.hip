@@ -98,17 +98,15 @@ constexpr int kPartialU = 4;  // sharded partial pass: passes (entries per lane)
 // lane (measured 1.196 against 1.213 ms per c3 step, 5 runs each on two boxes)
 constexpr int kFwdTeam = 32, kFwdU = 2;
 constexpr int kFwdGrid = 2048;  // forward blocks at most (grid-stride over samples beyond)
-#ifndef FM_XP_FUSE_GRID
-#define FM_XP_FUSE_GRID 2048
-#endif
-#ifndef FM_XP_FUSE_U
-#define FM_XP_FUSE_U 3
-#endif
+// the fused forward (kTrainFused): 3 passes in flight (24 rows per sample at k = 16, so a 39-entry
+// sample takes two rounds instead of three); c3 step -2 to -4 % against 2 passes, 4 passes slower
+// (tools/r03_xp2.sh, profiles/r03_v7/ab)
+constexpr int kFuseU = 3;
 
-// Singleton rows.  fm_batch_prepare splits the batch's sorted view into the runs of two or more
-// entries (the only ones that need a per-feature reduction; k_split_*) and the singletons.  At the
-// start of the step k_tag_multi marks every row with two or more entries in the row header's t
-// field, the word that otherwise only says present (t >= 0) or absent (t = -1):
+// Singleton rows.  fm_batch_prepare sorts the batch (side stream); at the start of the step the
+// split (k_split_*, main stream) keeps the runs of two or more entries (the only ones that need a
+// per-feature reduction) and marks every such row in the row header's t field, the word that
+// otherwise only says present (t >= 0) or absent (t = -1):
 //   present, multi at epoch E : t = kTagPresent + (E & kTagMask)   (>= 2^30; normal t < 2^30)
 //   absent,  multi at epoch E : t = -2 - (E & kTagMask)            (<= -2: still "absent")
 // so every reader that asks t >= 0 is unchanged, and the fused forward, which loads the header of
@@ -1302,22 +1300,15 @@ void launch_fwd_t(const TableView& T, const BatchDev& b, StepWork& w, const Step
   w.loss_part.ensure(sizeof(double2) * blocks);
   FwdOut tr = xo ? *xo : none;  // train mode: xo->fused = the singleton rows' updates in the forward
   auto kern = k_forward<GS, TEAM, kTrain, U>;
-  dim3 g2 = grid;
   if constexpr (GS <= 4 && TEAM >= 16) {
     if (tr.fused) {
       tr.sp = p;
-      kern = k_forward<GS, TEAM, kTrainFused, FM_XP_FUSE_U>;
-      int64_t fb = (b.n_rows + TPB - 1) / TPB;
-      if (fb > FM_XP_FUSE_GRID) fb = FM_XP_FUSE_GRID;
-      if (fb < 1) fb = 1;
-      g2 = dim3((unsigned)fb);
-      *nblk = fb;
-      w.loss_part.ensure(sizeof(double2) * fb);
+      kern = k_forward<GS, TEAM, kTrainFused, kFuseU>;
     }
   } else {
     FM_REQUIRE(!tr.fused, "the fused forward serves kp <= 16");
   }
-  hipLaunchKernelGGL(kern, g2, blk, 0, st, T, b.row_ptr.as<int64_t>(),
+  hipLaunchKernelGGL(kern, grid, blk, 0, st, T, b.row_ptr.as<int64_t>(),
                      b.col.as<uint32_t>(), b.ent.as<uint2>(), b.xs.as<float>(), b.label.as<double>(), b.n_rows, p.w0, p.cumE,
                      w.S.as<float>(), s_rec_yl(T.kp) ? reinterpret_cast<float2*>(w.S.as<float>() + T.kp) : w.yl.as<float2>(),
                      (int64_t)s_rec_floats(T.kp), s_rec_yl(T.kp) ? (int64_t)s_rec_floats(T.kp) / 2 : (int64_t)1,
@@ -1576,18 +1567,24 @@ __global__ __launch_bounds__(kBlock) void k_explode(const int64_t* __restrict__ 
 // its offset in order (ballot ranks).  Integer work only: deterministic.
 constexpr int kSplitChunk = 1024;
 
+// entry p of the sorted view belongs to a run of two or more (multi); *first: it opens its run
 __device__ __forceinline__ bool split_multi(const uint32_t* __restrict__ skeys, int64_t N, int64_t p, uint32_t key,
-                                            int lane) {
+                                            int lane, bool* first = nullptr) {
   uint32_t prev = __shfl_up(key, 1), next = __shfl_down(key, 1);
   if (lane == 0) prev = p > 0 && p <= N ? skeys[p - 1] : 0xFFFFFFFFu;
   if (lane == 63) next = p + 1 < N ? skeys[p + 1] : 0xFFFFFFFFu;
   if (p == 0) prev = 0xFFFFFFFFu;      // (lane 0 only)
   if (p + 1 >= N) next = 0xFFFFFFFFu;  // the last entry has no successor
+  if (first) *first = prev != key;
   return p < N && (prev == key || next == key);
 }
 
+// TAG (the split at the step's start, main stream): the first entry of every multi run also writes
+// the epoch's multi tag into its row's header
+template <bool TAG>
 __global__ __launch_bounds__(kBlock) void k_split_count(const uint32_t* __restrict__ skeys, int64_t N,
-                                                        uint2* __restrict__ cnt, int64_t nchunks) {
+                                                        uint2* __restrict__ cnt, int64_t nchunks, TableView T,
+                                                        int32_t epoch) {
   const int lane = threadIdx.x & 63;
   const int64_t c = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
   if (c >= nchunks) return;  // wave-uniform
@@ -1595,7 +1592,12 @@ __global__ __launch_bounds__(kBlock) void k_split_count(const uint32_t* __restri
   for (int r = 0; r < kSplitChunk / 64; ++r) {
     const int64_t p = c * kSplitChunk + r * 64 + lane;
     const uint32_t key = p < N ? skeys[p] : 0xFFFFFFFEu;
-    const bool m = split_multi(skeys, N, p, key, lane);
+    bool first = false;
+    const bool m = split_multi(skeys, N, p, key, lane, &first);
+    if (TAG && m && first) {
+      int32_t* t = &T.hdr(key)->t;
+      *t = multi_tag(epoch, *t >= 0);
+    }
     nm += (uint32_t)__popcll(__ballot(m));
     ns += (uint32_t)__popcll(__ballot(p < N && !m));
   }
@@ -1663,21 +1665,8 @@ __global__ __launch_bounds__(kBlock) void k_split_scatter(const uint32_t* __rest
   }
 }
 
-// At the step's start (main stream, after the previous step's writes): the header of every row
-// with two or more entries gets the epoch's multi tag (the t word only; see "Singleton rows").
-__global__ __launch_bounds__(kBlock) void k_tag_multi(TableView T, const uint32_t* __restrict__ mkeys,
-                                                      const int64_t* __restrict__ n_dev, int32_t epoch) {
-  const int64_t n = n_dev[0];
-  for (int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x; p < n; p += (int64_t)gridDim.x * kBlock) {
-    const uint32_t key = mkeys[p];
-    if (p > 0 && mkeys[p - 1] == key) continue;
-    int32_t* t = &T.hdr(key)->t;
-    *t = multi_tag(epoch, *t >= 0);
-  }
-}
-
 void launch_split(const uint32_t* skeys, const uint2* sents, int64_t N, SplitWork& sw, uint32_t* mkeys, uint2* ments,
-                  int64_t* n_out, hipStream_t st) {
+                  int64_t* n_out, hipStream_t st, const TableView* tag_T, int32_t epoch) {
   const int64_t nchunks = (N + kSplitChunk - 1) / kSplitChunk;
   sw.cnt.ensure(sizeof(uint2) * (size_t)std::max<int64_t>(nchunks, 1));
   sw.off.ensure(sizeof(int64_t) * (size_t)std::max<int64_t>(nchunks, 1));
@@ -1686,19 +1675,18 @@ void launch_split(const uint32_t* skeys, const uint2* sents, int64_t N, SplitWor
     return;
   }
   const unsigned blocks = (unsigned)((nchunks + kBlock / 64 - 1) / (kBlock / 64));
-  hipLaunchKernelGGL(k_split_count, dim3(blocks), dim3(kBlock), 0, st, skeys, N, sw.cnt.as<uint2>(), nchunks);
+  if (tag_T)
+    hipLaunchKernelGGL(k_split_count<true>, dim3(blocks), dim3(kBlock), 0, st, skeys, N, sw.cnt.as<uint2>(), nchunks,
+                       *tag_T, epoch);
+  else
+    hipLaunchKernelGGL(k_split_count<false>, dim3(blocks), dim3(kBlock), 0, st, skeys, N, sw.cnt.as<uint2>(), nchunks,
+                       TableView{}, 0);
   hipLaunchKernelGGL(k_split_scan, dim3(1), dim3(1024), 0, st, sw.cnt.as<uint2>(), nchunks, sw.off.as<int64_t>(), n_out);
   hipLaunchKernelGGL(k_split_scatter, dim3(blocks), dim3(kBlock), 0, st, skeys, sents, N, sw.off.as<int64_t>(), nchunks,
                      mkeys, ments);
   FM_HIP_CHECK(hipGetLastError());
 }
 
-void launch_tag_multi(const TableView& T, const uint32_t* mkeys, const int64_t* n_dev, int64_t n_max, int32_t epoch,
-                      hipStream_t st) {
-  if (n_max <= 0) return;
-  hipLaunchKernelGGL(k_tag_multi, dim3(grid_for(n_max, kBlock, 256 * 8)), dim3(kBlock), 0, st, T, mkeys, n_dev, epoch);
-  FM_HIP_CHECK(hipGetLastError());
-}
 
 void launch_explode(const int64_t* row_ptr_in, const double* label_in, const int32_t* xoff, const uint32_t* col_in,
                     const float* x_in, int64_t B, int64_t N, int64_t* row_ptr, double* label, uint32_t* col, uint2* ent,

@@ -39,7 +39,7 @@ def single(gpu):
 
 def test_fused_single_table_trains_the_same_model(single):
     fused = _bench("--fuse", "on")
-    assert "tag" in fused["kernels"] and "tag" not in single["kernels"]
+    assert "split" in fused["kernels"] and "split" not in single["kernels"]
     assert fused["loss_sum_all_steps"] == pytest.approx(single["loss_sum_all_steps"], rel=1e-6)
 
 
