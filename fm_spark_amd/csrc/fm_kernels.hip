@@ -1605,20 +1605,31 @@ __global__ __launch_bounds__(kBlock) void k_split_count(const uint32_t* __restri
 }
 
 // one block: exclusive scan of the chunks' multi counts -> off[c]; totals -> n_out[0] (multi
-// entries), n_out[1] (singleton runs)
+// entries), n_out[1] (singleton runs).  It sits on the step's critical path (main stream, before
+// the forward), so each thread loads its kSplitPer consecutive chunk counts of a round at once: one
+// memory round trip per 16K chunks (a 16.7M-entry batch), not one per 1024.
+constexpr int kSplitPer = 16;
 __global__ __launch_bounds__(1024) void k_split_scan(const uint2* __restrict__ cnt, int64_t nchunks,
                                                      int64_t* __restrict__ off, int64_t* __restrict__ n_out) {
   __shared__ int64_t wsum[16], ssum[16];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   int64_t carry = 0, singles = 0;
-  for (int64_t b = 0; b < nchunks; b += 1024) {
-    const int64_t i = b + threadIdx.x;
-    const uint2 v = i < nchunks ? cnt[i] : make_uint2(0u, 0u);
-    int64_t incl = v.x, sg = v.y;
+  for (int64_t b = 0; b < nchunks; b += 1024 * kSplitPer) {
+    const int64_t i0 = b + (int64_t)threadIdx.x * kSplitPer;
+    uint2 v[kSplitPer];
+#pragma unroll
+    for (int j = 0; j < kSplitPer; ++j) v[j] = i0 + j < nchunks ? cnt[i0 + j] : make_uint2(0u, 0u);
+    int64_t t = 0, sg = 0;
+#pragma unroll
+    for (int j = 0; j < kSplitPer; ++j) {
+      t += v[j].x;
+      sg += v[j].y;
+    }
+    int64_t incl = t;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
-      const int64_t t = __shfl_up(incl, o);
-      if (lane >= o) incl += t;
+      const int64_t u = __shfl_up(incl, o);
+      if (lane >= o) incl += u;
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) sg += __shfl_xor(sg, o);
@@ -1631,7 +1642,12 @@ __global__ __launch_bounds__(1024) void k_split_scan(const uint2* __restrict__ c
       tot += wsum[w];
       stot += ssum[w];
     }
-    if (i < nchunks) off[i] = carry + wpre + incl - (int64_t)v.x;
+    int64_t run = carry + wpre + incl - t;
+#pragma unroll
+    for (int j = 0; j < kSplitPer; ++j) {
+      if (i0 + j < nchunks) off[i0 + j] = run;
+      run += v[j].x;
+    }
     carry += tot;
     singles += stot;
     __syncthreads();
