@@ -188,6 +188,41 @@ def pmc_traffic(F, k, B, phase, fused=False, world=1):
     return None, None
 
 
+def sort_passes(num_rows):
+    """Digit passes of the feature-slot radix sort (fm_sort.hip digit_bits: at most 10-bit digits,
+    spread evenly, never narrower than 9 bits)."""
+    kb = max(1, int(num_rows - 1).bit_length())
+    p = -(-kb // 10)
+    rb = max(9, -(-kb // p))
+    return -(-kb // rb)
+
+
+def step_traffic(F, k, B, fused):
+    """Counted HBM bytes of one whole single-table step: every kernel's per-launch traffic in the
+    committed PMC passes of this workload times its launches per step (the sort's kernels once per
+    digit pass).  None unless every kernel of the step was counted."""
+    import glob
+
+    per_step = {"k_forward": 1, "k_segment_update": 1, "k_segment_combine": 1}
+    n = sort_passes(F)
+    per_step.update({"k_radix_count": n, "k_radix_scan_rows": n, "k_radix_scatter": n})
+    if fused:
+        per_step.update({"k_split_count": 1, "k_split_scan": 1, "k_split_scatter": 1})
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json"))):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if (d.get("num_features"), d.get("k"), d.get("batch_rows"), bool(d.get("fused", False)),
+                d.get("mode", "single"), d.get("world", 1)) != (F, k, B, fused, "single", 1):
+            continue
+        ks = d.get("kernels", {})
+        if all("traffic_bytes" in ks.get(kn, {}) for kn in per_step):
+            return (sum(ks[kn]["traffic_bytes"] * c for kn, c in per_step.items()),
+                    os.path.relpath(f, ROOT) + " (" + d.get("build", "") + ")")
+    return None, None
+
+
 def cpu_baseline(cfg, batch, steps):
     """The fp64 C restatement (oracle/fm_oracle.c, OpenMP) timed on this host's cores on a
     bounded sample of the same workload: `steps` mini-batch steps over the full table."""
@@ -625,6 +660,12 @@ def main():
             line["step_roofline"] = {"bytes_per_step": step_bytes,
                                      "achieved_GBs": step_bytes / (ms_per_step * 1e-3) / 1e9,
                                      "frac": step_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS}
+            if mode == "single":
+                st_t, st_src = step_traffic(F, k, B, fused)
+                if st_t:  # every kernel of the step, counted (PMC), against the step's time
+                    line["step_roofline"].update(traffic=st_t, traffic_GBs=st_t / (ms_per_step * 1e-3) / 1e9,
+                                                 traffic_frac=st_t / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                                                 traffic_source=st_src)
         if xg is not None:
             step_s = (median_ms or ms_per_step) * 1e-3
             if "entries_B" in xg:

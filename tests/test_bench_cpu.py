@@ -121,3 +121,13 @@ def test_profile_sampler_toggles_every_nth_step():
         s(i)
     s.off()
     assert calls == []
+
+
+def test_sort_passes_follow_the_digit_plan():
+    # fm_sort.hip digit_bits: 27-bit slots 3 x 9, 20-bit 2 x 10, 24-bit 3 x 9 (8 is below the minimum
+    # digit), 30-bit 3 x 10, 31-bit 4 x 9 (rounded up to the 9-bit minimum: 4 passes)
+    assert bench.sort_passes(100_000_000) == 3
+    assert bench.sort_passes(1_000_000) == 2
+    assert bench.sort_passes(1 << 24) == 3
+    assert bench.sort_passes(1 << 30) == 3
+    assert bench.sort_passes(1 << 31) == 4
