@@ -123,8 +123,11 @@ __device__ __forceinline__ bool is_multi(int32_t t, int32_t epoch) {
   return t >= kTagPresent ? t - kTagPresent == e : (t <= -2 && -2 - t == e);
 }
 
+#ifndef FM_XP_FWD_WAVES
+#define FM_XP_FWD_WAVES 1
+#endif
 template <int GS, int TEAM, int MODE, int U>
-__global__ __launch_bounds__(kBlock) void k_forward(TableView T, const int64_t* __restrict__ row_ptr,
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FM_XP_FWD_WAVES))) void k_forward(TableView T, const int64_t* __restrict__ row_ptr,
                                                     const uint32_t* __restrict__ col,
                                                     const uint2* __restrict__ ent, const float* __restrict__ xs,
                                                     const double* __restrict__ label, int64_t B,
