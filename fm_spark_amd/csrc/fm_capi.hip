@@ -274,7 +274,7 @@ int step_impl(fm_ctx* ctx, fm_batch* b, int32_t t, double step_size, double reg_
   hipEvent_t e0 = nullptr;
   FwdOut fx{};
   if (fused) {
-    // the multi tags need the split of this batch (prepared a step or more ahead on the side stream)
+    // the batch's sort (fm_batch_prepare, a step or more ahead on the side stream)
     FM_HIP_CHECK(hipStreamWaitEvent(ctx->stream, b->ready, 0));
     // the split of the sorted view into its multi runs, each multi row tagged as its run is found;
     // on the main stream (the side queue is the busier one: it carries every batch's sort), and
