@@ -124,13 +124,12 @@ __device__ __forceinline__ bool is_multi(int32_t t, int32_t epoch) {
 }
 
 // The fused forward at 5 waves per SIMD (96 VGPRs, a few spilled; 107 and 4 waves unbounded):
-// c3 step 0.98 against 1.03 ms, three alternating A/B pairs (profiles/r03_v9/ab).  Its latency-bound
-// gathers want waves in flight more than registers.  The other modes keep the compiler's choice.
-#ifndef FM_XP_FUSED_WAVES
-#define FM_XP_FUSED_WAVES 5
-#endif
+// c3 step 0.98 against 1.03 ms in three alternating A/B pairs on one box, 0.989 against 1.003-1.009
+// on another; 6 waves (80 VGPRs, more spills) 1.066 (profiles/r03_v9/ab, r03_v10/ab).  Its
+// latency-bound gathers want waves in flight more than registers.  The other modes keep the
+// compiler's choice.
 template <int MODE>
-constexpr int fwd_min_waves() { return MODE == kTrainFused ? FM_XP_FUSED_WAVES : 1; }
+constexpr int fwd_min_waves() { return MODE == kTrainFused ? 5 : 1; }
 template <int GS, int TEAM, int MODE, int U>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(fwd_min_waves<MODE>())))
 void k_forward(TableView T, const int64_t* __restrict__ row_ptr,

@@ -29,9 +29,6 @@ constexpr int kMinRB = 9;    // the block scans hold R / kBlock >= 1 digits per 
 constexpr int kRounds = 8;   // keys per thread per tile
 constexpr int kTile = kBlock * kRounds;  // 4096 keys per tile
 constexpr int kMaxRadix = 1 << kMaxRB;
-#ifndef FM_XP_SCAN_WAVE
-#define FM_XP_SCAN_WAVE 0
-#endif
 
 // Tile of a block: the tiles of one XCD (blocks b = x mod 8 are dispatched to XCD x) are
 // contiguous, so a digit's runs written by neighbouring tiles meet in the same L2 and leave it as
@@ -111,38 +108,6 @@ __global__ __launch_bounds__(kBlock) void k_radix_scan_rows(uint32_t* __restrict
     lds_barrier();
   }
   if (threadIdx.x == 0) digit_tot[blockIdx.x] = carry;
-}
-
-// One wave per digit row (4 rows per 256-thread block): each lane loads its kScanPer consecutive
-// tile counts of a round at once and the wave scans their sums -- one memory round trip per 64 x
-// kScanPer tiles and no block barrier (the block-per-row scan takes two to five dependent rounds
-// with barriers, 20-35 us per pass beside the step's kernels at c2 / c5).
-constexpr int kScanPer = 16;
-__global__ __launch_bounds__(256) void k_radix_scan_rows_w(uint32_t* __restrict__ counts, int64_t ntiles, int R,
-                                                          uint32_t* __restrict__ digit_tot) {
-  const int lane = threadIdx.x & 63;
-  const int d = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (d >= R) return;  // wave-uniform
-  uint32_t* row = counts + (int64_t)d * ntiles;
-  uint32_t carry = 0;
-  for (int64_t b = 0; b < ntiles; b += 64 * kScanPer) {
-    const int64_t i0 = b + (int64_t)lane * kScanPer;
-    uint32_t v[kScanPer];
-#pragma unroll
-    for (int j = 0; j < kScanPer; ++j) v[j] = i0 + j < ntiles ? row[i0 + j] : 0u;
-    uint32_t t = 0;
-#pragma unroll
-    for (int j = 0; j < kScanPer; ++j) t += v[j];
-    const uint32_t incl = wave_incl_scan_u32(t, lane);
-    uint32_t run = carry + incl - t;
-#pragma unroll
-    for (int j = 0; j < kScanPer; ++j) {
-      if (i0 + j < ntiles) row[i0 + j] = run;
-      run += v[j];
-    }
-    carry += __shfl(incl, 63);
-  }
-  if (lane == 0) digit_tot[d] = carry;
 }
 
 // Block-wide exclusive scan of R values held as D = R / kBlock consecutive values per thread.
@@ -320,11 +285,7 @@ static void radix_pass_impl(const uint32_t* kin, const P* vin, uint32_t* ko, P* 
                        SortWork& w, int64_t ntiles, hipStream_t st) {
   hipLaunchKernelGGL(k_radix_count<RB>, dim3((unsigned)blocks_for_tiles(ntiles)), dim3(kBlock), 0, st, kin, n, shift,
                      w.counts.as<uint32_t>(), ntiles);
-  if (FM_XP_SCAN_WAVE)
-    hipLaunchKernelGGL(k_radix_scan_rows_w, dim3((1u << RB) / 4), dim3(256), 0, st, w.counts.as<uint32_t>(), ntiles,
-                       1 << RB, w.digit_tot.as<uint32_t>());
-  else
-    hipLaunchKernelGGL(k_radix_scan_rows, dim3(1u << RB), dim3(kBlock), 0, st, w.counts.as<uint32_t>(), ntiles,
+  hipLaunchKernelGGL(k_radix_scan_rows, dim3(1u << RB), dim3(kBlock), 0, st, w.counts.as<uint32_t>(), ntiles,
                        w.digit_tot.as<uint32_t>());
   hipLaunchKernelGGL((k_radix_scatter<P, RB>), dim3((unsigned)blocks_for_tiles(ntiles)), dim3(kBlock), 0, st, kin,
                      vin, ko, vo, n, shift, w.counts.as<uint32_t>(), w.digit_tot.as<uint32_t>(), ntiles);
