@@ -543,7 +543,10 @@ struct UpdGeom {
 //    k_segment_combine.  Every sum runs in a fixed order: the step is bitwise reproducible.
 // k <= 64 (NF = 1): waves per SIMD the register allocation must allow (4 blocks/CU); without it the
 // compiler took 130 VGPRs at k = 16 (3 waves/SIMD): update -8.6 %, step -1.7 % (A/B 3 x 40 steps)
-constexpr int kUpdMinW = 4;
+#ifndef FM_XP_UPD_MINW
+#define FM_XP_UPD_MINW 4
+#endif
+constexpr int kUpdMinW = FM_XP_UPD_MINW;
 template <int Q, int NF, int D0>
 __global__ __launch_bounds__(kBlock, NF == 1 ? kUpdMinW : 1) void k_segment_update(SegArgs a) {
   using Geo = UpdGeom<Q, NF>;
