@@ -543,10 +543,9 @@ struct UpdGeom {
 //    k_segment_combine.  Every sum runs in a fixed order: the step is bitwise reproducible.
 // k <= 64 (NF = 1): waves per SIMD the register allocation must allow (4 blocks/CU); without it the
 // compiler took 130 VGPRs at k = 16 (3 waves/SIMD): update -8.6 %, step -1.7 % (A/B 3 x 40 steps)
-#ifndef FM_XP_UPD_MINW
-#define FM_XP_UPD_MINW 4
-#endif
-constexpr int kUpdMinW = FM_XP_UPD_MINW;
+// (round 3: 5 waves, 96 VGPRs with 32 B/lane spilled at k = 16, measured 0.981-0.984 against
+// 0.986-0.990 ms at c3 and 0.192-0.193 against 0.194-0.195 at c5: within the noise, not taken)
+constexpr int kUpdMinW = 4;
 template <int Q, int NF, int D0>
 __global__ __launch_bounds__(kBlock, NF == 1 ? kUpdMinW : 1) void k_segment_update(SegArgs a) {
   using Geo = UpdGeom<Q, NF>;
