@@ -430,16 +430,21 @@ def main():
                 t += 1
                 ctx.step(hosts[i % len(hosts)], t, STEP_SIZE, REG_PARAM, sync=False)
         else:
+            # the pipeline in its steady state: the batches of the first `depth` timed steps were
+            # sorted before the timed region (as the steps before them would have, in a training
+            # loop), and every timed step sorts the batch `depth` steps ahead -- K steps and K sorts
+            # inside the timed region, the last `depth` of them for batches stepped after it
+            if prefetch:
+                for j in range(depth):
+                    dbatches[j % len(dbatches)].prepare()
+                ctx.sync()
             t_start = time.perf_counter()
-        if prefetch and not args.host_path:
-            for j in range(min(depth, args.steps)):
-                dbatches[j % len(dbatches)].prepare()  # every batch's sort runs inside the timed region
         evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
         for i in range(0 if args.host_path else args.steps):
             t += 1
             prof_on(i)
             evs[i].record(main_stream)
-            if prefetch and i + depth < args.steps:
+            if prefetch:
                 dbatches[(i + depth) % len(dbatches)].prepare()  # sorted on the side stream during step i
             ctx.step_batch(dbatches[i % len(dbatches)], t, STEP_SIZE, REG_PARAM, sync=False)
         evs[args.steps].record(main_stream)
@@ -503,19 +508,27 @@ def main():
         if args.profile_kernels:
             ctx.profile_reset()
         prof_on = ProfileSampler(ctx, args)
+        # sharded, fm_batch_prepare is two-phase: it enqueues the batch's route and count gather, and
+        # reads the counts of the batch prepared before it (exchange + owner slot sort on the side
+        # streams); depth 2 gives each route a whole step to finish before the host reads its counts.
+        # The pipeline in its steady state: the first `depth` timed steps' batches were prepared
+        # before the timed region, and every timed step prepares the batch `depth` steps ahead (K
+        # steps and K prepares inside the timed region)
+        depth = max(1, min(args.prefetch_depth, nb - 1))
+        if prefetch:
+            for j in range(depth):
+                dbatches[j % nb].prepare()
+            ctx.sync()
+            for d in pl["devices"]:
+                torch.cuda.synchronize(d)
+            if dist is not None:
+                dist.barrier()
         t_start = time.perf_counter()
-        # batch i + 1's batch-only work (sharded: route, entry exchange and slot sort; replicated: its
-        # sort) is enqueued on the side streams behind step i: inside the timed region, off the
+        # batch i + depth's batch-only work (sharded: route, entry exchange and slot sort; replicated:
+        # its sort) is enqueued on the side streams behind step i: inside the timed region, off the
         # critical path
         evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)] if main_stream else None
         h_step, h_prep = [], []  # host time in each call: the GPU never waits on the host if their sum < the step
-        # sharded, fm_batch_prepare is two-phase: it enqueues the batch's route and count gather, and
-        # reads the counts of the batch prepared before it (exchange + owner slot sort on the side
-        # streams); depth 2 gives each route a whole step to finish before the host reads its counts
-        depth = max(1, min(args.prefetch_depth, nb - 1))
-        if prefetch:
-            for j in range(min(depth, args.steps)):
-                dbatches[j % nb].prepare()
         for i in range(args.steps):
             t += 1
             prof_on(i)
@@ -524,7 +537,7 @@ def main():
             h0 = time.perf_counter()
             ctx.step_batch(dbatches[i % nb], t, STEP_SIZE, REG_PARAM, sync=False)
             h1 = time.perf_counter()
-            if prefetch and i + depth < args.steps:
+            if prefetch:
                 dbatches[(i + depth) % nb].prepare()
                 h_prep.append(time.perf_counter() - h1)
             h_step.append(h1 - h0)
@@ -633,6 +646,10 @@ def main():
                        "launch": mode},
             "loss_sum_all_steps": float(np.sum(losses)),
         }
+        if args.trainer == "lib" and not args.host_path and not args.no_prefetch:
+            line["timed_work"] = (f"{args.steps} steps and {args.steps} batch preparations (sorts / routes) inside the "
+                                  f"timed region: the pipeline in its steady state, each step preparing the batch "
+                                  f"{depth} steps ahead (the first {depth} timed steps' batches were prepared before it)")
         if prof:
             kern = {name: {"avg_ms": ms / max(n, 1), "launches": n} for name, (ms, n) in prof.items()}
             line["kernels"] = kern
