@@ -198,7 +198,6 @@ struct SplitWork {
 void launch_split(const uint32_t* skeys, const uint2* sents, int64_t N, SplitWork& sw, uint32_t* mkeys, uint2* ments,
                   int64_t* n_out, hipStream_t st,
                   const TableView* tag_T = nullptr, int32_t epoch = 0);
-// the step's multi tags: every row starting a run of mkeys[0 .. n_dev[0]) (n_max: host bound)
 void launch_segment_update(const TableView& T, int64_t N, const SegSource& src, StepWork& w, const StepParams& p,
                            const uint32_t* skeys, const uint2* sents, int64_t n_loss_blocks, double* stats_out,
                            hipStream_t st, float* emit = nullptr);

@@ -128,10 +128,11 @@ __device__ __forceinline__ bool is_multi(int32_t t, int32_t epoch) {
 // on another; 6 waves (80 VGPRs, more spills) 1.066 (profiles/r03_v9/ab, r03_v10/ab).  Its
 // latency-bound gathers want waves in flight more than registers.  The other modes keep the
 // compiler's choice.
-template <int MODE>
-constexpr int fwd_min_waves() { return MODE == kTrainFused ? 5 : 1; }
+template <int MODE, int GS>
+constexpr int fwd_min_waves() { return MODE == kTrainFused && GS == 4 ? 5 : 1; }  // k = 9..16 (smaller
+// k: the stash's LDS holds the block count below 5 waves anyway)
 template <int GS, int TEAM, int MODE, int U>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(fwd_min_waves<MODE>())))
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(fwd_min_waves<MODE, GS>())))
 void k_forward(TableView T, const int64_t* __restrict__ row_ptr,
                                                     const uint32_t* __restrict__ col,
                                                     const uint2* __restrict__ ent, const float* __restrict__ xs,
@@ -1619,12 +1620,17 @@ __global__ __launch_bounds__(kBlock) void k_split_count(const uint32_t* __restri
 // the forward), so each thread loads its kSplitPer consecutive chunk counts of a round at once: one
 // memory round trip per 16K chunks (a 16.7M-entry batch), not one per 1024.
 constexpr int kSplitPer = 16;
-__global__ __launch_bounds__(1024) void k_split_scan(const uint2* __restrict__ cnt, int64_t nchunks,
-                                                     int64_t* __restrict__ off, int64_t* __restrict__ n_out) {
-  __shared__ int64_t wsum[16], ssum[16];
+#ifndef FM_XP_SCAN_NT
+#define FM_XP_SCAN_NT 1024
+#endif
+constexpr int kSplitScanNT = FM_XP_SCAN_NT;
+__global__ __launch_bounds__(kSplitScanNT) void k_split_scan(const uint2* __restrict__ cnt, int64_t nchunks,
+                                                             int64_t* __restrict__ off, int64_t* __restrict__ n_out) {
+  constexpr int NW = kSplitScanNT / 64;
+  __shared__ int64_t wsum[NW], ssum[NW];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   int64_t carry = 0, singles = 0;
-  for (int64_t b = 0; b < nchunks; b += 1024 * kSplitPer) {
+  for (int64_t b = 0; b < nchunks; b += kSplitScanNT * kSplitPer) {
     const int64_t i0 = b + (int64_t)threadIdx.x * kSplitPer;
     uint2 v[kSplitPer];
 #pragma unroll
@@ -1647,7 +1653,7 @@ __global__ __launch_bounds__(1024) void k_split_scan(const uint2* __restrict__ c
     if (lane == 0) ssum[wave] = sg;
     __syncthreads();
     int64_t wpre = 0, tot = 0, stot = 0;
-    for (int w = 0; w < 16; ++w) {
+    for (int w = 0; w < NW; ++w) {
       wpre += w < wave ? wsum[w] : 0;
       tot += wsum[w];
       stot += ssum[w];
@@ -1707,7 +1713,7 @@ void launch_split(const uint32_t* skeys, const uint2* sents, int64_t N, SplitWor
   else
     hipLaunchKernelGGL(k_split_count<false>, dim3(blocks), dim3(kBlock), 0, st, skeys, N, sw.cnt.as<uint2>(), nchunks,
                        TableView{}, 0);
-  hipLaunchKernelGGL(k_split_scan, dim3(1), dim3(1024), 0, st, sw.cnt.as<uint2>(), nchunks, sw.off.as<int64_t>(), n_out);
+  hipLaunchKernelGGL(k_split_scan, dim3(1), dim3(kSplitScanNT), 0, st, sw.cnt.as<uint2>(), nchunks, sw.off.as<int64_t>(), n_out);
   hipLaunchKernelGGL(k_split_scatter, dim3(blocks), dim3(kBlock), 0, st, skeys, sents, N, sw.off.as<int64_t>(), nchunks,
                      mkeys, ments);
   FM_HIP_CHECK(hipGetLastError());
