@@ -81,7 +81,7 @@ def parse():
                    help="single table: time fm_step with the host CSR each call (PCIe-inclusive, as a JNI "
                         "caller sees it) instead of device-resident batches; reported, never the headline")
     p.add_argument("--prefetch-depth", type=int, default=2,
-                   help="how many steps ahead a batch is prepared: sorted (and split) on the side stream, or "
+                   help="how many steps ahead a batch is prepared: sorted on the side stream, or "
                         "sharded, routed on the route stream")
     p.add_argument("--fuse", default="auto", choices=["auto", "on", "off"],
                    help="single table, k <= 16: the fused step (the forward updates the rows whose feature has one "
