@@ -82,7 +82,7 @@ def parse():
                         "caller sees it) instead of device-resident batches; reported, never the headline")
     p.add_argument("--prefetch-depth", type=int, default=2,
                    help="how many steps ahead a batch is prepared: sorted on the side stream, or "
-                        "sharded, routed on the route stream")
+                        "sharded, routed (and its entries exchanged and slot-sorted) on the side streams")
     p.add_argument("--fuse", default="auto", choices=["auto", "on", "off"],
                    help="single table, k <= 16: the fused step (the forward updates the rows whose feature has one "
                         "entry in the batch; fm_config.fuse_single): auto = the library's default (tables larger "
