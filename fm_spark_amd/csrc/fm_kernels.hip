@@ -1620,10 +1620,10 @@ __global__ __launch_bounds__(kBlock) void k_split_count(const uint32_t* __restri
 // the forward), so each thread loads its kSplitPer consecutive chunk counts of a round at once: one
 // memory round trip per 16K chunks (a 16.7M-entry batch), not one per 1024.
 constexpr int kSplitPer = 16;
-#ifndef FM_XP_SCAN_NT
-#define FM_XP_SCAN_NT 1024
-#endif
-constexpr int kSplitScanNT = FM_XP_SCAN_NT;
+// one 256-thread block (three rounds for a c3 batch's 10K chunks): it finds room on a CU beside the
+// sort's blocks sooner than a 1024-thread one -- c3 step 0.971-0.975 against 0.992-0.995 ms (1024)
+// and 0.978-0.982 (64), three alternating reps (profiles/r03_v13/ab)
+constexpr int kSplitScanNT = 256;
 __global__ __launch_bounds__(kSplitScanNT) void k_split_scan(const uint2* __restrict__ cnt, int64_t nchunks,
                                                              int64_t* __restrict__ off, int64_t* __restrict__ n_out) {
   constexpr int NW = kSplitScanNT / 64;
