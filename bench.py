@@ -80,9 +80,11 @@ def parse():
     p.add_argument("--host-path", action="store_true",
                    help="single table: time fm_step with the host CSR each call (PCIe-inclusive, as a JNI "
                         "caller sees it) instead of device-resident batches; reported, never the headline")
-    p.add_argument("--prefetch-depth", type=int, default=2,
+    p.add_argument("--prefetch-depth", type=int, default=0,
                    help="how many steps ahead a batch is prepared: sorted on the side stream, or "
-                        "sharded, routed (and its entries exchanged and slot-sorted) on the side streams")
+                        "sharded, routed (and its entries exchanged and slot-sorted) on the side streams; 0 = 1 for "
+                        "the single table (c3, 20-step runs: 0.990-0.997 against 1.000-1.004 ms for 2, 1.017-1.024 for "
+                        "3; profiles/r03_v15/depth), 2 for a group (two-phase prepare: each route gets a step)")
     p.add_argument("--fuse", default="auto", choices=["auto", "on", "off"],
                    help="single table, k <= 16: the fused step (the forward updates the rows whose feature has one "
                         "entry in the batch; fm_config.fuse_single): auto = the library's default (tables larger "
@@ -428,7 +430,7 @@ def main():
             ctx.profile_reset()
         prof_on = ProfileSampler(ctx, args)
         prefetch = not args.no_prefetch
-        depth = max(1, min(args.prefetch_depth, len(dbatches) - 1))
+        depth = max(1, min(args.prefetch_depth or 1, len(dbatches) - 1))
         if args.host_path:
             hosts = [CSRHost(b.row_ptr, b.col, b.val, b.label) for b in host_batches]
             prefetch = False
@@ -521,7 +523,7 @@ def main():
         # The pipeline in its steady state: the first `depth` timed steps' batches were prepared
         # before the timed region, and every timed step prepares the batch `depth` steps ahead (K
         # steps and K prepares inside the timed region)
-        depth = max(1, min(args.prefetch_depth, nb - 1))
+        depth = max(1, min(args.prefetch_depth or 2, nb - 1))
         if prefetch:
             for j in range(depth):
                 dbatches[j % nb].prepare()
