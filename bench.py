@@ -93,6 +93,11 @@ def parse():
                    help="N > 1: 'lib' = the multi-GPU fm_ctx, every exchange inside libfm_hip over RCCL (the "
                         "C-ABI path); 'torch' (torch.distributed.run only) = the torch.distributed test harness "
                         "(fm_spark_amd/distributed.py) driving the fm_shard_* phases")
+    p.add_argument("--fit-iters", type=int, default=8,
+                   help="N = 1: after the timed region, run the estimator's resident mini-batch loop "
+                        "(fm_spark_amd.ml.run_minibatch_sgd_resident, what FactorizationMachinesSGD.fit runs after its "
+                        "randomSplit replay) over a resident synthetic dataset of this many batches' rows, split by "
+                        "the randomSplit replay into as many iterations, for fit_ms_per_iter; 0 = skip")
     p.add_argument("--host-path-steps", type=int, default=12,
                    help="N = 1: after the timed region, time this many fm_step calls with the host CSR "
                         "(PCIe-inclusive, what a JNI caller gets) for host_path_ms_per_step; 0 = skip")
@@ -150,6 +155,46 @@ def host_path_leg(ctx, host_batches, t, steps, torch):
     return median_step_ms(evs), mean, t
 
 
+def fit_leg(ctx, F, B, zipf_s, lab, iters, parts=16):
+    """The estimator's mini-batch loop on a resident dataset (what FactorizationMachinesSGD.fit runs
+    after its randomSplit replay, fm_spark_amd/ml.py run_minibatch_sgd_resident): a synthetic dataset
+    of `iters` x B rows in `parts` partitions is uploaded once (dfData.cache(), SGD.scala:93), split
+    by the randomSplit replay into `iters` splits of about B rows (randomSplit normalises the
+    weights: each split gets 1/iters of the rows, :111-112), and the loop runs twice: once to grow
+    the two rotating batches' buffers, once timed (host clock around the whole loop, the final sync
+    included: the pipeline's fill -- the first split's gather and sort, nothing to overlap -- counts
+    against it)."""
+    from fm_spark_amd._native import CSRHost
+    from fm_spark_amd.data import synthetic_batch
+    from fm_spark_amd.ml import run_minibatch_sgd_resident
+    from fm_spark_amd.sampler import random_split_csr
+
+    t0 = time.perf_counter()
+    ds = concat_batches([synthetic_batch(B, F, batch_index=7000 + i, zipf_s=zipf_s, **lab) for i in range(iters)])
+    n = ds.n_rows
+    sizes = [n * (i + 1) // parts - n * i // parts for i in range(parts)]
+    split_of, _, order = random_split_csr(sizes, ds.label, ds.row_ptr, ds.col, ds.val, F, [0.1] * iters, 1234)
+    splits = [order[split_of[order] == i] for i in range(iters)]
+    t_split = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    data = ctx.batch(CSRHost(ds.row_ptr, ds.col, ds.val, ds.label))
+    ctx.sync()
+    t_upload = time.perf_counter() - t0
+    run_minibatch_sgd_resident(ctx, data, splits, STEP_SIZE, REG_PARAM)  # untimed: buffers grown
+    t0 = time.perf_counter()
+    losses = run_minibatch_sgd_resident(ctx, data, splits, STEP_SIZE, REG_PARAM)
+    dt = time.perf_counter() - t0
+    data.close()
+    rows = [len(r) for r in splits]
+    return {"fit_ms_per_iter": 1e3 * dt / iters, "iterations": iters, "rows_per_iter_mean": float(np.mean(rows)),
+            "samples_per_s": float(np.sum(rows)) / dt, "dataset_rows": n, "partitions": parts,
+            "finite_losses": bool(np.all(np.isfinite(losses))),
+            "setup_s": {"generate_and_split": t_split, "upload_once": t_upload},
+            "what": "FactorizationMachinesSGD.fit's mini-batch loop on the resident dataset: each randomSplit split "
+                    "gathered on the device from its row list (fm_batch_from_rows) and sorted on the side stream "
+                    "while the previous split steps; host clock over the whole loop incl. the pipeline fill"}
+
+
 def log(msg):
     print(msg, file=sys.stderr, flush=True)
 
@@ -172,6 +217,28 @@ def pmc_traffic(F, k, B, phase, fused=False, world=1):
     FETCH_SIZE/WRITE_SIZE corrections; "fused" says which step variant the passes measured, "mode"
     whether the single-table step or the sharded owner phases).  None when no pass of this exact
     workload and variant is committed."""
+    mode = "sharded" if phase.startswith("owner_") else "single"
+    for f, d in _pmc_files(F, k, B, fused, mode, world):
+        ks = d.get("kernels", {})
+        names = PHASE_KERNELS.get(phase, [])
+        if names and all("traffic_bytes" in ks.get(n, {}) for n in names):
+            return sum(ks[n]["traffic_bytes"] for n in names), os.path.relpath(f, ROOT) + " (" + d.get("build", "") + ")"
+    return None, None
+
+
+# Random-line request ceiling of the L2 (TCC_HIT + TCC_MISS per second) on MI355X, measured by
+# tools/gather_bench.hip with the same counters (profiles/r04_gather): the rate random 64/128-B row
+# gathers saturate at, whatever bytes each request carries.  The gather-bound kernels are judged
+# against it as well as against HBM bytes.
+L2_REQ_CEILING_GPS = None
+try:
+    with open(os.path.join(ROOT, "profiles", "gather_ceiling.json")) as _fh:
+        L2_REQ_CEILING_GPS = float(json.load(_fh)["l2_requests_per_s"]) / 1e9
+except (OSError, ValueError, KeyError):
+    pass
+
+
+def _pmc_files(F, k, B, fused, mode, world):
     import glob
 
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json"))):
@@ -179,15 +246,39 @@ def pmc_traffic(F, k, B, phase, fused=False, world=1):
             d = json.load(open(f))
         except (OSError, ValueError):
             continue
-        mode = "sharded" if phase.startswith("owner_") else "single"
         if (d.get("num_features"), d.get("k"), d.get("batch_rows"), bool(d.get("fused", False)),
-                d.get("mode", "single"), d.get("world", 1)) != (F, k, B, fused, mode, world):
-            continue
+                d.get("mode", "single"), d.get("world", 1)) == (F, k, B, fused, mode, world):
+            yield f, d
+
+
+def _requests(kc):
+    c = kc.get("counters", {})
+    if "TCC_HIT_sum" in c and "TCC_MISS_sum" in c:
+        return c["TCC_HIT_sum"] + c["TCC_MISS_sum"]
+    return None
+
+
+def pmc_requests(F, k, B, phase, fused=False, world=1):
+    """L2 requests (TCC_HIT + TCC_MISS) per launch of `phase` from the committed PMC passes, or None."""
+    mode = "sharded" if phase.startswith("owner_") else "single"
+    for f, d in _pmc_files(F, k, B, fused, mode, world):
         ks = d.get("kernels", {})
         names = PHASE_KERNELS.get(phase, [])
-        if names and all("traffic_bytes" in ks.get(n, {}) for n in names):
-            return sum(ks[n]["traffic_bytes"] for n in names), os.path.relpath(f, ROOT) + " (" + d.get("build", "") + ")"
+        vals = [_requests(ks.get(n, {})) for n in names]
+        if names and all(v is not None for v in vals):
+            return sum(vals), os.path.relpath(f, ROOT)
     return None, None
+
+
+def requests_roof(req, seconds):
+    """The request-rate side of the roofline: L2 requests per second against the measured random-line
+    ceiling (L2_REQ_CEILING_GPS)."""
+    if not req or not seconds:
+        return None
+    rate = req / seconds / 1e9
+    return {"l2_requests": req, "achieved_G_per_s": rate, "ceiling_G_per_s": L2_REQ_CEILING_GPS,
+            "frac": rate / L2_REQ_CEILING_GPS if L2_REQ_CEILING_GPS else None,
+            "ceiling_source": "profiles/gather_ceiling.json (tools/gather_bench.hip, TCC_HIT + TCC_MISS)"}
 
 
 def sort_passes(num_rows):
@@ -200,29 +291,24 @@ def sort_passes(num_rows):
 
 
 def step_traffic(F, k, B, fused):
-    """Counted HBM bytes of one whole single-table step: every kernel's per-launch traffic in the
-    committed PMC passes of this workload times its launches per step (the sort's kernels once per
-    digit pass).  None unless every kernel of the step was counted."""
-    import glob
-
+    """Counted HBM bytes and L2 requests of one whole single-table step: every kernel's per-launch
+    figures in the committed PMC passes of this workload times its launches per step (the file's
+    "per_step" map when it has one, else the sort's kernels once per digit pass).  None unless
+    every kernel of the step was counted."""
     per_step = {"k_forward": 1, "k_segment_update": 1, "k_segment_combine": 1}
     n = sort_passes(F)
     per_step.update({"k_radix_count": n, "k_radix_scan_rows": n, "k_radix_scatter": n})
     if fused:
         per_step.update({"k_split_count": 1, "k_split_scan": 1, "k_split_scatter": 1})
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json"))):
-        try:
-            d = json.load(open(f))
-        except (OSError, ValueError):
-            continue
-        if (d.get("num_features"), d.get("k"), d.get("batch_rows"), bool(d.get("fused", False)),
-                d.get("mode", "single"), d.get("world", 1)) != (F, k, B, fused, "single", 1):
-            continue
+    for f, d in _pmc_files(F, k, B, fused, "single", 1):
         ks = d.get("kernels", {})
-        if all("traffic_bytes" in ks.get(kn, {}) for kn in per_step):
-            return (sum(ks[kn]["traffic_bytes"] * c for kn, c in per_step.items()),
+        ps = d.get("per_step", per_step)
+        if all("traffic_bytes" in ks.get(kn, {}) for kn in ps):
+            req = [_requests(ks[kn]) for kn in ps]
+            return (sum(ks[kn]["traffic_bytes"] * c for kn, c in ps.items()),
+                    sum(r * c for r, c in zip(req, ps.values())) if all(r is not None for r in req) else None,
                     os.path.relpath(f, ROOT) + " (" + d.get("build", "") + ")")
-    return None, None
+    return None, None, None
 
 
 def cpu_baseline(cfg, batch, steps):
@@ -394,6 +480,8 @@ def main():
     z = host_batches[0].nnz / host_batches[0].n_rows
 
     median_ms = None
+    fit = None
+    fused = False
     host_path = None
     host_trace = None
     xg = None
@@ -472,8 +560,12 @@ def main():
                          "samples_per_s": B / (hmed * 1e-3) if hmed else None,
                          "what": "fm_step with the host CSR each call: 8 B/entry + row_ptr + fp64 labels over PCIe, "
                                  "device-side explode, then the step (two upload slots, copies overlap the previous step)"}
+        fit = None
+        if args.fit_iters > 0 and not args.host_path:
+            fit = fit_leg(ctx, F, B, zipf_s, lab, args.fit_iters)
         U_mean = float(np.mean([uniques[i % len(dbatches)] for i in range(args.steps)]))
-        fused = "split" in prof
+        # the step variant from the context itself (fm_fuse_active), not from which phases were profiled
+        fused = ctx.fuse_active and prefetch
         single_frac = singleton_fraction([host_batches[i % len(host_batches)] for i in range(args.steps)])
         parallelism = "single table" + (", fused step (singleton rows updated by the forward)" if fused else "") + \
             ((", next batch sorted during the current step" if depth == 1 else
@@ -670,7 +762,6 @@ def main():
             # "owner_forward" / "owner_update" do the same on the rank's own rows (per rank: the
             # entries an owner receives ~ its own batch's, the rows it updates ~ U / world)
             algo = {"forward": fwd_b, "update": upd_b, "owner_forward": fwd_b, "owner_update": upd_b}
-            fused = "split" in kern
             if fused:
                 # the fused forward also reads and writes the singleton rows (their 8(k+1) B each of
                 # the update's share); the segmented update keeps the rows with two or more entries
@@ -682,16 +773,34 @@ def main():
             line["roofline"] = {"bound": "hbm", "kernel": dom, "achieved": ach, "peak": HBM_PEAK_GBS,
                                 "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "traffic": traffic,
                                 "algorithmic_bytes": algo[dom], "traffic_source": tsrc}
+            # the ceiling that binds a random-row gather: L2 line requests per second
+            reqs = {}
+            for ph in ("forward", "update", "owner_forward", "owner_update"):
+                if ph in kern:
+                    rq, _ = pmc_requests(F, k, B, ph, fused, world)
+                    rr = requests_roof(rq, kern[ph]["avg_ms"] * 1e-3)
+                    if rr:
+                        reqs[ph] = rr
+            if reqs:
+                line["roofline"]["requests"] = reqs.get(dom)
+                line["roofline"]["requests_by_kernel"] = reqs
+            if args.k == 0 and k == 16:
+                # k = 16: a row's 68 algorithmic bytes sit in a 128-B record (one line per random access),
+                # so at the ~6.3 TB/s random-line rate the forward's HBM fraction is capped near
+                # 68/128 x 6.3/8 = 0.42 ("Ceilings of this design")
+                line["roofline"]["layout_cap_frac"] = 68.0 / 128.0 * 6.3 / 8.0
             step_bytes = fwd_b + upd_b
             line["step_roofline"] = {"bytes_per_step": step_bytes,
                                      "achieved_GBs": step_bytes / (ms_per_step * 1e-3) / 1e9,
                                      "frac": step_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS}
             if mode == "single":
-                st_t, st_src = step_traffic(F, k, B, fused)
+                st_t, st_r, st_src = step_traffic(F, k, B, fused)
                 if st_t:  # every kernel of the step, counted (PMC), against the step's time
                     line["step_roofline"].update(traffic=st_t, traffic_GBs=st_t / (ms_per_step * 1e-3) / 1e9,
                                                  traffic_frac=st_t / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
                                                  traffic_source=st_src)
+                if st_r:
+                    line["step_roofline"]["requests"] = requests_roof(st_r, ms_per_step * 1e-3)
         if xg is not None:
             step_s = (median_ms or ms_per_step) * 1e-3
             if "entries_B" in xg:
@@ -709,6 +818,10 @@ def main():
         if host_path:
             line["host_path_ms_per_step"] = host_path["median_ms_per_step"]
             line["host_path"] = host_path
+        if fit:
+            line["fit_ms_per_iter"] = fit["fit_ms_per_iter"]
+            fit["vs_step"] = fit["fit_ms_per_iter"] / ms_per_step
+            line["fit"] = fit
         if not args.no_cpu_baseline and world == 1:  # the CPU baseline belongs to the N = 1 line
             try:
                 line["cpu_baseline"] = cpu_baseline(cfg, host_batches[0], args.cpu_steps)

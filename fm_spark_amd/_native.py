@@ -92,6 +92,8 @@ SIGNATURES = {
     "fm_batch_create": (C.c_int, [_P, C.POINTER(fm_csr), C.POINTER(_P)]),
     "fm_batch_destroy": (None, [_P]),
     "fm_batch_prepare": (C.c_int, [_P, _P]),
+    "fm_batch_from_rows": (C.c_int, [_P, _P, _I64P, C.c_int64, C.POINTER(_P)]),
+    "fm_fuse_active": (C.c_int32, [_P]),
     "fm_batch_rows": (C.c_int64, [_P]),
     "fm_batch_nnz": (C.c_int64, [_P]),
     "fm_step": (C.c_int, [_P, C.POINTER(fm_csr), C.c_int32, C.c_double, C.c_double, C.POINTER(fm_step_out)]),

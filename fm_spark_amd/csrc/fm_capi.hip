@@ -210,6 +210,12 @@ fm_batch* host_batch(fm_ctx* ctx) {
   return ctx->host_batch.get();
 }
 
+// A batch refilled by fm_batch_from_rows is written on the side stream: a reader on stream st waits
+// for that (a no-op for batches that were never refilled).
+void wait_built(const fm_batch* b, hipStream_t st) {
+  if (b->built) FM_HIP_CHECK(hipStreamWaitEvent(st, b->built, 0));
+}
+
 void reserve_work(fm_ctx* ctx, int64_t B, int64_t N) {
   StepWork& w = ctx->work;
   w.S.ensure(sizeof(float) * (size_t)std::max<int64_t>(B, 1) * s_rec_floats(ctx->kp));
@@ -250,6 +256,7 @@ int step_impl(fm_ctx* ctx, fm_batch* b, int32_t t, double step_size, double reg_
   p.cum_next = p.cumE + p.lam;
   p.w0 = ctx->cfg.w0;
   const TableView T = ctx->view();
+  wait_built(b, ctx->stream);
   int64_t nfwd = 0;
   const uint32_t* skeys = nullptr;
   const uint2* sents = nullptr;
@@ -296,10 +303,9 @@ int step_impl(fm_ctx* ctx, fm_batch* b, int32_t t, double step_size, double reg_
   // the shared sort workspace is read by the main stream only when the batch was sorted inline
   // (not prepared): only then must the next fm_batch_prepare's sort wait for this update
   if (!prepared) FM_HIP_CHECK(hipEventRecord(ctx->ev_upd_done, ctx->stream));
-  if (prepared) {
-    FM_HIP_CHECK(hipEventRecord(b->last_use, ctx->stream));
-    b->prepared = false;
-  }
+  // the last read of the batch (its next fm_batch_prepare or fm_batch_from_rows refill waits for it)
+  if (b->last_use) FM_HIP_CHECK(hipEventRecord(b->last_use, ctx->stream));
+  b->prepared = false;
   ctx->prof_end("update", e0, ctx->stream);
   if (emit) return FM_OK;
   ctx->epoch += 1;
@@ -562,6 +568,8 @@ int fm_batch_create(fm_ctx* ctx, const fm_csr* csr, fm_batch** out) {
     if (ctx->group) return group_batch_create(ctx, csr, out);
     std::unique_ptr<fm_batch> b(new fm_batch());
     upload_batch(ctx, csr, b.get(), true);
+    // kept for fm_batch_from_rows (a cached dataset's splits sized on the host)
+    b->host_rp.assign(csr->row_ptr, csr->row_ptr + csr->n_rows + 1);
     *out = b.release();
     return FM_OK;
   });
@@ -612,6 +620,88 @@ int fm_batch_prepare(fm_ctx* ctx, fm_batch* b) {
     b->prepared = true;
     return FM_OK;
   });
+}
+
+int fm_batch_from_rows(fm_ctx* ctx, const fm_batch* data, const int64_t* rows, int64_t n, fm_batch** out) {
+  return guarded(ctx, [&]() -> int {
+    FM_REQUIRE(out != nullptr && data != nullptr, "null argument");
+    FM_REQUIRE(!ctx->group, "fm_batch_from_rows: single-GPU contexts (a multi-GPU context's dataset is split over its "
+                            "ranks; step its splits from host CSRs)");
+    FM_REQUIRE(data->owner == ctx, "data belongs to another context");
+    FM_REQUIRE(n >= 0 && n < (int64_t(1) << 31), "n out of range");
+    FM_REQUIRE(n == 0 || rows != nullptr, "null rows");
+    const int64_t Bd = data->dev.n_rows;
+    FM_REQUIRE((int64_t)data->host_rp.size() == Bd + 1,
+               "data must be a batch made by fm_batch_create or fm_batch_from_rows");
+    fm_batch* b = *out;
+    std::unique_ptr<fm_batch> fresh;
+    if (b == nullptr) {
+      fresh.reset(new fm_batch());
+      b = fresh.get();
+      b->owner = ctx;
+      b->device = ctx->cfg.device;
+    } else {
+      FM_REQUIRE(b->owner == ctx && b != data && !b->grp, "out must be a batch of this context other than data");
+    }
+    // the rows' result row_ptr on the host, from the dataset's (validated on the way)
+    std::vector<int64_t> rp((size_t)n + 1);
+    rp[0] = 0;
+    for (int64_t i = 0; i < n; ++i) {
+      const int64_t r = rows[i];
+      FM_REQUIRE(r >= 0 && r < Bd, "row index out of [0, rows of data)");
+      rp[i + 1] = rp[i] + (data->host_rp[r + 1] - data->host_rp[r]);
+    }
+    const int64_t N = rp[n];
+    FM_REQUIRE(N < (int64_t(1) << 31), "nnz must be < 2^31 per batch");
+    if (!b->ready) {
+      FM_HIP_CHECK(hipEventCreateWithFlags(&b->ready, hipEventDisableTiming));
+      FM_HIP_CHECK(hipEventCreateWithFlags(&b->last_use, hipEventDisableTiming));
+      FM_HIP_CHECK(hipEventRecord(b->last_use, ctx->stream));
+    }
+    if (!b->built) {
+      FM_HIP_CHECK(hipEventCreateWithFlags(&b->built, hipEventDisableTiming));
+      FM_HIP_CHECK(hipEventCreateWithFlags(&b->sel_copied, hipEventDisableTiming));
+      FM_HIP_CHECK(hipEventRecord(b->sel_copied, ctx->side));
+    }
+    // the staging {rows, row_ptr} of this batch's previous selection has been copied out
+    FM_HIP_CHECK(hipEventSynchronize(b->sel_copied));
+    const size_t img = sizeof(int64_t) * (2 * (size_t)n + 1);
+    b->sel_pin.ensure(img);
+    int64_t* hp = reinterpret_cast<int64_t*>(b->sel_pin.p);
+    if (n > 0) std::memcpy(hp, rows, sizeof(int64_t) * n);
+    std::memcpy(hp + n, rp.data(), sizeof(int64_t) * (n + 1));
+    // batch-only work on the side stream, behind every queued step that reads this batch
+    FM_HIP_CHECK(hipStreamWaitEvent(ctx->side, b->last_use, 0));
+    b->dev.n_rows = n;
+    b->dev.nnz = N;
+    b->max_id = data->max_id;
+    b->dev.row_ptr.ensure(sizeof(int64_t) * (n + 1));
+    b->dev.col.ensure(sizeof(uint32_t) * std::max<int64_t>(N, 4) + 16);
+    b->dev.ent.ensure(sizeof(uint32_t) * 2 * std::max<int64_t>(N, 4) + 16);
+    b->dev.xs.ensure(sizeof(float) * std::max<int64_t>(N, 4) + 16);
+    b->dev.label.ensure(sizeof(double) * std::max<int64_t>(n, 4) + 16);
+    b->up.ensure(img + 16);
+    FM_HIP_CHECK(hipMemcpyAsync(b->up.p, b->sel_pin.p, img, hipMemcpyHostToDevice, ctx->side));
+    FM_HIP_CHECK(hipEventRecord(b->sel_copied, ctx->side));
+    if (n > 0) {
+      const int64_t* up = b->up.as<int64_t>();
+      launch_select_rows(data->dev, up, up + n, n, b->dev, ctx->side);
+    } else {
+      FM_HIP_CHECK(hipMemcpyAsync(b->dev.row_ptr.p, b->up.as<int64_t>(), sizeof(int64_t), hipMemcpyDeviceToDevice,
+                                  ctx->side));
+    }
+    FM_HIP_CHECK(hipEventRecord(b->built, ctx->side));
+    b->prepared = false;  // a refilled batch is sorted again by its own fm_batch_prepare
+    b->host_rp.swap(rp);
+    if (fresh) *out = fresh.release();
+    return FM_OK;
+  });
+}
+
+int32_t fm_fuse_active(fm_ctx* ctx) {
+  if (!ctx) return -1;
+  if (ctx->group) return 0;  // multi-GPU contexts step unfused
+  return fuse_on(ctx) ? 1 : 0;
 }
 
 int64_t fm_batch_rows(const fm_batch* b) { return b ? b->dev.n_rows : -1; }
@@ -705,6 +795,7 @@ int fm_predict_batch(fm_ctx* ctx, fm_batch* b, double lo, double hi, double* pre
     if (B == 0) return FM_OK;
     DevBuf dp;
     dp.ensure(sizeof(double) * B);
+    wait_built(b, ctx->stream);
     hipEvent_t e0 = ctx->prof_begin(ctx->stream);
     launch_predict(ctx->view(), b->dev, ctx->cum_host.back(), ctx->cfg.w0, lo, hi, dp.as<double>(), ctx->stream);
     ctx->prof_end("predict", e0, ctx->stream);
@@ -719,6 +810,7 @@ int fm_init_from_batch(fm_ctx* ctx, fm_batch* b, int64_t* n_present) {
   return guarded(ctx, [&]() -> int {
     FM_REQUIRE(b != nullptr && b->owner == ctx, "batch belongs to another context");
     if (ctx->group) return group_init_from_batch(ctx, b, n_present);
+    wait_built(b, ctx->stream);
     launch_init_entries(ctx->view(), b->dev.col.as<uint32_t>(), b->dev.nnz, ctx->cfg.seed, ctx->cfg.init_sd, ctx->epoch,
                         ctx->cum_host.back(), ctx->stream);
     if (n_present) {

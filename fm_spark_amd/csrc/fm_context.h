@@ -105,18 +105,25 @@ struct fm_batch {
   DevBuf split_n;
   bool split = false;
   hipEvent_t ready = nullptr;     // recorded on the side stream after the prepared sort
-  hipEvent_t last_use = nullptr;  // recorded on the main stream after a step read skeys/sents
+  hipEvent_t last_use = nullptr;  // recorded on the main stream after a step read the batch
   bool prepared = false;
+  // fm_batch_from_rows: the host copy of row_ptr that sizes a selection of this batch's rows without
+  // a device read (kept by fm_batch_create and fm_batch_from_rows), the selection's pinned staging
+  // {rows, row_ptr} and its events (side stream: staging copied out; the batch's rows written --
+  // every main-stream reader of dev waits for `built`)
+  std::vector<int64_t> host_rp;
+  Pinned sel_pin;
+  hipEvent_t sel_copied = nullptr, built = nullptr;
   std::unique_ptr<ShardBatchState> sh;  // sharded contexts only
   std::unique_ptr<GroupBatch, GroupBatchDeleter> grp;  // a multi-GPU context's batch: its per-rank parts
   ~fm_batch() {
     grp.reset();
     (void)hipSetDevice(device);
     if (sh) sh->release(device);
-    if (ready) (void)hipEventSynchronize(ready);
-    if (last_use) (void)hipEventSynchronize(last_use);
-    if (ready) (void)hipEventDestroy(ready);
-    if (last_use) (void)hipEventDestroy(last_use);
+    for (hipEvent_t e : {ready, last_use, sel_copied, built})
+      if (e) (void)hipEventSynchronize(e);
+    for (hipEvent_t e : {ready, last_use, sel_copied, built})
+      if (e) (void)hipEventDestroy(e);
     skeys.release();
     sents.release();
     fkeys.release();

@@ -234,4 +234,9 @@ void launch_explode(const int64_t* row_ptr_in, const double* label_in, const int
                     const float* x_in, int64_t B, int64_t N, int64_t* row_ptr, double* label, uint32_t* col, uint2* ent,
                     float* xs, hipStream_t st);
 
+// fm_batch_from_rows: dst row s = src row rows[s] (device rows[B]); row_ptr_in[B + 1] (device) is the
+// result's row_ptr, computed by the host from the source's
+void launch_select_rows(const BatchDev& src, const int64_t* rows, const int64_t* row_ptr_in, int64_t B, BatchDev& dst,
+                        hipStream_t st);
+
 }  // namespace fmhip

@@ -197,13 +197,18 @@ void k_forward(TableView T, const int64_t* __restrict__ row_ptr,
   int nst = 0;          // singletons of the current sample met by this lane group
   int pend = 0;         // updated rows of the previous sample waiting in slots rs + j RPP, j < pend
   const int span = 4 + ((16 - ((kp + 4) & 15)) & 15);  // header + zero pad of its 64-B granule
-  auto flush = [&]() {
+  // pp = the neighbour group's pend, exchanged while the whole team is active (flush() itself runs
+  // from two call sites: a group without an entry in the sample flushes before the entry loop, one
+  // with entries inside it, so the two groups of a pair may flush at different points; each then
+  // writes its own rows' V and the neighbour's headers from the count taken here, and neither
+  // group's slots change before both have flushed -- a group stashes only after its own flush, and
+  // only when it has entries)
+  auto flush = [&](int pp) {
     if constexpr (GS >= 2) {
       // paired: each updated record leaves in ONE store instruction of 2 GS lanes -- the group
       // writes its row's V, the neighbour group (rs ^ 1) that row's header granule (span <= 4 GS)
       // -- first the even groups' rows, then the odd groups' (a record written by two half-record
       // instructions costs more: DESIGN.md §5, paired row stores)
-      const int pp = __shfl_xor(pend, GS);  // the neighbour group's count
       const bool even = (rs & 1) == 0;
       const int n = pend > pp ? pend : pp;
       for (int j = 0; j < n; ++j) {
@@ -242,9 +247,12 @@ void k_forward(TableView T, const int64_t* __restrict__ row_ptr,
     const double ys = MODE == kTrainFused ? label[s] : 0.0;
     double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0, vv = 0.0, wx = 0.0;
     uint32_t npres = 0;  // kPredict: learned entries of the sample (this lane's share)
+    // the neighbour group's count of rows waiting from the previous sample, taken here, where every
+    // lane of the team is active (a shuffle from a lane outside the exec mask reads garbage)
+    const int pp_s = STASH && GS >= 2 ? __shfl_xor(pend, GS) : 0;
     if (STASH) {
       nst = 0;
-      if (e0 + rs >= e1) flush();  // no entry of this sample for the lane group: nothing to wait behind
+      if (e0 + rs >= e1) flush(pp_s);  // no entry of this sample for the lane group: nothing to wait behind
     }
     for (int64_t eb = e0 + rs; eb < e1; eb += U * RPP) {
       uint32_t id[U];
@@ -259,7 +267,7 @@ void k_forward(TableView T, const int64_t* __restrict__ row_ptr,
         // the batch's x stream (4 B per entry); the partial pass's entries carry x themselves
         x[j] = ok[j] ? (PARTIAL ? __uint_as_float(ent[e].y) : xs[e]) : 0.f;
       }
-      if (STASH && eb == e0 + rs) flush();  // the previous sample's rows: ids in, gathers not yet issued
+      if (STASH && eb == e0 + rs) flush(pp_s);  // the previous sample's rows: ids in, gathers not yet issued
       RowHdr h[U];
       float4 v[U];
 #pragma unroll
@@ -454,7 +462,7 @@ void k_forward(TableView T, const int64_t* __restrict__ row_ptr,
       }
     }
   }
-  if (STASH) flush();  // the last sample's rows
+  if (STASH) flush(GS >= 2 ? __shfl_xor(pend, GS) : 0);  // the last sample's rows (the whole wave active)
   if (MODE != kTrain && MODE != kTrainFused) return;
   // deterministic block reduction of the loss partials
   __shared__ double red[2][kBlock / 64];
@@ -1571,6 +1579,36 @@ __global__ __launch_bounds__(kBlock) void k_explode(const int64_t* __restrict__ 
   }
 }
 
+// fm_batch_from_rows: output row s is row rows[s] of a resident dataset (the randomSplit split of
+// the cached dfData, FactorizationMachinesSGD.scala:93, 111-112).  One team of 16 lanes per output
+// row copies the source row's ids and fp32 x (8 B per entry, contiguous) and writes the exploded
+// {s, x} entries; row_ptr (computed by the host from the dataset's row_ptr) and the labels are
+// written alongside (grid-stride, the same pass).
+__global__ __launch_bounds__(kBlock) void k_select_rows(const int64_t* __restrict__ src_rp, const uint32_t* __restrict__ src_col,
+                                                       const float* __restrict__ src_xs, const double* __restrict__ src_lab,
+                                                       const int64_t* __restrict__ rows, const int64_t* __restrict__ rp_in,
+                                                       int64_t B, int64_t* __restrict__ rp, double* __restrict__ lab,
+                                                       uint32_t* __restrict__ col, uint2* __restrict__ ent,
+                                                       float* __restrict__ xs) {
+  constexpr int T = 16;
+  const int tl = threadIdx.x % T;
+  const int64_t gtid = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int64_t nthreads = (int64_t)gridDim.x * kBlock;
+  for (int64_t i = gtid; i <= B; i += nthreads) rp[i] = rp_in[i];
+  for (int64_t i = gtid; i < B; i += nthreads) lab[i] = src_lab[rows[i]];
+  for (int64_t s = gtid / T; s < B; s += nthreads / T) {
+    const int64_t e0 = rp_in[s], e1 = rp_in[s + 1];
+    const int64_t d = src_rp[rows[s]] - e0;  // source entry of output entry e: e + d
+    for (int64_t e = e0 + tl; e < e1; e += T) {
+      const uint32_t c = src_col[e + d];
+      const float x = src_xs[e + d];
+      col[e] = c;
+      xs[e] = x;
+      ent[e] = make_uint2((uint32_t)s, __float_as_uint(x));
+    }
+  }
+}
+
 // ------------------------------------------------------- singleton split (fm_batch_prepare)
 // The sorted view of a batch -> the entries of its runs of two or more (stable: the order the
 // segmented update needs) and the number of singleton runs.  One wave per chunk of 1024 sorted
@@ -1726,6 +1764,15 @@ void launch_explode(const int64_t* row_ptr_in, const double* label_in, const int
   (void)N;
   hipLaunchKernelGGL(k_explode, dim3(grid_for(std::max<int64_t>(B, 1) * 16, kBlock, 256 * 8)), dim3(kBlock), 0, st,
                      row_ptr_in, label_in, xoff, col_in, x_in, B, row_ptr, label, col, ent, xs);
+  FM_HIP_CHECK(hipGetLastError());
+}
+
+void launch_select_rows(const BatchDev& src, const int64_t* rows, const int64_t* row_ptr_in, int64_t B, BatchDev& dst,
+                        hipStream_t st) {
+  hipLaunchKernelGGL(k_select_rows, dim3(grid_for(std::max<int64_t>(B, 1) * 16, kBlock, 256 * 8)), dim3(kBlock), 0, st,
+                     src.row_ptr.as<int64_t>(), src.col.as<uint32_t>(), src.xs.as<float>(), src.label.as<double>(), rows,
+                     row_ptr_in, B, dst.row_ptr.as<int64_t>(), dst.label.as<double>(), dst.col.as<uint32_t>(),
+                     dst.ent.as<uint2>(), dst.xs.as<float>());
   FM_HIP_CHECK(hipGetLastError());
 }
 

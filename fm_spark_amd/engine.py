@@ -25,14 +25,29 @@ class StepOut:
 class DeviceBatch:
     """A CSR mini-batch resident in HBM (fm_batch_create)."""
 
-    def __init__(self, ctx: "FMContext", csr: N.CSRHost):
+    def __init__(self, ctx: "FMContext", csr: N.CSRHost | None):
         self._lib = N.load()
         self.ctx = ctx
         h = C.c_void_p()
-        N.check(self._lib.fm_batch_create(ctx.handle, C.byref(csr.c), C.byref(h)), "fm_batch_create")
         self.handle = h
-        self.n_rows = csr.n_rows
-        self.nnz = csr.nnz
+        self.n_rows = self.nnz = 0
+        if csr is not None:
+            N.check(self._lib.fm_batch_create(ctx.handle, C.byref(csr.c), C.byref(h)), "fm_batch_create")
+            self.n_rows = csr.n_rows
+            self.nnz = csr.nnz
+
+    def select_rows(self, data: "DeviceBatch", rows):
+        """Refill this batch with rows[i] of the resident dataset `data`, on the device
+        (fm_batch_from_rows); returns self."""
+        rows = np.ascontiguousarray(rows, dtype=np.int64)
+        h = self.handle if self.handle else C.c_void_p()
+        N.check(self._lib.fm_batch_from_rows(self.ctx.handle, data.handle, N.ptr(rows, C.c_int64), len(rows),
+                                             C.byref(h)), "fm_batch_from_rows")
+        self.handle = h
+        self.n_rows = len(rows)
+        self.nnz = int(self._lib.fm_batch_nnz(h))
+        self._data = data  # the dataset stays alive while this batch's gather may be queued
+        return self
 
     def prepare(self):
         """Sort this batch by feature on the side stream ahead of its step (fm_batch_prepare)."""
@@ -187,6 +202,18 @@ class FMContext:
     # ------------------------------------------------------------------- stepping
     def batch(self, csr: N.CSRHost) -> DeviceBatch:
         return DeviceBatch(self, csr)
+
+    def batch_from_rows(self, data: DeviceBatch, rows, into: DeviceBatch | None = None) -> DeviceBatch:
+        """The mini-batch of rows `rows` of the resident dataset `data`, gathered on the device
+        (fm_batch_from_rows); `into` (a batch of this context) is refilled in place instead of
+        creating one."""
+        b = into if into is not None else DeviceBatch(self, None)
+        return b.select_rows(data, rows)
+
+    @property
+    def fuse_active(self) -> bool:
+        """Whether prepared batches of this context take the fused step (fm_fuse_active)."""
+        return int(self._lib.fm_fuse_active(self.handle)) == 1
 
     def step(self, csr: N.CSRHost, t: int, step_size: float, reg_param: float, sync: bool = True):
         """One iteration from a host CSR.  sync=False only enqueues (the host buffers are free on

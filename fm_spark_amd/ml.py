@@ -347,9 +347,15 @@ class FactorizationMachinesSGD:
         return schema
 
     # fit (SGD.scala:76-216) --------------------------------------------------------------
-    def fit(self, dataset: DataFrame, initial_tables=None) -> FactorizationMachinesModel:
+    def fit(self, dataset: DataFrame, initial_tables=None, pipelined: bool | None = None) -> FactorizationMachinesModel:
         """createInitialModel (:218-252) + addSampleId + runMiniBatchSGD (:88-216).
-        ``initial_tables`` = (ids, w, V) injects M0 (the reference's draw is unseeded, P9)."""
+        ``initial_tables`` = (ids, w, V) injects M0 (the reference's draw is unseeded, P9).
+        ``pipelined`` (default: on for a single-GPU estimator): the dataset is kept on the device
+        (dfData.cache(), :93), each randomSplit split is gathered there from its row list
+        (fm_batch_from_rows) and sorted on the side stream while the previous iteration steps, and
+        the steps only enqueue; the loss log lines (:139) are written, in iteration order, when the
+        loop has run.  False: every split crosses PCIe as a host CSR and its step returns its loss
+        (the same model: the splits hold the same rows in the same order)."""
         p = self._params
         _check_schema(dataset, p["featuresCol"], p["labelCol"])
         k = p["dimFactorization"]
@@ -359,12 +365,20 @@ class FactorizationMachinesSGD:
         F = p["numFeatures"] or (int(col.max()) + 1 if len(col) else 1)
         ctx = FMContext(F, k, device=p["device"], seed=p["seed"], init_sd=p["initialSd"], w0=0.0,
                         parallel=p["parallel"], n_gpus=p["nGpus"], devices=p["devices"], transport=p["transport"])
+        single = ctx.parallel is None
+        if pipelined is None:
+            pipelined = single
+        if pipelined and not single:
+            raise ValueError("pipelined fit needs a single-GPU estimator (fm_batch_from_rows)")
+        # dfData.cache() (:93): the exploded dataset uploaded once
+        data = ctx.batch(N.CSRHost(rp, col, val, labels)) if (pipelined or initial_tables is None) and len(labels) \
+            else None
         if initial_tables is not None:
             ctx.load_tables(*initial_tables)
         elif len(col):
             # createInitialModel (:224-241): the draw for every distinct active feature id, on the
             # device over the whole dataset's entries
-            ctx.init_from_batch(ctx.batch(N.CSRHost(rp, col, val, labels)))
+            ctx.init_from_batch(data)
         # randomSplit(Array.fill(maxIter)(miniBatchFraction), 1234L) (:111-112)
         order_cols = []
         extra = None
@@ -384,27 +398,72 @@ class FactorizationMachinesSGD:
         split_of, _, order = random_split(dataset.partition_sizes, labels, vectors,
                                           [p["miniBatchFraction"]] * p["maxIter"], 1234, "".join(order_cols),
                                           extra=extra)
-        for i in range(p["maxIter"]):
-            it = i + 1  # iter = index + 1 (:119)
-            rows = [int(r) for r in order if split_of[r] == i]  # per-partition sorted order
-            if not rows:
-                log.warning("Iteration (%d/%d). The size of sampled batch is zero", it, p["maxIter"])
-                continue
-            sub_rp = np.zeros(len(rows) + 1, dtype=np.int64)
-            sub_col, sub_val = [], []
-            for j, r in enumerate(rows):
-                a, b = rp[r], rp[r + 1]
-                sub_col.append(col[a:b])
-                sub_val.append(val[a:b])
-                sub_rp[j + 1] = sub_rp[j] + (b - a)
-            csr = N.CSRHost(sub_rp, np.concatenate(sub_col) if sub_col else np.zeros(0, np.int32),
-                            np.concatenate(sub_val) if sub_val else np.zeros(0), labels[rows])
-            out = ctx.step(csr, it, p["stepSize"], p["regParam"])
-            log.info("Loss of Iteration (%d/%d): %s", it, p["maxIter"], out.loss_sum)
+        # split i's rows in per-partition sorted order (the order Spark's sampled partitions keep)
+        splits = [order[split_of[order] == i] for i in range(p["maxIter"])]
+        if pipelined:
+            run_minibatch_sgd_resident(ctx, data, splits, p["stepSize"], p["regParam"])
+        else:
+            for i, rows in enumerate(splits):
+                it = i + 1  # iter = index + 1 (:119)
+                if len(rows) == 0:
+                    log.warning("Iteration (%d/%d). The size of sampled batch is zero", it, p["maxIter"])
+                    continue
+                csr = _select_csr(rp, col, val, labels, rows)
+                out = ctx.step(csr, it, p["stepSize"], p["regParam"])
+                log.info("Loss of Iteration (%d/%d): %s", it, p["maxIter"], out.loss_sum)
         model = FactorizationMachinesModel(self.uid, k, 0.0, ctx=ctx)
         model.setMinLabel(p["minLabel"]).setMaxLabel(p["maxLabel"])
         model.parent = self
         return model
+
+
+def _select_csr(rp, col, val, labels, rows) -> N.CSRHost:
+    """The host CSR of the given rows (the synchronous fit's per-split batch)."""
+    rows = np.asarray(rows, dtype=np.int64)
+    lens = rp[rows + 1] - rp[rows]
+    sub_rp = np.zeros(len(rows) + 1, dtype=np.int64)
+    np.cumsum(lens, out=sub_rp[1:])
+    idx = np.repeat(rp[rows] - sub_rp[:-1], lens) + np.arange(sub_rp[-1], dtype=np.int64)
+    return N.CSRHost(sub_rp, col[idx], val[idx], labels[rows])
+
+
+def run_minibatch_sgd_resident(ctx: FMContext, data, splits, step_size: float, reg_param: float,
+                               max_iter: int | None = None):
+    """The foldLeft of runMiniBatchSGD (FactorizationMachinesSGD.scala:114-211) over a dataset kept
+    on the device (`data`, dfData.cache() at :93): split i's rows (`splits[i]`, the randomSplit row
+    lists) are gathered there into one of two batches used in turn (fm_batch_from_rows) and sorted
+    on the side stream (fm_batch_prepare) while iteration i - 1 steps; every step only enqueues
+    (fm_step_batch with out = NULL).  An empty split is skipped with the reference's warning
+    (:126-128).  The loss log lines (:134-139) are written in iteration order after the loop, from
+    the device's loss history.  Returns the loss sums of the executed iterations."""
+    n_iter = len(splits) if max_iter is None else max_iter
+    work = [(i, rows) for i, rows in enumerate(splits) if len(rows)]
+    bufs = [None, None]
+
+    def load(j):
+        b = ctx.batch_from_rows(data, work[j][1], into=bufs[j % 2])
+        bufs[j % 2] = b
+        b.prepare()
+
+    e0 = ctx.epoch
+    if work:
+        load(0)
+    for j, (i, _) in enumerate(work):
+        ctx.step_batch(bufs[j % 2], i + 1, step_size, reg_param, sync=False)  # iter = index + 1 (:119)
+        if j + 1 < len(work):
+            load(j + 1)  # gathered and sorted on the side stream while this step runs
+    ctx.sync()
+    hist = ctx.loss_history()[e0:]
+    done = {i: float(hist[j]) for j, (i, _) in enumerate(work)}
+    for i in range(len(splits)):
+        if i in done:
+            log.info("Loss of Iteration (%d/%d): %s", i + 1, n_iter, done[i])
+        else:
+            log.warning("Iteration (%d/%d). The size of sampled batch is zero", i + 1, n_iter)
+    for b in bufs:
+        if b is not None:
+            b.close()
+    return [done[i] for i, _ in work]
 
 
 # fm.regParam, fm.dimFactorization, ...: the Param handles spark.ml tuning keys grids by

@@ -186,6 +186,24 @@ void fm_batch_destroy(fm_batch* b);
  * this batch; a batch that was not prepared is sorted inside its step.  Stream-ordered, no
  * host synchronisation. */
 int fm_batch_prepare(fm_ctx* ctx, fm_batch* batch);
+/* The mini-batch of the given rows of a device-resident dataset, built on the device: row i of the
+ * result is row rows[i] of data (any order, repeats allowed), with its label.  Replaces the split
+ * of the cached training data that each SGD iteration consumes -- dfData.cache() and
+ * dfData.randomSplit(...) (FactorizationMachinesSGD.scala:93, 111-112): the dataset crosses PCIe
+ * once (fm_batch_create), each split is a row list (fm_random_split) gathered on the device.
+ * data: a batch of this context made by fm_batch_create or fm_batch_from_rows (the library keeps its
+ * row_ptr on the host too, so the result is sized without a device read).  *out == NULL: a new
+ * batch is created; otherwise *out (a batch of this context, not data) is refilled in place.  The
+ * gather runs on the context's side stream behind every queued step that reads *out, and the host
+ * returns once it is enqueued (rows is copied); steps, fm_batch_prepare, fm_predict_batch and
+ * fm_init_from_batch on the result are ordered after it.  data must stay alive until the gather has
+ * run (fm_sync).  Single-GPU contexts only (a multi-GPU context's batches are split over its ranks;
+ * FM_ERR_ARG). */
+int fm_batch_from_rows(fm_ctx* ctx, const fm_batch* data, const int64_t* rows, int64_t n, fm_batch** out);
+/* 1 if a batch prepared by fm_batch_prepare on this context takes the fused step (fm_config.fuse_single
+ * and the library's rule: single table, k <= 16, table above 256 MB unless FM_FUSE_ON), else 0;
+ * -1 for a null context. */
+int32_t fm_fuse_active(fm_ctx* ctx);
 int64_t fm_batch_rows(const fm_batch* b);
 int64_t fm_batch_nnz(const fm_batch* b);
 

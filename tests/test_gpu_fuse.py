@@ -1,9 +1,10 @@
 """GPU: the fused step (fm_config.fuse_single, on by default for prepared single-table batches with
 k <= 16).
 
-fm_batch_prepare sorts the batch and keeps only the runs of two or more entries (k_split_*); the
-step tags those rows' headers (k_tag_multi), the forward updates every untagged row -- a feature
-with one entry in the batch -- in place, and the segmented update walks the multi runs only.  The
+fm_batch_prepare sorts the batch; the step's split (k_split_count / scan / scatter) keeps only the
+runs of two or more entries and tags those rows' headers with the step's epoch as it finds them,
+the forward updates every untagged row -- a feature with one entry in the batch -- in place, and
+the segmented update walks the multi runs only.  The
 forward uses the update's arithmetic on the same fp32-rounded S, r and yhat; the multi runs are
 summed in the same entry order, but their pieces meet at other wave boundaries of the compacted
 view, so the fp64 run sums may differ in the last bits: the fused step must give the unfused step's
@@ -62,7 +63,9 @@ def _assert_bitwise(a, b):
 
 
 @pytest.mark.parametrize("k", [3, 8, 12, 16, 32])
-def test_fused_bitwise_equal_unfused_and_oracle(gpu, k):
+def test_fused_matches_unfused_and_oracle(gpu, k):
+    """Fused against unfused within the north_star tolerance (not bit for bit: the multi runs' fp64
+    pieces meet at other wave boundaries), against the fp64 oracle, and bitwise reproducible."""
     F = 20000
     csrs = [make_problem(700 + i, 1500, F, k, 12, hot=5 + i)[0] for i in range(3)]
     _, ids, w, V = make_problem(71, 1, F, k, 1)
@@ -142,3 +145,26 @@ def test_fused_all_singletons_and_all_multi(gpu):
     fused = _steps(True, [single, multi], F, k, ids, w, V, 4)
     unfused = _steps(False, [single, multi], F, k, ids, w, V, 4)
     _assert_same(fused, unfused)
+
+
+@pytest.mark.parametrize("k", [8, 16])
+def test_fused_teams_take_many_samples_of_mixed_lengths(gpu, k):
+    """40,000 rows, more than the forward's 2048 blocks x 8 teams, so every team walks several
+    samples, of 1..19 entries (odd lengths below the 8 / 16 entry slots of a pass included).  A lane
+    group with no entry in a sample flushes the previous sample's singleton rows before the entry
+    loop while its neighbour flushes inside it; each must still write the other's row headers (the
+    paired stores), or w misses its update and V is shrunk twice.  Three steps, the fused table
+    against the unfused one and the fp64 oracle, with an L1 strong enough to show a double shrink."""
+    F = 400_000
+    csrs = [make_problem(900 + i + k, 40_000, F, k, 10, empty_frac=0.05)[0] for i in range(2)]
+    _, ids, w, V = make_problem(76, 1, F, k, 1)
+    fused = _steps(True, csrs, F, k, ids, w, V, 3, reg=1e-2)
+    unfused = _steps(False, csrs, F, k, ids, w, V, 3, reg=1e-2)
+    _assert_same(fused, unfused)
+    model = R.Model.empty(F, k)
+    model.load(ids, w, V)
+    for t in range(1, 4):
+        ro = R.sgd_step_fast(model, csrs[(t - 1) % 2], t, 0.3, 1e-2)
+        np.testing.assert_allclose(fused[0][t - 1][0], ro.loss_sum, rtol=1e-6)
+        assert fused[0][t - 1][1] == ro.n_unique
+    assert_tables(model, fused[1])

@@ -1,0 +1,178 @@
+"""GPU: the dataset kept on the device (dfData.cache(), FactorizationMachinesSGD.scala:93) and each
+randomSplit split gathered there from its row list (fm_batch_from_rows, :111-112), then the
+pipelined fit (the next split gathered and sorted on the side stream while the current one steps).
+
+fm_batch_from_rows must give the batch a host CSR of the same rows gives -- the same rows, labels
+and entries in the same order, so every step on it is bitwise the host batch's step -- and the
+pipelined fit the synchronous fit's model and loss log."""
+
+import logging
+
+import numpy as np
+import pytest
+
+from fm_spark_amd.linalg import SparseVector
+from problems import make_problem
+from test_gpu_parity import to_host
+
+pytestmark = pytest.mark.gpu
+
+
+def _select(csr, rows):
+    from oracle import fm_ref as R
+
+    rows = np.asarray(rows, dtype=np.int64)
+    lens = csr.row_ptr[rows + 1] - csr.row_ptr[rows]
+    rp = np.zeros(len(rows) + 1, dtype=np.int64)
+    np.cumsum(lens, out=rp[1:])
+    idx = np.repeat(csr.row_ptr[rows] - rp[:-1], lens) + np.arange(rp[-1], dtype=np.int64)
+    return R.CSR(rp, csr.col[idx], csr.val[idx], csr.label[rows])
+
+
+def _run(fuse, F, k, ids, w, V, batches, prepare):
+    """Steps over a list of ('host', csr) / ('rows', data_csr, rows) batches; returns losses + table."""
+    from fm_spark_amd.engine import FMContext
+
+    ctx = FMContext(F, k, fuse=fuse)
+    ctx.load_tables(ids, w, V)
+    data = {}
+    into = None
+    out = []
+    for t, b in enumerate(batches, start=1):
+        if b[0] == "host":
+            db = ctx.batch(to_host(b[1]))
+        else:
+            key = id(b[1])
+            if key not in data:
+                data[key] = ctx.batch(to_host(b[1]))
+            into = ctx.batch_from_rows(data[key], b[2], into=into)  # one batch refilled in turn
+            db = into
+        if prepare:
+            db.prepare()
+        o = ctx.step_batch(db, t, 0.3, 1e-3)
+        out.append((o.loss_sum, o.n_rows, o.n_loss_rows, o.n_unique, o.executed))
+    tab = ctx.export_tables()
+    ctx.close()
+    return out, tab
+
+
+@pytest.mark.parametrize("fuse,prepare", [(False, False), (False, True), (True, True)])
+def test_from_rows_bitwise_equal_host_batch(gpu, fuse, prepare):
+    """Rows out of order, repeated rows, empty rows, a selection that grows the refilled batch, an
+    empty selection (nothing to do): every step bitwise the one on the host CSR of the same rows."""
+    F, k = 50_000, 16
+    data, ids, w, V = make_problem(1201, 6000, F, k, 12, empty_frac=0.1, hot=7)
+    rng = np.random.default_rng(3)
+    sels = [rng.permutation(6000)[:1500], np.sort(rng.choice(6000, 4000, replace=True)), np.arange(0),
+            rng.permutation(6000), np.arange(5990, 6000)]
+    a = _run(fuse, F, k, ids, w, V, [("rows", data, s) for s in sels], prepare)
+    b = _run(fuse, F, k, ids, w, V, [("host", _select(data, s)) for s in sels], prepare)
+    assert a[0] == b[0]
+    assert a[0][2][4] is False  # the empty selection: FM_NOTHING_TO_DO
+    for x, y in zip(a[1], b[1]):
+        assert np.array_equal(x, y)
+
+
+def test_from_rows_predict_and_errors(gpu):
+    from fm_spark_amd._native import FMError
+    from fm_spark_amd.engine import FMContext
+
+    F, k = 3000, 8
+    data, ids, w, V = make_problem(1202, 800, F, k, 6)
+    ctx = FMContext(F, k)
+    ctx.load_tables(ids, w, V)
+    d = ctx.batch(to_host(data))
+    rows = np.arange(799, -1, -3)
+    b = ctx.batch_from_rows(d, rows)
+    p_rows = ctx.predict_batch(b, 0.0, 1.0)
+    p_all = ctx.predict_batch(d, 0.0, 1.0)
+    np.testing.assert_array_equal(p_rows, p_all[rows])
+    with pytest.raises(FMError, match="row index"):
+        ctx.batch_from_rows(d, [0, 800])
+    with pytest.raises(FMError, match="other than data"):
+        ctx.batch_from_rows(d, [1, 2], into=d)
+    other = FMContext(F, k)
+    with pytest.raises(FMError, match="another context"):
+        other.batch_from_rows(d, [1, 2])
+    other.close()
+    ctx.close()
+
+
+def _dataset(n_rows, F, seed, parts):
+    from fm_spark_amd.data import synthetic_batch
+    from fm_spark_amd.ml import DataFrame
+
+    b = synthetic_batch(n_rows, F, batch_index=seed)
+    vecs = [SparseVector(F, b.col[b.row_ptr[i]:b.row_ptr[i + 1]], b.val[b.row_ptr[i]:b.row_ptr[i + 1]])
+            for i in range(b.n_rows)]
+    sizes = [n_rows * (i + 1) // parts - n_rows * i // parts for i in range(parts)]
+    return DataFrame({"label": [float(y) for y in b.label], "features": vecs}, sizes)
+
+
+def test_pipelined_fit_matches_synchronous_fit(gpu, caplog):
+    """The pipelined fit (resident dataset, device-gathered splits, side-stream sorts, enqueue-only
+    steps) against the synchronous one (a host CSR per split, each step read back): the same model
+    (rtol 1e-5; bitwise here, both unfused) and the same loss log lines (rel 1e-9), in order,
+    including a zero-size split's warning (maxIter 12 at fraction 0.05 over 60 rows leaves some
+    splits empty)."""
+    from fm_spark_amd.ml import FactorizationMachinesSGD
+
+    def est(it, frac):
+        return (FactorizationMachinesSGD().setDimFactorization(8).setMaxIter(it).setMiniBatchFraction(frac)
+                .setStepSize(0.5).setRegParam(1e-4).setNumFeatures(20_000).setSeed(5))
+
+    for n_rows, it, frac in ((4000, 6, 0.15), (60, 12, 0.05)):
+        df = _dataset(n_rows, 20_000, 31 + n_rows, 4)
+        logs = []
+        tabs = []
+        for pipe in (True, False):
+            caplog.clear()
+            with caplog.at_level(logging.INFO, logger="org.apache.spark.ml.fm"):
+                m = est(it, frac).fit(df, pipelined=pipe)
+            logs.append([(r.levelname, r.getMessage()) for r in caplog.records])
+            tabs.append(m._ctx.export_tables())
+        assert len(logs[0]) == it and len(logs[1]) == it
+        for (l1, m1), (l2, m2) in zip(*logs):
+            assert l1 == l2
+            h1, v1 = m1.rsplit(" ", 1)
+            h2, v2 = m2.rsplit(" ", 1)
+            assert h1 == h2
+            if l1 == "INFO":
+                assert float(v1) == pytest.approx(float(v2), rel=1e-9)
+        if n_rows == 60:
+            assert any(lv == "WARNING" for lv, _ in logs[0]), "expected a zero-size split"
+        np.testing.assert_array_equal(tabs[0][0], tabs[1][0])
+        np.testing.assert_allclose(tabs[0][1], tabs[1][1], rtol=1e-5, atol=1e-8)
+        np.testing.assert_allclose(tabs[0][2], tabs[1][2], rtol=1e-5, atol=1e-8)
+
+
+def test_resident_loop_fused_matches_host_steps(gpu):
+    """run_minibatch_sgd_resident on a fused context (fuse on, k = 16: singleton rows updated by the
+    forward) against the synchronous host-CSR steps of the same splits on a fused context: the
+    fused step of a prepared batch against the unprepared (unfused) step, so within the north_star
+    tolerance."""
+    from fm_spark_amd.engine import FMContext
+    from fm_spark_amd.ml import _select_csr, run_minibatch_sgd_resident
+
+    F, k = 60_000, 16
+    data, ids, w, V = make_problem(1203, 9000, F, k, 14, hot=11)
+    rng = np.random.default_rng(8)
+    split_of = rng.integers(-1, 5, size=data.n_rows)
+    splits = [np.flatnonzero(split_of == i) for i in range(5)]
+    ctx = FMContext(F, k, fuse=True)
+    ctx.load_tables(ids, w, V)
+    assert ctx.fuse_active
+    d = ctx.batch(to_host(data))
+    losses = run_minibatch_sgd_resident(ctx, d, splits, 0.3, 1e-4)
+    ref = FMContext(F, k, fuse=True)
+    ref.load_tables(ids, w, V)
+    rl = []
+    for i, rows in enumerate(splits):
+        rl.append(ref.step(_select_csr(data.row_ptr, data.col, data.val, data.label, rows), i + 1, 0.3, 1e-4).loss_sum)
+    np.testing.assert_allclose(losses, rl, rtol=1e-9)
+    a, b = ctx.export_tables(), ref.export_tables()
+    np.testing.assert_array_equal(a[0], b[0])
+    np.testing.assert_allclose(a[1], b[1], rtol=1e-5, atol=1e-8)
+    np.testing.assert_allclose(a[2], b[2], rtol=1e-5, atol=1e-8)
+    ctx.close()
+    ref.close()

@@ -120,3 +120,19 @@ def test_random_split_rejects_bad_weights():
 
     with pytest.raises(FMError):
         S.random_split([1], [0.0], [Vectors.dense(1.0)], [0.0, 0.0], 1, "LF")
+
+
+def test_random_split_csr_matches_vector_rows():
+    """The CSR entry point (no Vector objects: the bench's multi-million-row resident-fit dataset)
+    gives the split, sampleId and order of the same rows as SparseVectors."""
+    from fm_spark_amd.data import synthetic_batch
+    from fm_spark_amd.linalg import SparseVector
+
+    b = synthetic_batch(3000, 5000, batch_index=3)
+    vecs = [SparseVector(5000, b.col[b.row_ptr[i]:b.row_ptr[i + 1]], b.val[b.row_ptr[i]:b.row_ptr[i + 1]])
+            for i in range(b.n_rows)]
+    parts = [700, 800, 0, 1500]
+    want = S.random_split(parts, b.label, vecs, [0.1] * 8, 1234, "LF")
+    got = S.random_split_csr(parts, b.label, b.row_ptr, b.col, b.val, 5000, [0.1] * 8, 1234)
+    for x, y in zip(got, want):
+        assert np.array_equal(x, y)

@@ -1,0 +1,44 @@
+"""Join tools/gather_ceiling.hip's per-variant event times with the TCC_HIT + TCC_MISS counts of a
+rocprofv3 --pmc pass over the same binary: L2 requests per second per random-gather variant, and
+the ceiling (the largest rate) -> profiles/gather_ceiling.json, which bench.py's roofline.requests
+quotes.
+
+  python tools/gather_ceiling.py <bench stdout> <pmc dir> <out json>
+"""
+import csv
+import glob
+import json
+import os
+import re
+import sys
+from collections import defaultdict
+
+log, pmc, out = sys.argv[1], sys.argv[2], sys.argv[3]
+ms = {}
+for line in open(log):
+    m = re.match(r"VARIANT (gather<[^>]*>) ms=([0-9.]+) rows=(\d+)", line)
+    if m:
+        ms[m.group(1).replace(" ", "")] = (float(m.group(2)), int(m.group(3)))
+req = defaultdict(lambda: defaultdict(list))
+for f in glob.glob(os.path.join(pmc, "**", "*counter_collection.csv"), recursive=True):
+    for r in csv.DictReader(open(f)):
+        m = re.search(r"gather<[^>]*>", r["Kernel_Name"].replace(" ", ""))
+        if m:
+            req[m.group(0)][(int(r.get("Dispatch_Id") or 0))].append(float(r["Counter_Value"]))
+variants = {}
+for name, (t, n) in sorted(ms.items()):
+    per = [sum(v) for v in req.get(name, {}).values()]  # TCC_HIT_sum + TCC_MISS_sum per dispatch
+    if not per:
+        continue
+    r = sum(per) / len(per)
+    variants[name] = {"ms": t, "gathers": n, "l2_requests": r, "requests_per_gather": r / n,
+                      "l2_requests_per_s": r / (t * 1e-3)}
+ceil = max(variants.values(), key=lambda v: v["l2_requests_per_s"]) if variants else None
+res = {"what": "L2 requests (TCC_HIT_sum + TCC_MISS_sum) per second of random row gathers "
+               "(tools/gather_ceiling.hip: 10.2M gathers over a 100M-record table; <LPR lanes, U in flight, "
+               "record floats, 0 uniform / 1 40 % hot>)",
+       "variants": variants,
+       "l2_requests_per_s": ceil["l2_requests_per_s"] if ceil else None,
+       "source": {"log": log, "pmc": pmc}}
+open(out, "w").write(json.dumps(res, indent=1, sort_keys=True) + "\n")
+print(json.dumps({k: v["l2_requests_per_s"] / 1e9 for k, v in variants.items()}, indent=1))

@@ -1,0 +1,19 @@
+#!/bin/bash
+# GPU box, round 4 first pass: the changed GPU tests (fused flush fix, resident fit), the random-gather
+# request ceiling (tools/gather_ceiling.hip + one TCC PMC pass), then the driver's bench command.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+out=gpurun_out/${1:-r04_a}; mkdir -p $out
+timeout -k 10 900 python -u -m pytest tests/test_gpu_fuse.py tests/test_gpu_resident_fit.py tests/test_gpu_ml.py -x -v \
+    --timeout 300 --timeout-method thread > $out/pytest.log 2>&1
+rc=$?; tail -1 $out/pytest.log >&2; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 120 ./tools/_bin_gather_ceiling > $out/gather.log 2>&1 || exit $?
+cat $out/gather.log >&2
+timeout -k 10 180 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-include-regex gather -T --output-format csv \
+    -d $out/gather_pmc -o run -- ./tools/_bin_gather_ceiling > $out/gather_pmc.log 2>&1 || exit $?
+python tools/gather_ceiling.py $out/gather.log $out/gather_pmc $out/gather_ceiling.json >&2 || exit $?
+cp $out/gather_ceiling.json profiles/gather_ceiling.json
+timeout -k 10 400 python bench.py --gpus 1 --steps 20 --warmup 5 > $out/bench_c3.log 2>&1 || exit $?
+echo "c3 $(grep -o '"ms_per_step": [0-9.]*' $out/bench_c3.log | head -1) $(grep -o '"fit_ms_per_iter": [0-9.]*' $out/bench_c3.log | head -1)" >&2
+exit 0
