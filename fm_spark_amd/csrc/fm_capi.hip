@@ -156,6 +156,14 @@ static bool fuse_on(const fm_ctx* ctx) {
   return ctx->cfg.fuse_single == FM_FUSE_ON || table_bytes > 256.0 * 1024 * 1024;
 }
 
+// The bucket sort (fm_sort.hip) for a batch of N entries of this context, or the LSD passes
+// (fm_config.sort_algo; both stable, so the step is bitwise the same)
+static bool bucket_on(const fm_ctx* ctx, int64_t N) {
+  if (ctx->cfg.sort_algo == FM_SORT_LSD) return false;
+  if (bucket_hi_bits(N, bits_for(ctx->rows - 1)) == 0) return false;
+  return ctx->cfg.sort_algo == FM_SORT_BUCKET || N >= (int64_t(1) << 20);
+}
+
 static bool batch_fits(const fm_batch* b, const Staged& g) {
   return b->dev.row_ptr.bytes >= sizeof(int64_t) * (g.B + 1) &&
          b->dev.col.bytes >= sizeof(uint32_t) * std::max<int64_t>(g.N, 4) + 16 &&
@@ -273,23 +281,30 @@ int step_impl(fm_ctx* ctx, fm_batch* b, int32_t t, double step_size, double reg_
     FM_HIP_CHECK(hipEventRecord(ctx->ev_fork, ctx->stream));
     FM_HIP_CHECK(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
     hipEvent_t es = ctx->prof_begin(ctx->side);
-    radix_sort_pairs64(ctx->work.sort, b->dev.col.as<uint32_t>(), b->dev.ent.as<uint2>(), N,
-                       bits_for(ctx->rows - 1), ctx->side, &skeys, &sents);
+    if (bucket_on(ctx, N)) {
+      SortWork& sw = ctx->work.sort;
+      sw.ensure(N);
+      bucket_sort_pairs64(sw, b->dev.col.as<uint32_t>(), b->dev.ent.as<uint2>(), N, bits_for(ctx->rows - 1), ctx->side,
+                          sw.keys_b.as<uint32_t>(), sw.vals_b.as<uint2>(), nullptr);
+      skeys = sw.keys_b.as<uint32_t>();
+      sents = sw.vals_b.as<uint2>();
+    } else {
+      radix_sort_pairs64(ctx->work.sort, b->dev.col.as<uint32_t>(), b->dev.ent.as<uint2>(), N,
+                         bits_for(ctx->rows - 1), ctx->side, &skeys, &sents);
+    }
     ctx->prof_end("sort", es, ctx->side);
     FM_HIP_CHECK(hipEventRecord(ctx->ev_join, ctx->side));
   }
   hipEvent_t e0 = nullptr;
   FwdOut fx{};
   if (fused) {
-    // the batch's sort (fm_batch_prepare, a step or more ahead on the side stream)
+    // the batch's multi view (fm_batch_prepare, a step or more ahead on the side stream: sorted,
+    // singleton runs dropped)
     FM_HIP_CHECK(hipStreamWaitEvent(ctx->stream, b->ready, 0));
-    // the split of the sorted view into its multi runs, each multi row tagged as its run is found;
-    // on the main stream (the side queue is the busier one: it carries every batch's sort), and
-    // at the step because the tags name this step's epoch
+    // each multi run's row tagged with this step's epoch (so here, at the step, on the main stream)
     e0 = ctx->prof_begin(ctx->stream);
-    launch_split(b->fkeys.as<uint32_t>(), b->fents.as<uint2>(), N, ctx->split_work, b->skeys.as<uint32_t>(),
-                 b->sents.as<uint2>(), b->split_n.as<int64_t>(), ctx->stream, &T, p.epoch);
-    ctx->prof_end("split", e0, ctx->stream);
+    launch_tag_runs(T, b->skeys.as<uint32_t>(), b->split_n.as<int64_t>(), N, p.epoch, ctx->stream);
+    ctx->prof_end("tag", e0, ctx->stream);
     fx.fused = true;
   }
   e0 = ctx->prof_begin(ctx->stream);
@@ -340,6 +355,8 @@ int fm_create(const fm_config* cfg, fm_ctx** out) {
     FM_REQUIRE(cfg->init_sd >= 0.0, "init_sd must be >= 0");
     FM_REQUIRE(cfg->fuse_single == FM_FUSE_DEFAULT || cfg->fuse_single == FM_FUSE_ON || cfg->fuse_single == FM_FUSE_OFF,
                "fuse_single must be FM_FUSE_DEFAULT, FM_FUSE_ON or FM_FUSE_OFF");
+    FM_REQUIRE(cfg->sort_algo == FM_SORT_DEFAULT || cfg->sort_algo == FM_SORT_LSD || cfg->sort_algo == FM_SORT_BUCKET,
+               "sort_algo must be FM_SORT_DEFAULT, FM_SORT_LSD or FM_SORT_BUCKET");
     int ndev = 0;
     FM_HIP_CHECK(hipGetDeviceCount(&ndev));
     FM_REQUIRE(cfg->device >= 0 && cfg->device < ndev, "device ordinal out of range");
@@ -604,16 +621,27 @@ int fm_batch_prepare(fm_ctx* ctx, fm_batch* b) {
     const uint32_t* sk = nullptr;
     const uint2* sv = nullptr;
     b->split = fuse_on(ctx);
+    const int kb = bits_for(ctx->rows - 1);
+    const uint32_t* col = b->dev.col.as<uint32_t>();
+    const uint2* ent = b->dev.ent.as<uint2>();
     if (b->split) {
-      // sorted into the batch's own buffers; the step splits them into the multi runs (skeys / sents)
-      b->fkeys.ensure(sizeof(uint32_t) * N);
-      b->fents.ensure(sizeof(uint2) * N);
+      // the fused step's view: only the runs of two or more entries (skeys / sents), with
+      // {their count, the number of singleton runs} in split_n -- the bucket sort keeps them as it
+      // orders each bucket; after the LSD passes a split pass drops the singletons
       b->split_n.ensure(2 * sizeof(int64_t));
-      radix_sort_pairs64(ctx->work.sort, b->dev.col.as<uint32_t>(), b->dev.ent.as<uint2>(), N, bits_for(ctx->rows - 1),
-                         ctx->side, &sk, &sv, b->fkeys.as<uint32_t>(), b->fents.as<uint2>());
-    } else {
-      radix_sort_pairs64(ctx->work.sort, b->dev.col.as<uint32_t>(), b->dev.ent.as<uint2>(), N, bits_for(ctx->rows - 1),
-                         ctx->side, &sk, &sv, b->skeys.as<uint32_t>(), b->sents.as<uint2>());
+      if (!(bucket_on(ctx, N) && bucket_sort_pairs64(ctx->work.sort, col, ent, N, kb, ctx->side, b->skeys.as<uint32_t>(),
+                                                     b->sents.as<uint2>(), b->split_n.as<int64_t>()))) {
+        b->fkeys.ensure(sizeof(uint32_t) * N);
+        b->fents.ensure(sizeof(uint2) * N);
+        radix_sort_pairs64(ctx->work.sort, col, ent, N, kb, ctx->side, &sk, &sv, b->fkeys.as<uint32_t>(),
+                           b->fents.as<uint2>());
+        launch_split(b->fkeys.as<uint32_t>(), b->fents.as<uint2>(), N, ctx->split_work, b->skeys.as<uint32_t>(),
+                     b->sents.as<uint2>(), b->split_n.as<int64_t>(), ctx->side);
+      }
+    } else if (!(bucket_on(ctx, N) && bucket_sort_pairs64(ctx->work.sort, col, ent, N, kb, ctx->side,
+                                                          b->skeys.as<uint32_t>(), b->sents.as<uint2>(), nullptr))) {
+      radix_sort_pairs64(ctx->work.sort, col, ent, N, kb, ctx->side, &sk, &sv, b->skeys.as<uint32_t>(),
+                         b->sents.as<uint2>());
     }
     ctx->prof_end("sort", es, ctx->side);
     FM_HIP_CHECK(hipEventRecord(b->ready, ctx->side));
@@ -918,7 +946,7 @@ int fm_vector_sum_by_key(fm_ctx* ctx, const int32_t* keys, int64_t n, const doub
     FM_HIP_CHECK(hipMemcpy(out_sums, dos.p, sizeof(double) * nu * k, hipMemcpyDeviceToHost));
     *n_out = nu;
     DevBuf* bufs[] = {&dk, &dvec, &dok, &dos, &drun, &dn, &sw.keys_a, &sw.keys_b, &sw.vals_a, &sw.vals_b,
-                      &sw.counts, &sw.digit_tot};
+                      &sw.counts, &sw.digit_tot, &sw.bscratch, &sw.bstat};
     for (auto* bb : bufs) bb->release();
     return FM_OK;
   });

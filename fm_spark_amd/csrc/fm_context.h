@@ -101,7 +101,7 @@ struct fm_batch {
   // sorted view, or -- split = true -- only the runs of two or more entries, split_n = {their
   // count, the number of singleton runs} on the device (the fused step, fm_kernels.hip)
   DevBuf skeys, sents;
-  DevBuf fkeys, fents;  // split on the main stream: the whole sorted view, split by the step
+  DevBuf fkeys, fents;  // the LSD-sorted whole view a split pass reduces to the multi view (bucket sort: unused)
   DevBuf split_n;
   bool split = false;
   hipEvent_t ready = nullptr;     // recorded on the side stream after the prepared sort
@@ -180,7 +180,7 @@ struct fm_ctx {
   DevBuf sh_ent2;      // [n] uint2 {pair, x bits}: the slot sort's payload
   SortWork side_sort;  // radix sort workspace of the side stream
   SortWork route_sort;  // the route's owner partition (fm_shard_route)
-  SplitWork split_work;  // the fused step's split of its batch's sorted view (main stream)
+  SplitWork split_work;  // the split pass after an LSD-sorted fused batch (side stream, fm_batch_prepare)
   Pinned side_pinned;  // route counts (device -> host)
   // replicated step state (fm_repl_*)
   DevBuf repl_cnt;            // touched-row counts per apply block (uint32)
@@ -289,7 +289,8 @@ struct fm_ctx {
                       &route_sort.keys_a, &route_sort.keys_b, &route_sort.vals_a, &route_sort.vals_b,
                       &route_sort.counts, &route_sort.digit_tot,
                       &sh_okey, &sh_mask, &sh_tcnt, &sh_tot, &sh_pay, &sh_skey, &sh_ent2, &repl_cnt,
-                      &split_work.cnt, &split_work.off};
+                      &split_work.cnt, &split_work.off, &work.sort.bscratch, &work.sort.bstat,
+                      &side_sort.bscratch, &side_sort.bstat, &route_sort.bscratch, &route_sort.bstat};
     for (auto* b : bufs) b->release();
     if (own_stream && stream) (void)hipStreamDestroy(stream);
   }

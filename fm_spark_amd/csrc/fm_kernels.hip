@@ -1735,6 +1735,28 @@ __global__ __launch_bounds__(kBlock) void k_split_scatter(const uint32_t* __rest
   }
 }
 
+// The fused step's tags (main stream, at the step: they name its epoch): the first entry of every
+// run of the batch's multi view (prepared by fm_batch_prepare, n_dev[0] entries) writes the epoch's
+// multi tag into its row's header (4 B read-modify-write of one row per multi run).
+__global__ __launch_bounds__(kBlock) void k_tag_runs(const uint32_t* __restrict__ mkeys, const int64_t* __restrict__ n_dev,
+                                                    TableView T, int32_t epoch) {
+  const int64_t M = n_dev[0];
+  for (int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x; p < M; p += (int64_t)gridDim.x * kBlock) {
+    const uint32_t key = mkeys[p];
+    if (p == 0 || mkeys[p - 1] != key) {
+      int32_t* t = &T.hdr(key)->t;
+      *t = multi_tag(epoch, *t >= 0);
+    }
+  }
+}
+
+void launch_tag_runs(const TableView& T, const uint32_t* mkeys, const int64_t* n_dev, int64_t n_max, int32_t epoch,
+                     hipStream_t st) {
+  if (n_max <= 0) return;
+  hipLaunchKernelGGL(k_tag_runs, dim3(grid_for(n_max, kBlock, 256 * 8)), dim3(kBlock), 0, st, mkeys, n_dev, T, epoch);
+  FM_HIP_CHECK(hipGetLastError());
+}
+
 void launch_split(const uint32_t* skeys, const uint2* sents, int64_t N, SplitWork& sw, uint32_t* mkeys, uint2* ments,
                   int64_t* n_out, hipStream_t st, const TableView* tag_T, int32_t epoch) {
   const int64_t nchunks = (N + kSplitChunk - 1) / kSplitChunk;

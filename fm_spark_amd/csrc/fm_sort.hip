@@ -265,6 +265,468 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint32_t* __rest
   }
 }
 
+// ----------------------------------------------------------------------------- bucket sort
+// Two-phase stable sort of (feature slot, entry) pairs, 52 B per pair instead of the LSD passes' 84
+// (and 45 when only the multi runs are kept):
+//   phase 1  one radix pass above (count / scan / scatter) on the top H bits: every pair lands in
+//            its bucket, in input order;
+//   phase 2  one 1024-thread block per bucket (k_bucket_sort) orders the bucket by its low L bits in
+//            LDS -- one or two in-LDS passes of <= 9 bits over packed words {sub-key << (32 - L) |
+//            index in bucket}, the ranks from wave ballots, each lane holding its wave's part of the
+//            bucket in registers -- and writes it out, gathering payloads by index from the bucket's
+//            own (L2-resident) range.
+// A feature's run never leaves its bucket, so phase 2 also knows every run whole: in SPLIT mode (the
+// fused step's view, fm_kernels.hip "Singleton rows") it keeps only the entries of runs of two or
+// more, compacted at the start of the bucket's range, and counts the rest; k_bucket_offsets scans
+// the per-bucket counts and k_bucket_compact closes the gaps.  That replaces the split kernels
+// (a count pass over all sorted keys, a scan, a scatter) that ran on the step's main stream.
+// A bucket larger than the LDS image (a hot feature's run with its neighbours): all one key, it is
+// already in stable order and is copied; mixed, its block takes two counting passes through a
+// global scratch (slow for one huge mixed bucket -- a feature in every row of a large batch -- but
+// such a bucket is walked by one block, dispatched first, beside all the others).
+constexpr int kBB = 1024;          // phase-2 block: 16 waves, one block per CU (the image takes 120 KB)
+constexpr int kBW = kBB / 64;
+constexpr int kBktCap = 30 * kBB;  // a bucket up to this size is ordered in LDS
+constexpr int kBktRB = 9;          // digit bits of one in-bucket pass (512 digits)
+constexpr int kBktNR = kBktCap / kBB;  // packed words per lane at most
+constexpr int kBktU = 4;           // output rounds of kBB entries whose loads are issued together
+static_assert(kBktCap <= 32768, "packed LDS words hold a 15-bit index next to a 17-bit sub-key");
+
+struct BktShared {
+  uint32_t arr[kBktCap];            // packed {sub, idx} in the order of the previous pass
+  uint32_t cnt[kBW][1 << kBktRB];   // per-wave digit counts -> running destinations
+  uint32_t wsum[kBktU][kBW];
+  uint32_t misc[4];
+};
+
+__device__ __forceinline__ uint64_t digit_peers(uint32_t d, bool valid, int rb) {
+  uint64_t peers = __ballot(valid);
+  for (int b = 0; b < rb; ++b) {
+    const bool bit = (d >> b) & 1u;
+    const uint64_t m = __ballot(bit);
+    peers &= bit ? m : ~m;
+  }
+  return peers;
+}
+
+// Exclusive scan of one value per thread over the 1024-thread block (wsum: kBW words).
+__device__ __forceinline__ uint32_t bkt_excl_scan(uint32_t v, uint32_t* wsum, int lane, int wave) {
+  const uint32_t incl = wave_incl_scan_u32(v, lane);
+  if (lane == 63) wsum[wave] = incl;
+  lds_barrier();
+  uint32_t pre = incl - v;
+#pragma unroll
+  for (int w = 0; w < kBW; ++w) pre += (w < wave) ? wsum[w] : 0u;
+  lds_barrier();
+  return pre;
+}
+
+struct BktIO {
+  const uint32_t* keys;  // the bucket's keys (phase-1 output)
+  const uint2* vals;     // its payloads
+  uint32_t* okeys;       // where the bucket's range starts in the output
+  uint2* ovals;
+  uint2* scratch;        // {sub, idx} per entry (oversized mixed buckets)
+  uint32_t hi;           // bucket << L
+  uint32_t lmask;        // (1 << L) - 1
+  int ib;                // 32 - L: index bits of the packed LDS word
+};
+
+// In-LDS pass for a bucket of m <= kBktCap entries, in place in S.arr (digit (sub >> shift) & 511).
+template <bool FROM_KEYS>
+__device__ __forceinline__ void bucket_pass_lds(BktShared& S, const BktIO& io, uint32_t m, int shift) {
+  constexpr int R = 1 << kBktRB;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint32_t M = (uint32_t)R - 1u;
+  const int dsh = io.ib + shift;
+  const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  const uint32_t part = ((m + kBW - 1) / kBW + 63u) & ~63u;
+  const uint32_t lo = min(m, (uint32_t)wave * part);
+  const int nvw = (int)(min(m, lo + part) - lo);
+  uint32_t v[kBktNR], loc[kBktNR];
+#pragma unroll
+  for (int r = 0; r < kBktNR; ++r) {
+    const uint32_t e = lo + r * 64 + lane;
+    v[r] = 0;
+    if (r * 64 + lane < nvw) v[r] = FROM_KEYS ? (((io.keys[e] & io.lmask) << io.ib) | e) : S.arr[e];
+  }
+  for (int d = tid; d < kBW * R; d += kBB) S.cnt[d / R][d % R] = 0;
+  lds_barrier();  // every part is in registers: S.arr may be overwritten below
+#pragma unroll
+  for (int r = 0; r < kBktNR; ++r) {
+    if (r * 64 >= nvw) break;
+    const bool valid = r * 64 + lane < nvw;
+    const uint32_t d = (v[r] >> dsh) & M;
+    const uint64_t peers = digit_peers(d, valid, kBktRB);
+    const uint32_t below = (uint32_t)__popcll(peers & lt_mask);
+    const uint32_t prev = S.cnt[wave][d];
+    __builtin_amdgcn_wave_barrier();
+    if (valid && below == 0) S.cnt[wave][d] = prev + (uint32_t)__popcll(peers);
+    __builtin_amdgcn_wave_barrier();
+    loc[r] = prev + below;
+  }
+  lds_barrier();
+  uint32_t t = 0;
+  if (tid < R) {
+#pragma unroll
+    for (int w = 0; w < kBW; ++w) {
+      const uint32_t x = S.cnt[w][tid];
+      S.cnt[w][tid] = t;
+      t += x;
+    }
+  }
+  const uint32_t base = bkt_excl_scan(t, S.wsum[0], lane, wave);
+  if (tid < R) {
+#pragma unroll
+    for (int w = 0; w < kBW; ++w) S.cnt[w][tid] += base;
+  }
+  lds_barrier();
+#pragma unroll
+  for (int r = 0; r < kBktNR; ++r) {
+    if (r * 64 + lane < nvw) S.arr[S.cnt[wave][(v[r] >> dsh) & M] + loc[r]] = v[r];
+  }
+  lds_barrier();
+}
+
+enum BktSrc { kSrcKeys = 0, kSrcScratch = 1 };
+enum BktDst { kDstScratch = 0, kDstOut = 1 };
+
+// One stable counting pass over a bucket too large for the LDS image, by digit (sub >> shift) &
+// (2^rb - 1), through global memory: wave w owns the contiguous part [w p, (w + 1) p) of the bucket;
+// a histogram sweep, a scan over (digit, wave), a rank sweep with wave-private running counts.
+template <int SRC, int DST>
+__device__ __forceinline__ void bucket_pass_global(BktShared& S, const BktIO& io, uint32_t m, int shift, int rb) {
+  constexpr int G = 8;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int R = 1 << rb;
+  const uint32_t M = (uint32_t)R - 1u;
+  const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  const uint32_t part = ((m + kBW - 1) / kBW + 63u) & ~63u;
+  const uint32_t lo = min(m, (uint32_t)wave * part), hi = min(m, lo + part);
+  auto load = [&](uint32_t e, uint32_t& sub, uint32_t& idx) {
+    if (SRC == kSrcKeys) {
+      sub = io.keys[e] & io.lmask;
+      idx = e;
+    } else {
+      const uint2 q = io.scratch[e];
+      sub = q.x;
+      idx = q.y;
+    }
+  };
+  for (int d = tid; d < kBW * R; d += kBB) S.cnt[d / R][d % R] = 0;
+  __syncthreads();
+  for (uint32_t e0 = lo; e0 < hi; e0 += 64 * G) {
+    uint32_t sub[G];
+#pragma unroll
+    for (int u = 0; u < G; ++u) {
+      const uint32_t e = e0 + u * 64 + lane;
+      uint32_t idx;
+      sub[u] = 0;
+      if (e < hi) load(e, sub[u], idx);
+    }
+#pragma unroll
+    for (int u = 0; u < G; ++u) {
+      const bool valid = e0 + u * 64 + lane < hi;
+      const uint32_t d = (sub[u] >> shift) & M;
+      const uint64_t peers = digit_peers(d, valid, rb);
+      if (valid && __popcll(peers & lt_mask) == 0) S.cnt[wave][d] += (uint32_t)__popcll(peers);
+    }
+  }
+  __syncthreads();
+  uint32_t t = 0;
+  if (tid < R) {
+#pragma unroll
+    for (int w = 0; w < kBW; ++w) {
+      const uint32_t x = S.cnt[w][tid];
+      S.cnt[w][tid] = t;
+      t += x;
+    }
+  }
+  const uint32_t base = bkt_excl_scan(t, S.wsum[0], lane, wave);
+  if (tid < R) {
+#pragma unroll
+    for (int w = 0; w < kBW; ++w) S.cnt[w][tid] += base;
+  }
+  lds_barrier();
+  for (uint32_t e0 = lo; e0 < hi; e0 += 64 * G) {
+    uint32_t sub[G], idx[G], pos[G];
+#pragma unroll
+    for (int u = 0; u < G; ++u) {
+      const uint32_t e = e0 + u * 64 + lane;
+      sub[u] = 0;
+      idx[u] = 0;
+      if (e < hi) load(e, sub[u], idx[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < G; ++u) {
+      const bool valid = e0 + u * 64 + lane < hi;
+      const uint32_t d = (sub[u] >> shift) & M;
+      const uint64_t peers = digit_peers(d, valid, rb);
+      const uint32_t below = (uint32_t)__popcll(peers & lt_mask);
+      const uint32_t prev = S.cnt[wave][d];
+      __builtin_amdgcn_wave_barrier();
+      if (valid && below == 0) S.cnt[wave][d] = prev + (uint32_t)__popcll(peers);
+      __builtin_amdgcn_wave_barrier();
+      pos[u] = prev + below;
+    }
+    if (DST == kDstOut) {
+      uint2 v[G];
+#pragma unroll
+      for (int u = 0; u < G; ++u)
+        if (e0 + u * 64 + lane < hi) v[u] = io.vals[idx[u]];
+#pragma unroll
+      for (int u = 0; u < G; ++u) {
+        if (e0 + u * 64 + lane < hi) {
+          io.okeys[pos[u]] = io.hi | sub[u];
+          io.ovals[pos[u]] = v[u];
+        }
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < G; ++u)
+        if (e0 + u * 64 + lane < hi) io.scratch[pos[u]] = make_uint2(sub[u], idx[u]);
+    }
+  }
+  __syncthreads();  // the next pass reads what this one wrote and resets cnt
+}
+
+// SPLIT, oversized mixed bucket: the sorted bucket in okeys / ovals[0, m) -> its multi entries
+// compacted in place at the start (stable; a round's reads all land in registers before any of its
+// writes, which go at or below the round's first position).  Returns the multi count.
+__device__ __forceinline__ uint32_t bucket_compact_in_place(BktShared& S, const BktIO& io, uint32_t m) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  uint32_t carry = 0, prev_last = 0xFFFFFFFFu;  // block-uniform
+  for (uint32_t j0 = 0; j0 < m; j0 += kBB) {
+    const uint32_t j = j0 + tid;
+    const bool valid = j < m;
+    const uint32_t key = valid ? io.okeys[j] : 0xFFFFFFFEu;
+    const uint2 val = valid ? io.ovals[j] : make_uint2(0u, 0u);
+    const uint32_t after = j0 + kBB < m ? io.okeys[j0 + kBB] : 0xFFFFFFFFu;
+    S.arr[tid] = key;
+    __syncthreads();  // every read of the round done (the workgroup fence waits for the loads too)
+    const uint32_t prev = tid > 0 ? S.arr[tid - 1] : prev_last;
+    const uint32_t next = tid + 1 < kBB ? S.arr[tid + 1] : after;
+    const bool multi = valid && (prev == key || next == key);
+    const uint64_t bm = __ballot(multi);
+    if (lane == 0) S.wsum[0][wave] = (uint32_t)__popcll(bm);
+    __syncthreads();
+    uint32_t pre = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < kBW; ++w) {
+      pre += w < wave ? S.wsum[0][w] : 0u;
+      tot += S.wsum[0][w];
+    }
+    if (multi) {
+      const uint32_t d = carry + pre + (uint32_t)__popcll(bm & lt_mask);
+      io.okeys[d] = key;
+      io.ovals[d] = val;
+    }
+    prev_last = S.arr[kBB - 1];
+    carry += tot;
+    __syncthreads();  // S.arr / wsum reused; this round's writes drain before the next round's reads
+  }
+  return carry;
+}
+
+// Phase-2 dispatch order: buckets that outgrow the LDS image (their block walks global memory,
+// several times longer) first, so they start with the first wave of blocks instead of forming the
+// kernel's tail; then the rest in bucket order.  One block.
+__global__ __launch_bounds__(kBB) void k_bucket_order(const uint32_t* __restrict__ btot, int nb, uint32_t cap,
+                                                      uint32_t* __restrict__ order) {
+  __shared__ uint32_t wsum[kBW];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  uint32_t carry = 0;  // block-uniform
+  for (int pass = 0; pass < 2; ++pass) {
+    for (int b0 = 0; b0 < nb; b0 += kBB) {
+      const int b = b0 + tid;
+      const bool big = b < nb && btot[b] > cap;
+      const uint32_t f = (b < nb && (pass == 0 ? big : !big)) ? 1u : 0u;
+      const uint32_t pre = bkt_excl_scan(f, wsum, lane, wave);
+      if (f) order[carry + pre] = (uint32_t)b;
+      uint32_t t = 0;
+#pragma unroll
+      for (int w = 0; w < kBW; ++w) t += wsum[w];
+      lds_barrier();
+      carry += t;
+    }
+  }
+}
+
+// Phase 2: block i sorts bucket order[i] (btot[b] pairs starting at the sum of the buckets below
+// it).  SPLIT: the bucket's multi entries go compacted to the start of its range of keys_out /
+// vals_out, bstat[b] = {multi entries, singleton runs}; else the whole bucket, in order.
+template <bool SPLIT>
+__global__ __launch_bounds__(kBB) void k_bucket_sort(const uint32_t* __restrict__ keys_in,
+                                                     const uint2* __restrict__ vals_in, uint32_t* __restrict__ keys_out,
+                                                     uint2* __restrict__ vals_out, const uint32_t* __restrict__ btot,
+                                                     int L, uint2* __restrict__ scratch,
+                                                     const uint32_t* __restrict__ order, uint2* __restrict__ bstat) {
+  __shared__ BktShared S;
+  const int b = (int)order[blockIdx.x];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  uint32_t acc = 0;
+  for (int i = tid; i < b; i += kBB) acc += btot[i];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+  if (lane == 0) S.wsum[0][wave] = acc;
+  lds_barrier();
+  uint32_t start = 0;
+#pragma unroll
+  for (int w = 0; w < kBW; ++w) start += S.wsum[0][w];
+  const uint32_t m = btot[b];
+  lds_barrier();  // wsum is reused below
+  if (m == 0) {   // block-uniform
+    if (SPLIT && tid == 0) bstat[b] = make_uint2(0u, 0u);
+    return;
+  }
+  BktIO io;
+  io.keys = keys_in + start;
+  io.vals = vals_in + start;
+  io.okeys = keys_out + start;
+  io.ovals = vals_out + start;
+  io.scratch = scratch + start;
+  io.hi = (uint32_t)b << L;
+  io.lmask = (1u << L) - 1u;
+  io.ib = 32 - L;
+  const uint32_t cap = min((uint32_t)kBktCap, 1u << min(io.ib, 31));
+  uint32_t mcnt = 0;
+  if (m <= cap) {
+    bucket_pass_lds<true>(S, io, m, 0);
+    if (L > kBktRB) bucket_pass_lds<false>(S, io, m, kBktRB);
+    // the bucket in order in S.arr: coalesced key and payload writes, payloads gathered by index from
+    // the bucket's own range
+    const uint32_t imask = (1u << io.ib) - 1u;
+    for (uint32_t j0 = 0; j0 < m; j0 += kBktU * kBB) {
+      uint32_t w[kBktU], pos[kBktU];
+      bool keep[kBktU];
+#pragma unroll
+      for (int u = 0; u < kBktU; ++u) {
+        const uint32_t j = j0 + u * kBB + tid;
+        w[u] = j < m ? S.arr[j] : 0u;
+        pos[u] = j;
+        keep[u] = j < m;
+        if (SPLIT) {
+          const uint32_t sub = w[u] >> io.ib;
+          const bool same_prev = j < m && j > 0 && (S.arr[j - 1] >> io.ib) == sub;
+          const bool same_next = j + 1 < m && (S.arr[j + 1] >> io.ib) == sub;
+          keep[u] = same_prev || same_next;
+          const uint64_t bm = __ballot(keep[u]);
+          pos[u] = (uint32_t)__popcll(bm & lt_mask);
+          if (lane == 0) S.wsum[u][wave] = (uint32_t)__popcll(bm);
+        }
+      }
+      if (SPLIT) {
+        lds_barrier();
+        uint32_t base = mcnt;
+#pragma unroll
+        for (int u = 0; u < kBktU; ++u) {
+          uint32_t pre = 0, tot = 0;
+#pragma unroll
+          for (int wv = 0; wv < kBW; ++wv) {
+            const uint32_t c = S.wsum[u][wv];
+            pre += wv < wave ? c : 0u;
+            tot += c;
+          }
+          pos[u] += base + pre;
+          base += tot;
+        }
+        mcnt = base;
+        lds_barrier();  // wsum is rewritten by the next rounds
+      }
+      uint2 pv[kBktU];
+#pragma unroll
+      for (int u = 0; u < kBktU; ++u)
+        if (keep[u]) pv[u] = io.vals[w[u] & imask];
+#pragma unroll
+      for (int u = 0; u < kBktU; ++u) {
+        if (keep[u]) {
+          io.okeys[pos[u]] = io.hi | (w[u] >> io.ib);
+          io.ovals[pos[u]] = pv[u];
+        }
+      }
+    }
+  } else {
+    // all one key?  Then the bucket is one run, already in stable order
+    uint32_t lo = 0xFFFFFFFFu, hi = 0u;
+    for (uint32_t j = tid; j < m; j += kBB) {
+      const uint32_t k = io.keys[j];
+      lo = min(lo, k);
+      hi = max(hi, k);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      lo = min(lo, (uint32_t)__shfl_xor((int)lo, o));
+      hi = max(hi, (uint32_t)__shfl_xor((int)hi, o));
+    }
+    if (lane == 0) {
+      S.wsum[0][wave] = lo;
+      S.wsum[1][wave] = hi;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int w = 0; w < kBW; ++w) {
+      lo = min(lo, S.wsum[0][w]);
+      hi = max(hi, S.wsum[1][w]);
+    }
+    __syncthreads();
+    if (lo == hi) {
+      for (uint32_t j = tid; j < m; j += kBB) {
+        io.okeys[j] = io.keys[j];
+        io.ovals[j] = io.vals[j];
+      }
+      mcnt = m;  // m > cap >= 2: one run of two or more
+    } else {
+      const int rb0 = L <= kBktRB ? L : kBktRB, rb1 = L - rb0;
+      if (rb1 == 0) {
+        bucket_pass_global<kSrcKeys, kDstOut>(S, io, m, 0, rb0);
+      } else {
+        bucket_pass_global<kSrcKeys, kDstScratch>(S, io, m, 0, rb0);
+        bucket_pass_global<kSrcScratch, kDstOut>(S, io, m, rb0, rb1);
+      }
+      if (SPLIT) mcnt = bucket_compact_in_place(S, io, m);
+    }
+  }
+  if (SPLIT && tid == 0) bstat[b] = make_uint2(mcnt, m - mcnt);
+}
+
+// SPLIT: the buckets' starts (from their sizes) and the multi view's offsets (from their multi
+// counts), exclusive scans over at most 1024 buckets; n_out[0] = multi entries, n_out[1] = singleton
+// runs.  One block.
+__global__ __launch_bounds__(kBB) void k_bucket_offsets(const uint32_t* __restrict__ btot,
+                                                        const uint2* __restrict__ bstat, int nb,
+                                                        uint2* __restrict__ boff, int64_t* __restrict__ n_out) {
+  __shared__ uint32_t wsum[kBW];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint32_t sz = tid < nb ? btot[tid] : 0u;
+  const uint2 st = tid < nb ? bstat[tid] : make_uint2(0u, 0u);
+  const uint32_t start = bkt_excl_scan(sz, wsum, lane, wave);
+  const uint32_t moff = bkt_excl_scan(st.x, wsum, lane, wave);
+  const uint32_t sing = bkt_excl_scan(st.y, wsum, lane, wave);
+  if (tid < nb) boff[tid] = make_uint2(start, moff);
+  if (tid == nb - 1) {
+    n_out[0] = (int64_t)moff + st.x;
+    n_out[1] = (int64_t)sing + st.y;
+  }
+}
+
+// SPLIT: bucket b's multi entries, compacted at its range's start in the gapped view, to their
+// place in the dense multi view.  One block per bucket.
+__global__ __launch_bounds__(256) void k_bucket_compact(const uint32_t* __restrict__ gkeys,
+                                                        const uint2* __restrict__ gvals,
+                                                        const uint2* __restrict__ bstat,
+                                                        const uint2* __restrict__ boff, uint32_t* __restrict__ mkeys,
+                                                        uint2* __restrict__ mvals) {
+  const int b = blockIdx.x;
+  const uint32_t n = bstat[b].x;
+  const uint2 o = boff[b];
+  for (uint32_t j = threadIdx.x; j < n; j += 256) {
+    mkeys[o.y + j] = gkeys[o.x + j];
+    mvals[o.y + j] = gvals[o.x + j];
+  }
+}
+
 }  // namespace
 
 void SortWork::ensure(int64_t n) {
@@ -276,7 +738,8 @@ void SortWork::ensure(int64_t n) {
   vals_b.ensure(sizeof(uint64_t) * c);
   const int64_t ntiles = (c + kTile - 1) / kTile;
   counts.ensure(sizeof(uint32_t) * kMaxRadix * ntiles);
-  digit_tot.ensure(sizeof(uint32_t) * kMaxRadix);
+  digit_tot.ensure(sizeof(uint32_t) * kMaxRadix * 2);  // digit totals, then the bucket sort's block order
+  bstat.ensure(sizeof(uint2) * kMaxRadix * 2);         // per bucket {multi, singleton runs}, then {start, moff}
   cap = c;
 }
 
@@ -374,6 +837,61 @@ void radix_sort_pairs64(SortWork& w, const uint32_t* keys_in, const uint2* vals_
                         hipStream_t st, const uint32_t** keys_out, const uint2** vals_out, uint32_t* final_keys,
                         uint2* final_vals) {
   radix_sort_impl<uint2>(w, keys_in, vals_in, n, key_bits, st, keys_out, vals_out, final_keys, final_vals);
+}
+
+}  // namespace fmhip
+
+namespace fmhip {
+
+int bucket_hi_bits(int64_t n, int key_bits) {
+  if (n < 1 || n >= (int64_t(1) << 32) - 1) return 0;
+  const int H = n / 512 > 8192 ? 10 : 9;  // buckets of about 5K - 10K pairs at the sizes that matter
+  if (key_bits < H + 1 || key_bits - H > 2 * kBktRB) return 0;  // one pass would do / too many low bits
+  return H;
+}
+
+bool bucket_sort_pairs64(SortWork& w, const uint32_t* keys_in, const uint2* vals_in, int64_t n, int key_bits,
+                         hipStream_t st, uint32_t* final_keys, uint2* final_vals, int64_t* split_out) {
+  const int H = bucket_hi_bits(n, key_bits);
+  if (H == 0) return false;
+  FM_REQUIRE(final_keys && final_vals && vals_in, "bucket sort: null buffer");
+  w.ensure(n);
+  w.bscratch.ensure(sizeof(uint2) * w.cap);  // {sub, idx} of oversized mixed buckets
+  const int L = key_bits - H;
+  const int nb = 1 << H;
+  const int64_t ntiles = (n + kTile - 1) / kTile;
+  uint32_t* kbuf[2] = {w.keys_a.as<uint32_t>(), w.keys_b.as<uint32_t>()};
+  uint2* vbuf[2] = {w.vals_a.as<uint2>(), w.vals_b.as<uint2>()};
+  const uint32_t* kin = keys_in;
+  if ((reinterpret_cast<uintptr_t>(keys_in) & 15u) != 0) {  // the count kernel reads uint4
+    FM_HIP_CHECK(hipMemcpyAsync(kbuf[1], keys_in, sizeof(uint32_t) * n, hipMemcpyDeviceToDevice, st));
+    kin = kbuf[1];
+  }
+  // phase 1: the top H bits
+  if (H == 9)
+    radix_pass<uint2, 9>(kin, vals_in, kbuf[0], vbuf[0], n, L, w, ntiles, st);
+  else
+    radix_pass<uint2, 10>(kin, vals_in, kbuf[0], vbuf[0], n, L, w, ntiles, st);
+  const uint32_t* btot = w.digit_tot.as<uint32_t>();
+  uint32_t* order = w.digit_tot.as<uint32_t>() + kMaxRadix;
+  uint2* bstat = w.bstat.as<uint2>();
+  uint2* boff = bstat + kMaxRadix;
+  const uint32_t cap = std::min<uint32_t>((uint32_t)kBktCap, 1u << std::min(32 - L, 31));
+  hipLaunchKernelGGL(k_bucket_order, dim3(1), dim3(kBB), 0, st, btot, nb, cap, order);
+  if (split_out) {
+    // phase 2 into the gapped view (kbuf[1] / vbuf[1]: the multi entries at each bucket's start),
+    // then the gaps closed into the final buffers
+    hipLaunchKernelGGL(k_bucket_sort<true>, dim3(nb), dim3(kBB), 0, st, kbuf[0], vbuf[0], kbuf[1], vbuf[1], btot, L,
+                       w.bscratch.as<uint2>(), (const uint32_t*)order, bstat);
+    hipLaunchKernelGGL(k_bucket_offsets, dim3(1), dim3(kBB), 0, st, btot, (const uint2*)bstat, nb, boff, split_out);
+    hipLaunchKernelGGL(k_bucket_compact, dim3(nb), dim3(256), 0, st, kbuf[1], vbuf[1], (const uint2*)bstat,
+                       (const uint2*)boff, final_keys, final_vals);
+  } else {
+    hipLaunchKernelGGL(k_bucket_sort<false>, dim3(nb), dim3(kBB), 0, st, kbuf[0], vbuf[0], final_keys, final_vals, btot,
+                       L, w.bscratch.as<uint2>(), (const uint32_t*)order, bstat);
+  }
+  FM_HIP_CHECK(hipGetLastError());
+  return true;
 }
 
 }  // namespace fmhip

@@ -5,7 +5,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 out=gpurun_out/${1:-r04_a}; mkdir -p $out
-timeout -k 10 900 python -u -m pytest tests/test_gpu_fuse.py tests/test_gpu_resident_fit.py tests/test_gpu_ml.py -x -v \
+timeout -k 10 900 python -u -m pytest tests/test_gpu_bucket.py tests/test_gpu_fuse.py tests/test_gpu_resident_fit.py tests/test_gpu_ml.py -x -v \
     --timeout 300 --timeout-method thread > $out/pytest.log 2>&1
 rc=$?; tail -1 $out/pytest.log >&2; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 120 ./tools/_bin_gather_ceiling > $out/gather.log 2>&1 || exit $?
