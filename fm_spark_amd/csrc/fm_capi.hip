@@ -150,15 +150,17 @@ static Staged stage_csr(fm_ctx* ctx, const fm_csr* c, bool check_range, Pinned& 
 // the 256-MB Infinity Cache, where the update's re-read of the singleton rows goes to HBM -- a
 // cache-resident table re-reads them on-die, and the split and tags would cost more than they save
 // (c2 / c5: 0.245 / 0.273 ms per step fused against 0.184 / 0.208 unfused, profiles/r03_v1).
-static bool fuse_on(const fm_ctx* ctx) {
-  if (ctx->cfg.fuse_single == FM_FUSE_OFF || ctx->kp > 16 || ctx->cfg.shard_count != 1) return false;
+bool fuse_rule(const fm_ctx* ctx) {
+  if (ctx->cfg.fuse_single == FM_FUSE_OFF || ctx->kp > 16) return false;
   const double table_bytes = (double)ctx->rows * ctx->stride * sizeof(float);
   return ctx->cfg.fuse_single == FM_FUSE_ON || table_bytes > 256.0 * 1024 * 1024;
 }
 
+static bool fuse_on(const fm_ctx* ctx) { return ctx->cfg.shard_count == 1 && fuse_rule(ctx); }
+
 // The bucket sort (fm_sort.hip) for a batch of N entries of this context, or the LSD passes
 // (fm_config.sort_algo; both stable, so the step is bitwise the same)
-static bool bucket_on(const fm_ctx* ctx, int64_t N) {
+bool bucket_on(const fm_ctx* ctx, int64_t N) {
   if (ctx->cfg.sort_algo == FM_SORT_LSD) return false;
   if (bucket_hi_bits(N, bits_for(ctx->rows - 1)) == 0) return false;
   return ctx->cfg.sort_algo == FM_SORT_BUCKET || N >= (int64_t(1) << 20);

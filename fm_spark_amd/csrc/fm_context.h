@@ -62,6 +62,11 @@ struct ShardBatchState {
   DevBuf src_off;            // [R+1] int64 source offsets of the received entries, then [R+1] pair offsets
   DevBuf pair_ptr;           // [P+1] int64 entry offsets of the pairs
   DevBuf skeys, sents;       // received entries sorted by slot: slots / {pair, x bits}
+  // fused owner step (split): skeys / sents hold only the runs of two or more entries, split_n
+  // {their count, singleton runs} on the device; fkeys / fents the LSD-sorted whole view a split
+  // pass reduces (the bucket sort keeps the multi runs itself)
+  bool split = false;
+  DevBuf split_n, fkeys, fents;
   hipEvent_t ready_fwd = nullptr;  // side stream: pair table done
   hipEvent_t ready_upd = nullptr;  // side stream: slot sort done
   hipEvent_t last_use = nullptr;   // main stream: the iteration's update has read everything
@@ -72,7 +77,7 @@ struct ShardBatchState {
     for (hipEvent_t e : {ready_fwd, ready_upd, last_use})
       if (e) (void)hipEventDestroy(e);
     ready_fwd = ready_upd = last_use = nullptr;
-    for (DevBuf* b : {&pairidx, &poff, &src_off, &pair_ptr, &skeys, &sents}) b->release();
+    for (DevBuf* b : {&pairidx, &poff, &src_off, &pair_ptr, &skeys, &sents, &split_n, &fkeys, &fents}) b->release();
   }
 };
 
@@ -358,6 +363,11 @@ inline int bits_for(int64_t max_value) {
 }
 
 // shared host helpers (fm_capi.hip)
+// the fused step's rule (fm_config.fuse_single, kp <= 16, tables above 256 MB unless FUSE_ON), for the
+// single table (fuse_on) and the sharded owner step alike; and whether a batch of N entries takes
+// the bucket sort (fm_config.sort_algo)
+bool fuse_rule(const fm_ctx* ctx);
+bool bucket_on(const fm_ctx* ctx, int64_t N);
 void upload_batch(fm_ctx* ctx, const fm_csr* c, fm_batch* b, bool check_range);
 void reserve_work(fm_ctx* ctx, int64_t B, int64_t N);
 

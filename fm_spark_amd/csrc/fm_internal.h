@@ -207,6 +207,10 @@ struct SplitWork {
 void launch_split(const uint32_t* skeys, const uint2* sents, int64_t N, SplitWork& sw, uint32_t* mkeys, uint2* ments,
                   int64_t* n_out, hipStream_t st,
                   const TableView* tag_T = nullptr, int32_t epoch = 0);
+// the fused sharded owner step: the rows of the received entries' singleton features, pair by pair
+// (pair_ptr [P + 1] over slot / ent, S records of rec floats: S then {r, yhat} at kp)
+void launch_owner_singletons(const TableView& T, const int64_t* pair_ptr, int64_t P, const uint32_t* slot,
+                             const uint2* ent, const float* srec, int rec, const StepParams& sp, hipStream_t st);
 // the fused step's multi tags for the runs of a prepared multi view (n_dev[0] <= n_max entries)
 void launch_tag_runs(const TableView& T, const uint32_t* mkeys, const int64_t* n_dev, int64_t n_max, int32_t epoch,
                      hipStream_t st);

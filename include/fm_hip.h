@@ -332,7 +332,9 @@ int fm_shard_route(fm_ctx* ctx, fm_batch* batch, void* send_slot, void* send_ent
 /* Phase 1b (owner): the n received entries (source-rank major: src_entries[r] from rank r, which
  * sent src_pairs[r] pairs) -> their pair table and their order by slot (stable: source rank,
  * then CSR order), kept with `batch`.  No host synchronisation.  recv_slot / recv_ent must stay
- * valid until the main stream has run fm_shard_owner_forward of this batch. */
+ * valid until the main stream has run fm_shard_owner_update of this batch (the fused owner step --
+ * fm_config.fuse_single's rule, kp <= 16 -- reads them again there to update the rows of features
+ * with one received entry pair by pair; otherwise until fm_shard_owner_forward). */
 int fm_shard_owner_prepare(fm_ctx* ctx, fm_batch* batch, const void* recv_slot, const void* recv_ent,
                            int64_t n, const int64_t* src_entries, const int64_t* src_pairs);
 /* Phase 2 (owner): partials_out[sum src_pairs] (source-major, sample order): per received pair

@@ -194,6 +194,38 @@ def test_c2_full_size_table_parity(gpu):
     np.testing.assert_allclose(gV, model.V, rtol=RTOL, atol=ATOL)
 
 
+def test_c2_replicated_r8_full_table_parity(gpu):
+    """c2's whole table replicated over R = 8 ranks of one context (COPY transport, every replica on
+    this GPU): each rank steps its eighth of the 64K-row mini-batch, the per-slot gradient sums cross
+    ranks as fp32 (the all-reduce of fm_repl_grad's buffer, include/fm_hip.h) and every replica
+    applies the same update.  Five steps against the fp64 oracle over the whole table: the fp32
+    cross-rank sums stay within the north_star tolerance (rtol 1e-5; the largest relative error
+    over values >= 1e-6 is printed)."""
+    from fm_spark_amd.data import synthetic_batch
+    from fm_spark_amd.engine import FMContext
+
+    F, k, B, NR = 1_000_000, 8, 65536, 8
+    hb = [synthetic_batch(B, F, batch_index=60 + i) for i in range(5)]
+    ctx = FMContext(F, k, seed=7, init_sd=0.01, parallel="replicated", n_gpus=NR, devices=[0] * NR, transport="copy")
+    ctx.init_random_range(0, F)
+    ids, w, V = ctx.export_tables()
+    assert len(ids) == F
+    model = R.Model.empty(F, k)
+    model.load(ids, w, V)
+    for t, b in enumerate(hb, start=1):
+        ref = R.sgd_step_fast(model, R.CSR(b.row_ptr, b.col, b.val, b.label), t, STEP, REG)
+        out = ctx.step(_host(b), t, STEP, REG)
+        assert out.n_unique == ref.n_unique and out.n_loss_rows == ref.n_loss_rows
+        assert out.loss_sum == pytest.approx(ref.loss_sum, rel=RTOL)
+    gi, gw, gV = ctx.export_tables()
+    ctx.close()
+    np.testing.assert_array_equal(gi, np.arange(F))
+    np.testing.assert_allclose(gw, model.w, rtol=RTOL, atol=ATOL)
+    np.testing.assert_allclose(gV, model.V, rtol=RTOL, atol=ATOL)
+    big = np.abs(model.V) >= 1e-6
+    print(f"c2 replicated x{NR}: max relative V error {np.max(np.abs(gV[big] - model.V[big]) / np.abs(model.V[big])):.3e}")
+
+
 def test_c3_whole_table_parity_against_c_oracle(gpu):
     """c3 at full size, every row: the whole 100M x k = 16 table, initialised with the device's
     seeded draw on both sides (oracle_init_device_draw replicates it), stepped twice -- the device

@@ -79,6 +79,54 @@ def test_group_sharded_step_matches_oracle(gpu, R, k, F, hot, transport):
     ctx.close()
 
 
+@pytest.mark.parametrize("R,k,sort,transport", [
+    (1, 16, "bucket", "copy"), (2, 8, "lsd", "copy"), (3, 16, "lsd", "copy"), (8, 16, "bucket", "copy"),
+    (1, 16, "bucket", "rccl"),
+])
+def test_group_sharded_fused_owner_step(gpu, R, k, sort, transport):
+    """The fused owner step (fm_config.fuse_single on): each owner's slot sort keeps only the runs of
+    two or more received entries, the singleton features' rows are updated pair by pair from their S
+    records after the S exchange, the segmented update walks the multi runs.  Against the fp64
+    oracle and against the unfused owner step (counts exact, loss 1e-9, tables rtol 1e-5), from host
+    CSRs and from prepared device batches, with a hot feature and rows absent from the model."""
+    F = 4001
+    _, ids, w, V = make_problem(33, 1, F, k, 1)
+    keep = ids[ids % 5 != 0]  # a fifth of the rows absent: singletons and multi runs create them
+    probs = [make_problem(140 + t, 400 + 37 * t, F, k, 9, hot=17)[0] for t in range(1, 5)]
+    model = R_.Model.empty(F, k)
+    model.load(keep, w[keep], V[keep])
+    out = {}
+    for fuse in (True, False):
+        ctx = _ctx(F, k, R, transport=transport, fuse=fuse, sort=sort)
+        ctx.load_tables(keep, w[keep], V[keep])
+        res = []
+        for t in (1, 2):
+            res.append(ctx.step(_host(probs[t - 1]), t, 0.3, 1e-3))
+        bs = [ctx.batch(_host(p)) for p in probs[2:]]
+        bs[0].prepare()
+        for t in (3, 4):
+            res.append(ctx.step_batch(bs[t - 3], t, 0.3, 1e-3, sync=True))
+            if t == 3:
+                bs[1].prepare()
+        out[fuse] = ([(o.loss_sum, o.n_rows, o.n_loss_rows, o.n_unique) for o in res], ctx.export_tables())
+        ctx.close()
+    for t in range(1, 5):
+        ref = R_.sgd_step_fast(model, probs[t - 1], t, 0.3, 1e-3)
+        got = out[True][0][t - 1]
+        assert got[0] == pytest.approx(ref.loss_sum, rel=1e-5)
+        assert got[1:] == (ref.n_rows, ref.n_loss_rows, ref.n_unique)
+    for (a, b) in zip(out[True][0], out[False][0]):
+        assert a[1:] == b[1:]
+        assert a[0] == pytest.approx(b[0], rel=1e-9)
+    gi, gw, gV = out[True][1]
+    np.testing.assert_array_equal(gi, np.nonzero(model.present)[0])
+    np.testing.assert_allclose(gw, model.w[gi], rtol=1e-5, atol=1e-8)
+    np.testing.assert_allclose(gV, model.V[gi], rtol=1e-5, atol=1e-8)
+    np.testing.assert_array_equal(gi, out[False][1][0])
+    np.testing.assert_allclose(gw, out[False][1][1], rtol=1e-5, atol=1e-8)
+    np.testing.assert_allclose(gV, out[False][1][2], rtol=1e-5, atol=1e-8)
+
+
 @pytest.mark.parametrize("R,transport", [(3, "copy"), (1, "rccl")])
 def test_group_sharded_prepare_two_ahead(gpu, R, transport):
     """fm_batch_prepare on a sharded group is two-phase: it enqueues the batch's route and count
