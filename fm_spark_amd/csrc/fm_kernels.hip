@@ -1776,33 +1776,33 @@ __global__ __launch_bounds__(kBlock) void k_owner_single(TableView T, const int6
       }
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-      const RowHdr h = hs[j];
-      if (is_multi(h.t, sp.epoch)) continue;
-      float* r = T.v(ids[j]);
-      const float4 vq = vs[j];
-      const double xd = (double)xs2[j];
-      const float acf = (float)(sp.cumE - h.cum);  // pending L1 of the row
-      const double t = xd * rj, b = (xd * xd) * rj;
-      const double gwe = (xd - 1.0) * yh + rj;  // x yhat - y (SGD.scala:145)
-      if (qok) {
-        const float4 v = shrink4f(vq, acf);
-        const double g0 = fma((double)Sq.x, t, 0.0) - (double)v.x * b, g1 = fma((double)Sq.y, t, 0.0) - (double)v.y * b;
-        const double g2 = fma((double)Sq.z, t, 0.0) - (double)v.z * b, g3 = fma((double)Sq.w, t, 0.0) - (double)v.w * b;
-        const float4 u = make_float4((float)fma(g0, -sp.scale_v, (double)v.x), (float)fma(g1, -sp.scale_v, (double)v.y),
-                                     (float)fma(g2, -sp.scale_v, (double)v.z), (float)fma(g3, -sp.scale_v, (double)v.w));
-        st_row4(r + 4 * g, shrink4f(u, lamf));
-      }
-      for (int i = 4 * g; i < span; i += 4 * GS) {  // the header and the zero pad of its granule
-        float4 hq = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (i == 0) {
-          RowHdr o;
-          o.w = upd_w(shrink1f(h.w, acf), 0.0 + gwe, sp);  // SGD.scala:150, :171
-          o.t = sp.epoch + 1;
-          o.cum = sp.cum_next;
-          hq = *reinterpret_cast<const float4*>(&o);
+        const RowHdr h = hs[j];
+        if (is_multi(h.t, sp.epoch)) continue;
+        float* r = T.v(ids[j]);
+        const float4 vq = vs[j];
+        const double xd = (double)xs2[j];
+        const float acf = (float)(sp.cumE - h.cum);  // pending L1 of the row
+        const double t = xd * rj, b = (xd * xd) * rj;
+        const double gwe = (xd - 1.0) * yh + rj;  // x yhat - y (SGD.scala:145)
+        if (qok) {
+          const float4 v = shrink4f(vq, acf);
+          const double g0 = fma((double)Sq.x, t, 0.0) - (double)v.x * b, g1 = fma((double)Sq.y, t, 0.0) - (double)v.y * b;
+          const double g2 = fma((double)Sq.z, t, 0.0) - (double)v.z * b, g3 = fma((double)Sq.w, t, 0.0) - (double)v.w * b;
+          const float4 u = make_float4((float)fma(g0, -sp.scale_v, (double)v.x), (float)fma(g1, -sp.scale_v, (double)v.y),
+                                       (float)fma(g2, -sp.scale_v, (double)v.z), (float)fma(g3, -sp.scale_v, (double)v.w));
+          st_row4(r + 4 * g, shrink4f(u, lamf));
         }
-        st_row4(r + kp + i, hq);
-      }
+        for (int i = 4 * g; i < span; i += 4 * GS) {  // the header and the zero pad of its granule
+          float4 hq = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (i == 0) {
+            RowHdr o;
+            o.w = upd_w(shrink1f(h.w, acf), 0.0 + gwe, sp);  // SGD.scala:150, :171
+            o.t = sp.epoch + 1;
+            o.cum = sp.cum_next;
+            hq = *reinterpret_cast<const float4*>(&o);
+          }
+          st_row4(r + kp + i, hq);
+        }
       }
     }
   }
