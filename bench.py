@@ -811,8 +811,14 @@ def main():
                                         xgmi_frac_at_step_time=(egress / step_s / 1e9 / (XGMI_LINK_GBS * (world - 1))
                                                                 if world > 1 else None))
             else:
-                line["exchange"] = dict(xg, per="per iteration, the gradient all-reduce",
-                                        ring_GBs_at_step_time=xg["ring_bytes_per_rank"] / step_s / 1e9)
+                # the replicated leg: the dense fp32 gradient buffer [F][kp + 4] all-reduced every iteration
+                # (ring: 2 (R - 1) / R of it leaves each rank), against the step's own algorithmic bytes
+                line["exchange"] = dict(xg, per="per iteration, the gradient all-reduce (fp32 sums across ranks)",
+                                        ring_GBs_at_step_time=xg["ring_bytes_per_rank"] / step_s / 1e9,
+                                        xgmi_peak_GBs=XGMI_LINK_GBS * max(world - 1, 0),
+                                        xgmi_frac_at_step_time=(xg["ring_bytes_per_rank"] / step_s / 1e9 /
+                                                                (XGMI_LINK_GBS * (world - 1)) if world > 1 else None),
+                                        vs_step_algorithmic_bytes=xg["allreduce_B"] / max(fwd_b + upd_b, 1.0))
         if host_trace:
             line["host_trace"] = host_trace
         if host_path:
