@@ -10,6 +10,11 @@ timeout -k 10 900 python -u -m pytest tests/test_gpu_bucket.py tests/test_gpu_fu
     tests/test_gpu_ml.py tests/test_gpu_group.py tests/test_gpu_shard.py -x -v \
     --timeout 300 --timeout-method thread > $out/pytest.log 2>&1
 rc=$?; tail -1 $out/pytest.log >&2; [ $rc -ne 0 ] && exit $rc
+for sk in 3 0 2; do
+  SORT_CHECK_ONLY=1 timeout -k 10 120 ./tools/_bin_sort_bench 10223616 27 $sk >> $out/sort_bench.log 2>&1
+  rc=$?; [ $rc -gt 1 ] && exit $rc
+done
+grep -E "ms|mismatch" $out/sort_bench.log >&2
 timeout -k 10 120 ./tools/_bin_gather_ceiling > $out/gather.log 2>&1 || exit $?
 timeout -k 10 180 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-include-regex gather -T --output-format csv \
     -d $out/gather_pmc -o run -- ./tools/_bin_gather_ceiling > $out/gather_pmc.log 2>&1 || exit $?

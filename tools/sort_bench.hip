@@ -1,5 +1,6 @@
-// Measurement tool (not product): time the library's radix_sort_pairs64 against rocPRIM's
-// device radix sort on the same 10M (uint32 key, uint64 payload) pairs, 27-bit keys.
+// Measurement tool (not product): time the library's sorts (LSD passes, bucket sort, bucket sort
+// with the singleton split) against rocPRIM's device radix sort on the same 10M (uint32 key,
+// uint64 payload) pairs, 27-bit keys, and check their output against it.
 #include <hip/hip_runtime.h>
 #include <cstring>
 #include <rocprim/device/device_radix_sort.hpp>
@@ -72,31 +73,67 @@ int main(int argc, char** argv) {
   float ms;
   CK(hipEventElapsedTime(&ms, a, b));
   printf("rocprim radix_sort_pairs n=%lld bits=%d: %.3f ms\n", (long long)n, bits, ms / R);
-  // ours: the LSD passes (FM_SORT_BUCKET=0) and the bucket sort (=1, forced at any n)
+  // ours: the LSD passes, the bucket sort (whole view) and the bucket sort's split (the fused step's
+  // multi view: only the entries of keys that occur twice or more, checked against rocPRIM's output)
   std::vector<uint32_t> k1(n), k2(n);
   std::vector<uint2> v1(n), v2(n);
   CK(hipMemcpy(k1.data(), dk2, 4 * n, hipMemcpyDeviceToHost));
   CK(hipMemcpy(v1.data(), dv2, 8 * n, hipMemcpyDeviceToHost));
+  std::vector<uint32_t> mk;
+  std::vector<uint2> mv;
+  int64_t singles = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    const bool m = (i > 0 && k1[i - 1] == k1[i]) || (i + 1 < n && k1[i + 1] == k1[i]);
+    if (m) {
+      mk.push_back(k1[i]);
+      mv.push_back(v1[i]);
+    } else {
+      ++singles;
+    }
+  }
   int64_t bad_total = 0;
-  for (int mode = 0; mode < 2; ++mode) {
-    setenv("FM_SORT_BUCKET", mode ? "1" : "0", 1);
-    setenv("FM_SORT_BUCKET_MIN", "0", 1);
+  uint32_t* fk;
+  uint2* fv;
+  int64_t* dn;
+  CK(hipMalloc(&fk, 4 * n));
+  CK(hipMalloc(&fv, 8 * n));
+  CK(hipMalloc(&dn, 16));
+  for (int mode = 0; mode < 3; ++mode) {
     fmhip::SortWork sw;
-    const uint32_t* ok;
-    const uint2* ov;
-    for (int w = 0; w < 3; ++w) fmhip::radix_sort_pairs64(sw, dk, dv, n, bits, st, &ok, &ov);
+    const uint32_t* ok = fk;
+    const uint2* ov = fv;
+    auto run = [&] {
+      if (mode == 0)
+        fmhip::radix_sort_pairs64(sw, dk, dv, n, bits, st, &ok, &ov);
+      else if (!fmhip::bucket_sort_pairs64(sw, dk, dv, n, bits, st, fk, fv, mode == 2 ? dn : nullptr))
+        printf("bucket sort not applicable\n");
+    };
+    for (int w = 0; w < 3; ++w) run();
     CK(hipEventRecord(a, st));
-    for (int r = 0; r < R; ++r) fmhip::radix_sort_pairs64(sw, dk, dv, n, bits, st, &ok, &ov);
+    for (int r = 0; r < R; ++r) run();
     CK(hipEventRecord(b, st));
     CK(hipEventSynchronize(b));
     CK(hipEventElapsedTime(&ms, a, b));
-    printf("fm_hip radix_sort_pairs64 %s n=%lld bits=%d skew=%d: %.3f ms\n", mode ? "bucket" : "lsd", (long long)n, bits,
-           skew, ms / R);
-    CK(hipMemcpy(k2.data(), ok, 4 * n, hipMemcpyDeviceToHost));
-    CK(hipMemcpy(v2.data(), ov, 8 * n, hipMemcpyDeviceToHost));
+    const char* nm = mode == 0 ? "lsd" : mode == 1 ? "bucket" : "bucket-split";
+    printf("fm_hip %s n=%lld bits=%d skew=%d: %.3f ms\n", nm, (long long)n, bits, skew, ms / R);
+    int64_t cnt = n, hn[2] = {0, 0};
+    if (mode == 2) {
+      CK(hipMemcpy(hn, dn, 16, hipMemcpyDeviceToHost));
+      cnt = hn[0];
+    }
+    CK(hipMemcpy(k2.data(), ok, 4 * cnt, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(v2.data(), ov, 8 * cnt, hipMemcpyDeviceToHost));
     int64_t bad = 0;
-    for (int64_t i = 0; i < n; ++i) bad += (k1[i] != k2[i]) || (v1[i].x != v2[i].x) || (v1[i].y != v2[i].y);
-    printf("mismatches vs rocprim (%s, both stable): %lld\n", mode ? "bucket" : "lsd", (long long)bad);
+    const std::vector<uint32_t>& wk = mode == 2 ? mk : k1;
+    const std::vector<uint2>& wv = mode == 2 ? mv : v1;
+    if (mode == 2 && (hn[0] != (int64_t)mk.size() || hn[1] != singles)) {
+      printf("split counts %lld / %lld, expected %lld / %lld\n", (long long)hn[0], (long long)hn[1],
+             (long long)mk.size(), (long long)singles);
+      bad += 1;
+    }
+    for (int64_t i = 0; i < (int64_t)wk.size() && i < cnt; ++i)
+      bad += (wk[i] != k2[i]) || (wv[i].x != v2[i].x) || (wv[i].y != v2[i].y);
+    printf("mismatches vs rocprim (%s): %lld\n", nm, (long long)bad);
     bad_total += bad;
   }
   if (getenv("SORT_CHECK_ONLY")) return bad_total ? 1 : 0;
