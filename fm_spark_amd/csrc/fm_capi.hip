@@ -655,11 +655,10 @@ int fm_batch_prepare(fm_ctx* ctx, fm_batch* b) {
 int fm_batch_from_rows(fm_ctx* ctx, const fm_batch* data, const int64_t* rows, int64_t n, fm_batch** out) {
   return guarded(ctx, [&]() -> int {
     FM_REQUIRE(out != nullptr && data != nullptr, "null argument");
-    FM_REQUIRE(!ctx->group, "fm_batch_from_rows: single-GPU contexts (a multi-GPU context's dataset is split over its "
-                            "ranks; step its splits from host CSRs)");
     FM_REQUIRE(data->owner == ctx, "data belongs to another context");
     FM_REQUIRE(n >= 0 && n < (int64_t(1) << 31), "n out of range");
     FM_REQUIRE(n == 0 || rows != nullptr, "null rows");
+    if (ctx->group) return group_batch_from_rows(ctx, data, rows, n, out);
     const int64_t Bd = data->dev.n_rows;
     FM_REQUIRE((int64_t)data->host_rp.size() == Bd + 1,
                "data must be a batch made by fm_batch_create or fm_batch_from_rows");

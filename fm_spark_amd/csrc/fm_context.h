@@ -392,6 +392,7 @@ void shard_combine_predict(fm_ctx* ctx, fm_batch* b, const void* partials_in, co
 int group_create(const fm_config* cfg, fm_ctx** out);
 int group_batch_create(fm_ctx* ctx, const fm_csr* csr, fm_batch** out);
 int group_batch_prepare(fm_ctx* ctx, fm_batch* b);
+int group_batch_from_rows(fm_ctx* ctx, const fm_batch* data, const int64_t* rows, int64_t n, fm_batch** out);
 int group_step(fm_ctx* ctx, const fm_csr* csr, int32_t t, double step_size, double reg_param, fm_step_out* out);
 int group_step_batch(fm_ctx* ctx, fm_batch* b, int32_t t, double step_size, double reg_param, fm_step_out* out);
 int group_predict(fm_ctx* ctx, const fm_csr* csr, double lo, double hi, double* pred);

@@ -118,6 +118,10 @@ struct GroupBatch {
   Pinned cnt_pin;
   std::vector<hipEvent_t> ev_cnt;  // per local rank: its side-stream work of phase 1 is done
   Group* g = nullptr;              // the group while this batch is its pending phase 2
+  // fm_batch_from_rows with this batch as the dataset: every local rank's full copy of it (member
+  // batches on each rank's device, made at the first selection), from which each rank gathers its
+  // share of a split's rows
+  std::vector<fm_batch*> full;
   ~GroupBatch();
 };
 
@@ -168,6 +172,8 @@ GroupBatch::~GroupBatch() {
     if (p.b) fm_batch_destroy(p.b);
     p.b = nullptr;
   }
+  for (fm_batch* f : full)
+    if (f) fm_batch_destroy(f);
 }
 
 void GroupDeleter::operator()(Group* g) const { delete g; }
@@ -370,6 +376,7 @@ void upload_parts(Group& g, const fm_csr* c, GroupBatch& gb, bool check_range) {
     if (!p.b) p.b = new fm_batch();
     p.device = r.device;
     on(r, [&] { upload_batch(r.m, &sub, p.b, check_range); });
+    p.b->host_rp.assign(rp.begin(), rp.end());  // fm_batch_from_rows sizes selections of it on the host
     p.rows = sub.n_rows;
     p.row0 = r0;
     p.nnz = sub.nnz;
@@ -890,6 +897,102 @@ int group_batch_create(fm_ctx* ctx, const fm_csr* csr, fm_batch** out) {
   upload_parts(grp(ctx), csr, *b->grp, true);
   sync_group_batch_view(b.get());
   *out = b.release();
+  return FM_OK;
+}
+
+namespace {
+
+// Local rank l's full copy of the group batch dg (its parts copied from every rank's device): the
+// source of that rank's fm_batch_from_rows gathers.  Made once per dataset.
+fm_batch* dataset_replica(Group& g, GroupBatch& dg, int l) {
+  if ((int)dg.full.size() != g.L) dg.full.assign(g.L, nullptr);
+  if (dg.full[l]) return dg.full[l];
+  Rank& r = g.ranks[l];
+  std::unique_ptr<fm_batch> f(new fm_batch());
+  f->owner = r.m;
+  f->device = r.device;
+  const int64_t B = dg.rows, N = dg.nnz;
+  std::vector<int64_t> rp;
+  rp.reserve(B + 1);
+  int64_t off = 0, mx = -1;
+  for (const GPart& q : dg.parts) {
+    FM_REQUIRE((int64_t)q.b->host_rp.size() == q.rows + 1, "group dataset part without its host row_ptr");
+    for (int64_t i = 0; i < q.rows; ++i) rp.push_back(off + q.b->host_rp[i]);
+    off += q.nnz;
+    mx = std::max(mx, q.b->max_id);
+  }
+  rp.push_back(off);
+  FM_REQUIRE(off == N && (int64_t)rp.size() == B + 1, "group dataset parts do not add up");
+  on(r, [&] {
+    f->dev.n_rows = B;
+    f->dev.nnz = N;
+    f->max_id = mx;
+    f->dev.row_ptr.ensure(sizeof(int64_t) * (B + 1));
+    f->dev.col.ensure(sizeof(uint32_t) * std::max<int64_t>(N, 4) + 16);
+    f->dev.xs.ensure(sizeof(float) * std::max<int64_t>(N, 4) + 16);
+    f->dev.label.ensure(sizeof(double) * std::max<int64_t>(B, 4) + 16);
+    FM_HIP_CHECK(hipMemcpy(f->dev.row_ptr.p, rp.data(), sizeof(int64_t) * (B + 1), hipMemcpyHostToDevice));
+    int64_t e = 0, row = 0;
+    for (const GPart& q : dg.parts) {
+      if (q.nnz > 0) {
+        FM_HIP_CHECK(hipMemcpyPeer(f->dev.col.as<uint32_t>() + e, r.device, q.b->dev.col.p, q.device, sizeof(uint32_t) * q.nnz));
+        FM_HIP_CHECK(hipMemcpyPeer(f->dev.xs.as<float>() + e, r.device, q.b->dev.xs.p, q.device, sizeof(float) * q.nnz));
+      }
+      if (q.rows > 0)
+        FM_HIP_CHECK(hipMemcpyPeer(f->dev.label.as<double>() + row, r.device, q.b->dev.label.p, q.device,
+                                   sizeof(double) * q.rows));
+      e += q.nnz;
+      row += q.rows;
+    }
+  });
+  f->host_rp.swap(rp);
+  dg.full[l] = f.release();
+  return dg.full[l];
+}
+
+}  // namespace
+
+int group_batch_from_rows(fm_ctx* ctx, const fm_batch* data, const int64_t* rows, int64_t n, fm_batch** out) {
+  Group& g = grp(ctx);
+  FM_REQUIRE(data != nullptr && data->owner == ctx && data->grp, "data belongs to another context");
+  GroupBatch& dg = *const_cast<fm_batch*>(data)->grp;
+  for (int64_t i = 0; i < n; ++i) FM_REQUIRE(rows[i] >= 0 && rows[i] < dg.rows, "row index out of [0, rows of data)");
+  std::unique_ptr<fm_batch> fresh;
+  fm_batch* b = *out;
+  if (!b) {
+    fresh.reset(new_group_batch(ctx));
+    b = fresh.get();
+  }
+  FM_REQUIRE(b->owner == ctx && b->grp && b != data, "out must be a batch of this context other than data");
+  GroupBatch& gb = *b->grp;
+  drop_route(g, gb);  // a routed plan of the old contents is dropped before its buffers are reused
+  gb.parts.resize(g.L);
+  gb.prefetched = false;
+  gb.rows = n;
+  gb.nnz = 0;
+  std::vector<std::vector<int64_t>> cnt(g.L, std::vector<int64_t>(1));
+  for (int l = 0; l < g.L; ++l) {
+    Rank& r = g.ranks[l];
+    GPart& p = gb.parts[l];
+    const int64_t r0 = n * l / g.L, r1 = n * (l + 1) / g.L;  // the split's rows by rows, as upload_parts
+    fm_batch* src = dataset_replica(g, dg, l);
+    mcheck(fm_batch_from_rows(r.m, src, rows + r0, r1 - r0, &p.b), "fm_batch_from_rows");
+    p.device = r.device;
+    p.rows = r1 - r0;
+    p.row0 = r0;
+    p.nnz = fm_batch_nnz(p.b);
+    gb.nnz += p.nnz;
+    cnt[l][0] = p.rows;
+  }
+  // the global miniBatchSize: this process's rows, or every process's (one host wait for the counts)
+  if (g.nprocs == 1) {
+    gb.global_rows = n;
+  } else {
+    const std::vector<int64_t> all = allgather(g, cnt, 1);
+    gb.global_rows = std::accumulate(all.begin(), all.end(), int64_t(0));
+  }
+  sync_group_batch_view(b);
+  if (fresh) *out = fresh.release();
   return FM_OK;
 }
 

@@ -350,8 +350,9 @@ class FactorizationMachinesSGD:
     def fit(self, dataset: DataFrame, initial_tables=None, pipelined: bool | None = None) -> FactorizationMachinesModel:
         """createInitialModel (:218-252) + addSampleId + runMiniBatchSGD (:88-216).
         ``initial_tables`` = (ids, w, V) injects M0 (the reference's draw is unseeded, P9).
-        ``pipelined`` (default: on for a single-GPU estimator): the dataset is kept on the device
-        (dfData.cache(), :93), each randomSplit split is gathered there from its row list
+        ``pipelined`` (default: on): the dataset is kept on the device (every GPU of a multi-GPU estimator
+        gathers its share of a split from its own copy)
+        -- dfData.cache(), :93 --, each randomSplit split is gathered there from its row list
         (fm_batch_from_rows) and sorted on the side stream while the previous iteration steps, and
         the steps only enqueue; the loss log lines (:139) are written, in iteration order, when the
         loop has run.  False: every split crosses PCIe as a host CSR and its step returns its loss
@@ -365,11 +366,8 @@ class FactorizationMachinesSGD:
         F = p["numFeatures"] or (int(col.max()) + 1 if len(col) else 1)
         ctx = FMContext(F, k, device=p["device"], seed=p["seed"], init_sd=p["initialSd"], w0=0.0,
                         parallel=p["parallel"], n_gpus=p["nGpus"], devices=p["devices"], transport=p["transport"])
-        single = ctx.parallel is None
         if pipelined is None:
-            pipelined = single
-        if pipelined and not single:
-            raise ValueError("pipelined fit needs a single-GPU estimator (fm_batch_from_rows)")
+            pipelined = True
         # dfData.cache() (:93): the exploded dataset uploaded once
         data = ctx.batch(N.CSRHost(rp, col, val, labels)) if (pipelined or initial_tables is None) and len(labels) \
             else None

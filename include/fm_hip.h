@@ -205,8 +205,9 @@ int fm_batch_prepare(fm_ctx* ctx, fm_batch* batch);
  * gather runs on the context's side stream behind every queued step that reads *out, and the host
  * returns once it is enqueued (rows is copied); steps, fm_batch_prepare, fm_predict_batch and
  * fm_init_from_batch on the result are ordered after it.  data must stay alive until the gather has
- * run (fm_sync).  Single-GPU contexts only (a multi-GPU context's batches are split over its ranks;
- * FM_ERR_ARG). */
+ * run (fm_sync).  A multi-GPU context splits the selected rows contiguously over its local ranks,
+ * as fm_batch_create splits a host CSR; each rank gathers its share from its own copy of the
+ * dataset (made on its device from the dataset's parts at the first selection). */
 int fm_batch_from_rows(fm_ctx* ctx, const fm_batch* data, const int64_t* rows, int64_t n, fm_batch** out);
 /* 1 if a batch prepared by fm_batch_prepare on this context takes the fused step (fm_config.fuse_single
  * and the library's rule: single table, k <= 16, table above 256 MB unless FM_FUSE_ON), else 0;

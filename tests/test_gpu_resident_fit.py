@@ -176,3 +176,39 @@ def test_resident_loop_fused_matches_host_steps(gpu):
     np.testing.assert_allclose(a[2], b[2], rtol=1e-5, atol=1e-8)
     ctx.close()
     ref.close()
+
+
+@pytest.mark.parametrize("mode", ["sharded", "replicated"])
+def test_from_rows_on_a_multi_gpu_context(gpu, mode):
+    """fm_batch_from_rows on a 3-rank context (COPY transport on this GPU): each rank gathers its
+    contiguous share of the selection from its own copy of the dataset; the steps are the steps of
+    the host CSR of the same rows, bitwise (the same rows reach the same ranks in the same order)."""
+    from fm_spark_amd.engine import FMContext
+
+    F, k, R = 3000, 8, 3
+    data, ids, w, V = make_problem(1205, 2500, F, k, 9, hot=4)
+    rng = np.random.default_rng(12)
+    sels = [rng.permutation(2500)[:900], np.sort(rng.choice(2500, 1300)), rng.permutation(2500)[:2]]
+
+    def run(use_rows):
+        ctx = FMContext(F, k, parallel=mode, n_gpus=R, devices=[0] * R, transport="copy")
+        ctx.load_tables(ids, w, V)
+        d = ctx.batch(to_host(data))
+        into, out = None, []
+        for t, s in enumerate(sels, start=1):
+            if use_rows:
+                into = ctx.batch_from_rows(d, s, into=into)
+                b = into
+            else:
+                b = ctx.batch(to_host(_select(data, s)))
+            b.prepare()
+            o = ctx.step_batch(b, t, 0.3, 1e-3)
+            out.append((o.loss_sum, o.n_rows, o.n_loss_rows, o.n_unique))
+        tab = ctx.export_tables()
+        ctx.close()
+        return out, tab
+
+    a, b = run(True), run(False)
+    assert a[0] == b[0]
+    for x, y in zip(a[1], b[1]):
+        assert np.array_equal(x, y)
