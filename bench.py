@@ -89,6 +89,9 @@ def parse():
                    help="single table, k <= 16: the fused step (the forward updates the rows whose feature has one "
                         "entry in the batch; fm_config.fuse_single): auto = the library's default (tables larger "
                         "than the 256-MB Infinity Cache), on, off")
+    p.add_argument("--sort", default="default", choices=["default", "lsd", "bucket"],
+                   help="how a batch's entries are grouped by feature (fm_config.sort_algo): default = the library's "
+                        "choice (the bucket sort for batches of 2^20+ entries), lsd, bucket")
     p.add_argument("--trainer", default="lib", choices=["lib", "torch"],
                    help="N > 1: 'lib' = the multi-GPU fm_ctx, every exchange inside libfm_hip over RCCL (the "
                         "C-ABI path); 'torch' (torch.distributed.run only) = the torch.distributed test harness "
@@ -279,6 +282,17 @@ def requests_roof(req, seconds):
     return {"l2_requests": req, "achieved_G_per_s": rate, "ceiling_G_per_s": L2_REQ_CEILING_GPS,
             "frac": rate / L2_REQ_CEILING_GPS if L2_REQ_CEILING_GPS else None,
             "ceiling_source": "profiles/gather_ceiling.json (tools/gather_bench.hip, TCC_HIT + TCC_MISS)"}
+
+
+def grouping(sort, n, num_rows):
+    """Which sort groups a batch of n entries by feature slot (fm_capi.hip bucket_on, fm_sort.hip
+    bucket_hi_bits): "bucket" or "lsd"."""
+    kb = max(1, int(num_rows - 1).bit_length())
+    H = 10 if n // 512 > 8192 else 9
+    fits = 0 < n < 2**32 - 1 and kb >= H + 1 and kb - H <= 18
+    if sort == "lsd" or not fits:
+        return "lsd"
+    return "bucket" if sort == "bucket" or n >= 2**20 else "lsd"
 
 
 def sort_passes(num_rows):
@@ -487,7 +501,7 @@ def main():
     xg = None
     if mode == "single":
         ctx = FMContext(F, k, device=local_rank, seed=20261015, init_sd=INIT_SD,
-                        fuse={"auto": None, "on": True, "off": False}[args.fuse])
+                        fuse={"auto": None, "on": True, "off": False}[args.fuse], sort=args.sort)
         # launch on a torch stream of our own so torch events can bracket every step on it
         main_stream = torch.cuda.Stream()
         torch.cuda.set_stream(main_stream)
@@ -586,7 +600,8 @@ def main():
             dist.broadcast(idt, src=0)
             cid = bytes(idt.tolist())
         ctx = FMContext(F, k, seed=20261015, init_sd=INIT_SD, parallel=par, n_gpus=L, devices=pl["devices"],
-                        transport="rccl", n_procs=world if mode == "procs" else 1, proc_rank=rank, comm_id=cid)
+                        transport="rccl", n_procs=world if mode == "procs" else 1, proc_rank=rank, comm_id=cid,
+                        fuse={"auto": None, "on": True, "off": False}[args.fuse], sort=args.sort)
         main_stream = None
         if L == 1:  # launch on a torch stream so torch events time each step on it
             main_stream = torch.cuda.Stream()
@@ -744,7 +759,8 @@ def main():
             "config": {"workload": f"{args.config}: {desc}", "num_features": F, "k": k, "batch_rows_per_gpu": B,
                        "global_batch": B * world, "nnz_per_row": z, "rows_updated_per_gpu": U_mean,
                        "step_size": STEP_SIZE, "reg_param": REG_PARAM, "parallelism": parallelism,
-                       "launch": mode},
+                       "launch": mode,
+                       "grouping": grouping(args.sort, int(z * B), F // max(world, 1) if mode != "single" else F)},
             "loss_sum_all_steps": float(np.sum(losses)),
         }
         if args.trainer == "lib" and not args.host_path and not args.no_prefetch:
