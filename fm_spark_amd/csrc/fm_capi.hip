@@ -6,8 +6,10 @@
 #include <cmath>
 #include <cstring>
 #include <atomic>
+#include <cstdio>
 #include <map>
 #include <memory>
+#include <set>
 #include <thread>
 #include <utility>
 
@@ -17,6 +19,15 @@ namespace fmhip {
 
 static thread_local std::string g_last_error;
 void set_error(const std::string& msg) { g_last_error = msg; }
+
+void report_stale(hipError_t e) {
+  if (e == hipSuccess) return;
+  static std::mutex mu;
+  static std::set<int> seen;
+  std::lock_guard<std::mutex> lk(mu);
+  if (seen.insert((int)e).second)
+    fprintf(stderr, "[libfm_hip] cleared a stale HIP error left by an earlier call: %d %s\n", (int)e, hipGetErrorString(e));
+}
 
 void DevBuf::ensure(size_t n) {
   if (n <= bytes && p) return;

@@ -303,6 +303,8 @@ struct fm_ctx {
 
 
 namespace fmhip {
+void report_stale(hipError_t e);  // fm_capi.hip
+
 template <class F>
 int guarded(fm_ctx* ctx, F&& f) {
   if (!ctx) {
@@ -320,6 +322,10 @@ int guarded(fm_ctx* ctx, F&& f) {
     }
   } restore{prev_dev};
   try {
+    // a sticky error left by an earlier call whose status was ignored (a destructor's event waits)
+    // belongs to no launch of this call: reported on stderr once per code, then cleared, so that the
+    // launch checks below see their own launches only
+    report_stale(hipGetLastError());
     FM_HIP_CHECK(hipSetDevice(ctx->cfg.device));
     return f();
   } catch (const Error& e) {

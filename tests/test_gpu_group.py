@@ -109,6 +109,8 @@ def test_group_sharded_fused_owner_step(gpu, R, k, sort, transport):
             if t == 3:
                 bs[1].prepare()
         out[fuse] = ([(o.loss_sum, o.n_rows, o.n_loss_rows, o.n_unique) for o in res], ctx.export_tables())
+        for b in bs:
+            b.close()
         ctx.close()
     for t in range(1, 5):
         ref = R_.sgd_step_fast(model, probs[t - 1], t, 0.3, 1e-3)
