@@ -51,3 +51,23 @@ def test_fit_intercept_param_survives_copy_and_param_maps():
     assert fm.copy({"fitIntercept": False}).getFitIntercept() is False
     with pytest.raises(TypeError):
         fm.copy({"fitIntercept": 1.5})
+
+
+def test_select_csr_gathers_rows_in_order():
+    """The synchronous fit's per-split host CSR (_select_csr): rows in the given order, repeats and
+    empty rows kept, entries and labels carried along."""
+    import numpy as np
+
+    from fm_spark_amd.ml import _select_csr
+
+    rp = np.array([0, 2, 2, 5, 6], dtype=np.int64)
+    col = np.array([1, 4, 0, 2, 3, 7], dtype=np.int32)
+    val = np.arange(6, dtype=np.float64) + 0.5
+    lab = np.array([0.0, 1.0, 0.0, 1.0])
+    c = _select_csr(rp, col, val, lab, [3, 1, 2, 0, 2])
+    assert c.row_ptr.tolist() == [0, 1, 1, 4, 6, 9]
+    assert c.col.tolist() == [7, 0, 2, 3, 1, 4, 0, 2, 3]
+    assert c.val.tolist() == [5.5, 2.5, 3.5, 4.5, 0.5, 1.5, 2.5, 3.5, 4.5]
+    assert c.label.tolist() == [1.0, 1.0, 0.0, 0.0, 0.0]
+    e = _select_csr(rp, col, val, lab, [])
+    assert e.row_ptr.tolist() == [0] and e.n_rows == 0 and e.nnz == 0
