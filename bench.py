@@ -288,7 +288,9 @@ def grouping(sort, n, num_rows):
     """Which sort groups a batch of n entries by feature slot (fm_capi.hip bucket_on, fm_sort.hip
     bucket_hi_bits): "bucket" or "lsd"."""
     kb = max(1, int(num_rows - 1).bit_length())
-    H = 10 if n // 512 > 8192 else 9
+    H = 9
+    while H < 11 and n // (1 << H) > 30 * 1024 // 3:  # buckets of about a third of the 30K-entry LDS image
+        H += 1
     fits = 0 < n < 2**32 - 1 and kb >= H + 1 and kb - H <= 18
     if sort == "lsd" or not fits:
         return "lsd"

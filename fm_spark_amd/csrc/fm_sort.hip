@@ -22,7 +22,8 @@ namespace fmhip {
 
 namespace {
 
-constexpr int kMaxRB = 10;   // digit width at most (27-bit feature slots: 3 passes of 9 bits)
+constexpr int kMaxRB = 11;   // digit width at most (the bucket sort's top-bit pass)
+constexpr int kLsdMaxRB = 10;  // the LSD passes' digits at most (27-bit feature slots: 3 passes of 9 bits)
 constexpr int kBlock = 512;  // 8 waves x 8 keys per lane; two blocks (16 waves) per CU
 constexpr int kWaves = kBlock / 64;
 constexpr int kMinRB = 9;    // the block scans hold R / kBlock >= 1 digits per thread
@@ -284,7 +285,10 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint32_t* __rest
 // already in stable order and is copied; mixed, its block takes two counting passes through a
 // global scratch (slow for one huge mixed bucket -- a feature in every row of a large batch -- but
 // such a bucket is walked by one block, dispatched first, beside all the others).
-constexpr int kBB = 1024;          // phase-2 block: 16 waves, one block per CU (the image takes 120 KB)
+#ifndef FM_BKT_BB
+#define FM_BKT_BB 1024
+#endif
+constexpr int kBB = FM_BKT_BB;     // phase-2 block: 16 waves, one block per CU (the image takes 120 KB)
 constexpr int kBW = kBB / 64;
 constexpr int kBktCap = 30 * kBB;  // a bucket up to this size is ordered in LDS
 constexpr int kBktRB = 9;          // digit bits of one in-bucket pass (512 digits)
@@ -699,15 +703,30 @@ __global__ __launch_bounds__(kBB) void k_bucket_offsets(const uint32_t* __restri
                                                         uint2* __restrict__ boff, int64_t* __restrict__ n_out) {
   __shared__ uint32_t wsum[kBW];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const uint32_t sz = tid < nb ? btot[tid] : 0u;
-  const uint2 st = tid < nb ? bstat[tid] : make_uint2(0u, 0u);
-  const uint32_t start = bkt_excl_scan(sz, wsum, lane, wave);
-  const uint32_t moff = bkt_excl_scan(st.x, wsum, lane, wave);
-  const uint32_t sing = bkt_excl_scan(st.y, wsum, lane, wave);
-  if (tid < nb) boff[tid] = make_uint2(start, moff);
-  if (tid == nb - 1) {
-    n_out[0] = (int64_t)moff + st.x;
-    n_out[1] = (int64_t)sing + st.y;
+  uint32_t c_start = 0, c_moff = 0, c_sing = 0;  // block-uniform carries
+  for (int b0 = 0; b0 < nb; b0 += kBB) {
+    const int b = b0 + tid;
+    const uint32_t sz = b < nb ? btot[b] : 0u;
+    const uint2 st = b < nb ? bstat[b] : make_uint2(0u, 0u);
+    const uint32_t start = bkt_excl_scan(sz, wsum, lane, wave);
+    const uint32_t moff = bkt_excl_scan(st.x, wsum, lane, wave);
+    const uint32_t sing = bkt_excl_scan(st.y, wsum, lane, wave);
+    if (b < nb) boff[b] = make_uint2(c_start + start, c_moff + moff);
+    // the round's totals, from its last thread
+    if (tid == kBB - 1) {
+      wsum[0] = start + sz;
+      wsum[1] = moff + st.x;
+      wsum[2] = sing + st.y;
+    }
+    lds_barrier();
+    c_start += wsum[0];
+    c_moff += wsum[1];
+    c_sing += wsum[2];
+    lds_barrier();
+  }
+  if (tid == 0) {
+    n_out[0] = (int64_t)c_moff;
+    n_out[1] = (int64_t)c_sing;
   }
 }
 
@@ -769,7 +788,7 @@ static void radix_pass(const uint32_t* kin, const P* vin, uint32_t* ko, P* vo, i
 // slots: 3 passes of 9 bits), never narrower than kMinRB bits.
 inline int digit_bits(int key_bits, int* passes) {
   const int kb = key_bits < 1 ? 1 : key_bits;
-  int p = (kb + kMaxRB - 1) / kMaxRB;
+  int p = (kb + kLsdMaxRB - 1) / kLsdMaxRB;
   int rb = (kb + p - 1) / p;
   if (rb < kMinRB) rb = kMinRB;
   p = (kb + rb - 1) / rb;
@@ -845,7 +864,10 @@ namespace fmhip {
 
 int bucket_hi_bits(int64_t n, int key_bits) {
   if (n < 1 || n >= (int64_t(1) << 32) - 1) return 0;
-  const int H = n / 512 > 8192 ? 10 : 9;  // buckets of about 5K - 10K pairs at the sizes that matter
+  // buckets of about a third of the LDS image on average (hot features fill some to the image and
+  // beyond), 9 to 11 top bits
+  int H = 9;
+  while (H < kMaxRB && n / (int64_t(1) << H) > kBktCap / 3) ++H;
   if (key_bits < H + 1 || key_bits - H > 2 * kBktRB) return 0;  // one pass would do / too many low bits
   return H;
 }
@@ -868,10 +890,11 @@ bool bucket_sort_pairs64(SortWork& w, const uint32_t* keys_in, const uint2* vals
     kin = kbuf[1];
   }
   // phase 1: the top H bits
-  if (H == 9)
-    radix_pass<uint2, 9>(kin, vals_in, kbuf[0], vbuf[0], n, L, w, ntiles, st);
-  else
-    radix_pass<uint2, 10>(kin, vals_in, kbuf[0], vbuf[0], n, L, w, ntiles, st);
+  switch (H) {
+    case 9: radix_pass<uint2, 9>(kin, vals_in, kbuf[0], vbuf[0], n, L, w, ntiles, st); break;
+    case 10: radix_pass<uint2, 10>(kin, vals_in, kbuf[0], vbuf[0], n, L, w, ntiles, st); break;
+    default: radix_pass<uint2, 11>(kin, vals_in, kbuf[0], vbuf[0], n, L, w, ntiles, st); break;
+  }
   const uint32_t* btot = w.digit_tot.as<uint32_t>();
   uint32_t* order = w.digit_tot.as<uint32_t>() + kMaxRadix;
   uint2* bstat = w.bstat.as<uint2>();
