@@ -336,10 +336,11 @@ struct BktIO {
   int ib;                // 32 - L: index bits of the packed LDS word
 };
 
-// In-LDS pass for a bucket of m <= kBktCap entries, in place in S.arr (digit (sub >> shift) & 511).
+// In-LDS pass for a bucket of m <= kBktCap entries, in place in S.arr (digit (sub >> shift) &
+// (2^rb - 1), rb <= 9: the ranks take rb ballots per 64 entries).
 template <bool FROM_KEYS>
-__device__ __forceinline__ void bucket_pass_lds(BktShared& S, const BktIO& io, uint32_t m, int shift) {
-  constexpr int R = 1 << kBktRB;
+__device__ __forceinline__ void bucket_pass_lds(BktShared& S, const BktIO& io, uint32_t m, int shift, int rb) {
+  const int R = 1 << rb;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint32_t M = (uint32_t)R - 1u;
   const int dsh = io.ib + shift;
@@ -361,7 +362,7 @@ __device__ __forceinline__ void bucket_pass_lds(BktShared& S, const BktIO& io, u
     if (r * 64 >= nvw) break;
     const bool valid = r * 64 + lane < nvw;
     const uint32_t d = (v[r] >> dsh) & M;
-    const uint64_t peers = digit_peers(d, valid, kBktRB);
+    const uint64_t peers = digit_peers(d, valid, rb);
     const uint32_t below = (uint32_t)__popcll(peers & lt_mask);
     const uint32_t prev = S.cnt[wave][d];
     __builtin_amdgcn_wave_barrier();
@@ -597,8 +598,8 @@ __global__ __launch_bounds__(kBB) void k_bucket_sort(const uint32_t* __restrict_
   const uint32_t cap = min((uint32_t)kBktCap, 1u << min(io.ib, 31));
   uint32_t mcnt = 0;
   if (m <= cap) {
-    bucket_pass_lds<true>(S, io, m, 0);
-    if (L > kBktRB) bucket_pass_lds<false>(S, io, m, kBktRB);
+    bucket_pass_lds<true>(S, io, m, 0, L < kBktRB ? L : kBktRB);
+    if (L > kBktRB) bucket_pass_lds<false>(S, io, m, kBktRB, L - kBktRB);
     // the bucket in order in S.arr: coalesced key and payload writes, payloads gathered by index from
     // the bucket's own range
     const uint32_t imask = (1u << io.ib) - 1u;
