@@ -671,6 +671,7 @@ def main():
         losses = ctx.loss_history()
         assert np.all(np.isfinite(losses)), "non-finite loss"
         R = world
+        fused = ctx.fuse_active and par == "sharded"  # the fused owner step (selects the matching PMC file)
         # rows one rank updates: sharded, the global distinct ids over the owners; replicated, every
         # replica applies every touched row
         U_mean = float(np.mean(uniques)) / (R if par == "sharded" else 1)
@@ -780,7 +781,7 @@ def main():
             # "owner_forward" / "owner_update" do the same on the rank's own rows (per rank: the
             # entries an owner receives ~ its own batch's, the rows it updates ~ U / world)
             algo = {"forward": fwd_b, "update": upd_b, "owner_forward": fwd_b, "owner_update": upd_b}
-            if fused:
+            if fused and mode == "single":
                 # the fused forward also reads and writes the singleton rows (their 8(k+1) B each of
                 # the update's share); the segmented update keeps the rows with two or more entries
                 algo["forward"] = fwd_b + upd_b * single_frac

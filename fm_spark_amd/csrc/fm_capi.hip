@@ -740,7 +740,8 @@ int fm_batch_from_rows(fm_ctx* ctx, const fm_batch* data, const int64_t* rows, i
 
 int32_t fm_fuse_active(fm_ctx* ctx) {
   if (!ctx) return -1;
-  if (ctx->group) return 0;  // multi-GPU contexts step unfused
+  if (ctx->group)  // a sharded group's owners take the fused owner step by the same rule; replicas never fuse
+    return ctx->cfg.parallel == FM_PARALLEL_SHARDED && fuse_rule(group_member0(ctx)) ? 1 : 0;
   return fuse_on(ctx) ? 1 : 0;
 }
 

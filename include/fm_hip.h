@@ -210,8 +210,9 @@ int fm_batch_prepare(fm_ctx* ctx, fm_batch* batch);
  * dataset (made on its device from the dataset's parts at the first selection). */
 int fm_batch_from_rows(fm_ctx* ctx, const fm_batch* data, const int64_t* rows, int64_t n, fm_batch** out);
 /* 1 if a batch prepared by fm_batch_prepare on this context takes the fused step (fm_config.fuse_single
- * and the library's rule: single table, k <= 16, table above 256 MB unless FM_FUSE_ON), else 0;
- * -1 for a null context. */
+ * and the library's rule: k <= 16, table above 256 MB unless FM_FUSE_ON; a row-sharded context's
+ * owners take the fused owner step by the same rule, per member table; replicated contexts never
+ * fuse), else 0; -1 for a null context. */
 int32_t fm_fuse_active(fm_ctx* ctx);
 int64_t fm_batch_rows(const fm_batch* b);
 int64_t fm_batch_nnz(const fm_batch* b);
