@@ -6,7 +6,9 @@
 #include <cmath>
 #include <cstring>
 #include <atomic>
+#include <condition_variable>
 #include <cstdio>
+#include <functional>
 #include <map>
 #include <memory>
 #include <set>
@@ -46,20 +48,108 @@ void DevBuf::release() {
   bytes = 0;
 }
 
-// f(lo, hi) over [0, n) in contiguous chunks on up to 16 host threads (the GPU box's CPU share per
-// GPU); small ranges run inline.
+// A persistent pool of host threads (up to 16: the GPU box's CPU share per GPU) for the host passes
+// of fm_step's upload and fm_batch_from_rows: spawning the threads per call cost about as much as
+// the work.  One job at a time (callers serialise on run_mu); the calling thread works too.
+class HostPool {
+ public:
+  static HostPool& get() {
+    static HostPool p;
+    return p;
+  }
+  int threads() const { return (int)workers_.size() + 1; }
+  // f(i) for every i in [0, n)
+  void run(int n, const std::function<void(int)>& f) {
+    if (n <= 0) return;
+    std::lock_guard<std::mutex> job_lk(run_mu_);
+    if (n == 1 || workers_.empty()) {
+      for (int i = 0; i < n; ++i) f(i);
+      return;
+    }
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      job_ = &f;
+      njobs_ = n;
+      next_.store(0);
+      done_ = 0;
+      ++gen_;
+    }
+    cv_.notify_all();
+    work();
+    std::unique_lock<std::mutex> lk(mu_);
+    done_cv_.wait(lk, [&] { return done_ == njobs_; });
+    job_ = nullptr;
+  }
+  ~HostPool() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : workers_) t.join();
+  }
+
+ private:
+  HostPool() {
+    const int hw = std::max(1, (int)std::thread::hardware_concurrency());
+    const int T = std::min(16, hw);
+    for (int t = 1; t < T; ++t) workers_.emplace_back([this] { loop(); });
+  }
+  void work() {
+    int mine = 0;
+    for (int i = next_.fetch_add(1); i < njobs_; i = next_.fetch_add(1)) {
+      (*job_)(i);
+      ++mine;
+    }
+    if (mine) {
+      std::lock_guard<std::mutex> lk(mu_);
+      done_ += mine;
+      if (done_ == njobs_) done_cv_.notify_all();
+    }
+  }
+  void loop() {
+    uint64_t seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return stop_ || (gen_ != seen && job_ != nullptr); });
+        if (stop_) return;
+        seen = gen_;
+      }
+      work();
+    }
+  }
+  std::vector<std::thread> workers_;
+  std::mutex run_mu_, mu_;
+  std::condition_variable cv_, done_cv_;
+  const std::function<void(int)>* job_ = nullptr;
+  int njobs_ = 0, done_ = 0;
+  std::atomic<int> next_{0};
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+};
+
+// How many contiguous chunks parallel_chunks cuts [0, n) into (one per pool thread, at least
+// min_per_thread items each).
+static int64_t chunk_count(int64_t n, int64_t min_per_thread) {
+  return std::max<int64_t>(1, std::min<int64_t>(HostPool::get().threads(), n / std::max<int64_t>(min_per_thread, 1)));
+}
+
+// f(t, lo, hi) for chunk t = [n t / T, n (t + 1) / T) of T chunks, on the pool's threads.
 template <class F>
-static void parallel_chunks(int64_t n, int64_t min_per_thread, F&& f) {
-  const int64_t hw = std::max<int64_t>(1, (int64_t)std::thread::hardware_concurrency());
-  const int64_t T = std::max<int64_t>(1, std::min<int64_t>({16, hw, n / std::max<int64_t>(min_per_thread, 1)}));
+static void parallel_chunks_t(int64_t n, int64_t T, F&& f) {
   if (T <= 1) {
-    f(int64_t(0), n);
+    f(int64_t(0), int64_t(0), n);
     return;
   }
-  std::vector<std::thread> th;
-  th.reserve(T);
-  for (int64_t t = 0; t < T; ++t) th.emplace_back([&, t] { f(n * t / T, n * (t + 1) / T); });
-  for (auto& x : th) x.join();
+  const std::function<void(int)> job = [&](int t) { f((int64_t)t, n * t / T, n * (t + 1) / T); };
+  HostPool::get().run((int)T, job);
+}
+
+// f(lo, hi) over [0, n) in contiguous chunks on the pool's threads; small ranges run inline.
+template <class F>
+static void parallel_chunks(int64_t n, int64_t min_per_thread, F&& f) {
+  parallel_chunks_t(n, chunk_count(n, min_per_thread), [&](int64_t, int64_t lo, int64_t hi) { f(lo, hi); });
 }
 
 // Host CSR -> pinned staging [row_ptr int64 B+1][label f64 B][xoff int32 B][col u32 N][x f32 N]:
@@ -672,7 +762,7 @@ int fm_batch_from_rows(fm_ctx* ctx, const fm_batch* data, const int64_t* rows, i
     if (ctx->group) return group_batch_from_rows(ctx, data, rows, n, out);
     const int64_t Bd = data->dev.n_rows;
     FM_REQUIRE((int64_t)data->host_rp.size() == Bd + 1,
-               "data must be a batch made by fm_batch_create or fm_batch_from_rows");
+               "data must be a batch made by fm_batch_create");
     fm_batch* b = *out;
     std::unique_ptr<fm_batch> fresh;
     if (b == nullptr) {
@@ -683,16 +773,6 @@ int fm_batch_from_rows(fm_ctx* ctx, const fm_batch* data, const int64_t* rows, i
     } else {
       FM_REQUIRE(b->owner == ctx && b != data && !b->grp, "out must be a batch of this context other than data");
     }
-    // the rows' result row_ptr on the host, from the dataset's (validated on the way)
-    std::vector<int64_t> rp((size_t)n + 1);
-    rp[0] = 0;
-    for (int64_t i = 0; i < n; ++i) {
-      const int64_t r = rows[i];
-      FM_REQUIRE(r >= 0 && r < Bd, "row index out of [0, rows of data)");
-      rp[i + 1] = rp[i] + (data->host_rp[r + 1] - data->host_rp[r]);
-    }
-    const int64_t N = rp[n];
-    FM_REQUIRE(N < (int64_t(1) << 31), "nnz must be < 2^31 per batch");
     if (!b->ready) {
       FM_HIP_CHECK(hipEventCreateWithFlags(&b->ready, hipEventDisableTiming));
       FM_HIP_CHECK(hipEventCreateWithFlags(&b->last_use, hipEventDisableTiming));
@@ -707,9 +787,41 @@ int fm_batch_from_rows(fm_ctx* ctx, const fm_batch* data, const int64_t* rows, i
     FM_HIP_CHECK(hipEventSynchronize(b->sel_copied));
     const size_t img = sizeof(int64_t) * (2 * (size_t)n + 1);
     b->sel_pin.ensure(img);
-    int64_t* hp = reinterpret_cast<int64_t*>(b->sel_pin.p);
-    if (n > 0) std::memcpy(hp, rows, sizeof(int64_t) * n);
-    std::memcpy(hp + n, rp.data(), sizeof(int64_t) * (n + 1));
+    int64_t* hrows = reinterpret_cast<int64_t*>(b->sel_pin.p);
+    int64_t* rp = hrows + n;
+    // the rows and their result row_ptr straight into the pinned staging, from the dataset's row_ptr
+    // (validated on the way): random reads of the dataset's row_ptr, about 2 ms for 256K rows on one
+    // thread -- longer than the GPU step -- so on the pool's threads, each chunk's running lengths,
+    // then the chunks' offsets
+    rp[0] = 0;
+    const int64_t* hrp = data->host_rp.data();
+    const int64_t T = chunk_count(n, 8192);
+    std::vector<int64_t> tot(T + 1, 0);
+    std::atomic<int> bad{0};
+    parallel_chunks_t(n, T, [&](int64_t t, int64_t lo, int64_t hi) {
+      int64_t acc = 0;
+      for (int64_t i = lo; i < hi; ++i) {
+        const int64_t r = rows[i];
+        if (r < 0 || r >= Bd) {
+          bad.store(1);
+          return;
+        }
+        hrows[i] = r;
+        acc += hrp[r + 1] - hrp[r];
+        rp[i + 1] = acc;
+      }
+      tot[t + 1] = acc;
+    });
+    FM_REQUIRE(!bad.load(), "row index out of [0, rows of data)");
+    for (int64_t t = 0; t < T; ++t) tot[t + 1] += tot[t];  // the chunks' offsets
+    if (T > 1)
+      parallel_chunks_t(n, T, [&](int64_t t, int64_t lo, int64_t hi) {
+        const int64_t add = tot[t];
+        if (add)
+          for (int64_t i = lo; i < hi; ++i) rp[i + 1] += add;
+      });
+    const int64_t N = rp[n];
+    FM_REQUIRE(N < (int64_t(1) << 31), "nnz must be < 2^31 per batch");
     // batch-only work on the side stream, behind every queued step that reads this batch
     FM_HIP_CHECK(hipStreamWaitEvent(ctx->side, b->last_use, 0));
     b->dev.n_rows = n;
@@ -732,7 +844,7 @@ int fm_batch_from_rows(fm_ctx* ctx, const fm_batch* data, const int64_t* rows, i
     }
     FM_HIP_CHECK(hipEventRecord(b->built, ctx->side));
     b->prepared = false;  // a refilled batch is sorted again by its own fm_batch_prepare
-    b->host_rp.swap(rp);
+    b->host_rp.clear();   // a selection is not itself a dataset (fm_batch_create's batches are)
     if (fresh) *out = fresh.release();
     return FM_OK;
   });

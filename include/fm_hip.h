@@ -199,8 +199,8 @@ int fm_batch_prepare(fm_ctx* ctx, fm_batch* batch);
  * of the cached training data that each SGD iteration consumes -- dfData.cache() and
  * dfData.randomSplit(...) (FactorizationMachinesSGD.scala:93, 111-112): the dataset crosses PCIe
  * once (fm_batch_create), each split is a row list (fm_random_split) gathered on the device.
- * data: a batch of this context made by fm_batch_create or fm_batch_from_rows (the library keeps its
- * row_ptr on the host too, so the result is sized without a device read).  *out == NULL: a new
+ * data: a batch of this context made by fm_batch_create (the library keeps its row_ptr on the host
+ * too, so the result is sized without a device read; the host pass runs on a pool of host threads).  *out == NULL: a new
  * batch is created; otherwise *out (a batch of this context, not data) is refilled in place.  The
  * gather runs on the context's side stream behind every queued step that reads *out, and the host
  * returns once it is enqueued (rows is copied); steps, fm_batch_prepare, fm_predict_batch and
