@@ -17,11 +17,14 @@ done
 cat $out/sort_bench_512.log >&2
 for rep in ${REPS:-1 2 3}; do
   for c in ${CONFIGS:-c3 c2 c5}; do
-    for v in lsd b1024 b512; do
-      lib=""; srt=default
+    vs="lsd b1024 b512"
+    [ $c != c3 ] && vs="$vs fon"   # c2 / c5: the fused step now that the split left the main stream
+    for v in $vs; do
+      lib=""; srt=default; fz=auto
       [ $v = lsd ] && srt=lsd
       [ $v = b512 ] && lib=$V512
-      FM_HIP_LIB=$lib timeout -k 10 300 python bench.py $B --config $c --sort $srt > $out/ab_${c}_${v}_$rep.log 2>&1 || exit $?
+      [ $v = fon ] && fz=on
+      FM_HIP_LIB=$lib timeout -k 10 300 python bench.py $B --config $c --sort $srt --fuse $fz > $out/ab_${c}_${v}_$rep.log 2>&1 || exit $?
       echo "$c $v rep$rep $(ms $out/ab_${c}_${v}_$rep.log)" >&2
     done
   done
