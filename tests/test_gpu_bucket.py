@@ -142,3 +142,41 @@ def test_bucket_sort_against_oracle_and_c3_key_width(gpu):
     gw, gV, _ = res[0][1]
     np.testing.assert_allclose(gw, model.w, rtol=1e-5, atol=1e-8)
     np.testing.assert_allclose(gV, model.V, rtol=1e-5, atol=1e-8)
+
+
+def test_bucket_sort_oversized_bucket_at_c3_key_width(gpu):
+    """27-bit slots with a feature in every one of 60,000 rows: its bucket (18 low bits, a 16K-entry
+    LDS image) goes through the global-scratch passes (9 + 9 bits) and, fused, the in-place
+    compaction; another feature alone in its bucket in every row (copied as one run).  Fused and
+    unfused, bucket-sorted steps bitwise equal to the LSD-sorted ones over the touched rows."""
+    from fm_spark_amd.engine import FMContext
+
+    F, k = 100_000_000, 16
+    rng = np.random.default_rng(17)
+    hot_mixed, hot_alone = 12_345, 50_000_000  # bucket 0 (ids < 2^18) is full of other ids too
+    rows = []
+    for _ in range(60_000):
+        z = int(rng.integers(2, 20))
+        ids = rng.integers(0, F, size=z)
+        ids = ids[(ids >> 18) != (hot_alone >> 18)]
+        ids = np.concatenate([ids, rng.integers(0, 1 << 18, size=2), [hot_mixed, hot_alone]])
+        rows.append(np.unique(ids))
+    csr = _csr_from_rows(rows, rng, F)
+    touched = np.unique(csr.col).astype(np.int32)
+    for fuse in (True, False):
+        res = []
+        for sort in ("bucket", "lsd"):
+            ctx = FMContext(F, k, fuse=fuse, sort=sort, seed=3, init_sd=0.01)
+            ctx.init_from_batch(ctx.batch(to_host(csr)))
+            b = ctx.batch(to_host(csr))
+            ls = []
+            for t in (1, 2):
+                b.prepare()
+                o = ctx.step_batch(b, t, 0.3, 1e-4)
+                ls.append((o.loss_sum, o.n_unique))
+            res.append((ls, ctx.export_rows(touched)))
+            b.close()
+            ctx.close()
+        assert res[0][0] == res[1][0]
+        for x, y in zip(res[0][1], res[1][1]):
+            assert np.array_equal(x, y)
