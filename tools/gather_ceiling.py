@@ -19,26 +19,36 @@ for line in open(log):
     m = re.match(r"VARIANT (gather<[^>]*>) ms=([0-9.]+) rows=(\d+)", line)
     if m:
         ms[m.group(1).replace(" ", "")] = (float(m.group(2)), int(m.group(3)))
-req = defaultdict(lambda: defaultdict(list))
+# rocprofv3 -T truncates the kernel names to "gather": the dispatches are attributed to the
+# variants by order (each variant: 2 warm-up + 10 timed launches, in the order the tool prints them)
+disp = defaultdict(float)
 for f in glob.glob(os.path.join(pmc, "**", "*counter_collection.csv"), recursive=True):
     for r in csv.DictReader(open(f)):
-        m = re.search(r"gather<[^>]*>", r["Kernel_Name"].replace(" ", ""))
-        if m:
-            req[m.group(0)][(int(r.get("Dispatch_Id") or 0))].append(float(r["Counter_Value"]))
+        if r["Kernel_Name"].startswith("gather") or "gather<" in r["Kernel_Name"]:
+            disp[int(r.get("Dispatch_Id") or 0)] += float(r["Counter_Value"])  # TCC_HIT_sum + TCC_MISS_sum
+order = [d for d in sorted(disp)]
+req = {}
+for i, name in enumerate(ms):  # dict order = the tool's print order
+    chunk = order[12 * i: 12 * (i + 1)]
+    if len(chunk) == 12:
+        req[name] = [disp[d] for d in chunk[2:]]  # the timed launches
 variants = {}
-for name, (t, n) in sorted(ms.items()):
-    per = [sum(v) for v in req.get(name, {}).values()]  # TCC_HIT_sum + TCC_MISS_sum per dispatch
+for name, (t, n) in ms.items():
+    per = req.get(name, [])
     if not per:
         continue
     r = sum(per) / len(per)
     variants[name] = {"ms": t, "gathers": n, "l2_requests": r, "requests_per_gather": r / n,
                       "l2_requests_per_s": r / (t * 1e-3)}
 ceil = max(variants.values(), key=lambda v: v["l2_requests_per_s"]) if variants else None
+uni = [v for k, v in variants.items() if k.endswith(",0>")]
+ceil_uni = max(uni, key=lambda v: v["l2_requests_per_s"]) if uni else None
 res = {"what": "L2 requests (TCC_HIT_sum + TCC_MISS_sum) per second of random row gathers "
                "(tools/gather_ceiling.hip: 10.2M gathers over a 100M-record table; <LPR lanes, U in flight, "
                "record floats, 0 uniform / 1 40 % hot>)",
        "variants": variants,
        "l2_requests_per_s": ceil["l2_requests_per_s"] if ceil else None,
+       "uniform_l2_requests_per_s": ceil_uni["l2_requests_per_s"] if ceil_uni else None,
        "source": {"log": log, "pmc": pmc}}
 open(out, "w").write(json.dumps(res, indent=1, sort_keys=True) + "\n")
 print(json.dumps({k: v["l2_requests_per_s"] / 1e9 for k, v in variants.items()}, indent=1))
