@@ -243,9 +243,12 @@ except (OSError, ValueError, KeyError, TypeError):
     pass
 
 
-def _pmc_files(F, k, B, fused, mode, world):
+def _pmc_files(F, k, B, fused, mode, world, group=None):
+    """The committed PMC files of this workload; with `group` ("lsd" / "bucket"), those counted
+    with that grouping sort first, then those that do not say."""
     import glob
 
+    hits = []
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json"))):
         try:
             d = json.load(open(f))
@@ -253,7 +256,11 @@ def _pmc_files(F, k, B, fused, mode, world):
             continue
         if (d.get("num_features"), d.get("k"), d.get("batch_rows"), bool(d.get("fused", False)),
                 d.get("mode", "single"), d.get("world", 1)) == (F, k, B, fused, mode, world):
-            yield f, d
+            g = d.get("grouping")
+            if group is None or g in (None, group):
+                hits.append((g is None, f, d))
+    for _, f, d in sorted(hits, key=lambda h: h[0]):
+        yield f, d
 
 
 def _requests(kc):
@@ -294,12 +301,10 @@ def grouping(sort, n, num_rows):
     bucket_hi_bits): "bucket" or "lsd"."""
     kb = max(1, int(num_rows - 1).bit_length())
     H = 9
-    while H < 11 and n // (1 << H) > 30 * 1024 // 3:  # buckets of about a third of the 30K-entry LDS image
+    while H < 11 and n // (1 << H) > 30 * 512 // 3:  # buckets of about a third of the 15K-entry LDS image
         H += 1
     fits = 0 < n < 2**32 - 1 and kb >= H + 1 and kb - H <= 18
-    if sort == "lsd" or not fits:
-        return "lsd"
-    return "bucket" if sort == "bucket" or n >= 2**20 else "lsd"
+    return "bucket" if sort == "bucket" and fits else "lsd"
 
 
 def sort_passes(num_rows):
@@ -311,17 +316,41 @@ def sort_passes(num_rows):
     return -(-kb // rb)
 
 
-def step_traffic(F, k, B, fused):
+def step_kernels(F, n, sort, fused):
+    """Launches per single-table step of each kernel (fm_capi.hip step_impl / fm_batch_prepare,
+    fm_sort.hip): the forward, update and combine; the fused step's tags; the grouping sort's --
+    LSD: count / chunk scan / chunk top / scatter per digit pass (+ the split kernels, fused);
+    bucket: the top-bit pass, the big path's one or two passes, the plan and the phase-2 kernel
+    (+ the big path's split and the compaction, fused)."""
+    ps = {"k_forward": 1, "k_segment_update": 1, "k_segment_combine": 1}
+    if fused:
+        ps["k_tag_runs"] = 1
+    if grouping(sort, n, F) == "lsd":
+        passes = sort_passes(F)
+        if fused:
+            ps.update({"k_split_count": 1, "k_split_scan": 1, "k_split_scatter": 1})
+    else:
+        kb = max(1, int(F - 1).bit_length())
+        H = 9
+        while H < 11 and n // (1 << H) > 30 * 512 // 3:
+            H += 1
+        passes = 1 + (1 if kb - H <= 11 else 2)
+        ps.update({"k_big_plan": 1, "k_bucket_sort": 1})
+        if fused:
+            ps.update({"k_big_split_count": 1, "k_big_split_scan": 1, "k_big_split_write": 1,
+                       "k_bucket_offsets": 1, "k_bucket_compact": 1})
+    ps.update({"k_radix_count": passes, "k_radix_chunk_scan": passes, "k_radix_chunk_top": passes,
+               "k_radix_scatter": passes})
+    return ps
+
+
+def step_traffic(F, k, B, fused, n, sort):
     """Counted HBM bytes and L2 requests of one whole single-table step: every kernel's per-launch
     figures in the committed PMC passes of this workload times its launches per step (the file's
-    "per_step" map when it has one, else the sort's kernels once per digit pass).  None unless
-    every kernel of the step was counted."""
-    per_step = {"k_forward": 1, "k_segment_update": 1, "k_segment_combine": 1}
-    n = sort_passes(F)
-    per_step.update({"k_radix_count": n, "k_radix_scan_rows": n, "k_radix_scatter": n})
-    if fused:
-        per_step.update({"k_split_count": 1, "k_split_scan": 1, "k_split_scatter": 1})
-    for f, d in _pmc_files(F, k, B, fused, "single", 1):
+    "per_step" map when it has one, else step_kernels).  None unless every kernel of the step was
+    counted."""
+    per_step = step_kernels(F, n, sort, fused)
+    for f, d in _pmc_files(F, k, B, fused, "single", 1, grouping(sort, n, F)):
         ks = d.get("kernels", {})
         ps = d.get("per_step", per_step)
         if all("traffic_bytes" in ks.get(kn, {}) for kn in ps):
@@ -818,7 +847,7 @@ def main():
                                      "achieved_GBs": step_bytes / (ms_per_step * 1e-3) / 1e9,
                                      "frac": step_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS}
             if mode == "single":
-                st_t, st_r, st_src = step_traffic(F, k, B, fused)
+                st_t, st_r, st_src = step_traffic(F, k, B, fused, int(z * B), args.sort)
                 if st_t:  # every kernel of the step, counted (PMC), against the step's time
                     line["step_roofline"].update(traffic=st_t, traffic_GBs=st_t / (ms_per_step * 1e-3) / 1e9,
                                                  traffic_frac=st_t / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS,

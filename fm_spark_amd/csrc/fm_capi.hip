@@ -262,9 +262,10 @@ static bool fuse_on(const fm_ctx* ctx) { return ctx->cfg.shard_count == 1 && fus
 // The bucket sort (fm_sort.hip) for a batch of N entries of this context, or the LSD passes
 // (fm_config.sort_algo; both stable, so the step is bitwise the same)
 bool bucket_on(const fm_ctx* ctx, int64_t N) {
-  if (ctx->cfg.sort_algo == FM_SORT_LSD) return false;
-  if (bucket_hi_bits(N, bits_for(ctx->rows - 1)) == 0) return false;
-  return ctx->cfg.sort_algo == FM_SORT_BUCKET || N >= (int64_t(1) << 20);
+  // the bucket sort on request only: in the step it measured slower than the LSD passes at c3, c2
+  // and c5 (its top-bit pass scatters 1024-2048 digits per tile, runs of 2-4 entries, and phase 2
+  // gathers payloads by index: more L2 requests than the passes it saves)
+  return ctx->cfg.sort_algo == FM_SORT_BUCKET && bucket_hi_bits(N, bits_for(ctx->rows - 1)) != 0;
 }
 
 static bool batch_fits(const fm_batch* b, const Staged& g) {
@@ -1071,7 +1072,7 @@ int fm_vector_sum_by_key(fm_ctx* ctx, const int32_t* keys, int64_t n, const doub
     FM_HIP_CHECK(hipMemcpy(out_sums, dos.p, sizeof(double) * nu * k, hipMemcpyDeviceToHost));
     *n_out = nu;
     DevBuf* bufs[] = {&dk, &dvec, &dok, &dos, &drun, &dn, &sw.keys_a, &sw.keys_b, &sw.vals_a, &sw.vals_b,
-                      &sw.counts, &sw.digit_tot, &sw.bscratch, &sw.bstat};
+                      &sw.counts, &sw.digit_tot, &sw.bscratch, &sw.bstat, &sw.bplan};
     for (auto* bb : bufs) bb->release();
     return FM_OK;
   });

@@ -294,8 +294,9 @@ struct fm_ctx {
                       &route_sort.keys_a, &route_sort.keys_b, &route_sort.vals_a, &route_sort.vals_b,
                       &route_sort.counts, &route_sort.digit_tot,
                       &sh_okey, &sh_mask, &sh_tcnt, &sh_tot, &sh_pay, &sh_skey, &sh_ent2, &repl_cnt,
-                      &split_work.cnt, &split_work.off, &work.sort.bscratch, &work.sort.bstat,
-                      &side_sort.bscratch, &side_sort.bstat, &route_sort.bscratch, &route_sort.bstat};
+                      &split_work.cnt, &split_work.off, &work.sort.bscratch, &work.sort.bstat, &work.sort.bplan,
+                      &side_sort.bscratch, &side_sort.bstat, &side_sort.bplan, &route_sort.bscratch,
+                      &route_sort.bstat, &route_sort.bplan};
     for (auto* b : bufs) b->release();
     if (own_stream && stream) (void)hipStreamDestroy(stream);
   }

@@ -84,7 +84,8 @@ struct DevBuf {
 // ------------------------------------------------------------------- radix sort
 struct SortWork {
   DevBuf keys_a, keys_b, vals_a, vals_b, counts, digit_tot;
-  DevBuf bscratch, bstat;  // bucket sort: oversized buckets' scratch, per-bucket counts and offsets
+  DevBuf bscratch, bstat, bplan;  // bucket sort: the big path's middle pass, per-bucket counts and
+                                  // offsets, the big path's segments / tiles
   int64_t cap = 0;
   void ensure(int64_t n);
 };

@@ -1759,7 +1759,8 @@ __global__ __launch_bounds__(kBlock) void k_owner_single(TableView T, const int6
     const float2 ry = *reinterpret_cast<const float2*>(sr + kp);
     const double rj = (double)ry.x, yh = (double)ry.y;
     for (int64_t eb = e0 + rs; eb < e1; eb += 2 * RPP) {
-      // two entries' rows in flight per lane group: header and V quad of each issued together
+      // two entries in flight per lane group: their headers first, then the V quads of the untagged
+      // ones only (a multi run's row costs this pass one header read, not the whole record)
       uint32_t ids[2];
       float xs2[2];
       RowHdr hs[2];
@@ -1771,9 +1772,12 @@ __global__ __launch_bounds__(kBlock) void k_owner_single(TableView T, const int6
         ids[j] = ok ? slot[e] : 0u;
         xs2[j] = ok ? __uint_as_float(ent[e].y) : 0.f;
         hs[j] = ok ? *T.hdr(ids[j]) : RowHdr{0.f, -1, 0.0};
-        vs[j] = ok && qok ? reinterpret_cast<const float4*>(T.v(ids[j]))[g] : make_float4(0.f, 0.f, 0.f, 0.f);
         if (!ok) hs[j].t = multi_tag(sp.epoch, false);  // nothing to update
       }
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        vs[j] = !is_multi(hs[j].t, sp.epoch) && qok ? reinterpret_cast<const float4*>(T.v(ids[j]))[g]
+                                                     : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const RowHdr h = hs[j];

@@ -7,11 +7,16 @@
 //
 // Per pass (RB-bit digit, 9..10 bits: 27-bit feature slots take 3 passes of 9 bits; tiles of both
 // kernels grouped by XCD):
-//   count   : one 512-thread block per 4096-key tile, LDS histogram  -> counts[digit][tile]
-//   scan    : one block per digit, exclusive scan along tiles        -> counts, digit totals
+//   count   : one 512-thread block per 4096-key tile, LDS histogram  -> counts[tile][digit]
+//   chunk   : one block per 16 tiles, exclusive scan down each digit  -> counts, chunk sums
+//   top     : 32 digits per block, exclusive scan of the chunk sums   -> chunk prefixes, digit totals
 //   scatter : each wave ranks its 512 keys with RB ballots per round (wave64 match), the
 //             block stages the tile in LDS in digit order, then writes runs coalesced; tiles
 //             are mapped to XCDs in contiguous groups.
+// The per-tile counts are tile-major: a tile's 2^RB counts are one contiguous row, written and read
+// in 16 L2 requests (digit-major, the same counts cost one request per digit per tile, 1024 per tile
+// between the count and the scatter, a third of a c3 pass's L2 requests; the step is bound by the
+// L2 request rate).
 // HBM traffic per pass: 4 B (count) + (4 + P) B read + (4 + P) B write per pair.
 #include <type_traits>
 
@@ -30,6 +35,7 @@ constexpr int kMinRB = 9;    // the block scans hold R / kBlock >= 1 digits per 
 constexpr int kRounds = 8;   // keys per thread per tile
 constexpr int kTile = kBlock * kRounds;  // 4096 keys per tile
 constexpr int kMaxRadix = 1 << kMaxRB;
+constexpr int kChunk = 16;   // tiles per chunk of the count scan
 
 // Tile of a block: the tiles of one XCD (blocks b = x mod 8 are dispatched to XCD x) are
 // contiguous, so a digit's runs written by neighbouring tiles meet in the same L2 and leave it as
@@ -44,18 +50,60 @@ inline int64_t blocks_for_tiles(int64_t ntiles) { return (ntiles + 7) / 8 * 8; }
 
 static_assert(kTile % (4 * kBlock) == 0, "count block must divide the tile into uint4 rounds");
 
-template <int RB>
+// The bucket sort's oversized buckets (below): segments of the phase-1 output, each cut into
+// 4096-key tiles, sorted by the same three kernels; their tile count is known on the device only.
+struct BigPlan {
+  const uint4* seg;      // {start, size, first tile, bucket} per segment
+  const uint32_t* tseg;  // tile -> segment
+  const uint32_t* meta;  // {segments, tiles}
+};
+
+// Block -> tile for a tile count T read on the device (XCD-grouped as above); -1 past the end.
+__device__ __forceinline__ int64_t big_tile_of_block(uint32_t T) {
+  const uint32_t per = (T + 7) / 8;
+  const uint32_t q = blockIdx.x / 8;
+  if (q >= per) return -1;
+  const int64_t t = (int64_t)(blockIdx.x % 8) * per + q;
+  return t < T ? t : -1;
+}
+
+// Tile of a block: keys [base, end) of it (end: the array's or the segment's end), its column in
+// the per-digit counts, and (BIG) the segment.
+struct TileGeo {
+  int64_t tile, base, end;
+  uint4 seg;
+};
+
+template <bool BIG>
+__device__ __forceinline__ bool tile_geo(TileGeo& g, int64_t n, int64_t ntiles, const BigPlan& bp) {
+  if constexpr (BIG) {
+    g.tile = big_tile_of_block(bp.meta[1]);
+    if (g.tile < 0) return false;
+    g.seg = bp.seg[bp.tseg[g.tile]];
+    g.base = (int64_t)g.seg.x + (g.tile - (int64_t)g.seg.z) * kTile;
+    g.end = (int64_t)g.seg.x + g.seg.y;
+  } else {
+    g.tile = tile_of_block(ntiles);
+    if (g.tile >= ntiles) return false;
+    g.base = g.tile * kTile;
+    g.end = n;
+  }
+  return true;
+}
+
+template <int RB, bool BIG = false>
 __global__ __launch_bounds__(kBlock) void k_radix_count(const uint32_t* __restrict__ keys, int64_t n, int shift,
-                                                        uint32_t* __restrict__ counts, int64_t ntiles) {
+                                                        uint32_t* __restrict__ counts, int64_t ntiles,
+                                                        BigPlan bp) {
   constexpr int R = 1 << RB;
   constexpr uint32_t M = R - 1;
   __shared__ uint32_t hist[R];
-  const int64_t tile = tile_of_block(ntiles);
-  if (tile >= ntiles) return;  // block-uniform
+  TileGeo g;
+  if (!tile_geo<BIG>(g, n, ntiles, bp)) return;  // block-uniform
   for (int d = threadIdx.x; d < R; d += kBlock) hist[d] = 0;
   lds_barrier();
-  const int64_t base = tile * kTile;
-  if (base + kTile <= n) {
+  const int64_t base = g.base;
+  if (!BIG && base + kTile <= g.end) {  // segments start anywhere: no uint4 reads
     const uint4* k4 = reinterpret_cast<const uint4*>(keys + base);
 #pragma unroll
     for (int i = 0; i < kTile / (4 * kBlock); ++i) {
@@ -68,11 +116,11 @@ __global__ __launch_bounds__(kBlock) void k_radix_count(const uint32_t* __restri
   } else {
     for (int i = 0; i < kTile / kBlock; ++i) {
       const int64_t idx = base + (int64_t)i * kBlock + threadIdx.x;
-      if (idx < n) atomicAdd(&hist[(keys[idx] >> shift) & M], 1u);
+      if (idx < g.end) atomicAdd(&hist[(keys[idx] >> shift) & M], 1u);
     }
   }
   lds_barrier();
-  for (int d = threadIdx.x; d < R; d += kBlock) counts[(int64_t)d * ntiles + tile] = hist[d];
+  for (int d = threadIdx.x; d < R; d += kBlock) counts[g.tile * R + d] = hist[d];
 }
 
 __device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v, int lane) {
@@ -84,31 +132,76 @@ __device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v, int lane) {
   return v;
 }
 
-// Exclusive scan of each digit's row counts[d][0..ntiles), row totals -> digit_tot[d].
-__global__ __launch_bounds__(kBlock) void k_radix_scan_rows(uint32_t* __restrict__ counts, int64_t ntiles,
-                                                            uint32_t* __restrict__ digit_tot) {
-  __shared__ uint32_t wsum[kWaves];
-  uint32_t* row = counts + (int64_t)blockIdx.x * ntiles;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  uint32_t carry = 0;
-  for (int64_t b = 0; b < ntiles; b += kBlock) {
-    const int64_t i = b + threadIdx.x;
-    const uint32_t v = i < ntiles ? row[i] : 0u;
-    const uint32_t incl = wave_incl_scan_u32(v, lane);
-    if (lane == 63) wsum[wave] = incl;
-    lds_barrier();
-    uint32_t wpre = 0, tot = 0;
+// The count scan, level 1: block c takes tiles [16 c, 16 c + 16) and replaces each tile's counts by
+// the digit's exclusive prefix within the chunk; the chunk's sums -> csum[c][digit].  BIG: over the
+// device's tile count plus one empty tile past the end (its prefix: the segments' ends).
+template <int RB, bool BIG = false>
+__global__ __launch_bounds__(kBlock) void k_radix_chunk_scan(uint32_t* __restrict__ counts, int64_t ntiles,
+                                                             uint32_t* __restrict__ csum, BigPlan bp) {
+  constexpr int R = 1 << RB;
+  constexpr int D = R / kBlock;
+  const int64_t nt = BIG ? (int64_t)bp.meta[1] : ntiles;
+  const int64_t ext = nt + (BIG ? 1 : 0);
+  const int64_t t0 = (int64_t)blockIdx.x * kChunk;
+  if (t0 >= ext) return;
+  uint32_t v[kChunk][D];
 #pragma unroll
-    for (int w = 0; w < kWaves; ++w) {
-      const uint32_t s = wsum[w];
-      wpre += (w < wave) ? s : 0u;
-      tot += s;
+  for (int j = 0; j < kChunk; ++j)
+#pragma unroll
+    for (int i = 0; i < D; ++i) v[j][i] = t0 + j < nt ? counts[(t0 + j) * R + threadIdx.x + i * kBlock] : 0u;
+  uint32_t run[D];
+#pragma unroll
+  for (int i = 0; i < D; ++i) run[i] = 0;
+#pragma unroll
+  for (int j = 0; j < kChunk; ++j) {
+    if (t0 + j < ext) {
+#pragma unroll
+      for (int i = 0; i < D; ++i) {
+        counts[(t0 + j) * R + threadIdx.x + i * kBlock] = run[i];
+        run[i] += v[j][i];
+      }
     }
-    if (i < ntiles) row[i] = carry + wpre + incl - v;
-    carry += tot;
-    lds_barrier();
   }
-  if (threadIdx.x == 0) digit_tot[blockIdx.x] = carry;
+#pragma unroll
+  for (int i = 0; i < D; ++i) csum[(int64_t)blockIdx.x * R + threadIdx.x + i * kBlock] = run[i];
+}
+
+// The count scan, level 2: 32 digits per 256-thread block (a small block finds room on a CU beside
+// the sort's and the step's blocks sooner), 8 slices of the chunks per digit; csum ->
+// the digit's exclusive prefix over chunks, digit_tot[d] = the digit's total (not BIG).
+template <bool BIG = false>
+__global__ __launch_bounds__(256) void k_radix_chunk_top(uint32_t* __restrict__ csum, int64_t nchunks, int R,
+                                                         uint32_t* __restrict__ digit_tot, BigPlan bp) {
+  constexpr int kDig = 32, kSl = 8;
+  __shared__ uint32_t part[kSl][kDig];
+  const int dl = threadIdx.x % kDig, sl = threadIdx.x / kDig;
+  const int d = blockIdx.x * kDig + dl;
+  const int64_t nch = BIG ? ((int64_t)bp.meta[1] + 1 + kChunk - 1) / kChunk : nchunks;
+  const int64_t per = (nch + kSl - 1) / kSl;
+  const int64_t c0 = min(nch, sl * per), c1 = min(nch, c0 + per);
+  uint32_t s = 0;
+#pragma unroll 8
+  for (int64_t c = c0; c < c1; ++c) s += csum[c * R + d];
+  part[sl][dl] = s;
+  __syncthreads();
+  if (sl == 0) {
+    uint32_t run = 0;
+#pragma unroll
+    for (int q = 0; q < kSl; ++q) {
+      const uint32_t x = part[q][dl];
+      part[q][dl] = run;
+      run += x;
+    }
+    if (!BIG) digit_tot[d] = run;
+  }
+  __syncthreads();
+  uint32_t run = part[sl][dl];
+#pragma unroll 8
+  for (int64_t c = c0; c < c1; ++c) {
+    const uint32_t x = csum[c * R + d];
+    csum[c * R + d] = run;
+    run += x;
+  }
 }
 
 // Block-wide exclusive scan of R values held as D = R / kBlock consecutive values per thread.
@@ -142,14 +235,15 @@ __device__ __forceinline__ uint2 implicit_payload<uint2>(int64_t idx) {
   return make_uint2((uint32_t)idx, 0u);
 }
 
-template <class P, int RB>
+template <class P, int RB, bool BIG = false>
 __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint32_t* __restrict__ keys_in,
                                                           const P* __restrict__ vals_in,
                                                           uint32_t* __restrict__ keys_out,
                                                           P* __restrict__ vals_out, int64_t n,
                                                           int shift, const uint32_t* __restrict__ counts,
+                                                          const uint32_t* __restrict__ csum,
                                                           const uint32_t* __restrict__ digit_tot,
-                                                          int64_t ntiles) {
+                                                          int64_t ntiles, BigPlan bp) {
   constexpr int R = 1 << RB;
   constexpr uint32_t M = R - 1;
   constexpr int D = R / kBlock;  // digits per thread in the block scans
@@ -164,11 +258,12 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint32_t* __rest
   __shared__ uint32_t glob_off[R];
   __shared__ uint32_t wsum[kWaves];
 
-  const int64_t tile = tile_of_block(ntiles);
-  if (tile >= ntiles) return;  // block-uniform
+  TileGeo g;
+  if (!tile_geo<BIG>(g, n, ntiles, bp)) return;  // block-uniform
+  const int64_t tile = g.tile;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  const int64_t tile_base = tile * kTile;
+  const int64_t tile_base = g.base;
   const int64_t wbase = tile_base + (int64_t)wave * (kTile / kWaves);
   uint32_t my_key[kRounds], my_rank[kRounds];
   P my_val[kRounds];
@@ -176,7 +271,7 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint32_t* __rest
 #pragma unroll
   for (int r = 0; r < kRounds; ++r) {
     const int64_t idx = wbase + (int64_t)r * 64 + lane;
-    const bool valid = idx < n;
+    const bool valid = idx < g.end;
     my_key[r] = valid ? keys_in[idx] : 0u;
     my_val[r] = valid ? (vals_in ? vals_in[idx] : implicit_payload<P>(idx)) : P{};
   }
@@ -184,21 +279,36 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint32_t* __rest
   for (int w = 0; w < kWaves; ++w)
     for (int d = tid; d < R; d += kBlock) wave_hist[w][d] = 0;
 
-  // global base of (digit, this tile): exclusive scan of digit totals + row prefix.
-  {
+  // global base of (digit, this tile): exclusive scan of digit totals + row prefix.  BIG: the
+  // segment's digit totals and prefixes are differences of the rows' running prefixes at its first
+  // tile, at this tile and past its last tile.
+  // a tile's running prefix of digit d: its chunk's prefix + its own prefix within the chunk
+  auto prefix = [&](int64_t t, int d) { return csum[(t / kChunk) * R + d] + counts[t * R + d]; };
+  if constexpr (BIG) {
+    const int64_t h = g.seg.z, e = h + (g.seg.y + kTile - 1) / kTile;
+    uint32_t v[D], at_h[D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+      at_h[i] = prefix(h, tid * D + i);
+      v[i] = prefix(e, tid * D + i) - at_h[i];
+    }
+    block_excl_scan<D>(v, wsum, lane, wave);
+#pragma unroll
+    for (int i = 0; i < D; ++i) glob_off[tid * D + i] = g.seg.x + v[i] + prefix(tile, tid * D + i) - at_h[i];
+  } else {
     uint32_t v[D];
 #pragma unroll
     for (int i = 0; i < D; ++i) v[i] = digit_tot[tid * D + i];
     block_excl_scan<D>(v, wsum, lane, wave);
 #pragma unroll
-    for (int i = 0; i < D; ++i) glob_off[tid * D + i] = v[i] + counts[(int64_t)(tid * D + i) * ntiles + tile];
+    for (int i = 0; i < D; ++i) glob_off[tid * D + i] = v[i] + prefix(tile, tid * D + i);
   }
   lds_barrier();
 
 #pragma unroll
   for (int r = 0; r < kRounds; ++r) {
     const int64_t idx = wbase + (int64_t)r * 64 + lane;
-    const bool valid = idx < n;
+    const bool valid = idx < g.end;
     const uint32_t d = (my_key[r] >> shift) & M;
     uint64_t peers = __ballot(valid);
 #pragma unroll
@@ -252,7 +362,7 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint32_t* __rest
   }
   lds_barrier();
 
-  const int64_t rem = n - tile_base;
+  const int64_t rem = g.end - tile_base;
   const int tile_n = rem < kTile ? (int)rem : kTile;
 #pragma unroll
   for (int r = 0; r < kRounds; ++r) {  // unrolled: the rounds' LDS reads are issued together
@@ -271,7 +381,7 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint32_t* __rest
 // (and 45 when only the multi runs are kept):
 //   phase 1  one radix pass above (count / scan / scatter) on the top H bits: every pair lands in
 //            its bucket, in input order;
-//   phase 2  one 1024-thread block per bucket (k_bucket_sort) orders the bucket by its low L bits in
+//   phase 2  one 512-thread block per bucket (k_bucket_sort) orders the bucket by its low L bits in
 //            LDS -- one or two in-LDS passes of <= 9 bits over packed words {sub-key << (32 - L) |
 //            index in bucket}, the ranks from wave ballots, each lane holding its wave's part of the
 //            bucket in registers -- and writes it out, gathering payloads by index from the bucket's
@@ -281,14 +391,16 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint32_t* __rest
 // more, compacted at the start of the bucket's range, and counts the rest; k_bucket_offsets scans
 // the per-bucket counts and k_bucket_compact closes the gaps.  That replaces the split kernels
 // (a count pass over all sorted keys, a scan, a scatter) that ran on the step's main stream.
-// A bucket larger than the LDS image (a hot feature's run with its neighbours): all one key, it is
-// already in stable order and is copied; mixed, its block takes two counting passes through a
-// global scratch (slow for one huge mixed bucket -- a feature in every row of a large batch -- but
-// such a bucket is walked by one block, dispatched first, beside all the others).
+// A bucket larger than the LDS image (a hot feature's run with its neighbours, or a bucket of one
+// hot feature alone) is left by phase 2 to the "big path": the oversized buckets form a list of
+// segments of the phase-1 output (k_big_plan), cut into 4096-key tiles, and the LSD kernels above
+// order every segment by its low L bits at once, one or two 9-bit passes across all CUs; in SPLIT mode
+// three more kernels (k_big_split_*) keep each segment's multi entries.  A skewed batch's hot buckets
+// therefore cost what the same keys cost in the LSD sort, not one block's walk of a huge bucket.
 #ifndef FM_BKT_BB
-#define FM_BKT_BB 1024
+#define FM_BKT_BB 512
 #endif
-constexpr int kBB = FM_BKT_BB;     // phase-2 block: 16 waves, one block per CU (the image takes 120 KB)
+constexpr int kBB = FM_BKT_BB;     // phase-2 block: 8 waves, two blocks per CU (the image takes 60 KB)
 constexpr int kBW = kBB / 64;
 constexpr int kBktCap = 30 * kBB;  // a bucket up to this size is ordered in LDS
 constexpr int kBktRB = 9;          // digit bits of one in-bucket pass (512 digits)
@@ -313,7 +425,7 @@ __device__ __forceinline__ uint64_t digit_peers(uint32_t d, bool valid, int rb) 
   return peers;
 }
 
-// Exclusive scan of one value per thread over the 1024-thread block (wsum: kBW words).
+// Exclusive scan of one value per thread over the phase-2 block (wsum: kBW words).
 __device__ __forceinline__ uint32_t bkt_excl_scan(uint32_t v, uint32_t* wsum, int lane, int wave) {
   const uint32_t incl = wave_incl_scan_u32(v, lane);
   if (lane == 63) wsum[wave] = incl;
@@ -330,7 +442,6 @@ struct BktIO {
   const uint2* vals;     // its payloads
   uint32_t* okeys;       // where the bucket's range starts in the output
   uint2* ovals;
-  uint2* scratch;        // {sub, idx} per entry (oversized mixed buckets)
   uint32_t hi;           // bucket << L
   uint32_t lmask;        // (1 << L) - 1
   int ib;                // 32 - L: index bits of the packed LDS word
@@ -393,182 +504,20 @@ __device__ __forceinline__ void bucket_pass_lds(BktShared& S, const BktIO& io, u
   lds_barrier();
 }
 
-enum BktSrc { kSrcKeys = 0, kSrcScratch = 1 };
-enum BktDst { kDstScratch = 0, kDstOut = 1 };
-
-// One stable counting pass over a bucket too large for the LDS image, by digit (sub >> shift) &
-// (2^rb - 1), through global memory: wave w owns the contiguous part [w p, (w + 1) p) of the bucket;
-// a histogram sweep, a scan over (digit, wave), a rank sweep with wave-private running counts.
-template <int SRC, int DST>
-__device__ __forceinline__ void bucket_pass_global(BktShared& S, const BktIO& io, uint32_t m, int shift, int rb) {
-  constexpr int G = 8;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int R = 1 << rb;
-  const uint32_t M = (uint32_t)R - 1u;
-  const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  const uint32_t part = ((m + kBW - 1) / kBW + 63u) & ~63u;
-  const uint32_t lo = min(m, (uint32_t)wave * part), hi = min(m, lo + part);
-  auto load = [&](uint32_t e, uint32_t& sub, uint32_t& idx) {
-    if (SRC == kSrcKeys) {
-      sub = io.keys[e] & io.lmask;
-      idx = e;
-    } else {
-      const uint2 q = io.scratch[e];
-      sub = q.x;
-      idx = q.y;
-    }
-  };
-  for (int d = tid; d < kBW * R; d += kBB) S.cnt[d / R][d % R] = 0;
-  __syncthreads();
-  for (uint32_t e0 = lo; e0 < hi; e0 += 64 * G) {
-    uint32_t sub[G];
-#pragma unroll
-    for (int u = 0; u < G; ++u) {
-      const uint32_t e = e0 + u * 64 + lane;
-      uint32_t idx;
-      sub[u] = 0;
-      if (e < hi) load(e, sub[u], idx);
-    }
-#pragma unroll
-    for (int u = 0; u < G; ++u) {
-      const bool valid = e0 + u * 64 + lane < hi;
-      const uint32_t d = (sub[u] >> shift) & M;
-      const uint64_t peers = digit_peers(d, valid, rb);
-      if (valid && __popcll(peers & lt_mask) == 0) S.cnt[wave][d] += (uint32_t)__popcll(peers);
-    }
-  }
-  __syncthreads();
-  uint32_t t = 0;
-  if (tid < R) {
-#pragma unroll
-    for (int w = 0; w < kBW; ++w) {
-      const uint32_t x = S.cnt[w][tid];
-      S.cnt[w][tid] = t;
-      t += x;
-    }
-  }
-  const uint32_t base = bkt_excl_scan(t, S.wsum[0], lane, wave);
-  if (tid < R) {
-#pragma unroll
-    for (int w = 0; w < kBW; ++w) S.cnt[w][tid] += base;
-  }
-  lds_barrier();
-  for (uint32_t e0 = lo; e0 < hi; e0 += 64 * G) {
-    uint32_t sub[G], idx[G], pos[G];
-#pragma unroll
-    for (int u = 0; u < G; ++u) {
-      const uint32_t e = e0 + u * 64 + lane;
-      sub[u] = 0;
-      idx[u] = 0;
-      if (e < hi) load(e, sub[u], idx[u]);
-    }
-#pragma unroll
-    for (int u = 0; u < G; ++u) {
-      const bool valid = e0 + u * 64 + lane < hi;
-      const uint32_t d = (sub[u] >> shift) & M;
-      const uint64_t peers = digit_peers(d, valid, rb);
-      const uint32_t below = (uint32_t)__popcll(peers & lt_mask);
-      const uint32_t prev = S.cnt[wave][d];
-      __builtin_amdgcn_wave_barrier();
-      if (valid && below == 0) S.cnt[wave][d] = prev + (uint32_t)__popcll(peers);
-      __builtin_amdgcn_wave_barrier();
-      pos[u] = prev + below;
-    }
-    if (DST == kDstOut) {
-      uint2 v[G];
-#pragma unroll
-      for (int u = 0; u < G; ++u)
-        if (e0 + u * 64 + lane < hi) v[u] = io.vals[idx[u]];
-#pragma unroll
-      for (int u = 0; u < G; ++u) {
-        if (e0 + u * 64 + lane < hi) {
-          io.okeys[pos[u]] = io.hi | sub[u];
-          io.ovals[pos[u]] = v[u];
-        }
-      }
-    } else {
-#pragma unroll
-      for (int u = 0; u < G; ++u)
-        if (e0 + u * 64 + lane < hi) io.scratch[pos[u]] = make_uint2(sub[u], idx[u]);
-    }
-  }
-  __syncthreads();  // the next pass reads what this one wrote and resets cnt
-}
-
-// SPLIT, oversized mixed bucket: the sorted bucket in okeys / ovals[0, m) -> its multi entries
-// compacted in place at the start (stable; a round's reads all land in registers before any of its
-// writes, which go at or below the round's first position).  Returns the multi count.
-__device__ __forceinline__ uint32_t bucket_compact_in_place(BktShared& S, const BktIO& io, uint32_t m) {
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  uint32_t carry = 0, prev_last = 0xFFFFFFFFu;  // block-uniform
-  for (uint32_t j0 = 0; j0 < m; j0 += kBB) {
-    const uint32_t j = j0 + tid;
-    const bool valid = j < m;
-    const uint32_t key = valid ? io.okeys[j] : 0xFFFFFFFEu;
-    const uint2 val = valid ? io.ovals[j] : make_uint2(0u, 0u);
-    const uint32_t after = j0 + kBB < m ? io.okeys[j0 + kBB] : 0xFFFFFFFFu;
-    S.arr[tid] = key;
-    __syncthreads();  // every read of the round done (the workgroup fence waits for the loads too)
-    const uint32_t prev = tid > 0 ? S.arr[tid - 1] : prev_last;
-    const uint32_t next = tid + 1 < kBB ? S.arr[tid + 1] : after;
-    const bool multi = valid && (prev == key || next == key);
-    const uint64_t bm = __ballot(multi);
-    if (lane == 0) S.wsum[0][wave] = (uint32_t)__popcll(bm);
-    __syncthreads();
-    uint32_t pre = 0, tot = 0;
-#pragma unroll
-    for (int w = 0; w < kBW; ++w) {
-      pre += w < wave ? S.wsum[0][w] : 0u;
-      tot += S.wsum[0][w];
-    }
-    if (multi) {
-      const uint32_t d = carry + pre + (uint32_t)__popcll(bm & lt_mask);
-      io.okeys[d] = key;
-      io.ovals[d] = val;
-    }
-    prev_last = S.arr[kBB - 1];
-    carry += tot;
-    __syncthreads();  // S.arr / wsum reused; this round's writes drain before the next round's reads
-  }
-  return carry;
-}
-
-// Phase-2 dispatch order: buckets that outgrow the LDS image (their block walks global memory,
-// several times longer) first, so they start with the first wave of blocks instead of forming the
-// kernel's tail; then the rest in bucket order.  One block.
-__global__ __launch_bounds__(kBB) void k_bucket_order(const uint32_t* __restrict__ btot, int nb, uint32_t cap,
-                                                      uint32_t* __restrict__ order) {
-  __shared__ uint32_t wsum[kBW];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  uint32_t carry = 0;  // block-uniform
-  for (int pass = 0; pass < 2; ++pass) {
-    for (int b0 = 0; b0 < nb; b0 += kBB) {
-      const int b = b0 + tid;
-      const bool big = b < nb && btot[b] > cap;
-      const uint32_t f = (b < nb && (pass == 0 ? big : !big)) ? 1u : 0u;
-      const uint32_t pre = bkt_excl_scan(f, wsum, lane, wave);
-      if (f) order[carry + pre] = (uint32_t)b;
-      uint32_t t = 0;
-#pragma unroll
-      for (int w = 0; w < kBW; ++w) t += wsum[w];
-      lds_barrier();
-      carry += t;
-    }
-  }
-}
-
-// Phase 2: block i sorts bucket order[i] (btot[b] pairs starting at the sum of the buckets below
-// it).  SPLIT: the bucket's multi entries go compacted to the start of its range of keys_out /
-// vals_out, bstat[b] = {multi entries, singleton runs}; else the whole bucket, in order.
+// Phase 2: block b sorts bucket b (btot[b] pairs starting at the sum of the buckets below it), if
+// it fits the LDS image (else: the big path).  SPLIT: the bucket's multi entries go compacted to the
+// start of its range of keys_out / vals_out, bstat[b] = {multi entries, singleton runs}; else the
+// whole bucket, in order.
 template <bool SPLIT>
 __global__ __launch_bounds__(kBB) void k_bucket_sort(const uint32_t* __restrict__ keys_in,
                                                      const uint2* __restrict__ vals_in, uint32_t* __restrict__ keys_out,
                                                      uint2* __restrict__ vals_out, const uint32_t* __restrict__ btot,
-                                                     int L, uint2* __restrict__ scratch,
-                                                     const uint32_t* __restrict__ order, uint2* __restrict__ bstat) {
+                                                     int L, uint2* __restrict__ bstat) {
   __shared__ BktShared S;
-  const int b = (int)order[blockIdx.x];
+  const int b = (int)blockIdx.x;
+  const uint32_t m = btot[b];
+  const uint32_t cap = min((uint32_t)kBktCap, 1u << min(32 - L, 31));
+  if (m > cap) return;  // block-uniform: the big path's
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   uint32_t acc = 0;
@@ -580,7 +529,6 @@ __global__ __launch_bounds__(kBB) void k_bucket_sort(const uint32_t* __restrict_
   uint32_t start = 0;
 #pragma unroll
   for (int w = 0; w < kBW; ++w) start += S.wsum[0][w];
-  const uint32_t m = btot[b];
   lds_barrier();  // wsum is reused below
   if (m == 0) {   // block-uniform
     if (SPLIT && tid == 0) bstat[b] = make_uint2(0u, 0u);
@@ -591,13 +539,11 @@ __global__ __launch_bounds__(kBB) void k_bucket_sort(const uint32_t* __restrict_
   io.vals = vals_in + start;
   io.okeys = keys_out + start;
   io.ovals = vals_out + start;
-  io.scratch = scratch + start;
   io.hi = (uint32_t)b << L;
   io.lmask = (1u << L) - 1u;
   io.ib = 32 - L;
-  const uint32_t cap = min((uint32_t)kBktCap, 1u << min(io.ib, 31));
   uint32_t mcnt = 0;
-  if (m <= cap) {
+  {
     bucket_pass_lds<true>(S, io, m, 0, L < kBktRB ? L : kBktRB);
     if (L > kBktRB) bucket_pass_lds<false>(S, io, m, kBktRB, L - kBktRB);
     // the bucket in order in S.arr: coalesced key and payload writes, payloads gathered by index from
@@ -652,48 +598,160 @@ __global__ __launch_bounds__(kBB) void k_bucket_sort(const uint32_t* __restrict_
         }
       }
     }
-  } else {
-    // all one key?  Then the bucket is one run, already in stable order
-    uint32_t lo = 0xFFFFFFFFu, hi = 0u;
-    for (uint32_t j = tid; j < m; j += kBB) {
-      const uint32_t k = io.keys[j];
-      lo = min(lo, k);
-      hi = max(hi, k);
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      lo = min(lo, (uint32_t)__shfl_xor((int)lo, o));
-      hi = max(hi, (uint32_t)__shfl_xor((int)hi, o));
-    }
-    if (lane == 0) {
-      S.wsum[0][wave] = lo;
-      S.wsum[1][wave] = hi;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int w = 0; w < kBW; ++w) {
-      lo = min(lo, S.wsum[0][w]);
-      hi = max(hi, S.wsum[1][w]);
-    }
-    __syncthreads();
-    if (lo == hi) {
-      for (uint32_t j = tid; j < m; j += kBB) {
-        io.okeys[j] = io.keys[j];
-        io.ovals[j] = io.vals[j];
-      }
-      mcnt = m;  // m > cap >= 2: one run of two or more
-    } else {
-      const int rb0 = L <= kBktRB ? L : kBktRB, rb1 = L - rb0;
-      if (rb1 == 0) {
-        bucket_pass_global<kSrcKeys, kDstOut>(S, io, m, 0, rb0);
-      } else {
-        bucket_pass_global<kSrcKeys, kDstScratch>(S, io, m, 0, rb0);
-        bucket_pass_global<kSrcScratch, kDstOut>(S, io, m, rb0, rb1);
-      }
-      if (SPLIT) mcnt = bucket_compact_in_place(S, io, m);
-    }
   }
   if (SPLIT && tid == 0) bstat[b] = make_uint2(mcnt, m - mcnt);
+}
+
+// The big path's plan, one block: the oversized buckets (btot[b] > cap) as segments {start, size,
+// first tile, bucket} in bucket order, every tile's segment, meta = {segments, tiles}.
+__global__ __launch_bounds__(kBB) void k_big_plan(const uint32_t* __restrict__ btot, int nb, uint32_t cap,
+                                                  uint4* __restrict__ seg, uint32_t* __restrict__ tseg,
+                                                  uint32_t* __restrict__ meta) {
+  __shared__ uint32_t wsum[kBW];
+  __shared__ uint32_t tot[3];
+  __shared__ uint32_t first[kMaxRadix];  // first tile of each segment
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  uint32_t c_start = 0, c_seg = 0, c_tiles = 0;  // block-uniform carries
+  for (int b0 = 0; b0 < nb; b0 += kBB) {
+    const int b = b0 + tid;
+    const uint32_t sz = b < nb ? btot[b] : 0u;
+    const uint32_t big = sz > cap ? 1u : 0u;
+    const uint32_t tl = big ? (sz + kTile - 1) / kTile : 0u;
+    const uint32_t start = bkt_excl_scan(sz, wsum, lane, wave);
+    const uint32_t j = bkt_excl_scan(big, wsum, lane, wave);
+    const uint32_t t0 = bkt_excl_scan(tl, wsum, lane, wave);
+    if (big) {
+      seg[c_seg + j] = make_uint4(c_start + start, sz, c_tiles + t0, (uint32_t)b);
+      first[c_seg + j] = c_tiles + t0;
+    }
+    if (tid == kBB - 1) {
+      tot[0] = start + sz;
+      tot[1] = j + big;
+      tot[2] = t0 + tl;
+    }
+    lds_barrier();
+    c_start += tot[0];
+    c_seg += tot[1];
+    c_tiles += tot[2];
+    lds_barrier();
+  }
+  // a tile's segment: the last one starting at or before it
+  for (uint32_t t = tid; t < c_tiles; t += kBB) {
+    uint32_t lo = 0, hi = c_seg - 1;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi + 1) / 2;
+      if (first[mid] <= t)
+        lo = mid;
+      else
+        hi = mid - 1;
+    }
+    tseg[t] = lo;
+  }
+  if (tid == 0) {
+    meta[0] = c_seg;
+    meta[1] = c_tiles;
+  }
+}
+
+// Is the sorted entry idx of segment [lo, end) in a run of two or more?
+__device__ __forceinline__ bool big_multi(const uint32_t* __restrict__ keys, int64_t idx, int64_t lo, int64_t end,
+                                          uint32_t key) {
+  return (idx > lo && keys[idx - 1] == key) || (idx + 1 < end && keys[idx + 1] == key);
+}
+
+// SPLIT, big path: multi entries per sorted tile -> mt[tile].
+__global__ __launch_bounds__(kBlock) void k_big_split_count(const uint32_t* __restrict__ keys, BigPlan bp,
+                                                            uint32_t* __restrict__ mt) {
+  __shared__ uint32_t wsum[kWaves];
+  TileGeo g;
+  if (!tile_geo<true>(g, 0, 0, bp)) return;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t c = 0;
+#pragma unroll
+  for (int r = 0; r < kRounds; ++r) {
+    const int64_t idx = g.base + (int64_t)r * kBlock + threadIdx.x;
+    if (idx < g.end) c += big_multi(keys, idx, g.seg.x, g.end, keys[idx]) ? 1u : 0u;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+  if (lane == 0) wsum[wave] = c;
+  lds_barrier();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) t += wsum[w];
+    mt[g.tile] = t;
+  }
+}
+
+// SPLIT, big path, one block: mt -> exclusive prefix over all tiles (mt[tiles] = total), and each
+// oversized bucket's bstat = {multi entries, singleton runs}.
+__global__ __launch_bounds__(kBB) void k_big_split_scan(BigPlan bp, uint32_t* __restrict__ mt,
+                                                        uint2* __restrict__ bstat) {
+  __shared__ uint32_t wsum[kBW];
+  __shared__ uint32_t tot;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint32_t T = bp.meta[1], nseg = bp.meta[0];
+  uint32_t carry = 0;
+  for (uint32_t t0 = 0; t0 < T; t0 += kBB) {
+    const uint32_t t = t0 + tid;
+    const uint32_t v = t < T ? mt[t] : 0u;
+    const uint32_t pre = bkt_excl_scan(v, wsum, lane, wave);
+    if (t < T) mt[t] = carry + pre;
+    if (tid == kBB - 1) tot = pre + v;
+    lds_barrier();
+    carry += tot;
+    lds_barrier();
+  }
+  if (tid == 0) mt[T] = carry;
+  __syncthreads();  // the block's global writes of mt, visible to all its threads
+  for (uint32_t j = tid; j < nseg; j += kBB) {
+    const uint4 s = bp.seg[j];
+    const uint32_t e = s.z + (s.y + kTile - 1) / kTile;
+    const uint32_t multi = mt[e] - mt[s.z];
+    bstat[s.w] = make_uint2(multi, s.y - multi);
+  }
+}
+
+// SPLIT, big path: each sorted tile's multi entries straight to their place in the dense multi view
+// (the bucket's offset there, boff[b].y, + the tile's prefix within the segment), stable.  Each wave
+// walks its own 512 entries.
+__global__ __launch_bounds__(kBlock) void k_big_split_write(const uint32_t* __restrict__ keys,
+                                                            const uint2* __restrict__ vals, BigPlan bp,
+                                                            const uint32_t* __restrict__ mt,
+                                                            const uint2* __restrict__ boff,
+                                                            uint32_t* __restrict__ mkeys, uint2* __restrict__ mvals) {
+  __shared__ uint32_t wsum[kWaves];
+  TileGeo g;
+  if (!tile_geo<true>(g, 0, 0, bp)) return;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  const int64_t wbase = g.base + (int64_t)wave * (kTile / kWaves);
+  uint32_t key[kRounds];
+  bool multi[kRounds];
+  uint32_t c = 0;
+#pragma unroll
+  for (int r = 0; r < kRounds; ++r) {
+    const int64_t idx = wbase + (int64_t)r * 64 + lane;
+    key[r] = idx < g.end ? keys[idx] : 0u;
+    multi[r] = idx < g.end && big_multi(keys, idx, g.seg.x, g.end, key[r]);
+    c += (uint32_t)__popcll(__ballot(multi[r]));
+  }
+  if (lane == 0) wsum[wave] = c;
+  lds_barrier();
+  uint32_t dst = boff[g.seg.w].y + mt[g.tile] - mt[g.seg.z];
+#pragma unroll
+  for (int w = 0; w < kWaves; ++w) dst += w < wave ? wsum[w] : 0u;
+#pragma unroll
+  for (int r = 0; r < kRounds; ++r) {
+    const uint64_t bm = __ballot(multi[r]);
+    if (multi[r]) {
+      const uint32_t d = dst + (uint32_t)__popcll(bm & lt_mask);
+      mkeys[d] = key[r];
+      mvals[d] = vals[wbase + (int64_t)r * 64 + lane];
+    }
+    dst += (uint32_t)__popcll(bm);
+  }
 }
 
 // SPLIT: the buckets' starts (from their sizes) and the multi view's offsets (from their multi
@@ -732,13 +790,16 @@ __global__ __launch_bounds__(kBB) void k_bucket_offsets(const uint32_t* __restri
 }
 
 // SPLIT: bucket b's multi entries, compacted at its range's start in the gapped view, to their
-// place in the dense multi view.  One block per bucket.
+// place in the dense multi view.  One block per bucket that fits the LDS image (the big path's
+// buckets went there directly).
 __global__ __launch_bounds__(256) void k_bucket_compact(const uint32_t* __restrict__ gkeys,
                                                         const uint2* __restrict__ gvals,
                                                         const uint2* __restrict__ bstat,
-                                                        const uint2* __restrict__ boff, uint32_t* __restrict__ mkeys,
+                                                        const uint2* __restrict__ boff, const uint32_t* __restrict__ btot,
+                                                        uint32_t cap, uint32_t* __restrict__ mkeys,
                                                         uint2* __restrict__ mvals) {
   const int b = blockIdx.x;
+  if (btot[b] > cap) return;
   const uint32_t n = bstat[b].x;
   const uint2 o = boff[b];
   for (uint32_t j = threadIdx.x; j < n; j += 256) {
@@ -749,6 +810,10 @@ __global__ __launch_bounds__(256) void k_bucket_compact(const uint32_t* __restri
 
 }  // namespace
 
+// Rows of 2^RB counts the counts buffer holds for a sort of ntiles tiles: the tiles' (and one
+// past them), then the chunks' sums.
+inline int64_t count_rows(int64_t ntiles) { return ntiles + 1 + (ntiles + 1 + kChunk - 1) / kChunk; }
+
 void SortWork::ensure(int64_t n) {
   if (n <= cap) return;
   const int64_t c = n + n / 8 + 4096;
@@ -757,8 +822,8 @@ void SortWork::ensure(int64_t n) {
   vals_a.ensure(sizeof(uint64_t) * c);  // payloads up to 8 bytes
   vals_b.ensure(sizeof(uint64_t) * c);
   const int64_t ntiles = (c + kTile - 1) / kTile;
-  counts.ensure(sizeof(uint32_t) * kMaxRadix * ntiles);
-  digit_tot.ensure(sizeof(uint32_t) * kMaxRadix * 2);  // digit totals, then the bucket sort's block order
+  counts.ensure(sizeof(uint32_t) * kMaxRadix * count_rows(ntiles));
+  digit_tot.ensure(sizeof(uint32_t) * kMaxRadix);  // digit totals (the bucket sort: bucket sizes)
   bstat.ensure(sizeof(uint2) * kMaxRadix * 2);         // per bucket {multi, singleton runs}, then {start, moff}
   cap = c;
 }
@@ -766,12 +831,19 @@ void SortWork::ensure(int64_t n) {
 template <class P, int RB>
 static void radix_pass_impl(const uint32_t* kin, const P* vin, uint32_t* ko, P* vo, int64_t n, int shift,
                        SortWork& w, int64_t ntiles, hipStream_t st) {
+  const BigPlan none{};
+  uint32_t* counts = w.counts.as<uint32_t>();
+  uint32_t* csum = counts + (ntiles + 1) * (int64_t(1) << RB);
+  const int64_t nchunks = (ntiles + kChunk - 1) / kChunk;
   hipLaunchKernelGGL(k_radix_count<RB>, dim3((unsigned)blocks_for_tiles(ntiles)), dim3(kBlock), 0, st, kin, n, shift,
-                     w.counts.as<uint32_t>(), ntiles);
-  hipLaunchKernelGGL(k_radix_scan_rows, dim3(1u << RB), dim3(kBlock), 0, st, w.counts.as<uint32_t>(), ntiles,
-                       w.digit_tot.as<uint32_t>());
+                     counts, ntiles, none);
+  hipLaunchKernelGGL((k_radix_chunk_scan<RB, false>), dim3((unsigned)nchunks), dim3(kBlock), 0, st, counts, ntiles, csum,
+                     none);
+  hipLaunchKernelGGL(k_radix_chunk_top<false>, dim3((1u << RB) / 32), dim3(256), 0, st, csum, nchunks, 1 << RB,
+                     w.digit_tot.as<uint32_t>(), none);
   hipLaunchKernelGGL((k_radix_scatter<P, RB>), dim3((unsigned)blocks_for_tiles(ntiles)), dim3(kBlock), 0, st, kin,
-                     vin, ko, vo, n, shift, w.counts.as<uint32_t>(), w.digit_tot.as<uint32_t>(), ntiles);
+                     vin, ko, vo, n, shift, (const uint32_t*)counts, (const uint32_t*)csum,
+                     (const uint32_t*)w.digit_tot.as<uint32_t>(), ntiles, none);
   FM_HIP_CHECK(hipGetLastError());
 }
 
@@ -863,6 +935,23 @@ void radix_sort_pairs64(SortWork& w, const uint32_t* keys_in, const uint2* vals_
 
 namespace fmhip {
 
+// One LSD pass of the big path over the device-planned tiles (at most big_tiles of them).
+template <int RB>
+static void big_pass(const uint32_t* sk, const uint2* sv, uint32_t* dk, uint2* dv, int shift, SortWork& w,
+                     const BigPlan& bp, int64_t big_tiles, hipStream_t st) {
+  uint32_t* counts = w.counts.as<uint32_t>();
+  uint32_t* csum = counts + (big_tiles + 1) * (int64_t(1) << RB);
+  const unsigned gb = (unsigned)blocks_for_tiles(big_tiles);
+  const unsigned gc = (unsigned)((big_tiles + 1 + kChunk - 1) / kChunk);
+  hipLaunchKernelGGL((k_radix_count<RB, true>), dim3(gb), dim3(kBlock), 0, st, sk, (int64_t)0, shift, counts, (int64_t)0,
+                     bp);
+  hipLaunchKernelGGL((k_radix_chunk_scan<RB, true>), dim3(gc), dim3(kBlock), 0, st, counts, (int64_t)0, csum, bp);
+  hipLaunchKernelGGL(k_radix_chunk_top<true>, dim3((1u << RB) / 32), dim3(256), 0, st, csum, (int64_t)0, 1 << RB,
+                     (uint32_t*)nullptr, bp);
+  hipLaunchKernelGGL((k_radix_scatter<uint2, RB, true>), dim3(gb), dim3(kBlock), 0, st, sk, sv, dk, dv, (int64_t)0,
+                     shift, (const uint32_t*)counts, (const uint32_t*)csum, (const uint32_t*)nullptr, (int64_t)0, bp);
+}
+
 int bucket_hi_bits(int64_t n, int key_bits) {
   if (n < 1 || n >= (int64_t(1) << 32) - 1) return 0;
   // buckets of about a third of the LDS image on average (hot features fill some to the image and
@@ -878,13 +967,36 @@ bool bucket_sort_pairs64(SortWork& w, const uint32_t* keys_in, const uint2* vals
   const int H = bucket_hi_bits(n, key_bits);
   if (H == 0) return false;
   FM_REQUIRE(final_keys && final_vals && vals_in, "bucket sort: null buffer");
-  w.ensure(n);
-  w.bscratch.ensure(sizeof(uint2) * w.cap);  // {sub, idx} of oversized mixed buckets
   const int L = key_bits - H;
   const int nb = 1 << H;
+  const uint32_t cap = std::min<uint32_t>((uint32_t)kBktCap, 1u << std::min(32 - L, 31));
   const int64_t ntiles = (n + kTile - 1) / kTile;
+  // the big path: oversized buckets number at most n / (cap + 1), each adds at most one partial tile
+  const int64_t big_tiles = ntiles + n / ((int64_t)cap + 1) + 1;
+  // the big path's digits: one pass of 9..11 bits for L <= 11, else two of 9 (a digit reaching above
+  // bit L holds bucket bits, constant in a segment)
+  const int big_rb = L <= 9 ? 9 : L <= kMaxRB ? L : kBktRB;
+  const int passes = L <= kMaxRB ? 1 : 2;
+  w.ensure(n);
+  // every buffer sized before the first launch (growing one drains the device)
+  const size_t cnt_bytes = sizeof(uint32_t) * std::max<int64_t>((int64_t)kMaxRadix * count_rows((w.cap + kTile - 1) / kTile),
+                                                                 ((int64_t)1 << big_rb) * count_rows(big_tiles));
+  w.counts.ensure(cnt_bytes);
+  const size_t scr_keys = ((sizeof(uint32_t) * (size_t)w.cap) + 255) & ~size_t(255);
+  w.bscratch.ensure(scr_keys + sizeof(uint2) * (size_t)w.cap);  // the big path's middle pass
+  const size_t seg_bytes = sizeof(uint4) * kMaxRadix, tseg_bytes = (sizeof(uint32_t) * big_tiles + 15) & ~size_t(15);
+  w.bplan.ensure(seg_bytes + tseg_bytes + 16 + sizeof(uint32_t) * (big_tiles + 1));
+  char* plan = w.bplan.as<char>();
+  uint4* seg = reinterpret_cast<uint4*>(plan);
+  uint32_t* tseg = reinterpret_cast<uint32_t*>(plan + seg_bytes);
+  uint32_t* meta = reinterpret_cast<uint32_t*>(plan + seg_bytes + tseg_bytes);
+  uint32_t* mt = meta + 4;
+  const BigPlan bp{seg, tseg, meta};
+
   uint32_t* kbuf[2] = {w.keys_a.as<uint32_t>(), w.keys_b.as<uint32_t>()};
   uint2* vbuf[2] = {w.vals_a.as<uint2>(), w.vals_b.as<uint2>()};
+  uint32_t* skeys = w.bscratch.as<uint32_t>();
+  uint2* svals = reinterpret_cast<uint2*>(w.bscratch.as<char>() + scr_keys);
   const uint32_t* kin = keys_in;
   if ((reinterpret_cast<uintptr_t>(keys_in) & 15u) != 0) {  // the count kernel reads uint4
     FM_HIP_CHECK(hipMemcpyAsync(kbuf[1], keys_in, sizeof(uint32_t) * n, hipMemcpyDeviceToDevice, st));
@@ -897,22 +1009,43 @@ bool bucket_sort_pairs64(SortWork& w, const uint32_t* keys_in, const uint2* vals
     default: radix_pass<uint2, 11>(kin, vals_in, kbuf[0], vbuf[0], n, L, w, ntiles, st); break;
   }
   const uint32_t* btot = w.digit_tot.as<uint32_t>();
-  uint32_t* order = w.digit_tot.as<uint32_t>() + kMaxRadix;
   uint2* bstat = w.bstat.as<uint2>();
   uint2* boff = bstat + kMaxRadix;
-  const uint32_t cap = std::min<uint32_t>((uint32_t)kBktCap, 1u << std::min(32 - L, 31));
-  hipLaunchKernelGGL(k_bucket_order, dim3(1), dim3(kBB), 0, st, btot, nb, cap, order);
+  hipLaunchKernelGGL(k_big_plan, dim3(1), dim3(kBB), 0, st, btot, nb, cap, seg, tseg, meta);
+  // phase 2 (SPLIT: into the gapped view kbuf[1] / vbuf[1], the multi entries at each bucket's start)
+  uint32_t* pk = split_out ? kbuf[1] : final_keys;
+  uint2* pv = split_out ? vbuf[1] : final_vals;
+  if (split_out)
+    hipLaunchKernelGGL(k_bucket_sort<true>, dim3(nb), dim3(kBB), 0, st, kbuf[0], vbuf[0], pk, pv, btot, L, bstat);
+  else
+    hipLaunchKernelGGL(k_bucket_sort<false>, dim3(nb), dim3(kBB), 0, st, kbuf[0], vbuf[0], pk, pv, btot, L, bstat);
+  // the big path: LSD passes over the low L bits of every oversized bucket; its sorted segments end
+  // in the final buffers, or (SPLIT) where k_big_split_write reads them
+  const unsigned gb = (unsigned)blocks_for_tiles(big_tiles);  // the split kernels' grid
+  const uint32_t* sk = kbuf[0];
+  const uint2* sv = vbuf[0];
+  for (int p = 0; p < passes; ++p) {
+    const bool last = p == passes - 1;
+    uint32_t* dk = !last ? skeys : split_out ? (passes == 1 ? skeys : kbuf[0]) : final_keys;
+    uint2* dv = !last ? svals : split_out ? (passes == 1 ? svals : vbuf[0]) : final_vals;
+    switch (big_rb) {
+      case 9: big_pass<9>(sk, sv, dk, dv, big_rb * p, w, bp, big_tiles, st); break;
+      case 10: big_pass<10>(sk, sv, dk, dv, big_rb * p, w, bp, big_tiles, st); break;
+      default: big_pass<11>(sk, sv, dk, dv, big_rb * p, w, bp, big_tiles, st); break;
+    }
+    sk = dk;
+    sv = dv;
+  }
   if (split_out) {
-    // phase 2 into the gapped view (kbuf[1] / vbuf[1]: the multi entries at each bucket's start),
-    // then the gaps closed into the final buffers
-    hipLaunchKernelGGL(k_bucket_sort<true>, dim3(nb), dim3(kBB), 0, st, kbuf[0], vbuf[0], kbuf[1], vbuf[1], btot, L,
-                       w.bscratch.as<uint2>(), (const uint32_t*)order, bstat);
+    // the big path's multi counts, every bucket's offsets, then the multi entries into the final
+    // buffers: the big path's by tile, the others' by closing the gapped view's gaps
+    hipLaunchKernelGGL(k_big_split_count, dim3(gb), dim3(kBlock), 0, st, sk, bp, mt);
+    hipLaunchKernelGGL(k_big_split_scan, dim3(1), dim3(kBB), 0, st, bp, mt, bstat);
     hipLaunchKernelGGL(k_bucket_offsets, dim3(1), dim3(kBB), 0, st, btot, (const uint2*)bstat, nb, boff, split_out);
-    hipLaunchKernelGGL(k_bucket_compact, dim3(nb), dim3(256), 0, st, kbuf[1], vbuf[1], (const uint2*)bstat,
+    hipLaunchKernelGGL(k_big_split_write, dim3(gb), dim3(kBlock), 0, st, sk, sv, bp, (const uint32_t*)mt,
                        (const uint2*)boff, final_keys, final_vals);
-  } else {
-    hipLaunchKernelGGL(k_bucket_sort<false>, dim3(nb), dim3(kBB), 0, st, kbuf[0], vbuf[0], final_keys, final_vals, btot,
-                       L, w.bscratch.as<uint2>(), (const uint32_t*)order, bstat);
+    hipLaunchKernelGGL(k_bucket_compact, dim3(nb), dim3(256), 0, st, kbuf[1], vbuf[1], (const uint2*)bstat,
+                       (const uint2*)boff, btot, cap, final_keys, final_vals);
   }
   FM_HIP_CHECK(hipGetLastError());
   return true;

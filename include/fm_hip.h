@@ -50,7 +50,7 @@ extern "C" {
 #define FM_FUSE_DEFAULT 0 /* fm_config.fuse_single: the library's choice (tables above 256 MB) */
 #define FM_FUSE_ON 1
 #define FM_FUSE_OFF (-1)
-#define FM_SORT_DEFAULT 0 /* fm_config.sort_algo: the library's choice (the bucket sort for batches of 1M+ entries) */
+#define FM_SORT_DEFAULT 0 /* fm_config.sort_algo: the library's choice (the LSD sort; measured faster in the step) */
 #define FM_SORT_LSD 1     /* three-pass stable LSD radix sort */
 #define FM_SORT_BUCKET 2  /* two-phase bucket sort whenever the key width allows it */
 
@@ -87,9 +87,11 @@ typedef struct fm_batch fm_batch;
  *                sent while the next is computed (0 = the default, 4; 1 = one pass then one
  *                all-to-all; at most 64).  Every process of a job must pass the same value.
  * sort_algo    : how a single-table batch's entries are grouped by feature (FM_SORT_*): both sorts
- *                are stable, so the step is bitwise the same either way; FM_SORT_DEFAULT takes the
- *                bucket sort (one radix pass on the top bits, then each bucket ordered in LDS, the
- *                fused step's singleton split folded in) for batches of 2^20 entries or more.
+ *                are stable, so the step is bitwise the same either way.  FM_SORT_DEFAULT takes the
+ *                LSD passes; FM_SORT_BUCKET the bucket sort (one radix pass on the top bits, each
+ *                bucket ordered in LDS, the oversized ones by LSD passes across the chip, the fused
+ *                step's singleton split folded in), which sorts uniform keys faster alone but
+ *                measured slower inside the c3 / c2 / c5 steps.
  * Zero-initialise the struct: every field's 0 is its default. */
 typedef struct fm_config {
   int64_t num_features;

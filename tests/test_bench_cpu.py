@@ -134,14 +134,14 @@ def test_sort_passes_follow_the_digit_plan():
 
 
 def test_grouping_rule_follows_the_library():
-    """bench.grouping restates fm_capi.hip bucket_on / fm_sort.hip bucket_hi_bits: the bucket sort
-    from 2^20 entries when the key width allows one radix pass on the top 9-10 bits and at most 18
-    low bits; "lsd" always wins; "bucket" forces it down to any size that fits."""
+    """bench.grouping restates fm_capi.hip bucket_on / fm_sort.hip bucket_hi_bits: the LSD passes
+    unless "bucket" is asked for and the key width allows one radix pass on the top 9-11 bits with
+    at most 18 low bits."""
     import bench
 
-    assert bench.grouping("default", 10_223_616, 100_000_000) == "bucket"   # c3: 27-bit slots
-    assert bench.grouping("default", 2_555_904, 1_000_000) == "bucket"      # c2 / c5: 20 bits
-    assert bench.grouping("default", 500_000, 1_000_000) == "lsd"           # below 2^20 entries
+    assert bench.grouping("default", 10_223_616, 100_000_000) == "lsd"      # c3: the default is LSD
+    assert bench.grouping("bucket", 10_223_616, 100_000_000) == "bucket"    # c3: 27-bit slots
+    assert bench.grouping("bucket", 2_555_904, 1_000_000) == "bucket"       # c2 / c5: 20 bits
     assert bench.grouping("bucket", 500_000, 1_000_000) == "bucket"
     assert bench.grouping("lsd", 10_223_616, 100_000_000) == "lsd"
     assert bench.grouping("bucket", 1000, 500) == "lsd"                     # 9-bit keys: one pass does it
