@@ -190,7 +190,7 @@ static Staged stage_csr(fm_ctx* ctx, const fm_csr* c, bool check_range, Pinned& 
   g.o_xoff = g.o_lab + sizeof(double) * B;
   g.o_col = (g.o_xoff + sizeof(int32_t) * B + 15) / 16 * 16;
   g.o_x = (g.o_col + sizeof(uint32_t) * N + 15) / 16 * 16;
-  pin.ensure(g.o_x + sizeof(float) * N + 16);  // M <= N
+  pin.ensure_slack(g.o_x + sizeof(float) * N + 16);  // M <= N
   char* base = reinterpret_cast<char*>(pin.p);
   int64_t* rp = reinterpret_cast<int64_t*>(base);
   double* lab = reinterpret_cast<double*>(base + g.o_lab);
@@ -259,6 +259,12 @@ bool fuse_rule(const fm_ctx* ctx) {
 
 static bool fuse_on(const fm_ctx* ctx) { return ctx->cfg.shard_count == 1 && fuse_rule(ctx); }
 
+// The sharded owner's fused step: on request only (FM_FUSE_ON).  At c3 / world 1 it measured 1.40-1.49
+// ms per step against 1.16-1.26 unfused: the owner re-reads every received entry's
+// row after the S exchange either way, so the singleton pass saves only the S gathers of its runs,
+// and it adds a pass, the tags and a split to the owner's sort.
+bool owner_fuse(const fm_ctx* ctx) { return ctx->cfg.fuse_single == FM_FUSE_ON && ctx->kp <= 16; }
+
 // The bucket sort (fm_sort.hip) for a batch of N entries of this context, or the LSD passes
 // (fm_config.sort_algo; both stable, so the step is bitwise the same)
 bool bucket_on(const fm_ctx* ctx, int64_t N) {
@@ -287,12 +293,12 @@ static void copy_staged(fm_ctx* ctx, const Staged& g, const Pinned& pin, fm_batc
   b->max_id = g.max_id;
   b->dev.n_rows = B;
   b->dev.nnz = N;
-  b->dev.row_ptr.ensure(sizeof(int64_t) * (B + 1));
-  b->dev.col.ensure(sizeof(uint32_t) * std::max<int64_t>(N, 4) + 16);
-  b->dev.ent.ensure(sizeof(uint32_t) * 2 * std::max<int64_t>(N, 4) + 16);
-  b->dev.xs.ensure(sizeof(float) * std::max<int64_t>(N, 4) + 16);
-  b->dev.label.ensure(sizeof(double) * std::max<int64_t>(B, 4) + 16);
-  b->up.ensure(g.o_x + sizeof(float) * N + 16);
+  b->dev.row_ptr.ensure_slack(sizeof(int64_t) * (B + 1));
+  b->dev.col.ensure_slack(sizeof(uint32_t) * std::max<int64_t>(N, 4) + 16);
+  b->dev.ent.ensure_slack(sizeof(uint32_t) * 2 * std::max<int64_t>(N, 4) + 16);
+  b->dev.xs.ensure_slack(sizeof(float) * std::max<int64_t>(N, 4) + 16);
+  b->dev.label.ensure_slack(sizeof(double) * std::max<int64_t>(B, 4) + 16);
+  b->up.ensure_slack(g.o_x + sizeof(float) * N + 16);
   FM_HIP_CHECK(hipMemcpyAsync(b->up.p, pin.p, g.bytes, hipMemcpyHostToDevice, st));
   for (int r = 0; r < g.nruns; ++r)  // the packed value runs, each where its rows' xoff point
     if (g.run_n[r] > 0)
@@ -330,12 +336,12 @@ void wait_built(const fm_batch* b, hipStream_t st) {
 
 void reserve_work(fm_ctx* ctx, int64_t B, int64_t N) {
   StepWork& w = ctx->work;
-  w.S.ensure(sizeof(float) * (size_t)std::max<int64_t>(B, 1) * s_rec_floats(ctx->kp));
-  w.yl.ensure(sizeof(float2) * (size_t)std::max<int64_t>(B, 1));
+  w.S.ensure_slack(sizeof(float) * (size_t)std::max<int64_t>(B, 1) * s_rec_floats(ctx->kp));
+  w.yl.ensure_slack(sizeof(float2) * (size_t)std::max<int64_t>(B, 1));
   w.sort.ensure(std::max<int64_t>(N, 1));
   const int64_t nranges = (N + 255) / 256;  // update waves (fm_kernels.hip, kWaveEnt)
-  w.part.ensure(sizeof(double) * (size_t)std::max<int64_t>(nranges, 1) * 2 * (ctx->kp + 2));
-  w.ucnt.ensure(sizeof(uint32_t) * (size_t)std::max<int64_t>((N + 1023) / 1024, 1));
+  w.part.ensure_slack(sizeof(double) * (size_t)std::max<int64_t>(nranges, 1) * 2 * (ctx->kp + 2));
+  w.ucnt.ensure_slack(sizeof(uint32_t) * (size_t)std::max<int64_t>((N + 1023) / 1024, 1));
   w.loss_part.ensure(sizeof(double) * 2 * 256 * 8);
 }
 
@@ -716,8 +722,8 @@ int fm_batch_prepare(fm_ctx* ctx, fm_batch* b) {
       FM_HIP_CHECK(hipEventCreateWithFlags(&b->last_use, hipEventDisableTiming));
       FM_HIP_CHECK(hipEventRecord(b->last_use, ctx->stream));
     }
-    b->skeys.ensure(sizeof(uint32_t) * N);
-    b->sents.ensure(sizeof(uint2) * N);
+    b->skeys.ensure_slack(sizeof(uint32_t) * N);
+    b->sents.ensure_slack(sizeof(uint2) * N);
     // the shared sort workspace and this batch's view may still be read by an enqueued step
     FM_HIP_CHECK(hipStreamWaitEvent(ctx->side, ctx->ev_upd_done, 0));
     FM_HIP_CHECK(hipStreamWaitEvent(ctx->side, b->last_use, 0));
@@ -735,8 +741,8 @@ int fm_batch_prepare(fm_ctx* ctx, fm_batch* b) {
       b->split_n.ensure(2 * sizeof(int64_t));
       if (!(bucket_on(ctx, N) && bucket_sort_pairs64(ctx->work.sort, col, ent, N, kb, ctx->side, b->skeys.as<uint32_t>(),
                                                      b->sents.as<uint2>(), b->split_n.as<int64_t>()))) {
-        b->fkeys.ensure(sizeof(uint32_t) * N);
-        b->fents.ensure(sizeof(uint2) * N);
+        b->fkeys.ensure_slack(sizeof(uint32_t) * N);
+        b->fents.ensure_slack(sizeof(uint2) * N);
         radix_sort_pairs64(ctx->work.sort, col, ent, N, kb, ctx->side, &sk, &sv, b->fkeys.as<uint32_t>(),
                            b->fents.as<uint2>());
         launch_split(b->fkeys.as<uint32_t>(), b->fents.as<uint2>(), N, ctx->split_work, b->skeys.as<uint32_t>(),
@@ -787,7 +793,7 @@ int fm_batch_from_rows(fm_ctx* ctx, const fm_batch* data, const int64_t* rows, i
     // the staging {rows, row_ptr} of this batch's previous selection has been copied out
     FM_HIP_CHECK(hipEventSynchronize(b->sel_copied));
     const size_t img = sizeof(int64_t) * (2 * (size_t)n + 1);
-    b->sel_pin.ensure(img);
+    b->sel_pin.ensure_slack(img);
     int64_t* hrows = reinterpret_cast<int64_t*>(b->sel_pin.p);
     int64_t* rp = hrows + n;
     // the rows and their result row_ptr straight into the pinned staging, from the dataset's row_ptr
@@ -828,12 +834,12 @@ int fm_batch_from_rows(fm_ctx* ctx, const fm_batch* data, const int64_t* rows, i
     b->dev.n_rows = n;
     b->dev.nnz = N;
     b->max_id = data->max_id;
-    b->dev.row_ptr.ensure(sizeof(int64_t) * (n + 1));
-    b->dev.col.ensure(sizeof(uint32_t) * std::max<int64_t>(N, 4) + 16);
-    b->dev.ent.ensure(sizeof(uint32_t) * 2 * std::max<int64_t>(N, 4) + 16);
-    b->dev.xs.ensure(sizeof(float) * std::max<int64_t>(N, 4) + 16);
-    b->dev.label.ensure(sizeof(double) * std::max<int64_t>(n, 4) + 16);
-    b->up.ensure(img + 16);
+    b->dev.row_ptr.ensure_slack(sizeof(int64_t) * (n + 1));
+    b->dev.col.ensure_slack(sizeof(uint32_t) * std::max<int64_t>(N, 4) + 16);
+    b->dev.ent.ensure_slack(sizeof(uint32_t) * 2 * std::max<int64_t>(N, 4) + 16);
+    b->dev.xs.ensure_slack(sizeof(float) * std::max<int64_t>(N, 4) + 16);
+    b->dev.label.ensure_slack(sizeof(double) * std::max<int64_t>(n, 4) + 16);
+    b->up.ensure_slack(img + 16);
     FM_HIP_CHECK(hipMemcpyAsync(b->up.p, b->sel_pin.p, img, hipMemcpyHostToDevice, ctx->side));
     FM_HIP_CHECK(hipEventRecord(b->sel_copied, ctx->side));
     if (n > 0) {
@@ -854,7 +860,7 @@ int fm_batch_from_rows(fm_ctx* ctx, const fm_batch* data, const int64_t* rows, i
 int32_t fm_fuse_active(fm_ctx* ctx) {
   if (!ctx) return -1;
   if (ctx->group)  // a sharded group's owners take the fused owner step by the same rule; replicas never fuse
-    return ctx->cfg.parallel == FM_PARALLEL_SHARDED && fuse_rule(group_member0(ctx)) ? 1 : 0;
+    return ctx->cfg.parallel == FM_PARALLEL_SHARDED && owner_fuse(group_member0(ctx)) ? 1 : 0;
   return fuse_on(ctx) ? 1 : 0;
 }
 

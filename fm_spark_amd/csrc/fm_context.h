@@ -21,6 +21,9 @@ struct Pinned {
     FM_HIP_CHECK(hipHostMalloc(&p, n, hipHostMallocDefault));
     bytes = n;
   }
+  void ensure_slack(size_t n) {
+    if (n > bytes || !p) ensure(n + n / 8 + 4096);
+  }
   ~Pinned() {
     if (p) (void)hipHostFree(p);
   }
@@ -370,10 +373,11 @@ inline int bits_for(int64_t max_value) {
 }
 
 // shared host helpers (fm_capi.hip)
-// the fused step's rule (fm_config.fuse_single, kp <= 16, tables above 256 MB unless FUSE_ON), for the
-// single table (fuse_on) and the sharded owner step alike; and whether a batch of N entries takes
-// the bucket sort (fm_config.sort_algo)
+// the fused step's rule (fm_config.fuse_single, kp <= 16, tables above 256 MB unless FUSE_ON) for the
+// single table; the sharded owner's (FUSE_ON only); and whether a batch of N entries takes the
+// bucket sort (fm_config.sort_algo)
 bool fuse_rule(const fm_ctx* ctx);
+bool owner_fuse(const fm_ctx* ctx);
 bool bucket_on(const fm_ctx* ctx, int64_t N);
 void upload_batch(fm_ctx* ctx, const fm_csr* c, fm_batch* b, bool check_range);
 void reserve_work(fm_ctx* ctx, int64_t B, int64_t N);

@@ -76,6 +76,11 @@ struct DevBuf {
   void* p = nullptr;
   size_t bytes = 0;
   void ensure(size_t n);
+  // at least n bytes; a growth takes an eighth more (batches refilled with slightly different
+  // sizes, e.g. randomSplit splits, then stop growing: a growth drains the device)
+  void ensure_slack(size_t n) {
+    if (n > bytes || !p) ensure(n + n / 8 + 4096);
+  }
   void release();
   template <class T>
   T* as() const { return reinterpret_cast<T*>(p); }

@@ -1850,8 +1850,8 @@ void launch_tag_runs(const TableView& T, const uint32_t* mkeys, const int64_t* n
 void launch_split(const uint32_t* skeys, const uint2* sents, int64_t N, SplitWork& sw, uint32_t* mkeys, uint2* ments,
                   int64_t* n_out, hipStream_t st, const TableView* tag_T, int32_t epoch) {
   const int64_t nchunks = (N + kSplitChunk - 1) / kSplitChunk;
-  sw.cnt.ensure(sizeof(uint2) * (size_t)std::max<int64_t>(nchunks, 1));
-  sw.off.ensure(sizeof(int64_t) * (size_t)std::max<int64_t>(nchunks, 1));
+  sw.cnt.ensure_slack(sizeof(uint2) * (size_t)std::max<int64_t>(nchunks, 1));
+  sw.off.ensure_slack(sizeof(int64_t) * (size_t)std::max<int64_t>(nchunks, 1));
   if (N <= 0) {
     FM_HIP_CHECK(hipMemsetAsync(n_out, 0, 2 * sizeof(int64_t), st));
     return;

@@ -602,7 +602,7 @@ int fm_shard_owner_prepare(fm_ctx* ctx, fm_batch* b, const void* recv_slot, cons
     }
     FM_HIP_CHECK(hipEventRecord(S.ready_fwd, st));
     // the fused owner step (fm_shard_owner_update): the slot sort keeps only the runs of two or more
-    S.split = fuse_rule(ctx);
+    S.split = owner_fuse(ctx);
     if (S.split) {
       S.split_n.ensure(2 * sizeof(int64_t));
       if (n == 0) FM_HIP_CHECK(hipMemsetAsync(S.split_n.p, 0, 2 * sizeof(int64_t), st));

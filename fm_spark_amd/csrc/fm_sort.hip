@@ -29,12 +29,20 @@ namespace {
 
 constexpr int kMaxRB = 11;   // digit width at most (the bucket sort's top-bit pass)
 constexpr int kLsdMaxRB = 10;  // the LSD passes' digits at most (27-bit feature slots: 3 passes of 9 bits)
-constexpr int kBlock = 512;  // 8 waves x 8 keys per lane; two blocks (16 waves) per CU
+#ifndef FM_SORT_BLOCK
+#define FM_SORT_BLOCK 512
+#endif
+constexpr int kBlock = FM_SORT_BLOCK;  // 8 waves x 8 keys per lane; two blocks (16 waves) per CU
 constexpr int kWaves = kBlock / 64;
-constexpr int kMinRB = 9;    // the block scans hold R / kBlock >= 1 digits per thread
+constexpr int kMinRB = 9;    // digits of a pass at least
+// digits per thread in the block scans (a block wider than the radix: one, on the first R threads)
+template <int R>
+constexpr int digits_per_thread() { return R >= kBlock ? R / kBlock : 1; }
 constexpr int kRounds = 8;   // keys per thread per tile
 constexpr int kTile = kBlock * kRounds;  // 4096 keys per tile
 constexpr int kMaxRadix = 1 << kMaxRB;
+// the bucket sort's top-bit pass at most (an 11-bit scatter on 1024-thread blocks outgrows the LDS)
+constexpr int kBktMaxH = kBlock >= 1024 ? 10 : kMaxRB;
 constexpr int kChunk = 16;   // tiles per chunk of the count scan
 
 // Tile of a block: the tiles of one XCD (blocks b = x mod 8 are dispatched to XCD x) are
@@ -139,11 +147,11 @@ template <int RB, bool BIG = false>
 __global__ __launch_bounds__(kBlock) void k_radix_chunk_scan(uint32_t* __restrict__ counts, int64_t ntiles,
                                                              uint32_t* __restrict__ csum, BigPlan bp) {
   constexpr int R = 1 << RB;
-  constexpr int D = R / kBlock;
+  constexpr int D = digits_per_thread<R>();
   const int64_t nt = BIG ? (int64_t)bp.meta[1] : ntiles;
   const int64_t ext = nt + (BIG ? 1 : 0);
   const int64_t t0 = (int64_t)blockIdx.x * kChunk;
-  if (t0 >= ext) return;
+  if (t0 >= ext || (int)threadIdx.x >= R) return;
   uint32_t v[kChunk][D];
 #pragma unroll
   for (int j = 0; j < kChunk; ++j)
@@ -246,7 +254,8 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint32_t* __rest
                                                           int64_t ntiles, BigPlan bp) {
   constexpr int R = 1 << RB;
   constexpr uint32_t M = R - 1;
-  constexpr int D = R / kBlock;  // digits per thread in the block scans
+  constexpr int D = digits_per_thread<R>();  // digits per thread in the block scans
+  const bool own = (int)threadIdx.x * D < R;  // this thread holds digits in the block scans
   // per-wave digit counts and their prefixes stay below the 4096-key tile: 16-bit counters for the
   // 10-bit digits keep the block at 74 KB of LDS, two blocks per CU (32-bit: 90 KB, one block)
   using HistT = typename std::conditional<(RB >= 10), uint16_t, uint32_t>::type;
@@ -289,19 +298,21 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint32_t* __rest
     uint32_t v[D], at_h[D];
 #pragma unroll
     for (int i = 0; i < D; ++i) {
-      at_h[i] = prefix(h, tid * D + i);
-      v[i] = prefix(e, tid * D + i) - at_h[i];
+      at_h[i] = own ? prefix(h, tid * D + i) : 0u;
+      v[i] = own ? prefix(e, tid * D + i) - at_h[i] : 0u;
     }
     block_excl_scan<D>(v, wsum, lane, wave);
 #pragma unroll
-    for (int i = 0; i < D; ++i) glob_off[tid * D + i] = g.seg.x + v[i] + prefix(tile, tid * D + i) - at_h[i];
+    for (int i = 0; i < D; ++i)
+      if (own) glob_off[tid * D + i] = g.seg.x + v[i] + prefix(tile, tid * D + i) - at_h[i];
   } else {
     uint32_t v[D];
 #pragma unroll
-    for (int i = 0; i < D; ++i) v[i] = digit_tot[tid * D + i];
+    for (int i = 0; i < D; ++i) v[i] = own ? digit_tot[tid * D + i] : 0u;
     block_excl_scan<D>(v, wsum, lane, wave);
 #pragma unroll
-    for (int i = 0; i < D; ++i) glob_off[tid * D + i] = v[i] + prefix(tile, tid * D + i);
+    for (int i = 0; i < D; ++i)
+      if (own) glob_off[tid * D + i] = v[i] + prefix(tile, tid * D + i);
   }
   lds_barrier();
 
@@ -334,19 +345,23 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint32_t* __rest
     for (int i = 0; i < D; ++i) {
       const int d = tid * D + i;
       uint32_t acc = 0;
+      if (own) {
 #pragma unroll
-      for (int w = 0; w < kWaves; ++w) {
-        const uint32_t c = wave_hist[w][d];
-        wave_hist[w][d] = (HistT)acc;
-        acc += c;
+        for (int w = 0; w < kWaves; ++w) {
+          const uint32_t c = wave_hist[w][d];
+          wave_hist[w][d] = (HistT)acc;
+          acc += c;
+        }
       }
       v[i] = acc;
     }
     block_excl_scan<D>(v, wsum, lane, wave);
 #pragma unroll
     for (int i = 0; i < D; ++i) {
-      tile_start[tid * D + i] = v[i];
-      glob_off[tid * D + i] -= v[i];  // destination of staged element j of digit d: glob_off[d] + j
+      if (own) {
+        tile_start[tid * D + i] = v[i];
+        glob_off[tid * D + i] -= v[i];  // destination of staged element j of digit d: glob_off[d] + j
+      }
     }
   }
   lds_barrier();
@@ -850,11 +865,7 @@ static void radix_pass_impl(const uint32_t* kin, const P* vin, uint32_t* ko, P* 
 template <class P, int RB>
 static void radix_pass(const uint32_t* kin, const P* vin, uint32_t* ko, P* vo, int64_t n, int shift,
                        SortWork& w, int64_t ntiles, hipStream_t st) {
-  if constexpr ((1 << RB) >= kBlock) {
-    radix_pass_impl<P, RB>(kin, vin, ko, vo, n, shift, w, ntiles, st);
-  } else {
-    FM_REQUIRE(false, "sort digit narrower than the block");
-  }
+  radix_pass_impl<P, RB>(kin, vin, ko, vo, n, shift, w, ntiles, st);
 }
 
 // Digit width: the fewest passes of at most kMaxRB bits, spread evenly (27-bit feature
@@ -957,7 +968,7 @@ int bucket_hi_bits(int64_t n, int key_bits) {
   // buckets of about a third of the LDS image on average (hot features fill some to the image and
   // beyond), 9 to 11 top bits
   int H = 9;
-  while (H < kMaxRB && n / (int64_t(1) << H) > kBktCap / 3) ++H;
+  while (H < kBktMaxH && n / (int64_t(1) << H) > kBktCap / 3) ++H;
   if (key_bits < H + 1 || key_bits - H > 2 * kBktRB) return 0;  // one pass would do / too many low bits
   return H;
 }
@@ -975,8 +986,8 @@ bool bucket_sort_pairs64(SortWork& w, const uint32_t* keys_in, const uint2* vals
   const int64_t big_tiles = ntiles + n / ((int64_t)cap + 1) + 1;
   // the big path's digits: one pass of 9..11 bits for L <= 11, else two of 9 (a digit reaching above
   // bit L holds bucket bits, constant in a segment)
-  const int big_rb = L <= 9 ? 9 : L <= kMaxRB ? L : kBktRB;
-  const int passes = L <= kMaxRB ? 1 : 2;
+  const int big_rb = L <= 9 ? 9 : L <= kBktMaxH ? L : kBktRB;
+  const int passes = L <= kBktMaxH ? 1 : 2;
   w.ensure(n);
   // every buffer sized before the first launch (growing one drains the device)
   const size_t cnt_bytes = sizeof(uint32_t) * std::max<int64_t>((int64_t)kMaxRadix * count_rows((w.cap + kTile - 1) / kTile),
@@ -1006,7 +1017,9 @@ bool bucket_sort_pairs64(SortWork& w, const uint32_t* keys_in, const uint2* vals
   switch (H) {
     case 9: radix_pass<uint2, 9>(kin, vals_in, kbuf[0], vbuf[0], n, L, w, ntiles, st); break;
     case 10: radix_pass<uint2, 10>(kin, vals_in, kbuf[0], vbuf[0], n, L, w, ntiles, st); break;
-    default: radix_pass<uint2, 11>(kin, vals_in, kbuf[0], vbuf[0], n, L, w, ntiles, st); break;
+    default:
+      if constexpr (kBktMaxH >= 11) radix_pass<uint2, 11>(kin, vals_in, kbuf[0], vbuf[0], n, L, w, ntiles, st);
+      break;
   }
   const uint32_t* btot = w.digit_tot.as<uint32_t>();
   uint2* bstat = w.bstat.as<uint2>();
@@ -1031,7 +1044,9 @@ bool bucket_sort_pairs64(SortWork& w, const uint32_t* keys_in, const uint2* vals
     switch (big_rb) {
       case 9: big_pass<9>(sk, sv, dk, dv, big_rb * p, w, bp, big_tiles, st); break;
       case 10: big_pass<10>(sk, sv, dk, dv, big_rb * p, w, bp, big_tiles, st); break;
-      default: big_pass<11>(sk, sv, dk, dv, big_rb * p, w, bp, big_tiles, st); break;
+      default:
+        if constexpr (kBktMaxH >= 11) big_pass<11>(sk, sv, dk, dv, big_rb * p, w, bp, big_tiles, st);
+        break;
     }
     sk = dk;
     sv = dv;

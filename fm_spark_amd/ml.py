@@ -426,17 +426,21 @@ def _select_csr(rp, col, val, labels, rows) -> N.CSRHost:
 
 
 def run_minibatch_sgd_resident(ctx: FMContext, data, splits, step_size: float, reg_param: float,
-                               max_iter: int | None = None):
+                               max_iter: int | None = None, bufs: list | None = None):
     """The foldLeft of runMiniBatchSGD (FactorizationMachinesSGD.scala:114-211) over a dataset kept
     on the device (`data`, dfData.cache() at :93): split i's rows (`splits[i]`, the randomSplit row
     lists) are gathered there into one of two batches used in turn (fm_batch_from_rows) and sorted
     on the side stream (fm_batch_prepare) while iteration i - 1 steps; every step only enqueues
     (fm_step_batch with out = NULL).  An empty split is skipped with the reference's warning
     (:126-128).  The loss log lines (:134-139) are written in iteration order after the loop, from
-    the device's loss history.  Returns the loss sums of the executed iterations."""
+    the device's loss history.  Returns the loss sums of the executed iterations.  `bufs`: a list of
+    two batches (or Nones) to refill and leave open for the caller (another loop reuses their
+    device buffers); by default they are made here and closed at the end."""
     n_iter = len(splits) if max_iter is None else max_iter
     work = [(i, rows) for i, rows in enumerate(splits) if len(rows)]
-    bufs = [None, None]
+    own = bufs is None
+    if own:
+        bufs = [None, None]
 
     def load(j):
         b = ctx.batch_from_rows(data, work[j][1], into=bufs[j % 2])
@@ -458,9 +462,10 @@ def run_minibatch_sgd_resident(ctx: FMContext, data, splits, step_size: float, r
             log.info("Loss of Iteration (%d/%d): %s", i + 1, n_iter, done[i])
         else:
             log.warning("Iteration (%d/%d). The size of sampled batch is zero", i + 1, n_iter)
-    for b in bufs:
-        if b is not None:
-            b.close()
+    if own:
+        for b in bufs:
+            if b is not None:
+                b.close()
     return [done[i] for i, _ in work]
 
 

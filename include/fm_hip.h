@@ -82,7 +82,9 @@ typedef struct fm_batch fm_batch;
  *                k <= 16 takes the fused step -- the forward updates every row whose feature has one
  *                entry in the batch, the segmented update only the rest (the same table as the
  *                unfused step within fp64 summation order); FM_FUSE_DEFAULT (0): the same, for tables
- *                larger than the 256-MB Infinity Cache; FM_FUSE_OFF: never.
+ *                larger than the 256-MB Infinity Cache; FM_FUSE_OFF: never.  A row-sharded
+ *                context's owners take the fused owner step with FM_FUSE_ON only (it measured
+ *                slower than the unfused owner step at c3).
  * xchg_chunks  : sharded step with R > 1: the owners' partial pass runs in this many chunks, each
  *                sent while the next is computed (0 = the default, 4; 1 = one pass then one
  *                all-to-all; at most 64).  Every process of a job must pass the same value.
@@ -213,8 +215,8 @@ int fm_batch_prepare(fm_ctx* ctx, fm_batch* batch);
 int fm_batch_from_rows(fm_ctx* ctx, const fm_batch* data, const int64_t* rows, int64_t n, fm_batch** out);
 /* 1 if a batch prepared by fm_batch_prepare on this context takes the fused step (fm_config.fuse_single
  * and the library's rule: k <= 16, table above 256 MB unless FM_FUSE_ON; a row-sharded context's
- * owners take the fused owner step by the same rule, per member table; replicated contexts never
- * fuse), else 0; -1 for a null context. */
+ * owners take the fused owner step with FM_FUSE_ON and k <= 16; replicated contexts never fuse),
+ * else 0; -1 for a null context. */
 int32_t fm_fuse_active(fm_ctx* ctx);
 int64_t fm_batch_rows(const fm_batch* b);
 int64_t fm_batch_nnz(const fm_batch* b);
@@ -337,8 +339,8 @@ int fm_shard_route(fm_ctx* ctx, fm_batch* batch, void* send_slot, void* send_ent
  * sent src_pairs[r] pairs) -> their pair table and their order by slot (stable: source rank,
  * then CSR order), kept with `batch`.  No host synchronisation.  recv_slot / recv_ent must stay
  * valid until the main stream has run fm_shard_owner_update of this batch (the fused owner step --
- * fm_config.fuse_single's rule, kp <= 16 -- reads them again there to update the rows of features
- * with one received entry pair by pair; otherwise until fm_shard_owner_forward). */
+ * fm_config.fuse_single FM_FUSE_ON, kp <= 16 -- reads them again there to update the rows of
+ * features with one received entry pair by pair; otherwise until fm_shard_owner_forward). */
 int fm_shard_owner_prepare(fm_ctx* ctx, fm_batch* batch, const void* recv_slot, const void* recv_ent,
                            int64_t n, const int64_t* src_entries, const int64_t* src_pairs);
 /* Phase 2 (owner): partials_out[sum src_pairs] (source-major, sample order): per received pair

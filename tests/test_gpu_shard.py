@@ -109,7 +109,7 @@ def test_hip_shard_phases_match_single_table(gpu, R, k, F, hot, fuse):
     np.testing.assert_allclose(np.concatenate(gV)[order], model.V[gi[order]], rtol=1e-5, atol=1e-8)
 
 
-@pytest.mark.parametrize("fuse", [False, None])
+@pytest.mark.parametrize("fuse", [False, True])
 def test_hip_shard_c3_r8_matches_single_table(gpu, fuse):
     """Config c3's table at R = 8 (100M hashed features, k = 16, owner = id % 8), eight ranks of
     32K synthetic rows each (the bench's generator), two iterations of the sharded phases
@@ -122,7 +122,7 @@ def test_hip_shard_c3_r8_matches_single_table(gpu, fuse):
 
     F, k, R, B = 100_000_000, 16, 8, 32768
     ref = FMContext(F, k, seed=5, init_sd=0.01)
-    engines = [HipShardEngine(F, k, r, R, fuse=fuse) for r in range(R)]  # None: the default (fused: 1.6-GB shards)
+    engines = [HipShardEngine(F, k, r, R, fuse=fuse) for r in range(R)]
     for t in (1, 2):
         parts = [synthetic_batch(B, F, batch_index=100 * t + r) for r in range(R)]
         cat = _concat([R_.CSR(p.row_ptr, p.col, p.val, p.label) for p in parts])

@@ -35,8 +35,10 @@ ctx.sync()
 res = {"iters": iters, "rows": [len(s) for s in splits]}
 
 
-def loop(sync_each=False, acc=None):
-    bufs = [None, None]
+def loop(sync_each=False, acc=None, bufs=None):
+    own = bufs is None
+    if own:
+        bufs = [None, None]
 
     def timed(name, f):
         t0 = time.perf_counter()
@@ -59,18 +61,23 @@ def loop(sync_each=False, acc=None):
             load(j + 1)
     timed("sync", ctx.sync)
     dt = time.perf_counter() - t0
-    for b in bufs:
-        b.close()
+    if own:
+        for b in bufs:
+            b.close()
     return dt
 
 
-loop()  # buffers grown
+keep = [None, None]
+loop(bufs=keep)  # buffers grown
 for rep in range(2):
     acc = {}
-    dt = loop(acc=acc)
+    dt = loop(acc=acc, bufs=keep)
     res[f"pipelined_{rep}"] = {"ms_per_iter": 1e3 * dt / iters, "host_ms_per_iter": {k: 1e3 * v / iters for k, v in acc.items()}}
 acc = {}
-dt = loop(sync_each=True, acc=acc)
+dt = loop(acc=acc)
+res["pipelined_fresh_batches"] = {"ms_per_iter": 1e3 * dt / iters, "host_ms_per_iter": {k: 1e3 * v / iters for k, v in acc.items()}}
+acc = {}
+dt = loop(sync_each=True, acc=acc, bufs=keep)
 res["synced"] = {"ms_per_iter": 1e3 * dt / iters, "host_ms_per_iter": {k: 1e3 * v / iters for k, v in acc.items()}}
 # fm_batch_from_rows alone, into one batch
 b = None
