@@ -28,13 +28,19 @@ namespace fmhip {
 namespace {
 
 constexpr int kMaxRB = 11;   // digit width at most (the bucket sort's top-bit pass)
-constexpr int kLsdMaxRB = 10;  // the LSD passes' digits at most (27-bit feature slots: 3 passes of 9 bits)
+#ifndef FM_SORT_RB_MAX
+#define FM_SORT_RB_MAX 10
+#endif
+#ifndef FM_SORT_RB_MIN
+#define FM_SORT_RB_MIN 9
+#endif
+constexpr int kLsdMaxRB = FM_SORT_RB_MAX;  // the LSD passes' digits at most (27-bit feature slots: 3 passes of 9 bits)
 #ifndef FM_SORT_BLOCK
 #define FM_SORT_BLOCK 512
 #endif
 constexpr int kBlock = FM_SORT_BLOCK;  // 8 waves x 8 keys per lane; two blocks (16 waves) per CU
 constexpr int kWaves = kBlock / 64;
-constexpr int kMinRB = 9;    // digits of a pass at least
+constexpr int kMinRB = FM_SORT_RB_MIN;  // digits of a pass at least
 // digits per thread in the block scans (a block wider than the radix: one, on the first R threads)
 template <int R>
 constexpr int digits_per_thread() { return R >= kBlock ? R / kBlock : 1; }
@@ -912,6 +918,9 @@ static void radix_sort_impl(SortWork& w, const uint32_t* keys_in, const P* vals_
     uint32_t* ko = last ? final_keys : kbuf[which];
     P* vo = last ? final_vals : vbuf[which];
     switch (rb) {
+      case 6: radix_pass<P, 6>(kin, vin, ko, vo, n, shift, w, ntiles, st); break;
+      case 7: radix_pass<P, 7>(kin, vin, ko, vo, n, shift, w, ntiles, st); break;
+      case 8: radix_pass<P, 8>(kin, vin, ko, vo, n, shift, w, ntiles, st); break;
       case 9: radix_pass<P, 9>(kin, vin, ko, vo, n, shift, w, ntiles, st); break;
       default: radix_pass<P, 10>(kin, vin, ko, vo, n, shift, w, ntiles, st); break;
     }

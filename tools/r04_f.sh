@@ -19,7 +19,7 @@ for sk in 3 0; do
   done
 done
 B="--steps 20 --warmup 5 --no-cpu-baseline --host-path-steps 0 --fit-iters 0"
-for rep in 1 2; do
+for rep in ${REPS:-1 2}; do
   for c in c3 c2 c5; do
     for v in t512 sb1024; do
       lib=""; [ $v = sb1024 ] && lib=tools/_variants/sb1024/libfm_hip.so
