@@ -724,9 +724,11 @@ int fm_batch_prepare(fm_ctx* ctx, fm_batch* b) {
     }
     b->skeys.ensure_slack(sizeof(uint32_t) * N);
     b->sents.ensure_slack(sizeof(uint2) * N);
-    // the shared sort workspace and this batch's view may still be read by an enqueued step
+    // the shared sort workspace and this batch's view may still be read by an enqueued step; a batch
+    // refilled by fm_batch_from_rows is sorted once its gather is done
     FM_HIP_CHECK(hipStreamWaitEvent(ctx->side, ctx->ev_upd_done, 0));
     FM_HIP_CHECK(hipStreamWaitEvent(ctx->side, b->last_use, 0));
+    wait_built(b, ctx->side);
     hipEvent_t es = ctx->prof_begin(ctx->side);
     const uint32_t* sk = nullptr;
     const uint2* sv = nullptr;
@@ -829,8 +831,12 @@ int fm_batch_from_rows(fm_ctx* ctx, const fm_batch* data, const int64_t* rows, i
       });
     const int64_t N = rp[n];
     FM_REQUIRE(N < (int64_t(1) << 31), "nnz must be < 2^31 per batch");
-    // batch-only work on the side stream, behind every queued step that reads this batch
-    FM_HIP_CHECK(hipStreamWaitEvent(ctx->side, b->last_use, 0));
+    // batch-only work on the copy stream, behind every queued step that reads this batch: the copy
+    // of the next split overlaps the sort of the current one on the side stream (the sort waits
+    // for `built`, fm_batch_prepare)
+    if (!ctx->copy_stream) FM_HIP_CHECK(hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking));
+    hipStream_t gs = ctx->copy_stream;
+    FM_HIP_CHECK(hipStreamWaitEvent(gs, b->last_use, 0));
     b->dev.n_rows = n;
     b->dev.nnz = N;
     b->max_id = data->max_id;
@@ -840,16 +846,15 @@ int fm_batch_from_rows(fm_ctx* ctx, const fm_batch* data, const int64_t* rows, i
     b->dev.xs.ensure_slack(sizeof(float) * std::max<int64_t>(N, 4) + 16);
     b->dev.label.ensure_slack(sizeof(double) * std::max<int64_t>(n, 4) + 16);
     b->up.ensure_slack(img + 16);
-    FM_HIP_CHECK(hipMemcpyAsync(b->up.p, b->sel_pin.p, img, hipMemcpyHostToDevice, ctx->side));
-    FM_HIP_CHECK(hipEventRecord(b->sel_copied, ctx->side));
+    FM_HIP_CHECK(hipMemcpyAsync(b->up.p, b->sel_pin.p, img, hipMemcpyHostToDevice, gs));
+    FM_HIP_CHECK(hipEventRecord(b->sel_copied, gs));
     if (n > 0) {
       const int64_t* up = b->up.as<int64_t>();
-      launch_select_rows(data->dev, up, up + n, n, b->dev, ctx->side);
+      launch_select_rows(data->dev, up, up + n, n, b->dev, gs);
     } else {
-      FM_HIP_CHECK(hipMemcpyAsync(b->dev.row_ptr.p, b->up.as<int64_t>(), sizeof(int64_t), hipMemcpyDeviceToDevice,
-                                  ctx->side));
+      FM_HIP_CHECK(hipMemcpyAsync(b->dev.row_ptr.p, b->up.as<int64_t>(), sizeof(int64_t), hipMemcpyDeviceToDevice, gs));
     }
-    FM_HIP_CHECK(hipEventRecord(b->built, ctx->side));
+    FM_HIP_CHECK(hipEventRecord(b->built, gs));
     b->prepared = false;  // a refilled batch is sorted again by its own fm_batch_prepare
     b->host_rp.clear();   // a selection is not itself a dataset (fm_batch_create's batches are)
     if (fresh) *out = fresh.release();

@@ -378,6 +378,8 @@ inline int bits_for(int64_t max_value) {
 // bucket sort (fm_config.sort_algo)
 bool fuse_rule(const fm_ctx* ctx);
 bool owner_fuse(const fm_ctx* ctx);
+// stream st waits until a batch refilled by fm_batch_from_rows has been gathered (copy stream)
+void wait_built(const fm_batch* b, hipStream_t st);
 bool bucket_on(const fm_ctx* ctx, int64_t N);
 void upload_batch(fm_ctx* ctx, const fm_csr* c, fm_batch* b, bool check_range);
 void reserve_work(fm_ctx* ctx, int64_t B, int64_t N);

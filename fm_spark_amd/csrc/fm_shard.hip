@@ -474,8 +474,10 @@ void shard_route_launch(fm_ctx* ctx, fm_batch* b, void* send_slot, void* send_en
     const int64_t B = b->dev.n_rows, N = b->dev.nnz;
     FM_REQUIRE(N == 0 || (send_slot && send_ent), "null send buffer");
     if (!st) st = ctx->side;
-    // the batch's previous iteration may still read its requester state on the main stream
+    // the batch's previous iteration may still read its requester state on the main stream; a batch
+    // refilled by fm_batch_from_rows is routed once its gather is done
     FM_HIP_CHECK(hipStreamWaitEvent(st, S.last_use, 0));
+    wait_built(b, st);
     hipEvent_t e0 = ctx->prof_begin(st);
     const int64_t ntiles = std::max<int64_t>((B + kBlock - 1) / kBlock, 1);
     ctx->sh_okey.ensure(sizeof(uint32_t) * std::max<int64_t>(N, 4) + 16);

@@ -28,19 +28,14 @@ namespace fmhip {
 namespace {
 
 constexpr int kMaxRB = 11;   // digit width at most (the bucket sort's top-bit pass)
-#ifndef FM_SORT_RB_MAX
-#define FM_SORT_RB_MAX 10
-#endif
-#ifndef FM_SORT_RB_MIN
-#define FM_SORT_RB_MIN 9
-#endif
-constexpr int kLsdMaxRB = FM_SORT_RB_MAX;  // the LSD passes' digits at most (27-bit feature slots: 3 passes of 9 bits)
-#ifndef FM_SORT_BLOCK
-#define FM_SORT_BLOCK 512
-#endif
-constexpr int kBlock = FM_SORT_BLOCK;  // 8 waves x 8 keys per lane; two blocks (16 waves) per CU
+// the LSD passes' digits at most / at least (27-bit feature slots: 3 passes of 9 bits; 7- and 8-bit
+// digits, 4 passes at c3, measured slower in the step: DESIGN.md §5)
+constexpr int kLsdMaxRB = 10;
+// 8 waves x 8 keys per lane; two blocks (16 waves) per CU (8192-key tiles on 1024-thread blocks
+// measured slower in the step: DESIGN.md §5)
+constexpr int kBlock = 512;
 constexpr int kWaves = kBlock / 64;
-constexpr int kMinRB = FM_SORT_RB_MIN;  // digits of a pass at least
+constexpr int kMinRB = 9;
 // digits per thread in the block scans (a block wider than the radix: one, on the first R threads)
 template <int R>
 constexpr int digits_per_thread() { return R >= kBlock ? R / kBlock : 1; }
@@ -418,10 +413,7 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint32_t* __rest
 // order every segment by its low L bits at once, one or two 9-bit passes across all CUs; in SPLIT mode
 // three more kernels (k_big_split_*) keep each segment's multi entries.  A skewed batch's hot buckets
 // therefore cost what the same keys cost in the LSD sort, not one block's walk of a huge bucket.
-#ifndef FM_BKT_BB
-#define FM_BKT_BB 512
-#endif
-constexpr int kBB = FM_BKT_BB;     // phase-2 block: 8 waves, two blocks per CU (the image takes 60 KB)
+constexpr int kBB = 512;           // phase-2 block: 8 waves, two blocks per CU (the image takes 60 KB)
 constexpr int kBW = kBB / 64;
 constexpr int kBktCap = 30 * kBB;  // a bucket up to this size is ordered in LDS
 constexpr int kBktRB = 9;          // digit bits of one in-bucket pass (512 digits)
