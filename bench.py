@@ -321,18 +321,18 @@ def sort_passes(num_rows):
 
 def step_kernels(F, n, sort, fused):
     """Launches per single-table step of each kernel (fm_capi.hip step_impl / fm_batch_prepare,
-    fm_sort.hip): the forward, update and combine; the fused step's tags; the grouping sort's --
-    LSD: count / chunk scan / chunk top / scatter per digit pass (+ the split kernels, fused);
-    bucket: the top-bit pass, the big path's one or two passes, the plan and the phase-2 kernel
-    (+ the big path's split and the compaction, fused)."""
+    fm_sort.hip): the forward, update and combine; the grouping sort's -- LSD: count / chunk scan /
+    chunk top / scatter per digit pass (+ the split kernels at the step, which tag the multi rows,
+    fused); bucket: the top-bit pass, the big path's one or two passes, the plan and the phase-2
+    kernel (+ the big path's split, the compaction and the tag pass, fused)."""
     ps = {"k_forward": 1, "k_segment_update": 1, "k_segment_combine": 1}
-    if fused:
-        ps["k_tag_runs"] = 1
     if grouping(sort, n, F) == "lsd":
         passes = sort_passes(F)
-        if fused:
+        if fused:  # the split at the step, its count pass writing the multi tags
             ps.update({"k_split_count": 1, "k_split_scan": 1, "k_split_scatter": 1})
     else:
+        if fused:
+            ps["k_tag_runs"] = 1
         kb = max(1, int(F - 1).bit_length())
         H = 9
         while H < 11 and n // (1 << H) > 30 * 512 // 3:

@@ -411,10 +411,18 @@ int step_impl(fm_ctx* ctx, fm_batch* b, int32_t t, double step_size, double reg_
     // the batch's multi view (fm_batch_prepare, a step or more ahead on the side stream: sorted,
     // singleton runs dropped)
     FM_HIP_CHECK(hipStreamWaitEvent(ctx->stream, b->ready, 0));
-    // each multi run's row tagged with this step's epoch (so here, at the step, on the main stream)
+    // each multi run's row tagged with this step's epoch (so here, at the step, on the main stream):
+    // with the LSD view, by the split pass as it finds the runs; with the bucket sort's split view,
+    // by a pass over it
     e0 = ctx->prof_begin(ctx->stream);
-    launch_tag_runs(T, b->skeys.as<uint32_t>(), b->split_n.as<int64_t>(), N, p.epoch, ctx->stream);
-    ctx->prof_end("tag", e0, ctx->stream);
+    if (b->split_at_step) {
+      launch_split(b->fkeys.as<uint32_t>(), b->fents.as<uint2>(), N, ctx->split_work, b->skeys.as<uint32_t>(),
+                   b->sents.as<uint2>(), b->split_n.as<int64_t>(), ctx->stream, &T, p.epoch);
+      ctx->prof_end("split", e0, ctx->stream);
+    } else {
+      launch_tag_runs(T, b->skeys.as<uint32_t>(), b->split_n.as<int64_t>(), N, p.epoch, ctx->stream);
+      ctx->prof_end("tag", e0, ctx->stream);
+    }
     fx.fused = true;
   }
   e0 = ctx->prof_begin(ctx->stream);
@@ -733,13 +741,14 @@ int fm_batch_prepare(fm_ctx* ctx, fm_batch* b) {
     const uint32_t* sk = nullptr;
     const uint2* sv = nullptr;
     b->split = fuse_on(ctx);
+    b->split_at_step = false;
     const int kb = bits_for(ctx->rows - 1);
     const uint32_t* col = b->dev.col.as<uint32_t>();
     const uint2* ent = b->dev.ent.as<uint2>();
     if (b->split) {
       // the fused step's view: only the runs of two or more entries (skeys / sents), with
       // {their count, the number of singleton runs} in split_n -- the bucket sort keeps them as it
-      // orders each bucket; after the LSD passes a split pass drops the singletons
+      // orders each bucket; the LSD passes leave the whole view (fkeys / fents) to the step's split
       b->split_n.ensure(2 * sizeof(int64_t));
       if (!(bucket_on(ctx, N) && bucket_sort_pairs64(ctx->work.sort, col, ent, N, kb, ctx->side, b->skeys.as<uint32_t>(),
                                                      b->sents.as<uint2>(), b->split_n.as<int64_t>()))) {
@@ -747,8 +756,10 @@ int fm_batch_prepare(fm_ctx* ctx, fm_batch* b) {
         b->fents.ensure_slack(sizeof(uint2) * N);
         radix_sort_pairs64(ctx->work.sort, col, ent, N, kb, ctx->side, &sk, &sv, b->fkeys.as<uint32_t>(),
                            b->fents.as<uint2>());
-        launch_split(b->fkeys.as<uint32_t>(), b->fents.as<uint2>(), N, ctx->split_work, b->skeys.as<uint32_t>(),
-                     b->sents.as<uint2>(), b->split_n.as<int64_t>(), ctx->side);
+        // the step splits this view on the main stream, its count pass tagging the multi rows: c3
+        // 0.924-0.931 ms per step against 0.968-0.971 with the split here on the side stream and a
+        // separate tag pass at the step (three alternating reps, profiles/r04_i)
+        b->split_at_step = true;
       }
     } else if (!(bucket_on(ctx, N) && bucket_sort_pairs64(ctx->work.sort, col, ent, N, kb, ctx->side,
                                                           b->skeys.as<uint32_t>(), b->sents.as<uint2>(), nullptr))) {

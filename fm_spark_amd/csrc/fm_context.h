@@ -112,13 +112,14 @@ struct fm_batch {
   DevBuf fkeys, fents;  // the LSD-sorted whole view a split pass reduces to the multi view (bucket sort: unused)
   DevBuf split_n;
   bool split = false;
+  bool split_at_step = false;     // the LSD view in fkeys / fents, split (and tagged) by the step
   hipEvent_t ready = nullptr;     // recorded on the side stream after the prepared sort
   hipEvent_t last_use = nullptr;  // recorded on the main stream after a step read the batch
   bool prepared = false;
   // fm_batch_from_rows: the host copy of row_ptr that sizes a selection of this batch's rows without
   // a device read (kept by fm_batch_create and fm_batch_from_rows), the selection's pinned staging
-  // {rows, row_ptr} and its events (side stream: staging copied out; the batch's rows written --
-  // every main-stream reader of dev waits for `built`)
+  // {rows, row_ptr} and its events (copy stream: staging copied out; the batch's rows written --
+  // every reader of dev on another stream waits for `built`)
   std::vector<int64_t> host_rp;
   Pinned sel_pin;
   hipEvent_t sel_copied = nullptr, built = nullptr;
