@@ -21,6 +21,8 @@ for c in c2 c5; do
 done
 timeout -k 10 300 python bench.py $B --force-sharded > $out/bench_sh1.log 2>&1 || exit $?
 echo "sharded1 $(grep -o '"ms_per_step": [0-9.]*' $out/bench_sh1.log | head -1)" >&2
+timeout -k 10 300 python tools/fit_diag.py 8 > $out/fit_diag.json 2> $out/fit_diag.err || exit $?
+export PMC_GROUPS="FETCH_SIZE;WRITE_SIZE;TCC_HIT_sum TCC_MISS_sum"
 A="--steps 5 --warmup 2 --no-cpu-baseline --profile-kernels 0 --host-path-steps 0 --fit-iters 0"
 for c in c3 c2 c5; do
   PMC_OUT=$out/pmc/${c}_default BENCH_ARGS="--config $c $A" bash tools/pmc.sh || exit $?
