@@ -321,22 +321,27 @@ def sort_passes(num_rows):
 
 def step_kernels(F, n, sort, fused):
     """Launches per single-table step of each kernel (fm_capi.hip step_impl / fm_batch_prepare,
-    fm_sort.hip): the forward, update and combine; fused, the run count and its scan at the step
-    (the count pass tags the multi rows); the grouping sort's -- LSD: count / chunk scan / chunk
-    top / scatter per digit pass; bucket: the top-bit pass, the big path's one or two passes, the
-    plan and the phase-2 kernel."""
+    fm_sort.hip): the forward, update and combine; the grouping sort's -- LSD: count / chunk scan /
+    chunk top / scatter per digit pass (+ the split kernels at the step, which tag the multi rows,
+    fused); bucket: the top-bit pass, the big path's one or two passes, the plan and the phase-2
+    kernel (+ the big path's split, the compaction and the tag pass, fused)."""
     ps = {"k_forward": 1, "k_segment_update": 1, "k_segment_combine": 1}
-    if fused:  # the runs counted at the step, the count pass writing the multi tags
-        ps.update({"k_split_count": 1, "k_split_scan": 1})
     if grouping(sort, n, F) == "lsd":
         passes = sort_passes(F)
+        if fused:  # the split at the step, its count pass writing the multi tags
+            ps.update({"k_split_count": 1, "k_split_scan": 1, "k_split_scatter": 1})
     else:
+        if fused:
+            ps["k_tag_runs"] = 1
         kb = max(1, int(F - 1).bit_length())
         H = 9
         while H < 11 and n // (1 << H) > 30 * 512 // 3:
             H += 1
         passes = 1 + (1 if kb - H <= 11 else 2)
         ps.update({"k_big_plan": 1, "k_bucket_sort": 1})
+        if fused:
+            ps.update({"k_big_split_count": 1, "k_big_split_scan": 1, "k_big_split_write": 1,
+                       "k_bucket_offsets": 1, "k_bucket_compact": 1})
     ps.update({"k_radix_count": passes, "k_radix_chunk_scan": passes, "k_radix_chunk_top": passes,
                "k_radix_scatter": passes})
     return ps

@@ -379,7 +379,7 @@ int step_impl(fm_ctx* ctx, fm_batch* b, int32_t t, double step_size, double reg_
   const uint32_t* skeys = nullptr;
   const uint2* sents = nullptr;
   const bool prepared = b->prepared;
-  const bool fused = prepared && b->split;  // the fused step (fm_batch_prepare sorted the whole view)
+  const bool fused = prepared && b->split;  // the view holds the multi runs only (fm_batch_prepare)
   FM_REQUIRE(!(fused && emit), "a batch prepared for the fused step cannot feed fm_repl_grad");
   FM_REQUIRE(ctx->epoch < (1 << 29), "epoch count beyond the multi tags' range (2^29 steps)");
   if (prepared) {
@@ -408,17 +408,21 @@ int step_impl(fm_ctx* ctx, fm_batch* b, int32_t t, double step_size, double reg_
   hipEvent_t e0 = nullptr;
   FwdOut fx{};
   if (fused) {
-    // the batch's sorted view (fm_batch_prepare, a step or more ahead on the side stream)
+    // the batch's multi view (fm_batch_prepare, a step or more ahead on the side stream: sorted,
+    // singleton runs dropped)
     FM_HIP_CHECK(hipStreamWaitEvent(ctx->stream, b->ready, 0));
-    // the runs counted (multi entries, singleton runs) and each multi run's row tagged with this
-    // step's epoch by the count pass (so here, at the step, on the main stream); the update then
-    // walks the whole view, skipping the singleton runs
+    // each multi run's row tagged with this step's epoch (so here, at the step, on the main stream):
+    // with the LSD view, by the split pass as it finds the runs; with the bucket sort's split view,
+    // by a pass over it
     e0 = ctx->prof_begin(ctx->stream);
-    launch_split(b->fkeys.as<uint32_t>(), b->fents.as<uint2>(), N, ctx->split_work, nullptr, nullptr,
-                 b->split_n.as<int64_t>(), ctx->stream, &T, p.epoch, false);
-    skeys = b->fkeys.as<uint32_t>();
-    sents = b->fents.as<uint2>();
-    ctx->prof_end("split", e0, ctx->stream);
+    if (b->split_at_step) {
+      launch_split(b->fkeys.as<uint32_t>(), b->fents.as<uint2>(), N, ctx->split_work, b->skeys.as<uint32_t>(),
+                   b->sents.as<uint2>(), b->split_n.as<int64_t>(), ctx->stream, &T, p.epoch);
+      ctx->prof_end("split", e0, ctx->stream);
+    } else {
+      launch_tag_runs(T, b->skeys.as<uint32_t>(), b->split_n.as<int64_t>(), N, p.epoch, ctx->stream);
+      ctx->prof_end("tag", e0, ctx->stream);
+    }
     fx.fused = true;
   }
   e0 = ctx->prof_begin(ctx->stream);
@@ -428,7 +432,7 @@ int step_impl(fm_ctx* ctx, fm_batch* b, int32_t t, double step_size, double reg_
   e0 = ctx->prof_begin(ctx->stream);
   double* stats = ctx->loss_hist.as<double>() + 3 * (int64_t)ctx->epoch;
   launch_segment_update(T, b->dev, ctx->work, p, skeys, sents, nfwd, stats, ctx->stream, emit,
-                        fused ? b->split_n.as<int64_t>() : nullptr, fused);
+                        fused ? b->split_n.as<int64_t>() : nullptr);
   // the shared sort workspace is read by the main stream only when the batch was sorted inline
   // (not prepared): only then must the next fm_batch_prepare's sort wait for this update
   if (!prepared) FM_HIP_CHECK(hipEventRecord(ctx->ev_upd_done, ctx->stream));
@@ -726,6 +730,8 @@ int fm_batch_prepare(fm_ctx* ctx, fm_batch* b) {
       FM_HIP_CHECK(hipEventCreateWithFlags(&b->last_use, hipEventDisableTiming));
       FM_HIP_CHECK(hipEventRecord(b->last_use, ctx->stream));
     }
+    b->skeys.ensure_slack(sizeof(uint32_t) * N);
+    b->sents.ensure_slack(sizeof(uint2) * N);
     // the shared sort workspace and this batch's view may still be read by an enqueued step; a batch
     // refilled by fm_batch_from_rows is sorted once its gather is done
     FM_HIP_CHECK(hipStreamWaitEvent(ctx->side, ctx->ev_upd_done, 0));
@@ -735,29 +741,30 @@ int fm_batch_prepare(fm_ctx* ctx, fm_batch* b) {
     const uint32_t* sk = nullptr;
     const uint2* sv = nullptr;
     b->split = fuse_on(ctx);
+    b->split_at_step = false;
     const int kb = bits_for(ctx->rows - 1);
     const uint32_t* col = b->dev.col.as<uint32_t>();
     const uint2* ent = b->dev.ent.as<uint2>();
     if (b->split) {
-      // the fused step's view: the whole sorted view (fkeys / fents); the step counts its runs on
-      // the main stream, the count pass tagging every multi run's row, and the segmented update
-      // walks it skipping the singleton runs (the forward updates those rows).  The runs are counted
-      // at the step: c3 0.924-0.931 ms per step against 0.968-0.971 with a split in this prepare
-      // on the side stream and a tag pass at the step (three alternating reps, profiles/r04_i).
+      // the fused step's view: only the runs of two or more entries (skeys / sents), with
+      // {their count, the number of singleton runs} in split_n -- the bucket sort keeps them as it
+      // orders each bucket; the LSD passes leave the whole view (fkeys / fents) to the step's split
       b->split_n.ensure(2 * sizeof(int64_t));
-      b->fkeys.ensure_slack(sizeof(uint32_t) * N);
-      b->fents.ensure_slack(sizeof(uint2) * N);
-      if (!(bucket_on(ctx, N) && bucket_sort_pairs64(ctx->work.sort, col, ent, N, kb, ctx->side, b->fkeys.as<uint32_t>(),
-                                                     b->fents.as<uint2>(), nullptr)))
+      if (!(bucket_on(ctx, N) && bucket_sort_pairs64(ctx->work.sort, col, ent, N, kb, ctx->side, b->skeys.as<uint32_t>(),
+                                                     b->sents.as<uint2>(), b->split_n.as<int64_t>()))) {
+        b->fkeys.ensure_slack(sizeof(uint32_t) * N);
+        b->fents.ensure_slack(sizeof(uint2) * N);
         radix_sort_pairs64(ctx->work.sort, col, ent, N, kb, ctx->side, &sk, &sv, b->fkeys.as<uint32_t>(),
                            b->fents.as<uint2>());
-      } else {
-      b->skeys.ensure_slack(sizeof(uint32_t) * N);
-      b->sents.ensure_slack(sizeof(uint2) * N);
-      if (!(bucket_on(ctx, N) && bucket_sort_pairs64(ctx->work.sort, col, ent, N, kb, ctx->side, b->skeys.as<uint32_t>(),
-                                                     b->sents.as<uint2>(), nullptr)))
-        radix_sort_pairs64(ctx->work.sort, col, ent, N, kb, ctx->side, &sk, &sv, b->skeys.as<uint32_t>(),
-                           b->sents.as<uint2>());
+        // the step splits this view on the main stream, its count pass tagging the multi rows: c3
+        // 0.924-0.931 ms per step against 0.968-0.971 with the split here on the side stream and a
+        // separate tag pass at the step (three alternating reps, profiles/r04_i)
+        b->split_at_step = true;
+      }
+    } else if (!(bucket_on(ctx, N) && bucket_sort_pairs64(ctx->work.sort, col, ent, N, kb, ctx->side,
+                                                          b->skeys.as<uint32_t>(), b->sents.as<uint2>(), nullptr))) {
+      radix_sort_pairs64(ctx->work.sort, col, ent, N, kb, ctx->side, &sk, &sv, b->skeys.as<uint32_t>(),
+                         b->sents.as<uint2>());
     }
     ctx->prof_end("sort", es, ctx->side);
     FM_HIP_CHECK(hipEventRecord(b->ready, ctx->side));

@@ -105,13 +105,14 @@ struct fm_batch {
   BatchDev dev;
   int64_t max_id = -1;
   DevBuf up;  // device image of the host staging (fm_capi.hip copy_staged)
-  // feature-major view produced by fm_batch_prepare (consumed once by the next step): skeys / sents;
-  // for the fused step (split = true) fkeys / fents, whose runs the step counts into split_n =
-  // {multi entries, singleton runs} on the device (fm_kernels.hip)
+  // feature-major view produced by fm_batch_prepare (consumed once by the next step): the whole
+  // sorted view, or -- split = true -- only the runs of two or more entries, split_n = {their
+  // count, the number of singleton runs} on the device (the fused step, fm_kernels.hip)
   DevBuf skeys, sents;
-  DevBuf fkeys, fents;
+  DevBuf fkeys, fents;  // the LSD-sorted whole view a split pass reduces to the multi view (bucket sort: unused)
   DevBuf split_n;
   bool split = false;
+  bool split_at_step = false;     // the LSD view in fkeys / fents, split (and tagged) by the step
   hipEvent_t ready = nullptr;     // recorded on the side stream after the prepared sort
   hipEvent_t last_use = nullptr;  // recorded on the main stream after a step read the batch
   bool prepared = false;

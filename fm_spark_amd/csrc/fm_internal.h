@@ -195,28 +195,24 @@ struct SegSource {
   int64_t s_stride;
   const float2* yl;
   int64_t yl_stride;
-  // non-null: n_dev[1] singleton rows were updated by the fused forward (added to the distinct
-  // count), and the entries are the multi view, n_dev[0] (device) <= N of them -- or, skip_single,
-  // the whole sorted view (N entries) whose singleton runs the update skips
+  // non-null: the entry count is n_dev[0] (device) <= N, and n_dev[1] singleton rows were updated
+  // by the fused forward (added to the distinct count)
   const int64_t* n_dev = nullptr;
-  bool skip_single = false;
 };
 // emit != nullptr (replicated mode): the per-slot gradient sums go to emit[rows][kp + 4] as
 // [sum g_V (kp) | sum g_w | 1 (touched) | 0] instead of being applied to the table
 void launch_segment_update(const TableView& T, const BatchDev& b, StepWork& w, const StepParams& p,
                            const uint32_t* skeys, const uint2* sents, int64_t n_fwd_blocks,
-                           double* stats_out, hipStream_t st, float* emit = nullptr, const int64_t* n_dev = nullptr,
-                           bool skip_single = false);
-// The singleton split of a sorted view (fm_kernels.hip "Singleton rows"): the entries of runs of two
-// or more, in order, into mkeys / ments (capacity N); n_out[0] = their count, n_out[1] = the number
-// of singleton runs (device).  scatter = false: the counts only (the fused step's update then walks
-// the whole view, skipping the singleton runs); tag_T: the count pass also tags each multi run's row
+                           double* stats_out, hipStream_t st, float* emit = nullptr, const int64_t* n_dev = nullptr);
+// fm_batch_prepare's singleton split of a sorted view (fm_kernels.hip "Singleton rows"): the entries
+// of runs of two or more, in order, into mkeys / ments (capacity N); n_out[0] = their count,
+// n_out[1] = the number of singleton runs (device)
 struct SplitWork {
   DevBuf cnt, off;
 };
 void launch_split(const uint32_t* skeys, const uint2* sents, int64_t N, SplitWork& sw, uint32_t* mkeys, uint2* ments,
                   int64_t* n_out, hipStream_t st,
-                  const TableView* tag_T = nullptr, int32_t epoch = 0, bool scatter = true);
+                  const TableView* tag_T = nullptr, int32_t epoch = 0);
 // the fused sharded owner step: the rows of the received entries' singleton features, pair by pair
 // (pair_ptr [P + 1] over slot / ent, S records of rec floats: S then {r, yhat} at kp)
 void launch_owner_singletons(const TableView& T, const int64_t* pair_ptr, int64_t P, const uint32_t* slot,

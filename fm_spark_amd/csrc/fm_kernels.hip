@@ -502,11 +502,9 @@ struct SegArgs {
   StepParams p;
   uint32_t* ucnt;  // [update blocks]
   float* emit;     // replicated mode: per-slot gradient sums [rows][kp + 4] instead of the update
-  // non-null: n_dev[1] distinct singleton rows were updated by the forward, and the entries are a
-  // multi view of n_dev[0] <= N entries (counted on the device by k_split_*) -- or, skip_single,
-  // the whole sorted view of N entries, whose singleton runs phase 1 drops
+  // non-null: the entry count is n_dev[0] <= N (a prepared batch's multi runs, counted on the
+  // device by k_split_*), and n_dev[1] distinct singleton rows were updated by the forward
   const int64_t* n_dev;
-  bool skip_single;
 };
 
 constexpr uint32_t kFValid = 1u, kFEnd = 2u, kFStart = 4u;
@@ -576,7 +574,7 @@ __global__ __launch_bounds__(kBlock, NF == 1 ? kUpdMinW : 1) void k_segment_upda
   const int kp = T.kp;
   const uint32_t kNone = 0xFFFFFFFFu;
   auto li = [](int e) { return Geo::at(e % RL, e / RL); };
-  const int64_t N = a.n_dev && !a.skip_single ? a.n_dev[0] : a.N;
+  const int64_t N = a.n_dev ? a.n_dev[0] : a.N;
   // logical blocks of 4 waves x 256 entries (one per block of the grid; blocks beyond a device count exit)
   const int64_t nlblk = (N + (int64_t)kWaveEnt * (kBlock / 64) - 1) / ((int64_t)kWaveEnt * (kBlock / 64));
   for (int64_t lblk = blockIdx.x; lblk < nlblk; lblk += gridDim.x) {
@@ -605,11 +603,7 @@ __global__ __launch_bounds__(kBlock, NF == 1 ? kUpdMinW : 1) void k_segment_upda
       const uint32_t nf = i + 1 < NP ? __shfl(key[i + 1 < NP ? i + 1 : i], 0) : after;
       const uint32_t prev = lane == 0 ? pl : up;
       const uint32_t next = lane == 63 ? nf : dn;
-      // skip_single: a run of one entry is a singleton row the fused forward has updated; it leaves
-      // the walk here (no S record or row is loaded for it, and the multi runs keep the wave and
-      // group boundaries of the unfused step)
-      const bool single = a.skip_single && key[i] != kNone && key[i] != prev && key[i] != next;
-      const bool valid = key[i] != kNone && !single;
+      const bool valid = key[i] != kNone;
       const bool st = valid && key[i] != prev;
       const bool end = valid && key[i] != next;
       ucount += (uint32_t)__popcll(__ballot(st));
@@ -943,7 +937,7 @@ __global__ __launch_bounds__(kBlock) void k_segment_combine(SegArgs a, const dou
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int kp = a.T.kp;
   const int64_t W = kp + 2;
-  const int64_t N = a.n_dev && !a.skip_single ? a.n_dev[0] : a.N;
+  const int64_t N = a.n_dev ? a.n_dev[0] : a.N;
   const int64_t nranges = (N + a.L - 1) / a.L;
   __shared__ double run_sum[kBlock / 64][258];  // one long run's summed piece per wave (kp <= 256)
   if (blockIdx.x == 0) {
@@ -1382,12 +1376,11 @@ void launch_forward(const TableView& T, const BatchDev& b, StepWork& w, const St
 
 void launch_segment_update(const TableView& T, const BatchDev& b, StepWork& w, const StepParams& p,
                            const uint32_t* skeys, const uint2* sents, int64_t n_fwd_blocks,
-                           double* stats_out, hipStream_t st, float* emit, const int64_t* n_dev, bool skip_single) {
+                           double* stats_out, hipStream_t st, float* emit, const int64_t* n_dev) {
   SegSource src{w.S.as<float>(), s_rec_floats(T.kp),
                  s_rec_yl(T.kp) ? reinterpret_cast<const float2*>(w.S.as<float>() + T.kp) : w.yl.as<float2>(),
                  s_rec_yl(T.kp) ? s_rec_floats(T.kp) / 2 : 1};
   src.n_dev = n_dev;
-  src.skip_single = skip_single;
   launch_segment_update(T, b.nnz, src, w, p, skeys, sents, n_fwd_blocks, stats_out, st, emit);
 }
 
@@ -1416,7 +1409,6 @@ void launch_segment_update(const TableView& T, int64_t N, const SegSource& src, 
   a.ucnt = w.ucnt.as<uint32_t>();
   a.emit = emit;
   a.n_dev = src.n_dev;
-  a.skip_single = src.n_dev != nullptr && src.skip_single;
   if (ublocks > 0) {
     const dim3 grid((unsigned)ublocks), blk(kBlock);
     const int nq = T.kp / 4;  // column quads
@@ -1856,7 +1848,7 @@ void launch_tag_runs(const TableView& T, const uint32_t* mkeys, const int64_t* n
 }
 
 void launch_split(const uint32_t* skeys, const uint2* sents, int64_t N, SplitWork& sw, uint32_t* mkeys, uint2* ments,
-                  int64_t* n_out, hipStream_t st, const TableView* tag_T, int32_t epoch, bool scatter) {
+                  int64_t* n_out, hipStream_t st, const TableView* tag_T, int32_t epoch) {
   const int64_t nchunks = (N + kSplitChunk - 1) / kSplitChunk;
   sw.cnt.ensure_slack(sizeof(uint2) * (size_t)std::max<int64_t>(nchunks, 1));
   sw.off.ensure_slack(sizeof(int64_t) * (size_t)std::max<int64_t>(nchunks, 1));
@@ -1872,9 +1864,8 @@ void launch_split(const uint32_t* skeys, const uint2* sents, int64_t N, SplitWor
     hipLaunchKernelGGL(k_split_count<false>, dim3(blocks), dim3(kBlock), 0, st, skeys, N, sw.cnt.as<uint2>(), nchunks,
                        TableView{}, 0);
   hipLaunchKernelGGL(k_split_scan, dim3(1), dim3(kSplitScanNT), 0, st, sw.cnt.as<uint2>(), nchunks, sw.off.as<int64_t>(), n_out);
-  if (scatter)
-    hipLaunchKernelGGL(k_split_scatter, dim3(blocks), dim3(kBlock), 0, st, skeys, sents, N, sw.off.as<int64_t>(), nchunks,
-                       mkeys, ments);
+  hipLaunchKernelGGL(k_split_scatter, dim3(blocks), dim3(kBlock), 0, st, skeys, sents, N, sw.off.as<int64_t>(), nchunks,
+                     mkeys, ments);
   FM_HIP_CHECK(hipGetLastError());
 }
 
