@@ -1,7 +1,8 @@
-"""Measurement tool (not product): is the fused step (singleton rows updated by the forward, the
-update walking the whole sorted view without them) bitwise the unfused step?  The cases of
-tests/test_gpu_fuse.py; prints per case whether losses and tables are bitwise equal, and the
-largest relative table difference."""
+"""Measurement tool (not product): is the fused step (singleton rows updated by the forward) bitwise
+the unfused step?  The cases of tests/test_gpu_fuse.py; prints per case whether losses and tables
+are bitwise equal, and the largest relative table difference (round 4: bitwise with the update
+walking the whole sorted view, profiles/r04_j; not with the compacted multi view, whose run pieces
+meet at other wave boundaries)."""
 import json
 import os
 import sys
