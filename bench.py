@@ -164,7 +164,7 @@ def fit_leg(ctx, F, B, zipf_s, lab, iters, parts=16):
     of `iters` x B rows in `parts` partitions is uploaded once (dfData.cache(), SGD.scala:93), split
     by the randomSplit replay into `iters` splits of about B rows (randomSplit normalises the
     weights: each split gets 1/iters of the rows, :111-112), and the loop runs twice: once to grow
-    the two rotating batches' buffers (kept for the second), once timed (host clock around the whole loop, the final sync
+    the three rotating batches' buffers (kept for the second), once timed (host clock around the whole loop, the final sync
     included: the pipeline's fill -- the first split's gather and sort, nothing to overlap -- counts
     against it)."""
     from fm_spark_amd._native import CSRHost
@@ -183,7 +183,7 @@ def fit_leg(ctx, F, B, zipf_s, lab, iters, parts=16):
     data = ctx.batch(CSRHost(ds.row_ptr, ds.col, ds.val, ds.label))
     ctx.sync()
     t_upload = time.perf_counter() - t0
-    bufs = [None, None]  # the two rotating batches, kept across both loops
+    bufs = [None, None, None]  # the three rotating batches, kept across both loops
     run_minibatch_sgd_resident(ctx, data, splits, STEP_SIZE, REG_PARAM, bufs=bufs)  # untimed: buffers grown
     t0 = time.perf_counter()
     losses = run_minibatch_sgd_resident(ctx, data, splits, STEP_SIZE, REG_PARAM, bufs=bufs)

@@ -429,31 +429,36 @@ def run_minibatch_sgd_resident(ctx: FMContext, data, splits, step_size: float, r
                                max_iter: int | None = None, bufs: list | None = None):
     """The foldLeft of runMiniBatchSGD (FactorizationMachinesSGD.scala:114-211) over a dataset kept
     on the device (`data`, dfData.cache() at :93): split i's rows (`splits[i]`, the randomSplit row
-    lists) are gathered there into one of two batches used in turn (fm_batch_from_rows) and sorted
-    on the side stream (fm_batch_prepare) while iteration i - 1 steps; every step only enqueues
+    lists) are gathered there (fm_batch_from_rows, on the copy stream) two iterations ahead into one
+    of three batches used in turn, and sorted on the side stream (fm_batch_prepare) while iteration
+    i - 1 steps, so a sort never waits for its split's copy and gather; every step only enqueues
     (fm_step_batch with out = NULL).  An empty split is skipped with the reference's warning
     (:126-128).  The loss log lines (:134-139) are written in iteration order after the loop, from
     the device's loss history.  Returns the loss sums of the executed iterations.  `bufs`: a list of
-    two batches (or Nones) to refill and leave open for the caller (another loop reuses their
+    three batches (or Nones) to refill and leave open for the caller (another loop reuses their
     device buffers); by default they are made here and closed at the end."""
     n_iter = len(splits) if max_iter is None else max_iter
     work = [(i, rows) for i, rows in enumerate(splits) if len(rows)]
     own = bufs is None
     if own:
-        bufs = [None, None]
+        bufs = [None, None, None]
+    nb = len(bufs)
 
-    def load(j):
-        b = ctx.batch_from_rows(data, work[j][1], into=bufs[j % 2])
-        bufs[j % 2] = b
-        b.prepare()
+    def gather(j):
+        bufs[j % nb] = ctx.batch_from_rows(data, work[j][1], into=bufs[j % nb])
 
     e0 = ctx.epoch
     if work:
-        load(0)
+        gather(0)
+        bufs[0].prepare()
+    if len(work) > 1:
+        gather(1)
     for j, (i, _) in enumerate(work):
-        ctx.step_batch(bufs[j % 2], i + 1, step_size, reg_param, sync=False)  # iter = index + 1 (:119)
+        ctx.step_batch(bufs[j % nb], i + 1, step_size, reg_param, sync=False)  # iter = index + 1 (:119)
         if j + 1 < len(work):
-            load(j + 1)  # gathered and sorted on the side stream while this step runs
+            bufs[(j + 1) % nb].prepare()  # sorted on the side stream while this step runs
+        if j + 2 < len(work):
+            gather(j + 2)  # copied and gathered on the copy stream behind step j - 1
     ctx.sync()
     hist = ctx.loss_history()[e0:]
     done = {i: float(hist[j]) for j, (i, _) in enumerate(work)}

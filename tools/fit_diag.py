@@ -38,7 +38,7 @@ res = {"iters": iters, "rows": [len(s) for s in splits]}
 def loop(sync_each=False, acc=None, bufs=None):
     own = bufs is None
     if own:
-        bufs = [None, None]
+        bufs = [None, None, None]
 
     def timed(name, f):
         t0 = time.perf_counter()
@@ -47,18 +47,23 @@ def loop(sync_each=False, acc=None, bufs=None):
             acc[name] = acc.get(name, 0.0) + time.perf_counter() - t0
         return r
 
-    def load(j):
-        bufs[j % 2] = timed("from_rows", lambda: ctx.batch_from_rows(data, splits[j], into=bufs[j % 2]))
-        timed("prepare", bufs[j % 2].prepare)
+    nb = len(bufs)
+
+    def gather(j):
+        bufs[j % nb] = timed("from_rows", lambda: ctx.batch_from_rows(data, splits[j], into=bufs[j % nb]))
 
     t0 = time.perf_counter()
-    load(0)
+    gather(0)
+    timed("prepare", bufs[0].prepare)
+    gather(1)
     for j in range(iters):
-        timed("step", lambda: ctx.step_batch(bufs[j % 2], j + 1, bench.STEP_SIZE, bench.REG_PARAM, sync=False))
+        timed("step", lambda: ctx.step_batch(bufs[j % nb], j + 1, bench.STEP_SIZE, bench.REG_PARAM, sync=False))
         if sync_each:
             timed("sync", ctx.sync)
         if j + 1 < iters:
-            load(j + 1)
+            timed("prepare", bufs[(j + 1) % nb].prepare)
+        if j + 2 < iters:
+            gather(j + 2)
     timed("sync", ctx.sync)
     dt = time.perf_counter() - t0
     if own:
@@ -67,7 +72,7 @@ def loop(sync_each=False, acc=None, bufs=None):
     return dt
 
 
-keep = [None, None]
+keep = [None, None, None]
 loop(bufs=keep)  # buffers grown
 for rep in range(2):
     acc = {}
