@@ -146,3 +146,20 @@ def test_grouping_rule_follows_the_library():
     assert bench.grouping("lsd", 10_223_616, 100_000_000) == "lsd"
     assert bench.grouping("bucket", 1000, 500) == "lsd"                     # 9-bit keys: one pass does it
     assert bench.grouping("bucket", 20_000_000, 2**31 - 1) == "lsd"         # 31 bits: 21 low bits, too many
+
+
+def test_step_traffic_covers_every_kernel_of_the_default_steps():
+    """The committed PMC files (profiles/pmc_*.json) count every kernel bench.step_kernels says a c3
+    (fused, LSD), c2 and c5 step launches, so the line's step_roofline carries traffic and
+    requests; and the launch map follows the library's arrangement (the fused step's split at the
+    step with its scatter, no separate tag pass)."""
+    import bench
+
+    ps = bench.step_kernels(100_000_000, 10_223_616, "default", True)
+    assert ps["k_radix_scatter"] == 3 and ps["k_split_scatter"] == 1 and "k_tag_runs" not in ps
+    assert bench.step_kernels(1_000_000, 2_555_904, "default", False)["k_radix_count"] == 2
+    for cfg, fused in (("c3", True), ("c2", False), ("c5", False)):
+        F, k, B, _, _ = bench.CONFIGS[cfg]
+        t, r, src = bench.step_traffic(F, k, B, fused, int(39 * B), "default")
+        assert t and r and src, cfg
+        assert 1e8 < t < 1e10 and 1e6 < r < 1e8
