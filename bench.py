@@ -89,8 +89,6 @@ def parse():
                    help="single table, k <= 16: the fused step (the forward updates the rows whose feature has one "
                         "entry in the batch; fm_config.fuse_single): auto = the library's default (tables larger "
                         "than the 256-MB Infinity Cache), on, off")
-    p.add_argument("--main-priority", default="high", choices=["high", "default"],
-                   help="priority of the torch stream the single-table steps run on")
     p.add_argument("--sort", default="default", choices=["default", "lsd", "bucket"],
                    help="how a batch's entries are grouped by feature (fm_config.sort_algo): default = the library's "
                         "choice (the bucket sort for batches of 2^20+ entries), lsd, bucket")
@@ -544,8 +542,7 @@ def main():
         ctx = FMContext(F, k, device=local_rank, seed=20261015, init_sd=INIT_SD,
                         fuse={"auto": None, "on": True, "off": False}[args.fuse], sort=args.sort)
         # launch on a torch stream of our own so torch events can bracket every step on it
-        # the step's stream at high priority, as the library creates its own (fm_capi.hip fm_create)
-        main_stream = torch.cuda.Stream(priority=-1 if args.main_priority == "high" else 0)
+        main_stream = torch.cuda.Stream()
         torch.cuda.set_stream(main_stream)
         ctx.set_stream(main_stream.cuda_stream)
         ctx.init_random_range(0, F)
@@ -646,7 +643,7 @@ def main():
                         fuse={"auto": None, "on": True, "off": False}[args.fuse], sort=args.sort)
         main_stream = None
         if L == 1:  # launch on a torch stream so torch events time each step on it
-            main_stream = torch.cuda.Stream(priority=-1 if args.main_priority == "high" else 0)
+            main_stream = torch.cuda.Stream()
             torch.cuda.set_stream(main_stream)
             ctx.set_stream(main_stream.cuda_stream)
         ctx.init_random_range(0, F)

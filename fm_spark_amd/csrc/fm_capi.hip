@@ -263,11 +263,6 @@ static bool fuse_on(const fm_ctx* ctx) { return ctx->cfg.shard_count == 1 && fus
 // ms per step against 1.16-1.26 unfused: the owner re-reads every received entry's
 // row after the S exchange either way, so the singleton pass saves only the S gathers of its runs,
 // and it adds a pass, the tags and a split to the owner's sort.
-#ifndef FM_STREAM_PRIORITIES
-#define FM_STREAM_PRIORITIES 1
-#endif
-constexpr bool kStreamPriorities = FM_STREAM_PRIORITIES != 0;
-
 bool owner_fuse(const fm_ctx* ctx) { return ctx->cfg.fuse_single == FM_FUSE_ON && ctx->kp <= 16; }
 
 // The bucket sort (fm_sort.hip) for a batch of N entries of this context, or the LSD passes
@@ -488,15 +483,11 @@ int fm_create(const fm_config* cfg, fm_ctx** out) {
     c->cfg = *cfg;
     c->kp = (cfg->k + 3) / 4 * 4;
     c->rows = (cfg->num_features - cfg->shard_index + cfg->shard_count - 1) / cfg->shard_count;
-    // the step's kernels (the critical path) on a high-priority stream, the batch-only work (sorts,
-    // routes) beside them at the lowest: a small kernel of the step (the split's scan, the combine)
-    // gets a CU ahead of the waiting sort blocks
-    int prio_least = 0, prio_greatest = 0;
-    FM_HIP_CHECK(hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest));
-    if (!kStreamPriorities) prio_least = prio_greatest = 0;
-    FM_HIP_CHECK(hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, prio_greatest));
+    // (the step's stream at high priority and the side stream at the lowest measured slower: c3
+    // 0.984-0.996 against 0.946-0.951 ms)
+    FM_HIP_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     c->own_stream = true;
-    FM_HIP_CHECK(hipStreamCreateWithPriority(&c->side_own, hipStreamNonBlocking, prio_least));
+    FM_HIP_CHECK(hipStreamCreateWithFlags(&c->side_own, hipStreamNonBlocking));
     c->side = c->side_own;
     FM_HIP_CHECK(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
     FM_HIP_CHECK(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));

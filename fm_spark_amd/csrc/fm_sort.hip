@@ -45,10 +45,6 @@ constexpr int kMaxRadix = 1 << kMaxRB;
 // the bucket sort's top-bit pass at most (an 11-bit scatter on 1024-thread blocks outgrows the LDS)
 constexpr int kBktMaxH = kBlock >= 1024 ? 10 : kMaxRB;
 constexpr int kChunk = 16;   // tiles per chunk of the count scan
-#ifndef FM_COUNT_CHUNK
-#define FM_COUNT_CHUNK 1
-#endif
-constexpr bool kCountChunk = FM_COUNT_CHUNK != 0;  // count + level-1 scan in one kernel
 
 // Tile of a block: the tiles of one XCD (blocks b = x mod 8 are dispatched to XCD x) are
 // contiguous, so a digit's runs written by neighbouring tiles meet in the same L2 and leave it as
@@ -177,80 +173,6 @@ __global__ __launch_bounds__(kBlock) void k_radix_chunk_scan(uint32_t* __restric
   }
 #pragma unroll
   for (int i = 0; i < D; ++i) csum[(int64_t)blockIdx.x * R + threadIdx.x + i * kBlock] = run[i];
-}
-
-// Count and level-1 scan in one pass: block c takes tiles [16 c, 16 c + 16) in order, histograms
-// each in LDS (the next tile's keys already loading) and writes its counts as the digit's exclusive
-// prefix within the chunk; the chunk's sums -> csum[c][digit].  BIG: over the device's tile count
-// plus one empty tile past the end.
-template <int RB, bool BIG = false>
-__global__ __launch_bounds__(kBlock) void k_radix_count_chunk(const uint32_t* __restrict__ keys, int64_t n, int shift,
-                                                              uint32_t* __restrict__ counts, int64_t ntiles,
-                                                              uint32_t* __restrict__ csum, BigPlan bp) {
-  constexpr int R = 1 << RB;
-  constexpr uint32_t M = R - 1;
-  constexpr int D = digits_per_thread<R>();
-  constexpr int KT = kTile / kBlock;  // keys per thread per tile
-  __shared__ uint32_t hist[R];
-  const int64_t nt = BIG ? (int64_t)bp.meta[1] : ntiles;
-  const int64_t ext = nt + (BIG ? 1 : 0);
-  const int64_t t0 = (int64_t)blockIdx.x * kChunk;
-  if (t0 >= ext) return;  // block-uniform
-  const int tid = threadIdx.x;
-  // keys of tile t into registers; lim: the tile's key count (0 for the empty tile past the end)
-  auto load = [&](int64_t t, uint32_t (&k)[KT], int& lim) {
-    int64_t base = 0, end = 0;
-    if (t < nt) {
-      if constexpr (BIG) {
-        const uint4 sg = bp.seg[bp.tseg[t]];
-        base = (int64_t)sg.x + (t - (int64_t)sg.z) * kTile;
-        end = (int64_t)sg.x + sg.y;
-      } else {
-        base = t * kTile;
-        end = n;
-      }
-    }
-    lim = (int)min((int64_t)kTile, end - base);
-#pragma unroll
-    for (int i = 0; i < KT; ++i) {
-      const int64_t idx = base + (int64_t)i * kBlock + tid;
-      k[i] = idx < end ? keys[idx] : 0u;
-    }
-  };
-  uint32_t cur[KT], nxt[KT];
-  int lim_cur = 0, lim_nxt = 0;
-  load(t0, cur, lim_cur);
-  uint32_t run[D];
-#pragma unroll
-  for (int i = 0; i < D; ++i) run[i] = 0;
-  for (int j = 0; j < kChunk; ++j) {
-    const int64_t t = t0 + j;
-    if (t >= ext) break;  // block-uniform
-    if (j + 1 < kChunk && t + 1 < ext) load(t + 1, nxt, lim_nxt);
-    for (int d = tid; d < R; d += kBlock) hist[d] = 0;
-    lds_barrier();
-#pragma unroll
-    for (int i = 0; i < KT; ++i)
-      if (i * kBlock + tid < lim_cur) atomicAdd(&hist[(cur[i] >> shift) & M], 1u);
-    lds_barrier();
-#pragma unroll
-    for (int i = 0; i < D; ++i) {
-      const int d = tid + i * kBlock;
-      if (d < R) {
-        counts[t * R + d] = run[i];
-        run[i] += hist[d];
-      }
-    }
-    lds_barrier();  // hist is cleared for the next tile
-#pragma unroll
-    for (int i = 0; i < KT; ++i) cur[i] = nxt[i];
-    lim_cur = lim_nxt;
-  }
-#pragma unroll
-  for (int i = 0; i < D; ++i) {
-    const int d = tid + i * kBlock;
-    if (d < R) csum[(int64_t)blockIdx.x * R + d] = run[i];
-  }
 }
 
 // The count scan, level 2: 32 digits per 256-thread block (a small block finds room on a CU beside
@@ -926,15 +848,12 @@ static void radix_pass_impl(const uint32_t* kin, const P* vin, uint32_t* ko, P* 
   uint32_t* counts = w.counts.as<uint32_t>();
   uint32_t* csum = counts + (ntiles + 1) * (int64_t(1) << RB);
   const int64_t nchunks = (ntiles + kChunk - 1) / kChunk;
-  if (kCountChunk) {
-    hipLaunchKernelGGL((k_radix_count_chunk<RB, false>), dim3((unsigned)nchunks), dim3(kBlock), 0, st, kin, n, shift,
-                       counts, ntiles, csum, none);
-  } else {
-    hipLaunchKernelGGL(k_radix_count<RB>, dim3((unsigned)blocks_for_tiles(ntiles)), dim3(kBlock), 0, st, kin, n, shift,
-                       counts, ntiles, none);
-    hipLaunchKernelGGL((k_radix_chunk_scan<RB, false>), dim3((unsigned)nchunks), dim3(kBlock), 0, st, counts, ntiles,
-                       csum, none);
-  }
+  // (count and chunk scan fused into one kernel, a block walking its chunk's 16 tiles, measured
+  // slower: 0.349 against 0.317 ms standalone)
+  hipLaunchKernelGGL(k_radix_count<RB>, dim3((unsigned)blocks_for_tiles(ntiles)), dim3(kBlock), 0, st, kin, n, shift,
+                     counts, ntiles, none);
+  hipLaunchKernelGGL((k_radix_chunk_scan<RB, false>), dim3((unsigned)nchunks), dim3(kBlock), 0, st, counts, ntiles, csum,
+                     none);
   hipLaunchKernelGGL(k_radix_chunk_top<false>, dim3((1u << RB) / 32), dim3(256), 0, st, csum, nchunks, 1 << RB,
                      w.digit_tot.as<uint32_t>(), none);
   hipLaunchKernelGGL((k_radix_scatter<P, RB>), dim3((unsigned)blocks_for_tiles(ntiles)), dim3(kBlock), 0, st, kin,
@@ -1038,14 +957,9 @@ static void big_pass(const uint32_t* sk, const uint2* sv, uint32_t* dk, uint2* d
   uint32_t* csum = counts + (big_tiles + 1) * (int64_t(1) << RB);
   const unsigned gb = (unsigned)blocks_for_tiles(big_tiles);
   const unsigned gc = (unsigned)((big_tiles + 1 + kChunk - 1) / kChunk);
-  if (kCountChunk) {
-    hipLaunchKernelGGL((k_radix_count_chunk<RB, true>), dim3(gc), dim3(kBlock), 0, st, sk, (int64_t)0, shift, counts,
-                       (int64_t)0, csum, bp);
-  } else {
-    hipLaunchKernelGGL((k_radix_count<RB, true>), dim3(gb), dim3(kBlock), 0, st, sk, (int64_t)0, shift, counts,
-                       (int64_t)0, bp);
-    hipLaunchKernelGGL((k_radix_chunk_scan<RB, true>), dim3(gc), dim3(kBlock), 0, st, counts, (int64_t)0, csum, bp);
-  }
+  hipLaunchKernelGGL((k_radix_count<RB, true>), dim3(gb), dim3(kBlock), 0, st, sk, (int64_t)0, shift, counts, (int64_t)0,
+                     bp);
+  hipLaunchKernelGGL((k_radix_chunk_scan<RB, true>), dim3(gc), dim3(kBlock), 0, st, counts, (int64_t)0, csum, bp);
   hipLaunchKernelGGL(k_radix_chunk_top<true>, dim3((1u << RB) / 32), dim3(256), 0, st, csum, (int64_t)0, 1 << RB,
                      (uint32_t*)nullptr, bp);
   hipLaunchKernelGGL((k_radix_scatter<uint2, RB, true>), dim3(gb), dim3(kBlock), 0, st, sk, sv, dk, dv, (int64_t)0,

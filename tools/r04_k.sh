@@ -32,6 +32,4 @@ timeout -k 10 400 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --host
 echo "c3 $(grep -o '"ms_per_step": [0-9.]*' $out/bench_c3.log | head -1) $(grep -o '"fit_ms_per_iter": [0-9.]*' $out/bench_c3.log | head -1)" >&2
 timeout -k 10 400 python -u tools/shard_sim_bench.py --ranks 8 > $out/sim8.log 2>&1 || exit $?
 tail -12 $out/sim8.log >&2
-timeout -k 10 600 python -u tools/c4_rank_bench.py --iters 5 > $out/c4_bench.log 2>&1 || exit $?
-tail -6 $out/c4_bench.log >&2
 exit 0

@@ -6,12 +6,14 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 out=gpurun_out/${1:-r04_l}; mkdir -p $out
-timeout -k 10 600 python -u -m pytest tests/test_gpu_fuse.py tests/test_gpu_parity.py tests/test_gpu_resident_fit.py \
-    -x -v --timeout 300 --timeout-method thread > $out/pytest.log 2>&1
-rc=$?; tail -1 $out/pytest.log >&2; [ $rc -ne 0 ] && exit $rc
+if [ "${TESTS:-1}" = "1" ]; then
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_fuse.py tests/test_gpu_parity.py tests/test_gpu_resident_fit.py \
+      -x -v --timeout 300 --timeout-method thread > $out/pytest.log 2>&1
+  rc=$?; tail -1 $out/pytest.log >&2; [ $rc -ne 0 ] && exit $rc
+fi
 B="--steps 20 --warmup 5 --no-cpu-baseline --host-path-steps 0 --fit-iters 0"
-for rep in 1 2 3; do
-  for c in c3 c2 c5 sh1; do
+for rep in ${REPS:-1 2 3}; do
+  for c in ${CONFIGS:-c3 c2 c5 sh1}; do
     for v in tree nopri; do
       lib=""; pr=high; [ $v != tree ] && lib=tools/_variants/$v/libfm_hip.so && pr=default
       a="--config $c"; [ $c = sh1 ] && a="--config c3 --force-sharded"
