@@ -96,7 +96,7 @@ def parse():
                    help="N > 1: 'lib' = the multi-GPU fm_ctx, every exchange inside libfm_hip over RCCL (the "
                         "C-ABI path); 'torch' (torch.distributed.run only) = the torch.distributed test harness "
                         "(fm_spark_amd/distributed.py) driving the fm_shard_* phases")
-    p.add_argument("--fit-iters", type=int, default=8,
+    p.add_argument("--fit-iters", type=int, default=16,
                    help="N = 1: after the timed region, run the estimator's resident mini-batch loop "
                         "(fm_spark_amd.ml.run_minibatch_sgd_resident, what FactorizationMachinesSGD.fit runs after its "
                         "randomSplit replay) over a resident synthetic dataset of this many batches' rows, split by "
@@ -183,8 +183,12 @@ def fit_leg(ctx, F, B, zipf_s, lab, iters, parts=16):
     data = ctx.batch(CSRHost(ds.row_ptr, ds.col, ds.val, ds.label))
     ctx.sync()
     t_upload = time.perf_counter() - t0
-    bufs = [None, None, None]  # the three rotating batches, kept across both loops
+    bufs = [None, None, None]  # the three rotating batches, kept across the loops
     run_minibatch_sgd_resident(ctx, data, splits, STEP_SIZE, REG_PARAM, bufs=bufs)  # untimed: buffers grown
+    half = iters // 2
+    t0 = time.perf_counter()
+    run_minibatch_sgd_resident(ctx, data, splits[:half], STEP_SIZE, REG_PARAM, bufs=bufs)
+    dt_half = time.perf_counter() - t0
     t0 = time.perf_counter()
     losses = run_minibatch_sgd_resident(ctx, data, splits, STEP_SIZE, REG_PARAM, bufs=bufs)
     dt = time.perf_counter() - t0
@@ -193,12 +197,15 @@ def fit_leg(ctx, F, B, zipf_s, lab, iters, parts=16):
     data.close()
     rows = [len(r) for r in splits]
     return {"fit_ms_per_iter": 1e3 * dt / iters, "iterations": iters, "rows_per_iter_mean": float(np.mean(rows)),
+            "fit_ms_per_iter_steady": 1e3 * (dt - dt_half) / (iters - half) if iters > half else None,
             "samples_per_s": float(np.sum(rows)) / dt, "dataset_rows": n, "partitions": parts,
             "finite_losses": bool(np.all(np.isfinite(losses))),
             "setup_s": {"generate_and_split": t_split, "upload_once": t_upload},
             "what": "FactorizationMachinesSGD.fit's mini-batch loop on the resident dataset: each randomSplit split "
-                    "gathered on the device from its row list (fm_batch_from_rows) and sorted on the side stream "
-                    "while the previous split steps; host clock over the whole loop incl. the pipeline fill"}
+                    "gathered on the device from its row list (fm_batch_from_rows) two iterations ahead and sorted on "
+                    "the side stream while the previous split steps; host clock over the whole loop incl. the pipeline "
+                    "fill (fit_ms_per_iter), and the loop over all splits minus the loop over the first half, per "
+                    "iteration (fit_ms_per_iter_steady: the fill cancels)"}
 
 
 def log(msg):
@@ -883,6 +890,8 @@ def main():
         if fit:
             line["fit_ms_per_iter"] = fit["fit_ms_per_iter"]
             fit["vs_step"] = fit["fit_ms_per_iter"] / ms_per_step
+            if fit.get("fit_ms_per_iter_steady"):
+                fit["steady_vs_step"] = fit["fit_ms_per_iter_steady"] / ms_per_step
             line["fit"] = fit
         if not args.no_cpu_baseline and world == 1:  # the CPU baseline belongs to the N = 1 line
             try:
