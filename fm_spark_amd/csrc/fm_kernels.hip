@@ -38,6 +38,7 @@ namespace {
 constexpr int kBlock = 256;
 constexpr int kWaveEnt = 256;  // sorted entries per update wave
 constexpr int kUpdD = 2;   // entries whose rows a lane group loads per step
+// (two entries ahead at k = 5..8 or 13..16 measured slower at c2 / c5 / c3: profiles/r04_o)
 constexpr int kUpdD4 = 1;  // k = 13..16 (4 lanes per entry, paired row stores): one entry ahead keeps the
                            // kernel within the 5-wave register budget
 constexpr int kUpdD2 = 1;  // k = 5..8 (2 lanes per entry, paired row stores)
@@ -97,6 +98,10 @@ constexpr int kPartialU = 4;  // sharded partial pass: passes (entries per lane)
 // same 16 rows in flight per sample at k = 16 as 16 lanes x 4 passes, with fewer registers per
 // lane (measured 1.196 against 1.213 ms per c3 step, 5 runs each on two boxes)
 constexpr int kFwdTeam = 32, kFwdU = 2;
+// k <= 8 (one or two lanes per row): 3 passes in flight, 96 rows per team-sample round -- c2 0.171 /
+// 0.173 against 0.175 / 0.174 ms per step (median 0.162 against 0.165), at c5 (k = 16) slower
+// (profiles/r04_o)
+constexpr int kFwdUNarrow = 3;
 constexpr int kFwdGrid = 2048;  // forward blocks at most (grid-stride over samples beyond)
 // the fused forward (kTrainFused): 3 passes in flight (24 rows per sample at k = 16, so a 39-entry
 // sample takes two rounds instead of three); c3 step -2 to -4 % against 2 passes, 4 passes slower
@@ -1363,8 +1368,8 @@ void launch_forward(const TableView& T, const BatchDev& b, StepWork& w, const St
     return;
   }
   constexpr int TM = kFwdTeam, TU = kFwdU;
-  if (nq <= 1) launch_fwd_t<1, TM, TU>(T, b, w, p, st, nblk, partial_out, pred);
-  else if (nq <= 2) launch_fwd_t<2, TM, TU>(T, b, w, p, st, nblk, partial_out, pred);
+  if (nq <= 1) launch_fwd_t<1, TM, kFwdUNarrow>(T, b, w, p, st, nblk, partial_out, pred);
+  else if (nq <= 2) launch_fwd_t<2, TM, kFwdUNarrow>(T, b, w, p, st, nblk, partial_out, pred);
   else if (nq <= 4) launch_fwd_t<4, (TM < 4 ? 4 : TM), TU>(T, b, w, p, st, nblk, partial_out, pred);
   else if (nq <= 8) launch_fwd_t<8, (TM < 8 ? 8 : TM), TU>(T, b, w, p, st, nblk, partial_out, pred);
   else if (nq <= 16) launch_fwd_t<16, (TM < 16 ? 16 : TM), TU>(T, b, w, p, st, nblk, partial_out, pred);
