@@ -51,6 +51,10 @@ void DevBuf::release() {
 // A persistent pool of host threads (up to 16: the GPU box's CPU share per GPU) for the host passes
 // of fm_step's upload and fm_batch_from_rows: spawning the threads per call cost about as much as
 // the work.  One job at a time (callers serialise on run_mu); the calling thread works too.
+#ifndef FM_HOST_THREADS
+#define FM_HOST_THREADS 16
+#endif
+constexpr int kHostThreadsMax = FM_HOST_THREADS;
 class HostPool {
  public:
   static HostPool& get() {
@@ -92,7 +96,7 @@ class HostPool {
  private:
   HostPool() {
     const int hw = std::max(1, (int)std::thread::hardware_concurrency());
-    const int T = std::min(16, hw);
+    const int T = std::min(kHostThreadsMax, hw);
     for (int t = 1; t < T; ++t) workers_.emplace_back([this] { loop(); });
   }
   void work() {
