@@ -1585,53 +1585,32 @@ __global__ __launch_bounds__(kBlock) void k_explode(const int64_t* __restrict__ 
 }
 
 // fm_batch_from_rows: output row s is row rows[s] of a resident dataset (the randomSplit split of
-// the cached dfData, FactorizationMachinesSGD.scala:93, 111-112).  A block takes kSelRows output
-// rows: their output and source offsets in LDS, then its threads walk the rows' entries as one flat
-// range (each entry's row by a binary search in LDS), so every lane copies an entry and the writes
-// of col, x and the exploded {s, x} entries are coalesced across the block; row_ptr (computed by the
-// host from the dataset's row_ptr) and the labels are written alongside.  (A 16-lane team per row
-// took 103 us at c3: 39-entry rows leave a fifth of its lanes idle.)
-constexpr int kSelRows = 64;
+// the cached dfData, FactorizationMachinesSGD.scala:93, 111-112).  One team of 16 lanes per output
+// row copies the source row's ids and fp32 x (8 B per entry, contiguous) and writes the exploded
+// {s, x} entries; row_ptr (computed by the host from the dataset's row_ptr) and the labels are
+// written alongside (grid-stride, the same pass).
 __global__ __launch_bounds__(kBlock) void k_select_rows(const int64_t* __restrict__ src_rp, const uint32_t* __restrict__ src_col,
                                                        const float* __restrict__ src_xs, const double* __restrict__ src_lab,
                                                        const int64_t* __restrict__ rows, const int64_t* __restrict__ rp_in,
                                                        int64_t B, int64_t* __restrict__ rp, double* __restrict__ lab,
                                                        uint32_t* __restrict__ col, uint2* __restrict__ ent,
                                                        float* __restrict__ xs) {
-  __shared__ int64_t s_out[kSelRows + 1];  // output offset of each row, then the block's end
-  __shared__ int64_t s_src[kSelRows];      // source offset of each row
-  const int64_t r0 = (int64_t)blockIdx.x * kSelRows;
-  const int nr = (int)min((int64_t)kSelRows, B - r0);
-  const int tid = threadIdx.x;
-  if (tid < nr) {
-    const int64_t s = r0 + tid, r = rows[s];
-    const int64_t o = rp_in[s];
-    s_out[tid] = o;
-    s_src[tid] = src_rp[r];
-    rp[s] = o;
-    lab[s] = src_lab[r];
-  }
-  if (tid == 0) {
-    s_out[nr] = rp_in[r0 + nr];
-    if (r0 + nr == B) rp[B] = rp_in[B];
-  }
-  __syncthreads();
-  const int64_t e0 = s_out[0], e1 = s_out[nr];
-  for (int64_t e = e0 + tid; e < e1; e += kBlock) {
-    int lo = 0, hi = nr - 1;  // the last row starting at or before e (empty rows skipped)
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (s_out[mid] <= e)
-        lo = mid;
-      else
-        hi = mid - 1;
+  constexpr int T = 16;
+  const int tl = threadIdx.x % T;
+  const int64_t gtid = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int64_t nthreads = (int64_t)gridDim.x * kBlock;
+  for (int64_t i = gtid; i <= B; i += nthreads) rp[i] = rp_in[i];
+  for (int64_t i = gtid; i < B; i += nthreads) lab[i] = src_lab[rows[i]];
+  for (int64_t s = gtid / T; s < B; s += nthreads / T) {
+    const int64_t e0 = rp_in[s], e1 = rp_in[s + 1];
+    const int64_t d = src_rp[rows[s]] - e0;  // source entry of output entry e: e + d
+    for (int64_t e = e0 + tl; e < e1; e += T) {
+      const uint32_t c = src_col[e + d];
+      const float x = src_xs[e + d];
+      col[e] = c;
+      xs[e] = x;
+      ent[e] = make_uint2((uint32_t)s, __float_as_uint(x));
     }
-    const int64_t src = s_src[lo] + (e - s_out[lo]);
-    const uint32_t c = src_col[src];
-    const float x = src_xs[src];
-    col[e] = c;
-    xs[e] = x;
-    ent[e] = make_uint2((uint32_t)(r0 + lo), __float_as_uint(x));
   }
 }
 
@@ -1907,11 +1886,7 @@ void launch_explode(const int64_t* row_ptr_in, const double* label_in, const int
 
 void launch_select_rows(const BatchDev& src, const int64_t* rows, const int64_t* row_ptr_in, int64_t B, BatchDev& dst,
                         hipStream_t st) {
-  if (B <= 0) {  // the row_ptr of an empty selection (its one entry, 0)
-    FM_HIP_CHECK(hipMemcpyAsync(dst.row_ptr.p, row_ptr_in, sizeof(int64_t), hipMemcpyDeviceToDevice, st));
-    return;
-  }
-  hipLaunchKernelGGL(k_select_rows, dim3((unsigned)((B + kSelRows - 1) / kSelRows)), dim3(kBlock), 0, st,
+  hipLaunchKernelGGL(k_select_rows, dim3(grid_for(std::max<int64_t>(B, 1) * 16, kBlock, 256 * 8)), dim3(kBlock), 0, st,
                      src.row_ptr.as<int64_t>(), src.col.as<uint32_t>(), src.xs.as<float>(), src.label.as<double>(), rows,
                      row_ptr_in, B, dst.row_ptr.as<int64_t>(), dst.label.as<double>(), dst.col.as<uint32_t>(),
                      dst.ent.as<uint2>(), dst.xs.as<float>());
