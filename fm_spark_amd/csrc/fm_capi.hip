@@ -51,10 +51,8 @@ void DevBuf::release() {
 // A persistent pool of host threads (up to 16: the GPU box's CPU share per GPU) for the host passes
 // of fm_step's upload and fm_batch_from_rows: spawning the threads per call cost about as much as
 // the work.  One job at a time (callers serialise on run_mu); the calling thread works too.
-#ifndef FM_HOST_THREADS
-#define FM_HOST_THREADS 16
-#endif
-constexpr int kHostThreadsMax = FM_HOST_THREADS;
+// at most 16 threads (the GPU box's CPU share per GPU; 8 measured the same in the fit loop)
+constexpr int kHostThreadsMax = 16;
 class HostPool {
  public:
   static HostPool& get() {
