@@ -265,11 +265,6 @@ static bool fuse_on(const fm_ctx* ctx) { return ctx->cfg.shard_count == 1 && fus
 // ms per step against 1.16-1.26 unfused: the owner re-reads every received entry's
 // row after the S exchange either way, so the singleton pass saves only the S gathers of its runs,
 // and it adds a pass, the tags and a split to the owner's sort.
-#ifndef FM_SPLIT_AUX
-#define FM_SPLIT_AUX 1
-#endif
-constexpr bool kSplitAux = FM_SPLIT_AUX != 0;
-
 bool owner_fuse(const fm_ctx* ctx) { return ctx->cfg.fuse_single == FM_FUSE_ON && ctx->kp <= 16; }
 
 // The bucket sort (fm_sort.hip) for a batch of N entries of this context, or the LSD passes
@@ -423,17 +418,8 @@ int step_impl(fm_ctx* ctx, fm_batch* b, int32_t t, double step_size, double reg_
     // by a pass over it
     e0 = ctx->prof_begin(ctx->stream);
     if (b->split_at_step) {
-      // the count pass (tags) on the main stream; its scan and scatter -- the multi view, read by the
-      // update only -- on aux beside the forward
-      if (kSplitAux && !ctx->aux) {
-        FM_HIP_CHECK(hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking));
-        FM_HIP_CHECK(hipEventCreateWithFlags(&ctx->ev_counted, hipEventDisableTiming));
-        FM_HIP_CHECK(hipEventCreateWithFlags(&ctx->ev_split, hipEventDisableTiming));
-      }
       launch_split(b->fkeys.as<uint32_t>(), b->fents.as<uint2>(), N, ctx->split_work, b->skeys.as<uint32_t>(),
-                   b->sents.as<uint2>(), b->split_n.as<int64_t>(), ctx->stream, &T, p.epoch,
-                   kSplitAux ? ctx->aux : nullptr, ctx->ev_counted);
-      if (kSplitAux) FM_HIP_CHECK(hipEventRecord(ctx->ev_split, ctx->aux));
+                   b->sents.as<uint2>(), b->split_n.as<int64_t>(), ctx->stream, &T, p.epoch);
       ctx->prof_end("split", e0, ctx->stream);
     } else {
       launch_tag_runs(T, b->skeys.as<uint32_t>(), b->split_n.as<int64_t>(), N, p.epoch, ctx->stream);
@@ -445,7 +431,6 @@ int step_impl(fm_ctx* ctx, fm_batch* b, int32_t t, double step_size, double reg_
   launch_forward(T, b->dev, ctx->work, p, ctx->stream, &nfwd, nullptr, fused ? &fx : nullptr);
   ctx->prof_end("forward", e0, ctx->stream);
   if (!fused) FM_HIP_CHECK(hipStreamWaitEvent(ctx->stream, prepared ? b->ready : ctx->ev_join, 0));
-  if (fused && kSplitAux && b->split_at_step) FM_HIP_CHECK(hipStreamWaitEvent(ctx->stream, ctx->ev_split, 0));
   e0 = ctx->prof_begin(ctx->stream);
   double* stats = ctx->loss_hist.as<double>() + 3 * (int64_t)ctx->epoch;
   launch_segment_update(T, b->dev, ctx->work, p, skeys, sents, nfwd, stats, ctx->stream, emit,

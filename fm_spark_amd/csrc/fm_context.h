@@ -159,10 +159,6 @@ struct fm_ctx {
   hipStream_t side_own = nullptr;  // the context's own side stream (fm_set_side_stream may replace side)
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   hipEvent_t ev_upd_done = nullptr;  // last main-stream read of the shared sort workspace (an inline-sorted step)
-  // the fused step's split: its scan and scatter (the multi view only the update reads) on aux,
-  // beside the forward, once the count pass (the tags the forward reads) is done
-  hipStream_t aux = nullptr;
-  hipEvent_t ev_counted = nullptr, ev_split = nullptr;
   DevBuf rec;  // [rows * stride] float records (V row + header)
   int32_t stride = 0;
   std::vector<double> cum_host{0.0};  // cum[e] = sum of lambda over executed steps 1..e
@@ -288,10 +284,6 @@ struct fm_ctx {
     }
     for (auto e : free_events) (void)hipEventDestroy(e);
     if (side) (void)hipStreamSynchronize(side);
-    if (aux) (void)hipStreamSynchronize(aux);
-    if (aux) (void)hipStreamDestroy(aux);
-    if (ev_counted) (void)hipEventDestroy(ev_counted);
-    if (ev_split) (void)hipEventDestroy(ev_split);
     if (ev_fork) (void)hipEventDestroy(ev_fork);
     if (ev_join) (void)hipEventDestroy(ev_join);
     if (ev_upd_done) (void)hipEventDestroy(ev_upd_done);

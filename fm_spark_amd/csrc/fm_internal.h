@@ -210,11 +210,9 @@ void launch_segment_update(const TableView& T, const BatchDev& b, StepWork& w, c
 struct SplitWork {
   DevBuf cnt, off;
 };
-// st2 / ev: the scan and scatter on stream st2, after ev (recorded on st behind the count pass)
 void launch_split(const uint32_t* skeys, const uint2* sents, int64_t N, SplitWork& sw, uint32_t* mkeys, uint2* ments,
                   int64_t* n_out, hipStream_t st,
-                  const TableView* tag_T = nullptr, int32_t epoch = 0, hipStream_t st2 = nullptr,
-                  hipEvent_t ev = nullptr);
+                  const TableView* tag_T = nullptr, int32_t epoch = 0);
 // the fused sharded owner step: the rows of the received entries' singleton features, pair by pair
 // (pair_ptr [P + 1] over slot / ent, S records of rec floats: S then {r, yhat} at kp)
 void launch_owner_singletons(const TableView& T, const int64_t* pair_ptr, int64_t P, const uint32_t* slot,

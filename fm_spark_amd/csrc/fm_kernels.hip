@@ -1853,17 +1853,12 @@ void launch_tag_runs(const TableView& T, const uint32_t* mkeys, const int64_t* n
 }
 
 void launch_split(const uint32_t* skeys, const uint2* sents, int64_t N, SplitWork& sw, uint32_t* mkeys, uint2* ments,
-                  int64_t* n_out, hipStream_t st, const TableView* tag_T, int32_t epoch, hipStream_t st2,
-                  hipEvent_t ev) {
+                  int64_t* n_out, hipStream_t st, const TableView* tag_T, int32_t epoch) {
   const int64_t nchunks = (N + kSplitChunk - 1) / kSplitChunk;
   sw.cnt.ensure_slack(sizeof(uint2) * (size_t)std::max<int64_t>(nchunks, 1));
   sw.off.ensure_slack(sizeof(int64_t) * (size_t)std::max<int64_t>(nchunks, 1));
   if (N <= 0) {
     FM_HIP_CHECK(hipMemsetAsync(n_out, 0, 2 * sizeof(int64_t), st));
-    if (st2) {
-      FM_HIP_CHECK(hipEventRecord(ev, st));
-      FM_HIP_CHECK(hipStreamWaitEvent(st2, ev, 0));
-    }
     return;
   }
   const unsigned blocks = (unsigned)((nchunks + kBlock / 64 - 1) / (kBlock / 64));
@@ -1873,11 +1868,6 @@ void launch_split(const uint32_t* skeys, const uint2* sents, int64_t N, SplitWor
   else
     hipLaunchKernelGGL(k_split_count<false>, dim3(blocks), dim3(kBlock), 0, st, skeys, N, sw.cnt.as<uint2>(), nchunks,
                        TableView{}, 0);
-  if (st2) {
-    FM_HIP_CHECK(hipEventRecord(ev, st));
-    FM_HIP_CHECK(hipStreamWaitEvent(st2, ev, 0));
-    st = st2;
-  }
   hipLaunchKernelGGL(k_split_scan, dim3(1), dim3(kSplitScanNT), 0, st, sw.cnt.as<uint2>(), nchunks, sw.off.as<int64_t>(), n_out);
   hipLaunchKernelGGL(k_split_scatter, dim3(blocks), dim3(kBlock), 0, st, skeys, sents, N, sw.off.as<int64_t>(), nchunks,
                      mkeys, ments);
