@@ -71,3 +71,72 @@ def test_select_csr_gathers_rows_in_order():
     assert c.label.tolist() == [1.0, 1.0, 0.0, 0.0, 0.0]
     e = _select_csr(rp, col, val, lab, [])
     assert e.row_ptr.tolist() == [0] and e.n_rows == 0 and e.nnz == 0
+
+
+def test_resident_loop_orders_gather_prepare_step_per_buffer(caplog):
+    """run_minibatch_sgd_resident's host schedule on a recording context: every split is gathered,
+    then prepared, then stepped, in iteration order; a batch is regathered only after the step
+    that read it was enqueued; empty splits are skipped with the reference's warning
+    (FactorizationMachinesSGD.scala:126-128) and the losses come back in iteration order."""
+    import logging
+
+    from fm_spark_amd.ml import run_minibatch_sgd_resident
+
+    events = []
+
+    class Batch:
+        def __init__(self, n):
+            self.id, self.open = n, True
+
+        def prepare(self):
+            events.append(("prepare", self.id, self.rows))
+
+        def close(self):
+            self.open = False
+
+    class Ctx:
+        epoch = 7
+        made = []
+
+        def batch_from_rows(self, data, rows, into=None):
+            b = into if into is not None else Batch(len(self.made))
+            if into is None:
+                self.made.append(b)
+            b.rows = tuple(rows)
+            events.append(("gather", b.id, b.rows))
+            return b
+
+        def step_batch(self, b, it, step, reg, sync=True):
+            assert sync is False
+            events.append(("step", b.id, b.rows, it))
+
+        def sync(self):
+            events.append(("sync",))
+
+        def loss_history(self):
+            return [None] * 7 + [10.0 * (j + 1) for j in range(64)]
+
+    splits = [[0, 1], [], [2], [3, 4, 5], [6], [], [7, 8], [9]]
+    ctx = Ctx()
+    with caplog.at_level(logging.WARNING):
+        out = run_minibatch_sgd_resident(ctx, None, splits, 1.0, 0.0)
+    work = [(i, tuple(r)) for i, r in enumerate(splits) if r]
+    assert out == [10.0 * (j + 1) for j in range(len(work))]
+    assert len(ctx.made) == 3 and not any(b.open for b in ctx.made)
+    assert sum("size of sampled batch is zero" in r.getMessage() for r in caplog.records) == 2
+    steps = [e for e in events if e[0] == "step"]
+    assert [(e[2], e[3]) for e in steps] == [(r, i + 1) for i, r in work]
+    assert events[-1] == ("sync",)
+    for rows in (r for _, r in work):
+        g = events.index(next(e for e in events if e[0] == "gather" and e[2] == rows))
+        p = events.index(next(e for e in events if e[0] == "prepare" and e[2] == rows))
+        s = events.index(next(e for e in events if e[0] == "step" and e[2] == rows))
+        assert g < p < s
+    # a batch's contents stay put from its gather until its step was enqueued
+    live = {}
+    for e in events:
+        if e[0] == "gather":
+            assert e[1] not in live, "batch regathered before its step"
+            live[e[1]] = e[2]
+        elif e[0] == "step":
+            assert live.pop(e[1]) == e[2]
