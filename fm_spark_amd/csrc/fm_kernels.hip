@@ -1665,7 +1665,9 @@ __global__ __launch_bounds__(kBlock) void k_split_count(const uint32_t* __restri
 constexpr int kSplitPer = 16;
 // one 256-thread block (three rounds for a c3 batch's 10K chunks): it finds room on a CU beside the
 // sort's blocks sooner than a 1024-thread one -- c3 step 0.971-0.975 against 0.992-0.995 ms (1024)
-// and 0.978-0.982 (64), three alternating reps (profiles/r03_v13/ab)
+// and 0.978-0.982 (64), three alternating reps (profiles/r03_v13/ab).  Scanning in the count pass's
+// last block instead (a device-scope counter, a release fence per block) cost 1.355 against 0.973 ms:
+// each fence writes back the XCD's L2 (profiles/r04_v)
 constexpr int kSplitScanNT = 256;
 __global__ __launch_bounds__(kSplitScanNT) void k_split_scan(const uint2* __restrict__ cnt, int64_t nchunks,
                                                              int64_t* __restrict__ off, int64_t* __restrict__ n_out) {
