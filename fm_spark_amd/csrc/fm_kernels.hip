@@ -1667,7 +1667,8 @@ constexpr int kSplitPer = 16;
 // sort's blocks sooner than a 1024-thread one -- c3 step 0.971-0.975 against 0.992-0.995 ms (1024)
 // and 0.978-0.982 (64), three alternating reps (profiles/r03_v13/ab).  Scanning in the count pass's
 // last block instead (a device-scope counter, a release fence per block) cost 1.355 against 0.973 ms:
-// each fence writes back the XCD's L2 (profiles/r04_v)
+// each fence writes back the XCD's L2 (profiles/r04_v); no scan at all, each scatter block summing
+// the count pass's block totals before it, 1.025 against 0.976 ms (profiles/r04_w)
 constexpr int kSplitScanNT = 256;
 __global__ __launch_bounds__(kSplitScanNT) void k_split_scan(const uint2* __restrict__ cnt, int64_t nchunks,
                                                              int64_t* __restrict__ off, int64_t* __restrict__ n_out) {
