@@ -1661,9 +1661,11 @@ __global__ __launch_bounds__(kBlock) void k_split_count(const uint32_t* __restri
 // one block: exclusive scan of the chunks' multi counts -> off[c]; totals -> n_out[0] (multi
 // entries), n_out[1] (singleton runs).  It sits on the step's critical path (main stream, before
 // the forward), so each thread loads its kSplitPer consecutive chunk counts of a round at once: one
-// memory round trip per 16K chunks (a 16.7M-entry batch), not one per 1024.
-constexpr int kSplitPer = 16;
-// one 256-thread block (three rounds for a c3 batch's 10K chunks): it finds room on a CU beside the
+// memory round trip per 12K chunks (a 12.6M-entry batch: all of a c3 batch), not one per 1024.
+// 48 against 16 (three rounds at c3): c3 step 0.971-0.975 against 0.976-0.977 ms, three alternating
+// reps (profiles/r04_x); 222 VGPRs, no scratch.
+constexpr int kSplitPer = 48;
+// one 256-thread block: it finds room on a CU beside the
 // sort's blocks sooner than a 1024-thread one -- c3 step 0.971-0.975 against 0.992-0.995 ms (1024)
 // and 0.978-0.982 (64), three alternating reps (profiles/r03_v13/ab).  Scanning in the count pass's
 // last block instead (a device-scope counter, a release fence per block) cost 1.355 against 0.973 ms:
