@@ -160,16 +160,17 @@ def host_path_leg(ctx, host_batches, t, steps, torch):
 
 def fit_leg(ctx, F, B, zipf_s, lab, iters, parts=16):
     """The estimator's mini-batch loop on a resident dataset (what FactorizationMachinesSGD.fit runs
-    after its randomSplit replay, fm_spark_amd/ml.py run_minibatch_sgd_resident): a synthetic dataset
-    of `iters` x B rows in `parts` partitions is uploaded once (dfData.cache(), SGD.scala:93), split
-    by the randomSplit replay into `iters` splits of about B rows (randomSplit normalises the
-    weights: each split gets 1/iters of the rows, :111-112), and the loop runs twice: once to grow
-    the three rotating batches' buffers (kept for the second), once timed (host clock around the whole loop, the final sync
-    included: the pipeline's fill -- the first split's gather and sort, nothing to overlap -- counts
-    against it)."""
+    after its randomSplit replay, fm_spark_amd/ml.py run_minibatch_sgd_splits): a synthetic dataset
+    of `iters` x B rows in `parts` partitions, split by the randomSplit replay into `iters` splits of
+    about B rows (randomSplit normalises the weights: each split gets 1/iters of the rows, :111-112),
+    is uploaded once laid out split after split (dfData.cache(), SGD.scala:93; fm_batch_create_splits),
+    and the loop -- each split stepped in place through a view, sorted on the side stream while the
+    previous one steps -- runs twice: once to grow the views' sort buffers and the step workspace
+    (kept for the second), once timed (host clock around the whole loop, the final sync included:
+    the pipeline's fill -- the first split's sort, nothing to overlap -- counts against it)."""
     from fm_spark_amd._native import CSRHost
     from fm_spark_amd.data import synthetic_batch
-    from fm_spark_amd.ml import run_minibatch_sgd_resident
+    from fm_spark_amd.ml import _select_csr, run_minibatch_sgd_splits
     from fm_spark_amd.sampler import random_split_csr
 
     t0 = time.perf_counter()
@@ -178,19 +179,22 @@ def fit_leg(ctx, F, B, zipf_s, lab, iters, parts=16):
     sizes = [n * (i + 1) // parts - n * i // parts for i in range(parts)]
     split_of, _, order = random_split_csr(sizes, ds.label, ds.row_ptr, ds.col, ds.val, F, [0.1] * iters, 1234)
     splits = [order[split_of[order] == i] for i in range(iters)]
+    rest = order[split_of[order] < 0]
+    lay = _select_csr(ds.row_ptr, ds.col, ds.val, ds.label, np.concatenate(splits + [rest]).astype(np.int64))
+    split_rows = np.concatenate([[0], np.cumsum([len(r) for r in splits] + [len(rest)])])
     t_split = time.perf_counter() - t0
     t0 = time.perf_counter()
-    data = ctx.batch(CSRHost(ds.row_ptr, ds.col, ds.val, ds.label))
+    data = ctx.batch_splits(lay, split_rows)
     ctx.sync()
     t_upload = time.perf_counter() - t0
-    bufs = [None, None, None]  # the three rotating batches, kept across the loops
-    run_minibatch_sgd_resident(ctx, data, splits, STEP_SIZE, REG_PARAM, bufs=bufs)  # untimed: buffers grown
+    bufs = [None, None]  # the two views used in turn, kept across the loops
+    run_minibatch_sgd_splits(ctx, data, STEP_SIZE, REG_PARAM, n_iter=iters, bufs=bufs)  # untimed: buffers grown
     half = iters // 2
     t0 = time.perf_counter()
-    run_minibatch_sgd_resident(ctx, data, splits[:half], STEP_SIZE, REG_PARAM, bufs=bufs)
+    run_minibatch_sgd_splits(ctx, data, STEP_SIZE, REG_PARAM, n_iter=half, bufs=bufs)
     dt_half = time.perf_counter() - t0
     t0 = time.perf_counter()
-    losses = run_minibatch_sgd_resident(ctx, data, splits, STEP_SIZE, REG_PARAM, bufs=bufs)
+    losses = run_minibatch_sgd_splits(ctx, data, STEP_SIZE, REG_PARAM, n_iter=iters, bufs=bufs)
     dt = time.perf_counter() - t0
     for b in bufs:
         b.close()
@@ -201,11 +205,12 @@ def fit_leg(ctx, F, B, zipf_s, lab, iters, parts=16):
             "samples_per_s": float(np.sum(rows)) / dt, "dataset_rows": n, "partitions": parts,
             "finite_losses": bool(np.all(np.isfinite(losses))),
             "setup_s": {"generate_and_split": t_split, "upload_once": t_upload},
-            "what": "FactorizationMachinesSGD.fit's mini-batch loop on the resident dataset: each randomSplit split "
-                    "gathered on the device from its row list (fm_batch_from_rows) two iterations ahead and sorted on "
-                    "the side stream while the previous split steps; host clock over the whole loop incl. the pipeline "
-                    "fill (fit_ms_per_iter), and the loop over all splits minus the loop over the first half, per "
-                    "iteration (fit_ms_per_iter_steady: the fill cancels)"}
+            "what": "FactorizationMachinesSGD.fit's mini-batch loop on the resident dataset laid out split after "
+                    "split (fm_batch_create_splits): each randomSplit split stepped in place through a view "
+                    "(fm_batch_split_view: no copy, no gather) and sorted on the side stream while the previous split "
+                    "steps; host clock over the whole loop incl. the pipeline fill (fit_ms_per_iter), and the loop over "
+                    "all splits minus the loop over the first half, per iteration (fit_ms_per_iter_steady: the fill "
+                    "cancels)"}
 
 
 def log(msg):
@@ -244,11 +249,13 @@ def pmc_traffic(F, k, B, phase, fused=False, world=1):
 # gathers saturate at, whatever bytes each request carries.  The gather-bound kernels are judged
 # against it as well as against HBM bytes.
 L2_REQ_CEILING_GPS = L2_REQ_UNIFORM_GPS = None
+C3_SKELETON = None  # the fused forward's memory skeleton replayed on c3's own stream: {ms, l2_requests, ...}
 try:
     with open(os.path.join(ROOT, "profiles", "gather_ceiling.json")) as _fh:
         _gc = json.load(_fh)
     L2_REQ_CEILING_GPS = float(_gc["l2_requests_per_s"]) / 1e9          # best variant (40 % hot rows)
     L2_REQ_UNIFORM_GPS = float(_gc["uniform_l2_requests_per_s"]) / 1e9  # uniformly random rows
+    C3_SKELETON = (_gc.get("c3_stream") or {}).get("variants", {}).get("gather<8,5,32,3>")
 except (OSError, ValueError, KeyError, TypeError):
     pass
 
@@ -450,15 +457,12 @@ def plan_run(args, env, n_visible):
             "devices": [0]}
 
 
-def singleton_fraction(batches):
-    """Share of a batch's distinct feature ids that occur in exactly one entry (the rows the fused
-    step updates in its forward), averaged over the given batches."""
-    fr = {}
-    for b in batches:
-        if id(b) not in fr:
-            _, c = np.unique(b.col, return_counts=True)
-            fr[id(b)] = float(np.count_nonzero(c == 1)) / max(len(c), 1)
-    return float(np.mean([fr[id(b)] for b in batches]))
+def batch_ids(b):
+    """(U, singleton share) of a host batch: its distinct feature ids -- the rows a step updates, what
+    the device reports as n_unique -- and the share of them with exactly one entry (the rows the fused
+    step updates in its forward)."""
+    _, c = np.unique(b.col, return_counts=True)
+    return len(c), float(np.count_nonzero(c == 1)) / max(len(c), 1)
 
 
 def concat_batches(parts):
@@ -555,55 +559,49 @@ def main():
         ctx.init_random_range(0, F)
         dbatches = [ctx.batch(CSRHost(b.row_ptr, b.col, b.val, b.label)) for b in host_batches]
         ctx.reserve(B, max(b.nnz for b in host_batches))
-        uniques = {}
+        nb = len(dbatches)
+        # U and the singleton share of every batch, counted on the host (the device's n_unique)
+        ids_stats = [batch_ids(b) for b in host_batches]
         t = 0
-        # warmup steps take the timed steps' path (a prepared batch: the fused step where it applies),
-        # so every launch of a kernel in a profile of this command is the same variant
-        warm_prep = not args.no_prefetch and not args.host_path
-        for i in range(args.warmup):
+        prefetch = not args.no_prefetch and not args.host_path
+        depth = max(1, min(args.prefetch_depth or 1, nb - 1))
+        # the pipeline from the first warmup step on: the batches of the first `depth` steps are sorted
+        # before it (as the steps before them would have, in a training loop), and every step -- warmup
+        # and timed alike, one sequence g = 0, 1, ... -- sorts the batch `depth` steps ahead on the side
+        # stream while it runs.  So every launch of a kernel in a profile of this command is the same
+        # variant in the same overlap, and the timed region holds K steps and K sorts in the steady
+        # state (the last `depth` sorts for batches stepped after it).
+        if prefetch:
+            for j in range(depth):
+                dbatches[j % nb].prepare()
+        for g in range(args.warmup):
             t += 1
-            if warm_prep:
-                dbatches[i % len(dbatches)].prepare()
-            o = ctx.step_batch(dbatches[i % len(dbatches)], t, STEP_SIZE, REG_PARAM, sync=True)
-            uniques[i % len(dbatches)] = o.n_unique
-        for j in range(len(dbatches)):
-            if j not in uniques:  # count U for every batch (untimed)
-                t += 1
-                if warm_prep:
-                    dbatches[j].prepare()
-                uniques[j] = ctx.step_batch(dbatches[j], t, STEP_SIZE, REG_PARAM, sync=True).n_unique
-        torch.cuda.synchronize()
+            if prefetch:
+                dbatches[(g + depth) % nb].prepare()
+            ctx.step_batch(dbatches[g % nb], t, STEP_SIZE, REG_PARAM, sync=False)
         ctx.sync()
+        torch.cuda.synchronize()
         if args.profile_kernels:
             ctx.profile_reset()
         prof_on = ProfileSampler(ctx, args)
-        prefetch = not args.no_prefetch
-        depth = max(1, min(args.prefetch_depth or 1, len(dbatches) - 1))
+        g0 = args.warmup
         if args.host_path:
             hosts = [CSRHost(b.row_ptr, b.col, b.val, b.label) for b in host_batches]
-            prefetch = False
             t_start = time.perf_counter()
             for i in range(args.steps):
                 t += 1
-                ctx.step(hosts[i % len(hosts)], t, STEP_SIZE, REG_PARAM, sync=False)
+                ctx.step(hosts[(g0 + i) % len(hosts)], t, STEP_SIZE, REG_PARAM, sync=False)
         else:
-            # the pipeline in its steady state: the batches of the first `depth` timed steps were
-            # sorted before the timed region (as the steps before them would have, in a training
-            # loop), and every timed step sorts the batch `depth` steps ahead -- K steps and K sorts
-            # inside the timed region, the last `depth` of them for batches stepped after it
-            if prefetch:
-                for j in range(depth):
-                    dbatches[j % len(dbatches)].prepare()
-                ctx.sync()
             t_start = time.perf_counter()
         evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
         for i in range(0 if args.host_path else args.steps):
             t += 1
             prof_on(i)
             evs[i].record(main_stream)
+            g = g0 + i
             if prefetch:
-                dbatches[(i + depth) % len(dbatches)].prepare()  # sorted on the side stream during step i
-            ctx.step_batch(dbatches[i % len(dbatches)], t, STEP_SIZE, REG_PARAM, sync=False)
+                dbatches[(g + depth) % nb].prepare()  # sorted on the side stream during step g
+            ctx.step_batch(dbatches[g % nb], t, STEP_SIZE, REG_PARAM, sync=False)
         evs[args.steps].record(main_stream)
         ctx.sync()
         torch.cuda.synchronize()
@@ -623,10 +621,12 @@ def main():
         fit = None
         if args.fit_iters > 0 and not args.host_path:
             fit = fit_leg(ctx, F, B, zipf_s, lab, args.fit_iters)
-        U_mean = float(np.mean([uniques[i % len(dbatches)] for i in range(args.steps)]))
+        timed_b = [(g0 + i) % nb for i in range(args.steps)]
+        U_mean = float(np.mean([ids_stats[j][0] for j in timed_b]))
         # the step variant from the context itself (fm_fuse_active), not from which phases were profiled
         fused = ctx.fuse_active and prefetch
-        single_frac = singleton_fraction([host_batches[i % len(host_batches)] for i in range(args.steps)])
+        # the singleton rows' share of the rows updated, weighted by each timed batch's U
+        single_frac = float(np.sum([ids_stats[j][0] * ids_stats[j][1] for j in timed_b])) / max(U_mean * len(timed_b), 1.0)
         parallelism = "single table" + (", fused step (singleton rows updated by the forward)" if fused else "") + \
             ((", next batch sorted during the current step" if depth == 1 else
               f", batches sorted {depth} steps ahead on the side stream") if prefetch else "")
@@ -715,7 +715,7 @@ def main():
         losses = ctx.loss_history()
         assert np.all(np.isfinite(losses)), "non-finite loss"
         R = world
-        fused = ctx.fuse_active and par == "sharded"  # the fused owner step (selects the matching PMC file)
+        fused = False  # multi-GPU contexts never fuse (fm_fuse_active; selects the matching PMC file)
         # rows one rank updates: sharded, the global distinct ids over the owners; replicated, every
         # replica applies every touched row
         U_mean = float(np.mean(uniques)) / (R if par == "sharded" else 1)
@@ -825,17 +825,28 @@ def main():
             # "owner_forward" / "owner_update" do the same on the rank's own rows (per rank: the
             # entries an owner receives ~ its own batch's, the rows it updates ~ U / world)
             algo = {"forward": fwd_b, "update": upd_b, "owner_forward": fwd_b, "owner_update": upd_b}
+            algo_what = {"forward": "CSR (8z + 12 B per sample) + the gather of w and V (4z(k+1) B per sample)",
+                         "update": "read + write of every touched row (8(k+1) B per row)"}
             if fused and mode == "single":
-                # the fused forward also reads and writes the singleton rows (their 8(k+1) B each of
-                # the update's share); the segmented update keeps the rows with two or more entries
-                algo["forward"] = fwd_b + upd_b * single_frac
+                # the fused forward also writes the singleton rows back (4(k+1) B each: their read is
+                # the forward's own gather, already counted); the segmented update keeps the rows with
+                # two or more entries (read + write)
+                algo["forward"] = fwd_b + upd_b * single_frac / 2.0
                 algo["update"] = upd_b * (1.0 - single_frac)
+                algo_what["forward"] += " + the write-back of each singleton row (4(k+1) B; read by the gather)"
+                algo_what["update"] = "read + write of the rows with two or more entries (8(k+1) B per row)"
             dom = max((n for n in kern if n in algo), key=lambda n: kern[n]["avg_ms"])
             ach = algo[dom] / (kern[dom]["avg_ms"] * 1e-3) / 1e9
             traffic, tsrc = pmc_traffic(F, k, B, dom, fused, world)
             line["roofline"] = {"bound": "hbm", "kernel": dom, "achieved": ach, "peak": HBM_PEAK_GBS,
                                 "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "traffic": traffic,
-                                "algorithmic_bytes": algo[dom], "traffic_source": tsrc}
+                                "algorithmic_bytes": algo[dom], "algorithmic_bytes_what": algo_what.get(dom),
+                                "kernel_avg_ms": kern[dom]["avg_ms"],
+                                "kernel_avg_of": "HIP events on the kernel's launch stream, every "
+                                                 f"{max(1, args.profile_every)}. timed step (the warmup steps run the "
+                                                 "same pipeline, so a rocprofv3 --kernel-trace --stats of this command "
+                                                 "averages the same launches)",
+                                "traffic_source": tsrc}
             # the ceiling that binds a random-row gather: L2 line requests per second
             reqs = {}
             for ph in ("forward", "update", "owner_forward", "owner_update"):
@@ -847,6 +858,19 @@ def main():
             if reqs:
                 line["roofline"]["requests"] = reqs.get(dom)
                 line["roofline"]["requests_by_kernel"] = reqs
+            if C3_SKELETON and dom == "forward" and fused and mode == "single" and (F, k, B, zipf_s) == CONFIGS["c3"][:4]:
+                # the forward against its own access stream: tools/gather_ceiling.hip replays this batch
+                # stream's memory skeleton (CSR read, every row's record gathered, the singleton rows'
+                # records written back, the S records written; no arithmetic) alone on the GPU
+                fw_ms = kern[dom]["avg_ms"]
+                rq = (reqs.get("forward") or {}).get("l2_requests")
+                sk_rate = C3_SKELETON["l2_requests_per_s"] / 1e9
+                line["roofline"]["c3_stream"] = {
+                    "skeleton_ms": C3_SKELETON["ms"], "skeleton_l2_requests": C3_SKELETON["l2_requests"],
+                    "skeleton_G_per_s": sk_rate, "forward_ms_in_step": fw_ms,
+                    "time_frac": C3_SKELETON["ms"] / fw_ms,
+                    "requests_frac": (rq / (fw_ms * 1e-3) / 1e9) / sk_rate if rq else None,
+                    "source": "profiles/gather_ceiling.json c3_stream (tools/c3_stream.py + tools/gather_ceiling.hip)"}
             if args.k == 0 and k == 16:
                 # k = 16: a row's 68 algorithmic bytes sit in a 128-B record (one line per random access),
                 # so at the ~6.3 TB/s random-line rate the forward's HBM fraction is capped near

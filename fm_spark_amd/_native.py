@@ -95,6 +95,8 @@ SIGNATURES = {
     "fm_batch_destroy": (None, [_P]),
     "fm_batch_prepare": (C.c_int, [_P, _P]),
     "fm_batch_from_rows": (C.c_int, [_P, _P, _I64P, C.c_int64, C.POINTER(_P)]),
+    "fm_batch_create_splits": (C.c_int, [_P, C.POINTER(fm_csr), C.c_int32, _I64P, C.POINTER(_P)]),
+    "fm_batch_split_view": (C.c_int, [_P, _P, C.c_int32, C.POINTER(_P)]),
     "fm_fuse_active": (C.c_int32, [_P]),
     "fm_batch_rows": (C.c_int64, [_P]),
     "fm_batch_nnz": (C.c_int64, [_P]),

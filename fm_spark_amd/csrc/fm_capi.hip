@@ -261,12 +261,6 @@ bool fuse_rule(const fm_ctx* ctx) {
 
 static bool fuse_on(const fm_ctx* ctx) { return ctx->cfg.shard_count == 1 && fuse_rule(ctx); }
 
-// The sharded owner's fused step: on request only (FM_FUSE_ON).  At c3 / world 1 it measured 1.40-1.49
-// ms per step against 1.16-1.26 unfused: the owner re-reads every received entry's
-// row after the S exchange either way, so the singleton pass saves only the S gathers of its runs,
-// and it adds a pass, the tags and a split to the owner's sort.
-bool owner_fuse(const fm_ctx* ctx) { return ctx->cfg.fuse_single == FM_FUSE_ON && ctx->kp <= 16; }
-
 // The bucket sort (fm_sort.hip) for a batch of N entries of this context, or the LSD passes
 // (fm_config.sort_algo; both stable, so the step is bitwise the same)
 bool bucket_on(const fm_ctx* ctx, int64_t N) {
@@ -358,6 +352,7 @@ int step_impl(fm_ctx* ctx, fm_batch* b, int32_t t, double step_size, double reg_
   FM_REQUIRE(b != nullptr, "null batch");
   FM_REQUIRE(b->owner == ctx, "batch belongs to another context");
   FM_REQUIRE(ctx->cfg.shard_count == 1, "sharded contexts step through the fm_shard_* entry points");
+  FM_REQUIRE(b->split_rows.empty(), "a dataset made by fm_batch_create_splits is stepped through its split views");
   if (emit) FM_HIP_CHECK(hipMemsetAsync(emit, 0, sizeof(float) * (size_t)ctx->rows * (ctx->kp + 4), ctx->stream));
   if (b->dev.n_rows == 0) return FM_NOTHING_TO_DO;  // SGD.scala:126-128
   FM_REQUIRE(t >= 1, "iteration index t must be >= 1");
@@ -549,7 +544,11 @@ int fm_set_side_stream(fm_ctx* ctx, void* s) {
 int fm_sync(fm_ctx* ctx) {
   return guarded(ctx, [&]() -> int {
     if (ctx->group) return group_sync(ctx);
+    // every stream the context enqueues on: the step's, the side stream's preparations and the copy
+    // stream's fm_batch_from_rows gathers (after this the caller may free a dataset it gathered from)
     FM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    FM_HIP_CHECK(hipStreamSynchronize(ctx->side));
+    if (ctx->copy_stream) FM_HIP_CHECK(hipStreamSynchronize(ctx->copy_stream));
     return FM_OK;
   });
 }
@@ -727,6 +726,7 @@ int fm_batch_prepare(fm_ctx* ctx, fm_batch* b) {
     FM_REQUIRE(b != nullptr && b->owner == ctx, "batch belongs to another context");
     if (ctx->group) return group_batch_prepare(ctx, b);
     FM_REQUIRE(ctx->cfg.shard_count == 1, "fm_batch_prepare is for single-table contexts");
+    FM_REQUIRE(b->split_rows.empty(), "a dataset made by fm_batch_create_splits is prepared through its split views");
     const int64_t N = b->dev.nnz;
     if (N == 0) return FM_OK;
     if (!b->ready) {
@@ -795,8 +795,11 @@ int fm_batch_from_rows(fm_ctx* ctx, const fm_batch* data, const int64_t* rows, i
       b->owner = ctx;
       b->device = ctx->cfg.device;
     } else {
-      FM_REQUIRE(b->owner == ctx && b != data && !b->grp, "out must be a batch of this context other than data");
+      FM_REQUIRE(b->owner == ctx && b != data && !b->grp && b->split_rows.empty(),
+                 "out must be a batch of this context other than data");
     }
+    // a split view refilled as a selection: its borrowed pointers are dropped, its own buffers grown below
+    b->detach_view();
     if (!b->ready) {
       FM_HIP_CHECK(hipEventCreateWithFlags(&b->ready, hipEventDisableTiming));
       FM_HIP_CHECK(hipEventCreateWithFlags(&b->last_use, hipEventDisableTiming));
@@ -851,7 +854,13 @@ int fm_batch_from_rows(fm_ctx* ctx, const fm_batch* data, const int64_t* rows, i
     // for `built`, fm_batch_prepare)
     if (!ctx->copy_stream) FM_HIP_CHECK(hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking));
     hipStream_t gs = ctx->copy_stream;
+    // the refill rewrites what queued work may still read: the last step of the batch (b->last_use,
+    // recorded by the single-table step and by the sharded owner update on the main stream), the
+    // sharded iteration's own last read (sh->last_use) and a preparation never stepped (its sort on the
+    // side stream reads dev.col / dev.ent)
     FM_HIP_CHECK(hipStreamWaitEvent(gs, b->last_use, 0));
+    if (b->sh && b->sh->last_use) FM_HIP_CHECK(hipStreamWaitEvent(gs, b->sh->last_use, 0));
+    if (b->prepared && b->ready) FM_HIP_CHECK(hipStreamWaitEvent(gs, b->ready, 0));
     b->dev.n_rows = n;
     b->dev.nnz = N;
     b->max_id = data->max_id;
@@ -877,10 +886,90 @@ int fm_batch_from_rows(fm_ctx* ctx, const fm_batch* data, const int64_t* rows, i
   });
 }
 
+int fm_batch_create_splits(fm_ctx* ctx, const fm_csr* csr, int32_t n_splits, const int64_t* split_rows,
+                           fm_batch** out) {
+  return guarded(ctx, [&]() -> int {
+    FM_REQUIRE(out != nullptr && csr != nullptr, "null argument");
+    FM_REQUIRE(n_splits >= 1 && split_rows != nullptr, "n_splits must be >= 1");
+    FM_REQUIRE(split_rows[0] == 0 && split_rows[n_splits] == csr->n_rows, "split_rows must run from 0 to n_rows");
+    for (int32_t i = 0; i < n_splits; ++i) FM_REQUIRE(split_rows[i] <= split_rows[i + 1], "split_rows must be non-decreasing");
+    if (ctx->group) return group_batch_create_splits(ctx, csr, n_splits, split_rows, out);
+    std::unique_ptr<fm_batch> b(new fm_batch());
+    upload_batch(ctx, csr, b.get(), true);
+    b->host_rp.assign(csr->row_ptr, csr->row_ptr + csr->n_rows + 1);
+    b->split_rows.assign(split_rows, split_rows + n_splits + 1);
+    DevBuf dsr;
+    dsr.ensure(sizeof(int64_t) * (n_splits + 1));
+    FM_HIP_CHECK(hipMemcpyAsync(dsr.p, split_rows, sizeof(int64_t) * (n_splits + 1), hipMemcpyHostToDevice, ctx->stream));
+    b->split_rp.ensure(sizeof(int64_t) * (csr->n_rows + n_splits));
+    launch_split_rebase(b->dev, dsr.as<int64_t>(), n_splits, b->split_rp.as<int64_t>(), ctx->stream);
+    FM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    dsr.release();
+    *out = b.release();
+    return FM_OK;
+  });
+}
+
+int fm_batch_split_view(fm_ctx* ctx, const fm_batch* data, int32_t split, fm_batch** out) {
+  return guarded(ctx, [&]() -> int {
+    FM_REQUIRE(out != nullptr && data != nullptr, "null argument");
+    FM_REQUIRE(data->owner == ctx, "data belongs to another context");
+    if (ctx->group) return group_batch_split_view(ctx, data, split, out);
+    const int64_t ns = (int64_t)data->split_rows.size() - 1;
+    FM_REQUIRE(ns >= 1, "data must be a dataset made by fm_batch_create_splits");
+    FM_REQUIRE(split >= 0 && split < ns, "split index out of range");
+    fm_batch* b = *out;
+    std::unique_ptr<fm_batch> fresh;
+    if (b == nullptr) {
+      fresh.reset(new fm_batch());
+      b = fresh.get();
+      b->owner = ctx;
+      b->device = ctx->cfg.device;
+    } else {
+      FM_REQUIRE(b->owner == ctx && b != data && !b->grp && b->split_rows.empty(),
+                 "out must be a batch of this context other than data");
+    }
+    if (!b->view_of) {
+      // an owning batch becomes a view: its own buffers are freed once no queued work reads them
+      for (hipEvent_t e : {b->last_use, b->ready, b->built, b->sel_copied})
+        if (e) FM_HIP_CHECK(hipEventSynchronize(e));
+      for (DevBuf* d : {&b->dev.row_ptr, &b->dev.col, &b->dev.ent, &b->dev.xs, &b->dev.label, &b->up}) d->release();
+    }
+    if (!b->ready) {
+      FM_HIP_CHECK(hipEventCreateWithFlags(&b->ready, hipEventDisableTiming));
+      FM_HIP_CHECK(hipEventCreateWithFlags(&b->last_use, hipEventDisableTiming));
+      FM_HIP_CHECK(hipEventRecord(b->last_use, ctx->stream));
+    }
+    // the split's rows, entries and labels in place: pointers into data (no copy, no gather); the
+    // step's reads of a view are ordered like any batch's (data was complete when it was created)
+    const int64_t r0 = data->split_rows[split], r1 = data->split_rows[split + 1];
+    const int64_t e0 = data->host_rp[r0], e1 = data->host_rp[r1];
+    b->view_of = data;
+    b->dev.n_rows = r1 - r0;
+    b->dev.nnz = e1 - e0;
+    b->dev.row_ptr.p = data->split_rp.as<int64_t>() + r0 + split;
+    b->dev.row_ptr.bytes = sizeof(int64_t) * (r1 - r0 + 1);
+    b->dev.col.p = data->dev.col.as<uint32_t>() + e0;
+    b->dev.col.bytes = sizeof(uint32_t) * (e1 - e0);
+    b->dev.ent.p = data->dev.ent.as<uint2>() + e0;
+    b->dev.ent.bytes = sizeof(uint2) * (e1 - e0);
+    b->dev.xs.p = data->dev.xs.as<float>() + e0;
+    b->dev.xs.bytes = sizeof(float) * (e1 - e0);
+    b->dev.label.p = data->dev.label.as<double>() + r0;
+    b->dev.label.bytes = sizeof(double) * (r1 - r0);
+    b->max_id = data->max_id;
+    b->prepared = false;
+    b->host_rp.clear();
+    if (fresh) *out = fresh.release();
+    return FM_OK;
+  });
+}
+
 int32_t fm_fuse_active(fm_ctx* ctx) {
   if (!ctx) return -1;
-  if (ctx->group)  // a sharded group's owners take the fused owner step by the same rule; replicas never fuse
-    return ctx->cfg.parallel == FM_PARALLEL_SHARDED && owner_fuse(group_member0(ctx)) ? 1 : 0;
+  // a multi-GPU context never fuses: replicas feed fm_repl_grad the whole sorted view, and a sharded
+  // owner's fused step measured slower than the unfused one at R = 8 and at world 1
+  if (ctx->group) return 0;
   return fuse_on(ctx) ? 1 : 0;
 }
 

@@ -65,11 +65,6 @@ struct ShardBatchState {
   DevBuf src_off;            // [R+1] int64 source offsets of the received entries, then [R+1] pair offsets
   DevBuf pair_ptr;           // [P+1] int64 entry offsets of the pairs
   DevBuf skeys, sents;       // received entries sorted by slot: slots / {pair, x bits}
-  // fused owner step (split): skeys / sents hold only the runs of two or more entries, split_n
-  // {their count, singleton runs} on the device; fkeys / fents the LSD-sorted whole view a split
-  // pass reduces (the bucket sort keeps the multi runs itself)
-  bool split = false;
-  DevBuf split_n, fkeys, fents;
   hipEvent_t ready_fwd = nullptr;  // side stream: pair table done
   hipEvent_t ready_upd = nullptr;  // side stream: slot sort done
   hipEvent_t last_use = nullptr;   // main stream: the iteration's update has read everything
@@ -80,7 +75,7 @@ struct ShardBatchState {
     for (hipEvent_t e : {ready_fwd, ready_upd, last_use})
       if (e) (void)hipEventDestroy(e);
     ready_fwd = ready_upd = last_use = nullptr;
-    for (DevBuf* b : {&pairidx, &poff, &src_off, &pair_ptr, &skeys, &sents, &split_n, &fkeys, &fents}) b->release();
+    for (DevBuf* b : {&pairidx, &poff, &src_off, &pair_ptr, &skeys, &sents}) b->release();
   }
 };
 
@@ -123,6 +118,23 @@ struct fm_batch {
   std::vector<int64_t> host_rp;
   Pinned sel_pin;
   hipEvent_t sel_copied = nullptr, built = nullptr;
+  // fm_batch_create_splits: the dataset's split boundaries (row offsets [n_splits + 1]) and every
+  // split's own row_ptr rebased to its first entry (split_rp, [rows + n_splits]: split s at
+  // split_rows[s] + s); its entries' sample indices are relative to their split's first row, so the
+  // dataset itself is never stepped -- its splits are, through views
+  std::vector<int64_t> split_rows;
+  DevBuf split_rp;
+  // fm_batch_split_view: dev's buffers point into view_of's (borrowed: never grown, never freed here)
+  const fm_batch* view_of = nullptr;
+  // a view's borrowed pointers dropped (before the batch frees or grows its own)
+  void detach_view() {
+    if (!view_of) return;
+    for (DevBuf* d : {&dev.row_ptr, &dev.col, &dev.ent, &dev.xs, &dev.label}) {
+      d->p = nullptr;
+      d->bytes = 0;
+    }
+    view_of = nullptr;
+  }
   std::unique_ptr<ShardBatchState> sh;  // sharded contexts only
   std::unique_ptr<GroupBatch, GroupBatchDeleter> grp;  // a multi-GPU context's batch: its per-rank parts
   ~fm_batch() {
@@ -133,6 +145,8 @@ struct fm_batch {
       if (e) (void)hipEventSynchronize(e);
     for (hipEvent_t e : {ready, last_use, sel_copied, built})
       if (e) (void)hipEventDestroy(e);
+    detach_view();
+    split_rp.release();
     skeys.release();
     sents.release();
     fkeys.release();
@@ -189,7 +203,9 @@ struct fm_ctx {
   DevBuf sh_ent2;      // [n] uint2 {pair, x bits}: the slot sort's payload
   SortWork side_sort;  // radix sort workspace of the side stream
   SortWork route_sort;  // the route's owner partition (fm_shard_route)
-  SplitWork split_work;  // the split pass after an LSD-sorted fused batch (side stream, fm_batch_prepare)
+  // the split of an LSD-sorted view into its multi runs: only the single-table fused step runs it, at
+  // the step (main stream, step_impl), so one stream uses the workspace
+  SplitWork split_work;
   Pinned side_pinned;  // route counts (device -> host)
   // replicated step state (fm_repl_*)
   DevBuf repl_cnt;            // touched-row counts per apply block (uint32)
@@ -375,10 +391,8 @@ inline int bits_for(int64_t max_value) {
 
 // shared host helpers (fm_capi.hip)
 // the fused step's rule (fm_config.fuse_single, kp <= 16, tables above 256 MB unless FUSE_ON) for the
-// single table; the sharded owner's (FUSE_ON only); and whether a batch of N entries takes the
-// bucket sort (fm_config.sort_algo)
+// single table; and whether a batch of N entries takes the bucket sort (fm_config.sort_algo)
 bool fuse_rule(const fm_ctx* ctx);
-bool owner_fuse(const fm_ctx* ctx);
 // stream st waits until a batch refilled by fm_batch_from_rows has been gathered (copy stream)
 void wait_built(const fm_batch* b, hipStream_t st);
 bool bucket_on(const fm_ctx* ctx, int64_t N);
@@ -407,6 +421,9 @@ int group_create(const fm_config* cfg, fm_ctx** out);
 int group_batch_create(fm_ctx* ctx, const fm_csr* csr, fm_batch** out);
 int group_batch_prepare(fm_ctx* ctx, fm_batch* b);
 int group_batch_from_rows(fm_ctx* ctx, const fm_batch* data, const int64_t* rows, int64_t n, fm_batch** out);
+int group_batch_create_splits(fm_ctx* ctx, const fm_csr* csr, int32_t n_splits, const int64_t* split_rows,
+                              fm_batch** out);
+int group_batch_split_view(fm_ctx* ctx, const fm_batch* data, int32_t split, fm_batch** out);
 int group_step(fm_ctx* ctx, const fm_csr* csr, int32_t t, double step_size, double reg_param, fm_step_out* out);
 int group_step_batch(fm_ctx* ctx, fm_batch* b, int32_t t, double step_size, double reg_param, fm_step_out* out);
 int group_predict(fm_ctx* ctx, const fm_csr* csr, double lo, double hi, double* pred);

@@ -966,6 +966,10 @@ int group_batch_from_rows(fm_ctx* ctx, const fm_batch* data, const int64_t* rows
   FM_REQUIRE(b->owner == ctx && b->grp && b != data, "out must be a batch of this context other than data");
   GroupBatch& gb = *b->grp;
   drop_route(g, gb);  // a routed plan of the old contents is dropped before its buffers are reused
+  // a former dataset refilled as a selection: its per-rank full copies describe the old contents
+  for (fm_batch* f : gb.full)
+    if (f) fm_batch_destroy(f);
+  gb.full.clear();
   gb.parts.resize(g.L);
   gb.prefetched = false;
   gb.rows = n;
@@ -996,9 +1000,122 @@ int group_batch_from_rows(fm_ctx* ctx, const fm_batch* data, const int64_t* rows
   return FM_OK;
 }
 
+// A dataset laid out split by split (fm_batch_create_splits): local rank l holds its share of every
+// split -- the split's rows by rows over the local ranks, as a host CSR's are (upload_parts) -- as a
+// member dataset with the same number of splits, so split s of the group dataset is every rank's
+// split s (group_batch_split_view).
+int group_batch_create_splits(fm_ctx* ctx, const fm_csr* c, int32_t n_splits, const int64_t* split_rows,
+                              fm_batch** out) {
+  Group& g = grp(ctx);
+  FM_REQUIRE(c->n_rows >= 0 && c->nnz >= 0, "negative n_rows / nnz");
+  FM_REQUIRE(c->n_rows == 0 || (c->row_ptr && c->label), "null row_ptr / label");
+  FM_REQUIRE(c->nnz == 0 || (c->col && c->val), "null col / val");
+  const int64_t B = c->n_rows;
+  if (B > 0) {
+    FM_REQUIRE(c->row_ptr[0] == 0 && c->row_ptr[B] == c->nnz, "row_ptr must run from 0 to nnz");
+    for (int64_t i = 0; i < B; ++i) FM_REQUIRE(c->row_ptr[i] <= c->row_ptr[i + 1], "row_ptr must be non-decreasing");
+  } else {
+    FM_REQUIRE(c->nnz == 0, "nnz > 0 with n_rows == 0");
+  }
+  std::unique_ptr<fm_batch> b(new_group_batch(ctx));
+  GroupBatch& gb = *b->grp;
+  gb.parts.resize(g.L);
+  gb.rows = B;
+  gb.nnz = c->nnz;
+  std::vector<std::vector<int64_t>> rows(g.L, std::vector<int64_t>(1));
+  std::vector<int64_t> rp, msr;
+  std::vector<int32_t> col;
+  std::vector<double> val, lab;
+  for (int l = 0; l < g.L; ++l) {
+    rp.assign(1, 0);
+    msr.assign(1, 0);
+    col.clear();
+    val.clear();
+    lab.clear();
+    for (int32_t s = 0; s < n_splits; ++s) {
+      const int64_t ns = split_rows[s + 1] - split_rows[s];
+      const int64_t a = split_rows[s] + ns * l / g.L, z = split_rows[s] + ns * (l + 1) / g.L;
+      for (int64_t i = a; i < z; ++i) {
+        lab.push_back(c->label[i]);
+        col.insert(col.end(), c->col + c->row_ptr[i], c->col + c->row_ptr[i + 1]);
+        val.insert(val.end(), c->val + c->row_ptr[i], c->val + c->row_ptr[i + 1]);
+        rp.push_back((int64_t)col.size());
+      }
+      msr.push_back((int64_t)lab.size());
+    }
+    fm_csr sub{};
+    sub.n_rows = (int64_t)lab.size();
+    sub.nnz = (int64_t)col.size();
+    sub.row_ptr = rp.data();
+    sub.col = col.data();
+    sub.val = val.data();
+    sub.label = lab.data();
+    GPart& p = gb.parts[l];
+    mcheck(fm_batch_create_splits(g.ranks[l].m, &sub, n_splits, msr.data(), &p.b), "fm_batch_create_splits");
+    p.device = g.ranks[l].device;
+    p.rows = sub.n_rows;
+    p.row0 = 0;  // its rows are not one range of the dataset (the dataset is not predicted as a whole)
+    p.nnz = sub.nnz;
+    rows[l][0] = p.rows;
+  }
+  const std::vector<int64_t> all = allgather(g, rows, 1);
+  gb.global_rows = std::accumulate(all.begin(), all.end(), int64_t(0));
+  b->split_rows.assign(split_rows, split_rows + n_splits + 1);
+  sync_group_batch_view(b.get());
+  *out = b.release();
+  return FM_OK;
+}
+
+// Split s of a group dataset: every local rank's view of its own share (fm_batch_split_view); no copy.
+int group_batch_split_view(fm_ctx* ctx, const fm_batch* data, int32_t split, fm_batch** out) {
+  Group& g = grp(ctx);
+  FM_REQUIRE(data->grp && !data->split_rows.empty(), "data must be a dataset made by fm_batch_create_splits");
+  FM_REQUIRE(split >= 0 && split + 1 < (int32_t)data->split_rows.size(), "split index out of range");
+  const GroupBatch& dg = *data->grp;
+  std::unique_ptr<fm_batch> fresh;
+  fm_batch* b = *out;
+  if (!b) {
+    fresh.reset(new_group_batch(ctx));
+    b = fresh.get();
+  }
+  FM_REQUIRE(b->owner == ctx && b->grp && b != data && b->split_rows.empty(),
+             "out must be a batch of this context other than data");
+  GroupBatch& gb = *b->grp;
+  drop_route(g, gb);  // a routed plan of the old contents is dropped before the parts change
+  for (fm_batch* f : gb.full)
+    if (f) fm_batch_destroy(f);
+  gb.full.clear();
+  gb.parts.resize(g.L);
+  gb.prefetched = false;
+  const int64_t n = data->split_rows[split + 1] - data->split_rows[split];
+  gb.rows = n;
+  gb.nnz = 0;
+  std::vector<std::vector<int64_t>> cnt(g.L, std::vector<int64_t>(1));
+  for (int l = 0; l < g.L; ++l) {
+    GPart& p = gb.parts[l];
+    mcheck(fm_batch_split_view(g.ranks[l].m, dg.parts[l].b, split, &p.b), "fm_batch_split_view");
+    p.device = g.ranks[l].device;
+    p.rows = fm_batch_rows(p.b);
+    p.row0 = n * l / g.L;  // as group_batch_create_splits cut the split
+    p.nnz = fm_batch_nnz(p.b);
+    gb.nnz += p.nnz;
+    cnt[l][0] = p.rows;
+  }
+  if (g.nprocs == 1) {
+    gb.global_rows = n;
+  } else {
+    const std::vector<int64_t> all = allgather(g, cnt, 1);
+    gb.global_rows = std::accumulate(all.begin(), all.end(), int64_t(0));
+  }
+  sync_group_batch_view(b);
+  if (fresh) *out = fresh.release();
+  return FM_OK;
+}
+
 int group_batch_prepare(fm_ctx* ctx, fm_batch* b) {
   Group& g = grp(ctx);
   GroupBatch& gb = gbatch(ctx, b);
+  FM_REQUIRE(b->split_rows.empty(), "a dataset made by fm_batch_create_splits is prepared through its split views");
   if (g.sharded()) {
     // phase 2 of the batch prepared before this one (its routes ran beside the steps enqueued
     // since), then phase 1 of this one: the host waits only for route work an iteration old
@@ -1015,6 +1132,8 @@ int group_batch_prepare(fm_ctx* ctx, fm_batch* b) {
 }
 
 int group_step_batch(fm_ctx* ctx, fm_batch* b, int32_t t, double step_size, double reg_param, fm_step_out* out) {
+  FM_REQUIRE(b == nullptr || b->split_rows.empty(),
+             "a dataset made by fm_batch_create_splits is stepped through its split views");
   return step_group_batch(ctx, gbatch(ctx, b), t, step_size, reg_param, out);
 }
 
@@ -1035,6 +1154,7 @@ int group_predict(fm_ctx* ctx, const fm_csr* csr, double lo, double hi, double* 
 }
 
 int group_predict_batch(fm_ctx* ctx, fm_batch* b, double lo, double hi, double* pred) {
+  FM_REQUIRE(b == nullptr || b->split_rows.empty(), "a dataset made by fm_batch_create_splits is predicted by split");
   predict_group_batch(ctx, gbatch(ctx, b), lo, hi, pred);
   return FM_OK;
 }
@@ -1055,6 +1175,21 @@ int group_init_random(fm_ctx* ctx, const int32_t* ids, int64_t n, int64_t id_beg
 int group_init_from_batch(fm_ctx* ctx, fm_batch* b, int64_t* n_present) {
   Group& g = grp(ctx);
   GroupBatch& gb = gbatch(ctx, b);
+  if (g.sharded() && !b->split_rows.empty()) {
+    // a dataset laid out by splits: its entries' sample indices count from their split's first row,
+    // so the owner routing runs split by split (the draw depends on (seed, id, factor) only)
+    fm_batch* v = nullptr;
+    for (int32_t s = 0; s + 1 < (int32_t)b->split_rows.size(); ++s) {
+      group_batch_split_view(ctx, b, s, &v);
+      if (v->grp->nnz > 0) group_init_from_batch(ctx, v, nullptr);
+    }
+    if (v) {
+      group_sync(ctx);
+      fm_batch_destroy(v);
+    }
+    if (n_present) *n_present = group_num_present(ctx);
+    return FM_OK;
+  }
   if (g.sharded()) {
     // createInitialModel's distinct ids arrive at their owners through the step's own routing
     prefetch(g, gb);
@@ -1207,6 +1342,8 @@ int group_sync(fm_ctx* ctx) {
     on(r, [&] {
       FM_HIP_CHECK(hipStreamSynchronize(r.m->stream));
       FM_HIP_CHECK(hipStreamSynchronize(r.m->side));
+      if (r.m->copy_stream) FM_HIP_CHECK(hipStreamSynchronize(r.m->copy_stream));
+      if (r.xstream) FM_HIP_CHECK(hipStreamSynchronize(r.xstream));
     });
   return FM_OK;
 }

@@ -213,10 +213,6 @@ struct SplitWork {
 void launch_split(const uint32_t* skeys, const uint2* sents, int64_t N, SplitWork& sw, uint32_t* mkeys, uint2* ments,
                   int64_t* n_out, hipStream_t st,
                   const TableView* tag_T = nullptr, int32_t epoch = 0);
-// the fused sharded owner step: the rows of the received entries' singleton features, pair by pair
-// (pair_ptr [P + 1] over slot / ent, S records of rec floats: S then {r, yhat} at kp)
-void launch_owner_singletons(const TableView& T, const int64_t* pair_ptr, int64_t P, const uint32_t* slot,
-                             const uint2* ent, const float* srec, int rec, const StepParams& sp, hipStream_t st);
 // the fused step's multi tags for the runs of a prepared multi view (n_dev[0] <= n_max entries)
 void launch_tag_runs(const TableView& T, const uint32_t* mkeys, const int64_t* n_dev, int64_t n_max, int32_t epoch,
                      hipStream_t st);
@@ -260,5 +256,10 @@ void launch_explode(const int64_t* row_ptr_in, const double* label_in, const int
 // result's row_ptr, computed by the host from the source's
 void launch_select_rows(const BatchDev& src, const int64_t* rows, const int64_t* row_ptr_in, int64_t B, BatchDev& dst,
                         hipStream_t st);
+// fm_batch_create_splits: each split's own row_ptr (rebased to its first entry) into split_rp
+// [B + n_splits] and every entry's sample index made relative to its split's first row
+// (split_rows [n_splits + 1], device)
+void launch_split_rebase(const BatchDev& b, const int64_t* split_rows, int32_t n_splits, int64_t* split_rp,
+                         hipStream_t st);
 
 }  // namespace fmhip

@@ -1614,6 +1614,36 @@ __global__ __launch_bounds__(kBlock) void k_select_rows(const int64_t* __restric
   }
 }
 
+// fm_batch_create_splits: a dataset laid out split after split (split_rows [n_splits + 1] row offsets,
+// the randomSplit splits of the cached dfData in iteration order, FactorizationMachinesSGD.scala:93,
+// 111-112).  Each split's rows get their own row_ptr, rebased to the split's first entry, at
+// split_rp[split_rows[s] + s ..= split_rows[s + 1] + s] (zeroed beforehand, so an empty split's one
+// slot is 0), and each entry's sample index becomes relative to its split's first row: a split is
+// then a mini-batch in place (fm_batch_split_view), with no gather.  One team of 16 lanes per row.
+__global__ __launch_bounds__(kBlock) void k_split_rebase(const int64_t* __restrict__ rp, const int64_t* __restrict__ split_rows,
+                                                        int32_t n_splits, int64_t B, uint2* __restrict__ ent,
+                                                        int64_t* __restrict__ split_rp) {
+  constexpr int T = 16;
+  const int tl = threadIdx.x % T;
+  const int64_t gtid = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int64_t nthreads = (int64_t)gridDim.x * kBlock;
+  for (int64_t s = gtid / T; s < B; s += nthreads / T) {
+    int lo = 0, hi = n_splits;  // the split holding row s: split_rows[lo] <= s < split_rows[lo + 1]
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) / 2;
+      if (split_rows[mid] <= s) lo = mid;
+      else hi = mid;
+    }
+    const int64_t r0 = split_rows[lo], eb = rp[r0];
+    const int64_t e0 = rp[s], e1 = rp[s + 1];
+    if (tl == 0) {
+      split_rp[s + lo] = e0 - eb;
+      if (s + 1 == split_rows[lo + 1]) split_rp[s + 1 + lo] = e1 - eb;
+    }
+    for (int64_t e = e0 + tl; e < e1; e += T) ent[e].x = (uint32_t)(s - r0);
+  }
+}
+
 // ------------------------------------------------------- singleton split (fm_batch_prepare)
 // The sorted view of a batch -> the entries of its runs of two or more (stable: the order the
 // segmented update needs) and the number of singleton runs.  One wave per chunk of 1024 sorted
@@ -1747,96 +1777,6 @@ __global__ __launch_bounds__(kBlock) void k_split_scatter(const uint32_t* __rest
   }
 }
 
-// The sharded owner's singleton rows (fused owner step, fm_shard_owner_update): after the S rows
-// came back, a pass over the received entries in pair order -- each pair's S record (S, r, yhat)
-// read once, sequentially -- updates every entry's row whose header carries no multi tag (a feature
-// with one entry among everything this owner received), with the segmented update's arithmetic on
-// the same fp32 S, r and yhat (the fused forward's, fm_kernels.hip "Singleton rows"), so those
-// rows come out bitwise as the unfused owner step leaves them; the segmented update then walks the
-// multi runs only.  One team of 16 lanes per pair, GS lanes per row (kp <= 16).
-template <int GS>
-__global__ __launch_bounds__(kBlock) void k_owner_single(TableView T, const int64_t* __restrict__ pair_ptr, int64_t P,
-                                                        const uint32_t* __restrict__ slot, const uint2* __restrict__ ent,
-                                                        const float* __restrict__ srec, int rec, StepParams sp) {
-  constexpr int TEAM = 16, RPP = TEAM / GS;
-  const int tl = threadIdx.x % TEAM, g = tl % GS, rs = tl / GS;
-  const int kp = T.kp;
-  const bool qok = g * 4 < kp;
-  const int span = 4 + ((16 - ((kp + 4) & 15)) & 15);  // header + zero pad of its 64-B granule
-  const float lamf = (float)sp.lam;
-  for (int64_t p = ((int64_t)blockIdx.x * kBlock + threadIdx.x) / TEAM; p < P; p += (int64_t)gridDim.x * (kBlock / TEAM)) {
-    const int64_t e0 = pair_ptr[p], e1 = pair_ptr[p + 1];
-    const float* sr = srec + p * rec;
-    const float4 Sq = qok ? reinterpret_cast<const float4*>(sr)[g] : make_float4(0.f, 0.f, 0.f, 0.f);
-    const float2 ry = *reinterpret_cast<const float2*>(sr + kp);
-    const double rj = (double)ry.x, yh = (double)ry.y;
-    for (int64_t eb = e0 + rs; eb < e1; eb += 2 * RPP) {
-      // two entries in flight per lane group: their headers first, then the V quads of the untagged
-      // ones only (a multi run's row costs this pass one header read, not the whole record)
-      uint32_t ids[2];
-      float xs2[2];
-      RowHdr hs[2];
-      float4 vs[2];
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int64_t e = eb + j * RPP;
-        const bool ok = e < e1;
-        ids[j] = ok ? slot[e] : 0u;
-        xs2[j] = ok ? __uint_as_float(ent[e].y) : 0.f;
-        hs[j] = ok ? *T.hdr(ids[j]) : RowHdr{0.f, -1, 0.0};
-        if (!ok) hs[j].t = multi_tag(sp.epoch, false);  // nothing to update
-      }
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-        vs[j] = !is_multi(hs[j].t, sp.epoch) && qok ? reinterpret_cast<const float4*>(T.v(ids[j]))[g]
-                                                     : make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const RowHdr h = hs[j];
-        if (is_multi(h.t, sp.epoch)) continue;
-        float* r = T.v(ids[j]);
-        const float4 vq = vs[j];
-        const double xd = (double)xs2[j];
-        const float acf = (float)(sp.cumE - h.cum);  // pending L1 of the row
-        const double t = xd * rj, b = (xd * xd) * rj;
-        const double gwe = (xd - 1.0) * yh + rj;  // x yhat - y (SGD.scala:145)
-        if (qok) {
-          const float4 v = shrink4f(vq, acf);
-          const double g0 = fma((double)Sq.x, t, 0.0) - (double)v.x * b, g1 = fma((double)Sq.y, t, 0.0) - (double)v.y * b;
-          const double g2 = fma((double)Sq.z, t, 0.0) - (double)v.z * b, g3 = fma((double)Sq.w, t, 0.0) - (double)v.w * b;
-          const float4 u = make_float4((float)fma(g0, -sp.scale_v, (double)v.x), (float)fma(g1, -sp.scale_v, (double)v.y),
-                                       (float)fma(g2, -sp.scale_v, (double)v.z), (float)fma(g3, -sp.scale_v, (double)v.w));
-          st_row4(r + 4 * g, shrink4f(u, lamf));
-        }
-        for (int i = 4 * g; i < span; i += 4 * GS) {  // the header and the zero pad of its granule
-          float4 hq = make_float4(0.f, 0.f, 0.f, 0.f);
-          if (i == 0) {
-            RowHdr o;
-            o.w = upd_w(shrink1f(h.w, acf), 0.0 + gwe, sp);  // SGD.scala:150, :171
-            o.t = sp.epoch + 1;
-            o.cum = sp.cum_next;
-            hq = *reinterpret_cast<const float4*>(&o);
-          }
-          st_row4(r + kp + i, hq);
-        }
-      }
-    }
-  }
-}
-
-void launch_owner_singletons(const TableView& T, const int64_t* pair_ptr, int64_t P, const uint32_t* slot,
-                             const uint2* ent, const float* srec, int rec, const StepParams& sp, hipStream_t st) {
-  if (P <= 0) return;
-  FM_REQUIRE(T.kp <= 16, "the owner singleton pass serves kp <= 16");
-  const unsigned grid = grid_for(P * 16, kBlock, 256 * 8);
-  switch (T.kp / 4) {
-    case 1: hipLaunchKernelGGL(k_owner_single<1>, dim3(grid), dim3(kBlock), 0, st, T, pair_ptr, P, slot, ent, srec, rec, sp); break;
-    case 2: hipLaunchKernelGGL(k_owner_single<2>, dim3(grid), dim3(kBlock), 0, st, T, pair_ptr, P, slot, ent, srec, rec, sp); break;
-    default: hipLaunchKernelGGL(k_owner_single<4>, dim3(grid), dim3(kBlock), 0, st, T, pair_ptr, P, slot, ent, srec, rec, sp); break;
-  }
-  FM_HIP_CHECK(hipGetLastError());
-}
-
 // The fused step's tags (main stream, at the step: they name its epoch): the first entry of every
 // run of the batch's multi view (prepared by fm_batch_prepare, n_dev[0] entries) writes the epoch's
 // multi tag into its row's header (4 B read-modify-write of one row per multi run).
@@ -1897,6 +1837,16 @@ void launch_select_rows(const BatchDev& src, const int64_t* rows, const int64_t*
                      src.row_ptr.as<int64_t>(), src.col.as<uint32_t>(), src.xs.as<float>(), src.label.as<double>(), rows,
                      row_ptr_in, B, dst.row_ptr.as<int64_t>(), dst.label.as<double>(), dst.col.as<uint32_t>(),
                      dst.ent.as<uint2>(), dst.xs.as<float>());
+  FM_HIP_CHECK(hipGetLastError());
+}
+
+void launch_split_rebase(const BatchDev& b, const int64_t* split_rows, int32_t n_splits, int64_t* split_rp,
+                         hipStream_t st) {
+  const int64_t B = b.n_rows;
+  FM_HIP_CHECK(hipMemsetAsync(split_rp, 0, sizeof(int64_t) * (B + n_splits), st));
+  if (B == 0) return;
+  hipLaunchKernelGGL(k_split_rebase, dim3(grid_for(B * 16, kBlock, 256 * 8)), dim3(kBlock), 0, st,
+                     b.row_ptr.as<int64_t>(), split_rows, n_splits, B, b.ent.as<uint2>(), split_rp);
   FM_HIP_CHECK(hipGetLastError());
 }
 

@@ -603,12 +603,6 @@ int fm_shard_owner_prepare(fm_ctx* ctx, fm_batch* b, const void* recv_slot, cons
       FM_HIP_CHECK(hipGetLastError());
     }
     FM_HIP_CHECK(hipEventRecord(S.ready_fwd, st));
-    // the fused owner step (fm_shard_owner_update): the slot sort keeps only the runs of two or more
-    S.split = owner_fuse(ctx);
-    if (S.split) {
-      S.split_n.ensure(2 * sizeof(int64_t));
-      if (n == 0) FM_HIP_CHECK(hipMemsetAsync(S.split_n.p, 0, 2 * sizeof(int64_t), st));
-    }
     if (n > 0) {
       // the update's grouping: received entries sorted by slot (stable: source rank, then CSR order)
       S.skeys.ensure(sizeof(uint32_t) * n);
@@ -617,20 +611,10 @@ int fm_shard_owner_prepare(fm_ctx* ctx, fm_batch* b, const void* recv_slot, cons
       const uint2* sv = nullptr;
       const uint32_t* keys = reinterpret_cast<const uint32_t*>(recv_slot);
       const int kb = bits_for(std::max<int64_t>(ctx->rows - 1, 1));
-      int64_t* split_out = S.split ? S.split_n.as<int64_t>() : nullptr;
       if (!(bucket_on(ctx, n) &&
             bucket_sort_pairs64(ctx->side_sort, keys, ent2, n, kb, st, S.skeys.as<uint32_t>(), S.sents.as<uint2>(),
-                                split_out))) {
-        if (S.split) {
-          S.fkeys.ensure(sizeof(uint32_t) * n);
-          S.fents.ensure(sizeof(uint2) * n);
-          radix_sort_pairs64(ctx->side_sort, keys, ent2, n, kb, st, &sk, &sv, S.fkeys.as<uint32_t>(), S.fents.as<uint2>());
-          launch_split(S.fkeys.as<uint32_t>(), S.fents.as<uint2>(), n, ctx->split_work, S.skeys.as<uint32_t>(),
-                       S.sents.as<uint2>(), split_out, st);
-        } else {
-          radix_sort_pairs64(ctx->side_sort, keys, ent2, n, kb, st, &sk, &sv, S.skeys.as<uint32_t>(), S.sents.as<uint2>());
-        }
-      }
+                                nullptr)))
+        radix_sort_pairs64(ctx->side_sort, keys, ent2, n, kb, st, &sk, &sv, S.skeys.as<uint32_t>(), S.sents.as<uint2>());
     }
     FM_HIP_CHECK(hipEventRecord(S.ready_upd, st));
     ctx->prof_end("owner_prepare", e0, st);
@@ -804,19 +788,13 @@ int fm_shard_owner_update(fm_ctx* ctx, fm_batch* b, const void* s_recv, int32_t 
       FM_HIP_CHECK(hipGetLastError());
       src = SegSource{ctx->work.S.as<float>(), rec, reinterpret_cast<const float2*>(ctx->work.S.as<float>() + kp), rec / 2};
     }
-    FM_REQUIRE(!S.split || ctx->epoch < (1 << 29), "epoch count beyond the multi tags' range (2^29 steps)");
-    if (S.split && S.P > 0) {
-      // fused owner step: the multi runs' rows tagged with this epoch, the singleton rows updated pair
-      // by pair from their S records, then the segmented update over the multi runs only
-      const TableView T = ctx->view();
-      launch_tag_runs(T, S.skeys.as<uint32_t>(), S.split_n.as<int64_t>(), n, p.epoch, st);
-      launch_owner_singletons(T, S.pair_ptr.as<int64_t>(), S.P, S.recv_slot, S.recv_ent, src.S, (int)src.s_stride, p, st);
-      src.n_dev = S.split_n.as<int64_t>();
-    }
     launch_segment_update(ctx->view(), n, src, ctx->work, p, S.skeys.as<uint32_t>(), S.sents.as<uint2>(),
                           S.loss_blocks, stats, st);
     ctx->prof_end("owner_update", e0, st);
     FM_HIP_CHECK(hipEventRecord(S.last_use, st));
+    // the iteration's last main-stream read of this rank's batch (its combine read the labels before
+    // this): a refill of the batch (fm_batch_from_rows, copy stream) waits for it
+    if (b->last_use) FM_HIP_CHECK(hipEventRecord(b->last_use, st));
     ctx->epoch += 1;
     ctx->cum_host.push_back(p.cum_next);
     S.prepared = false;

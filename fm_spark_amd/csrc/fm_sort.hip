@@ -103,7 +103,7 @@ __device__ __forceinline__ bool tile_geo(TileGeo& g, int64_t n, int64_t ntiles, 
 template <int RB, bool BIG = false>
 __global__ __launch_bounds__(kBlock) void k_radix_count(const uint32_t* __restrict__ keys, int64_t n, int shift,
                                                         uint32_t* __restrict__ counts, int64_t ntiles,
-                                                        BigPlan bp) {
+                                                        BigPlan bp, bool vec) {
   constexpr int R = 1 << RB;
   constexpr uint32_t M = R - 1;
   __shared__ uint32_t hist[R];
@@ -112,7 +112,9 @@ __global__ __launch_bounds__(kBlock) void k_radix_count(const uint32_t* __restri
   for (int d = threadIdx.x; d < R; d += kBlock) hist[d] = 0;
   lds_barrier();
   const int64_t base = g.base;
-  if (!BIG && base + kTile <= g.end) {  // segments start anywhere: no uint4 reads
+  // uint4 reads of whole tiles when the keys are 16-byte aligned (a split view of a dataset starts
+  // anywhere; segments of the big path too)
+  if (!BIG && vec && base + kTile <= g.end) {
     const uint4* k4 = reinterpret_cast<const uint4*>(keys + base);
 #pragma unroll
     for (int i = 0; i < kTile / (4 * kBlock); ++i) {
@@ -173,6 +175,32 @@ __global__ __launch_bounds__(kBlock) void k_radix_chunk_scan(uint32_t* __restric
   }
 #pragma unroll
   for (int i = 0; i < D; ++i) csum[(int64_t)blockIdx.x * R + threadIdx.x + i * kBlock] = run[i];
+}
+
+// The same on 256-thread blocks for the LSD passes: block (c, slice) takes tiles [16 c, 16 c + 16) of
+// the 256 digits of its slice, one digit per thread -- a small block finds room on a CU beside the
+// step's and the sort's blocks sooner (c3 0.964-0.967 ms per step against 0.967-0.971 with one
+// 512-thread block per chunk, c2 0.167-0.173 against 0.170-0.176, c5 within the noise; three
+// alternating reps, profiles/r05_b/ab)
+template <int RB>
+__global__ __launch_bounds__(256) void k_radix_chunk_scan256(uint32_t* __restrict__ counts, int64_t ntiles,
+                                                             uint32_t* __restrict__ csum) {
+  constexpr int R = 1 << RB;
+  constexpr int TB = R < 256 ? R : 256;
+  constexpr int S = R / TB;  // digit slices
+  const int64_t c = blockIdx.x / S;
+  const int d = (int)(blockIdx.x % S) * TB + threadIdx.x;
+  const int64_t t0 = c * kChunk;
+  uint32_t v[kChunk];
+#pragma unroll
+  for (int j = 0; j < kChunk; ++j) v[j] = t0 + j < ntiles ? counts[(t0 + j) * R + d] : 0u;
+  uint32_t run = 0;
+#pragma unroll
+  for (int j = 0; j < kChunk; ++j) {
+    if (t0 + j < ntiles) counts[(t0 + j) * R + d] = run;
+    run += v[j];
+  }
+  csum[c * R + d] = run;
 }
 
 // The count scan, level 2: 32 digits per 256-thread block (a small block finds room on a CU beside
@@ -850,10 +878,12 @@ static void radix_pass_impl(const uint32_t* kin, const P* vin, uint32_t* ko, P* 
   const int64_t nchunks = (ntiles + kChunk - 1) / kChunk;
   // (count and chunk scan fused into one kernel, a block walking its chunk's 16 tiles, measured
   // slower: 0.349 against 0.317 ms standalone)
+  const bool vec = (reinterpret_cast<uintptr_t>(kin) & 15u) == 0;
   hipLaunchKernelGGL(k_radix_count<RB>, dim3((unsigned)blocks_for_tiles(ntiles)), dim3(kBlock), 0, st, kin, n, shift,
-                     counts, ntiles, none);
-  hipLaunchKernelGGL((k_radix_chunk_scan<RB, false>), dim3((unsigned)nchunks), dim3(kBlock), 0, st, counts, ntiles, csum,
-                     none);
+                     counts, ntiles, none, vec);
+  constexpr int TB = (1 << RB) < 256 ? (1 << RB) : 256;
+  hipLaunchKernelGGL(k_radix_chunk_scan256<RB>, dim3((unsigned)(nchunks * ((1 << RB) / TB))), dim3(TB), 0, st, counts,
+                     ntiles, csum);
   hipLaunchKernelGGL(k_radix_chunk_top<false>, dim3((1u << RB) / 32), dim3(256), 0, st, csum, nchunks, 1 << RB,
                      w.digit_tot.as<uint32_t>(), none);
   hipLaunchKernelGGL((k_radix_scatter<P, RB>), dim3((unsigned)blocks_for_tiles(ntiles)), dim3(kBlock), 0, st, kin,
@@ -900,14 +930,8 @@ static void radix_sort_impl(SortWork& w, const uint32_t* keys_in, const P* vals_
   uint32_t* kbuf[2] = {w.keys_a.as<uint32_t>(), w.keys_b.as<uint32_t>()};
   P* vbuf[2] = {w.vals_a.as<P>(), w.vals_b.as<P>()};
   int which = 0;
-  // the count kernel reads keys as uint4 when the tile is full: needs 16-byte alignment
-  const bool aligned = (reinterpret_cast<uintptr_t>(keys_in) & 15u) == 0;
   for (int p = 0; p < passes; ++p) {
     const int shift = lo_bit + rb * p;
-    if (p == 0 && !aligned) {
-      FM_HIP_CHECK(hipMemcpyAsync(kbuf[1], keys_in, sizeof(uint32_t) * n, hipMemcpyDeviceToDevice, st));
-      kin = kbuf[1];
-    }
     const bool last = p == passes - 1 && final_keys != nullptr;
     uint32_t* ko = last ? final_keys : kbuf[which];
     P* vo = last ? final_vals : vbuf[which];
@@ -958,7 +982,7 @@ static void big_pass(const uint32_t* sk, const uint2* sv, uint32_t* dk, uint2* d
   const unsigned gb = (unsigned)blocks_for_tiles(big_tiles);
   const unsigned gc = (unsigned)((big_tiles + 1 + kChunk - 1) / kChunk);
   hipLaunchKernelGGL((k_radix_count<RB, true>), dim3(gb), dim3(kBlock), 0, st, sk, (int64_t)0, shift, counts, (int64_t)0,
-                     bp);
+                     bp, false);
   hipLaunchKernelGGL((k_radix_chunk_scan<RB, true>), dim3(gc), dim3(kBlock), 0, st, counts, (int64_t)0, csum, bp);
   hipLaunchKernelGGL(k_radix_chunk_top<true>, dim3((1u << RB) / 32), dim3(256), 0, st, csum, (int64_t)0, 1 << RB,
                      (uint32_t*)nullptr, bp);

@@ -49,6 +49,18 @@ class DeviceBatch:
         self._data = data  # the dataset stays alive while this batch's gather may be queued
         return self
 
+    def view_split(self, data: "DeviceBatch", split: int):
+        """Re-point this batch at split `split` of the split-ordered dataset `data`
+        (fm_batch_split_view: no copy, no device work); returns self."""
+        h = self.handle if self.handle else C.c_void_p()
+        N.check(self._lib.fm_batch_split_view(self.ctx.handle, data.handle, int(split), C.byref(h)),
+                "fm_batch_split_view")
+        self.handle = h
+        self.n_rows = int(self._lib.fm_batch_rows(h))
+        self.nnz = int(self._lib.fm_batch_nnz(h))
+        self._data = data  # the dataset outlives the view (its rows are borrowed)
+        return self
+
     def prepare(self):
         """Sort this batch by feature on the side stream ahead of its step (fm_batch_prepare)."""
         N.check(self._lib.fm_batch_prepare(self.ctx.handle, self.handle), "fm_batch_prepare")
@@ -205,6 +217,26 @@ class FMContext:
     # ------------------------------------------------------------------- stepping
     def batch(self, csr: N.CSRHost) -> DeviceBatch:
         return DeviceBatch(self, csr)
+
+    def batch_splits(self, csr: N.CSRHost, split_rows) -> DeviceBatch:
+        """A dataset laid out split after split (fm_batch_create_splits): split s = rows
+        [split_rows[s], split_rows[s + 1]) of csr; each split is then stepped in place through
+        split_view."""
+        sr = np.ascontiguousarray(split_rows, dtype=np.int64)
+        b = DeviceBatch(self, None)
+        h = C.c_void_p()
+        N.check(self._lib.fm_batch_create_splits(self.handle, C.byref(csr.c), len(sr) - 1, N.ptr(sr, C.c_int64),
+                                                 C.byref(h)), "fm_batch_create_splits")
+        b.handle = h
+        b.n_rows, b.nnz = csr.n_rows, csr.nnz
+        b.split_rows = sr
+        return b
+
+    def split_view(self, data: DeviceBatch, split: int, into: DeviceBatch | None = None) -> DeviceBatch:
+        """Split `split` of a dataset made by batch_splits as a mini-batch, in place (fm_batch_split_view);
+        `into` (a view of this context) is re-pointed instead of creating one."""
+        b = into if into is not None else DeviceBatch(self, None)
+        return b.view_split(data, split)
 
     def batch_from_rows(self, data: DeviceBatch, rows, into: DeviceBatch | None = None) -> DeviceBatch:
         """The mini-batch of rows `rows` of the resident dataset `data`, gathered on the device

@@ -368,15 +368,6 @@ class FactorizationMachinesSGD:
                         parallel=p["parallel"], n_gpus=p["nGpus"], devices=p["devices"], transport=p["transport"])
         if pipelined is None:
             pipelined = True
-        # dfData.cache() (:93): the exploded dataset uploaded once
-        data = ctx.batch(N.CSRHost(rp, col, val, labels)) if (pipelined or initial_tables is None) and len(labels) \
-            else None
-        if initial_tables is not None:
-            ctx.load_tables(*initial_tables)
-        elif len(col):
-            # createInitialModel (:224-241): the draw for every distinct active feature id, on the
-            # device over the whole dataset's entries
-            ctx.init_from_batch(data)
         # randomSplit(Array.fill(maxIter)(miniBatchFraction), 1234L) (:111-112)
         order_cols = []
         extra = None
@@ -398,8 +389,29 @@ class FactorizationMachinesSGD:
                                           extra=extra)
         # split i's rows in per-partition sorted order (the order Spark's sampled partitions keep)
         splits = [order[split_of[order] == i] for i in range(p["maxIter"])]
+        data = None
+        if pipelined and len(labels):
+            # dfData.cache() (:93): the exploded dataset uploaded once, laid out split after split (the
+            # rows no split samples last, for createInitialModel), so every iteration's mini-batch is a
+            # contiguous range of it, stepped in place (fm_batch_split_view)
+            rest = order[split_of[order] < 0]
+            lay = np.concatenate(splits + [rest]).astype(np.int64)
+            split_rows = np.concatenate([[0], np.cumsum([len(r) for r in splits] + [len(rest)])])
+            data = ctx.batch_splits(_select_csr(rp, col, val, labels, lay), split_rows)
+        elif initial_tables is None and len(labels):
+            data = ctx.batch(N.CSRHost(rp, col, val, labels))
+        if initial_tables is not None:
+            ctx.load_tables(*initial_tables)
+        elif len(col):
+            # createInitialModel (:224-241): the draw for every distinct active feature id, on the
+            # device over the whole dataset's entries
+            ctx.init_from_batch(data)
         if pipelined:
-            run_minibatch_sgd_resident(ctx, data, splits, p["stepSize"], p["regParam"])
+            if data is not None:
+                run_minibatch_sgd_splits(ctx, data, p["stepSize"], p["regParam"], n_iter=p["maxIter"])
+            else:
+                for i in range(p["maxIter"]):
+                    log.warning("Iteration (%d/%d). The size of sampled batch is zero", i + 1, p["maxIter"])
         else:
             for i, rows in enumerate(splits):
                 it = i + 1  # iter = index + 1 (:119)
@@ -460,18 +472,69 @@ def run_minibatch_sgd_resident(ctx: FMContext, data, splits, step_size: float, r
         if j + 2 < len(work):
             gather(j + 2)  # copied and gathered on the copy stream behind step j - 1
     ctx.sync()
-    hist = ctx.loss_history()[e0:]
-    done = {i: float(hist[j]) for j, (i, _) in enumerate(work)}
-    for i in range(len(splits)):
-        if i in done:
-            log.info("Loss of Iteration (%d/%d): %s", i + 1, n_iter, done[i])
-        else:
-            log.warning("Iteration (%d/%d). The size of sampled batch is zero", i + 1, n_iter)
+    out = _log_losses(ctx, e0, [i for i, _ in work], len(splits), n_iter)
     if own:
         for b in bufs:
             if b is not None:
                 b.close()
-    return [done[i] for i, _ in work]
+    return out
+
+
+def _log_losses(ctx, e0, iters, n_splits, n_iter):
+    """The loss log lines of SGD.scala:134-139 (and the zero-size warning of :126-128) for splits
+    0 .. n_splits - 1, in iteration order, from the device's loss history of the executed iterations
+    `iters` (their steps start at epoch e0); returns their losses."""
+    hist = ctx.loss_history()[e0:]
+    done = {i: float(hist[j]) for j, i in enumerate(iters)}
+    for i in range(n_splits):
+        if i in done:
+            log.info("Loss of Iteration (%d/%d): %s", i + 1, n_iter, done[i])
+        else:
+            log.warning("Iteration (%d/%d). The size of sampled batch is zero", i + 1, n_iter)
+    return [done[i] for i in iters]
+
+
+def run_minibatch_sgd_splits(ctx: FMContext, data, step_size: float, reg_param: float, n_iter: int | None = None,
+                             bufs: list | None = None):
+    """The foldLeft of runMiniBatchSGD (FactorizationMachinesSGD.scala:114-211) over a dataset kept on
+    the device laid out split after split (`data`, FMContext.batch_splits: dfData.cache() at :93 with
+    the randomSplit splits of :111-112 in iteration order): iteration i steps split i in place
+    (fm_batch_split_view re-points one of two batches used in turn -- no copy, no gather), sorted on
+    the side stream (fm_batch_prepare) while iteration i - 1 steps; every step only enqueues.  An
+    empty split is skipped with the reference's warning (:126-128); the loss log lines (:134-139) are
+    written in iteration order after the loop.  n_iter: the iterations are splits 0 .. n_iter - 1
+    (default: every split; fit's dataset ends with a split of the rows no iteration samples and
+    passes maxIter).  `bufs`: a list of two views (or Nones) to re-point and leave open for the
+    caller.  Returns the loss sums of the executed iterations."""
+    sizes = np.diff(np.asarray(data.split_rows))
+    n_iter = len(sizes) if n_iter is None else int(n_iter)
+    if n_iter > len(sizes):
+        raise ValueError("n_iter exceeds the dataset's splits")
+    work = [i for i in range(n_iter) if sizes[i] > 0]
+    own = bufs is None
+    if own:
+        bufs = [None, None]
+    nb = len(bufs)
+
+    def view(j):
+        bufs[j % nb] = ctx.split_view(data, work[j], into=bufs[j % nb])
+
+    e0 = ctx.epoch
+    if work:
+        view(0)
+        bufs[0].prepare()
+    for j, i in enumerate(work):
+        ctx.step_batch(bufs[j % nb], i + 1, step_size, reg_param, sync=False)  # iter = index + 1 (:119)
+        if j + 1 < len(work):
+            view(j + 1)  # re-points the batch step j - 1 read (its sort waits for that step)
+            bufs[(j + 1) % nb].prepare()  # sorted on the side stream while this step runs
+    ctx.sync()
+    out = _log_losses(ctx, e0, work, n_iter, n_iter)
+    if own:
+        for b in bufs:
+            if b is not None:
+                b.close()
+    return out
 
 
 # fm.regParam, fm.dimFactorization, ...: the Param handles spark.ml tuning keys grids by

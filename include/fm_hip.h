@@ -82,9 +82,9 @@ typedef struct fm_batch fm_batch;
  *                k <= 16 takes the fused step -- the forward updates every row whose feature has one
  *                entry in the batch, the segmented update only the rest (the same table as the
  *                unfused step within fp64 summation order); FM_FUSE_DEFAULT (0): the same, for tables
- *                larger than the 256-MB Infinity Cache; FM_FUSE_OFF: never.  A row-sharded
- *                context's owners take the fused owner step with FM_FUSE_ON only (it measured
- *                slower than the unfused owner step at c3).
+ *                larger than the 256-MB Infinity Cache; FM_FUSE_OFF: never.  Multi-GPU contexts
+ *                never fuse (a sharded owner's fused step measured slower than the unfused one at
+ *                R = 8 and at world 1).
  * xchg_chunks  : sharded step with R > 1: the owners' partial pass runs in this many chunks, each
  *                sent while the next is computed (0 = the default, 4; 1 = one pass then one
  *                all-to-all; at most 64).  Every process of a job must pass the same value.
@@ -157,6 +157,8 @@ int fm_set_stream(fm_ctx* ctx, void* hip_stream);
  * step: fm_batch_prepare, fm_shard_route, fm_shard_owner_prepare.  NULL = the context's own
  * non-blocking side stream (the default). */
 int fm_set_side_stream(fm_ctx* ctx, void* hip_stream);
+/* Wait for everything the context has enqueued: its step stream, its side stream (preparations) and
+ * its copy stream (fm_step uploads, fm_batch_from_rows gathers); a multi-GPU context, every rank's. */
 int fm_sync(fm_ctx* ctx);
 /* Pre-size the per-step workspace so no step allocates. */
 int fm_reserve(fm_ctx* ctx, int64_t max_rows, int64_t max_nnz);
@@ -206,17 +208,36 @@ int fm_batch_prepare(fm_ctx* ctx, fm_batch* batch);
  * data: a batch of this context made by fm_batch_create (the library keeps its row_ptr on the host
  * too, so the result is sized without a device read; the host pass runs on a pool of host threads).  *out == NULL: a new
  * batch is created; otherwise *out (a batch of this context, not data) is refilled in place.  The
- * gather runs on the context's side stream behind every queued step that reads *out, and the host
- * returns once it is enqueued (rows is copied); steps, fm_batch_prepare, fm_predict_batch and
- * fm_init_from_batch on the result are ordered after it.  data must stay alive until the gather has
- * run (fm_sync).  A multi-GPU context splits the selected rows contiguously over its local ranks,
+ * gather runs on the context's copy stream behind every queued step, preparation and sharded
+ * iteration that reads *out, and the host returns once it is enqueued (rows is copied); steps,
+ * fm_batch_prepare, fm_predict_batch and fm_init_from_batch on the result are ordered after it.
+ * data must stay alive until the gather has run: fm_sync waits for the context's step, side and
+ * copy streams.  A multi-GPU context splits the selected rows contiguously over its local ranks,
  * as fm_batch_create splits a host CSR; each rank gathers its share from its own copy of the
  * dataset (made on its device from the dataset's parts at the first selection). */
 int fm_batch_from_rows(fm_ctx* ctx, const fm_batch* data, const int64_t* rows, int64_t n, fm_batch** out);
+/* A training dataset laid out split after split, made resident once: the rows of csr are the
+ * randomSplit splits of the cached dfData concatenated in iteration order (FactorizationMachinesSGD
+ * .scala:93, 111-112), split s = rows [split_rows[s], split_rows[s + 1]) (split_rows [n_splits + 1],
+ * from 0 to n_rows; a last split may hold the rows no iteration samples), each split's rows in the
+ * order its mini-batch takes them.  Each split is then a mini-batch in place: fm_batch_split_view
+ * hands it to fm_batch_prepare / fm_step_batch with no copy and no gather (fm_batch_from_rows stays
+ * for row lists that are not laid out beforehand).  The dataset itself is not stepped or prepared
+ * (FM_ERR_ARG; its entries count their sample from their split's first row); fm_init_from_batch
+ * (createInitialModel over every row) and fm_batch_from_rows accept it.  A multi-GPU context cuts
+ * every split by rows over its local ranks, as it cuts a host CSR.  Synchronous (returns when the
+ * dataset is on the device). */
+int fm_batch_create_splits(fm_ctx* ctx, const fm_csr* csr, int32_t n_splits, const int64_t* split_rows,
+                           fm_batch** out);
+/* Split `split` of a dataset made by fm_batch_create_splits as a mini-batch: its rows, entries and
+ * labels where they lie in data (borrowed -- data must outlive the view and every step queued on
+ * it).  *out == NULL: a new batch; otherwise *out (a view, or a batch of this context that becomes
+ * one) is re-pointed in place -- host-only, no device work, so a loop re-points the batch it has just
+ * stepped while that step still runs (its next fm_batch_prepare waits for it). */
+int fm_batch_split_view(fm_ctx* ctx, const fm_batch* data, int32_t split, fm_batch** out);
 /* 1 if a batch prepared by fm_batch_prepare on this context takes the fused step (fm_config.fuse_single
- * and the library's rule: k <= 16, table above 256 MB unless FM_FUSE_ON; a row-sharded context's
- * owners take the fused owner step with FM_FUSE_ON and k <= 16; replicated contexts never fuse),
- * else 0; -1 for a null context. */
+ * and the library's rule: a single-table context, k <= 16, table above 256 MB unless FM_FUSE_ON;
+ * multi-GPU contexts never fuse), else 0; -1 for a null context. */
 int32_t fm_fuse_active(fm_ctx* ctx);
 int64_t fm_batch_rows(const fm_batch* b);
 int64_t fm_batch_nnz(const fm_batch* b);
@@ -338,9 +359,7 @@ int fm_shard_route(fm_ctx* ctx, fm_batch* batch, void* send_slot, void* send_ent
 /* Phase 1b (owner): the n received entries (source-rank major: src_entries[r] from rank r, which
  * sent src_pairs[r] pairs) -> their pair table and their order by slot (stable: source rank,
  * then CSR order), kept with `batch`.  No host synchronisation.  recv_slot / recv_ent must stay
- * valid until the main stream has run fm_shard_owner_update of this batch (the fused owner step --
- * fm_config.fuse_single FM_FUSE_ON, kp <= 16 -- reads them again there to update the rows of
- * features with one received entry pair by pair; otherwise until fm_shard_owner_forward). */
+ * valid until the main stream has run fm_shard_owner_forward of this batch. */
 int fm_shard_owner_prepare(fm_ctx* ctx, fm_batch* batch, const void* recv_slot, const void* recv_ent,
                            int64_t n, const int64_t* src_entries, const int64_t* src_pairs);
 /* Phase 2 (owner): partials_out[sum src_pairs] (source-major, sample order): per received pair

@@ -83,11 +83,12 @@ def test_concat_batches_splits_back_by_rows():
         r0 += p.n_rows
 
 
-def test_singleton_fraction():
+def test_batch_ids():
     from fm_spark_amd.data import Batch
 
     b = Batch(row_ptr=np.array([0, 3, 5]), col=np.array([1, 2, 3, 3, 4], np.int32), val=np.ones(5), label=np.zeros(2))
-    assert bench.singleton_fraction([b, b]) == pytest.approx(3 / 4)
+    U, single = bench.batch_ids(b)  # ids 1, 2, 3, 4; 3 of them with one entry
+    assert U == 4 and single == pytest.approx(3 / 4)
 
 
 def test_pmc_traffic_matches_workload_variant_and_mode():

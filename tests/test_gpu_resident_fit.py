@@ -1,10 +1,12 @@
 """GPU: the dataset kept on the device (dfData.cache(), FactorizationMachinesSGD.scala:93) and each
-randomSplit split gathered there from its row list (fm_batch_from_rows, :111-112), then the
-pipelined fit (the next split gathered and sorted on the side stream while the current one steps).
+randomSplit split (:111-112) taken from it: laid out split after split and stepped in place
+(fm_batch_create_splits / fm_batch_split_view), or gathered there from its row list
+(fm_batch_from_rows); then the pipelined fit (the next split sorted on the side stream while the
+current one steps).
 
-fm_batch_from_rows must give the batch a host CSR of the same rows gives -- the same rows, labels
-and entries in the same order, so every step on it is bitwise the host batch's step -- and the
-pipelined fit the synchronous fit's model and loss log."""
+A split view and fm_batch_from_rows must give the batch a host CSR of the same rows gives -- the same
+rows, labels and entries in the same order, so every step on it is bitwise the host batch's step --
+and the pipelined fit the synchronous fit's model and loss log."""
 
 import logging
 
@@ -198,6 +200,141 @@ def test_from_rows_on_a_multi_gpu_context(gpu, mode):
         for t, s in enumerate(sels, start=1):
             if use_rows:
                 into = ctx.batch_from_rows(d, s, into=into)
+                b = into
+            else:
+                b = ctx.batch(to_host(_select(data, s)))
+            b.prepare()
+            o = ctx.step_batch(b, t, 0.3, 1e-3)
+            out.append((o.loss_sum, o.n_rows, o.n_loss_rows, o.n_unique))
+        tab = ctx.export_tables()
+        ctx.close()
+        return out, tab
+
+    a, b = run(True), run(False)
+    assert a[0] == b[0]
+    for x, y in zip(a[1], b[1]):
+        assert np.array_equal(x, y)
+
+
+def _layout(data, sels):
+    """The rows of the selections concatenated (the split-ordered dataset) and their split offsets."""
+    lay = np.concatenate([np.asarray(x, dtype=np.int64) for x in sels]) if sels else np.zeros(0, np.int64)
+    return _select(data, lay), np.concatenate([[0], np.cumsum([len(x) for x in sels])]).astype(np.int64)
+
+
+@pytest.mark.parametrize("fuse,prepare", [(False, False), (False, True), (True, True)])
+def test_split_views_bitwise_equal_host_batch(gpu, fuse, prepare):
+    """A dataset laid out split by split, each split stepped in place through a view re-pointed in
+    turn (ragged splits, an empty one, repeated rows, a last split never stepped): every step bitwise
+    the one on the host CSR of the same rows, and the view's predictions those of the host rows."""
+    from fm_spark_amd.engine import FMContext
+
+    F, k = 50_000, 16
+    data, ids, w, V = make_problem(1211, 6000, F, k, 12, empty_frac=0.1, hot=7)
+    rng = np.random.default_rng(4)
+    sels = [rng.permutation(6000)[:1500], np.sort(rng.choice(6000, 2000, replace=True)), np.arange(0),
+            rng.permutation(6000)[:700], np.arange(5990, 6000), np.arange(3000)]
+    steps = sels[:-1]
+    lay, split_rows = _layout(data, sels)
+
+    def run(views):
+        ctx = FMContext(F, k, fuse=fuse)
+        ctx.load_tables(ids, w, V)
+        d = ctx.batch_splits(to_host(lay), split_rows) if views else None
+        out, preds, into = [], [], None
+        for t, sel in enumerate(steps, start=1):
+            if views:
+                into = ctx.split_view(d, t - 1, into=into)
+                b = into
+            else:
+                b = ctx.batch(to_host(_select(data, sel)))
+            assert b.n_rows == len(sel)
+            preds.append(ctx.predict_batch(b, 0.0, 1.0) if len(sel) else None)
+            if prepare:
+                b.prepare()
+            o = ctx.step_batch(b, t, 0.3, 1e-3)
+            out.append((o.loss_sum, o.n_rows, o.n_loss_rows, o.n_unique, o.executed))
+        tab = ctx.export_tables()
+        ctx.close()
+        return out, preds, tab
+
+    a, b = run(True), run(False)
+    assert a[0] == b[0]
+    assert a[0][2][4] is False  # the empty split: FM_NOTHING_TO_DO
+    for x, y in zip(a[1], b[1]):
+        assert (x is None and y is None) or np.array_equal(x, y)
+    for x, y in zip(a[2], b[2]):
+        assert np.array_equal(x, y)
+
+
+def test_split_dataset_rules(gpu):
+    """The dataset itself is not stepped or prepared; a view's split index is checked; a view refilled
+    by fm_batch_from_rows (and a gathered batch turned into a view) steps as the host rows do;
+    createInitialModel over the split dataset draws exactly the rows a plain dataset draws."""
+    from fm_spark_amd._native import FMError
+    from fm_spark_amd.engine import FMContext
+
+    F, k = 3000, 8
+    data, ids, w, V = make_problem(1212, 900, F, k, 6)
+    sels = [np.arange(0, 300), np.arange(300, 900)[::-1]]
+    lay, split_rows = _layout(data, sels)
+    ctx = FMContext(F, k, seed=9)
+    d = ctx.batch_splits(to_host(lay), split_rows)
+    with pytest.raises(FMError, match="split views"):
+        ctx.step_batch(d, 1, 0.3, 1e-3)
+    with pytest.raises(FMError, match="split views"):
+        d.prepare()
+    with pytest.raises(FMError, match="split index"):
+        ctx.split_view(d, 2)
+    plain = ctx.batch(to_host(data))
+    with pytest.raises(FMError, match="fm_batch_create_splits"):
+        ctx.split_view(plain, 0)
+    # createInitialModel over either layout: the same rows, the same draws
+    n1 = ctx.init_from_batch(d)
+    ref = FMContext(F, k, seed=9)
+    n2 = ref.init_from_batch(ref.batch(to_host(data)))
+    assert n1 == n2
+    for x, y in zip(ctx.export_tables(), ref.export_tables()):
+        assert np.array_equal(x, y)
+    # view -> gathered batch -> view, stepped against the host rows
+    b = ctx.split_view(d, 1)
+    o1 = ctx.step_batch(b, 1, 0.3, 1e-3)
+    b = ctx.batch_from_rows(plain, sels[0], into=b)
+    o2 = ctx.step_batch(b, 2, 0.3, 1e-3)
+    b = ctx.split_view(d, 0, into=b)
+    o3 = ctx.step_batch(b, 3, 0.3, 1e-3)
+    r1 = ref.step(to_host(_select(data, sels[1])), 1, 0.3, 1e-3)
+    r2 = ref.step(to_host(_select(data, sels[0])), 2, 0.3, 1e-3)
+    r3 = ref.step(to_host(_select(data, sels[0])), 3, 0.3, 1e-3)
+    assert [(o.loss_sum, o.n_unique) for o in (o1, o2, o3)] == [(o.loss_sum, o.n_unique) for o in (r1, r2, r3)]
+    for x, y in zip(ctx.export_tables(), ref.export_tables()):
+        assert np.array_equal(x, y)
+    ctx.close()
+    ref.close()
+
+
+@pytest.mark.parametrize("mode", ["sharded", "replicated"])
+def test_split_views_on_a_multi_gpu_context(gpu, mode):
+    """fm_batch_create_splits on a 3-rank context (COPY transport on this GPU): every rank holds its
+    contiguous share of every split; each split view steps bitwise as the host CSR of the same rows;
+    createInitialModel over the split dataset (split by split through the owners, sharded) draws the
+    plain dataset's rows."""
+    from fm_spark_amd.engine import FMContext
+
+    F, k, R = 3000, 8, 3
+    data, ids, w, V = make_problem(1215, 2500, F, k, 9, hot=4)
+    rng = np.random.default_rng(13)
+    sels = [rng.permutation(2500)[:900], np.sort(rng.choice(2500, 1300)), rng.permutation(2500)[:2], np.arange(0)]
+    lay, split_rows = _layout(data, sels)
+
+    def run(views):
+        ctx = FMContext(F, k, parallel=mode, n_gpus=R, devices=[0] * R, transport="copy", seed=3)
+        d = ctx.batch_splits(to_host(lay), split_rows) if views else ctx.batch(to_host(lay))
+        ctx.init_from_batch(d)
+        into, out = None, []
+        for t, s in enumerate(sels[:3], start=1):
+            if views:
+                into = ctx.split_view(d, t - 1, into=into)
                 b = into
             else:
                 b = ctx.batch(to_host(_select(data, s)))

@@ -78,17 +78,17 @@ def _simulated_step(engines, batches, t, step_size, reg):
 
 # F = R * 2^s + 1 (513 at R = 2 and R = 4): owner 0 holds one slot more than the others, and that
 # slot (id F - 1, made hot) needs one more key bit than a rank with fewer rows would give it
-@pytest.mark.parametrize("R,k,F,hot,fuse", [(1, 8, 503, 11, None), (2, 16, 503, 11, None), (3, 5, 503, 11, None),
-                                            (4, 32, 503, 11, None), (2, 8, 513, 512, None), (4, 4, 513, 512, None),
-                                            (1, 16, 503, 11, True), (3, 8, 503, 11, True), (8, 16, 1031, 7, True)])
-def test_hip_shard_phases_match_single_table(gpu, R, k, F, hot, fuse):
-    """The fm_shard_* phases driven one by one (the all-to-alls done by slicing), unfused and, with
-    fuse on, the fused owner step (singleton rows updated pair by pair after the S exchange)."""
+@pytest.mark.parametrize("R,k,F,hot", [(1, 8, 503, 11), (2, 16, 503, 11), (3, 5, 503, 11), (4, 32, 503, 11),
+                                       (2, 8, 513, 512), (4, 4, 513, 512), (1, 16, 503, 11), (3, 8, 503, 11),
+                                       (8, 16, 1031, 7)])
+def test_hip_shard_phases_match_single_table(gpu, R, k, F, hot):
+    """The fm_shard_* phases driven one by one (the all-to-alls done by slicing) against the fp64
+    oracle step over the concatenated batches."""
     from fm_spark_amd._native import CSRHost
     from fm_spark_amd.distributed import HipShardEngine
 
     _, ids, w, V = make_problem(3, 1, F, k, 1)
-    engines = [HipShardEngine(F, k, r, R, fuse=fuse) for r in range(R)]
+    engines = [HipShardEngine(F, k, r, R) for r in range(R)]
     for e in engines:
         e.load_tables(ids, w, V)
     model = R_.Model.empty(F, k)
@@ -109,8 +109,7 @@ def test_hip_shard_phases_match_single_table(gpu, R, k, F, hot, fuse):
     np.testing.assert_allclose(np.concatenate(gV)[order], model.V[gi[order]], rtol=1e-5, atol=1e-8)
 
 
-@pytest.mark.parametrize("fuse", [False, True])
-def test_hip_shard_c3_r8_matches_single_table(gpu, fuse):
+def test_hip_shard_c3_r8_matches_single_table(gpu):
     """Config c3's table at R = 8 (100M hashed features, k = 16, owner = id % 8), eight ranks of
     32K synthetic rows each (the bench's generator), two iterations of the sharded phases
     against one single-table HIP step over the concatenated batches: losses, distinct counts
@@ -122,7 +121,7 @@ def test_hip_shard_c3_r8_matches_single_table(gpu, fuse):
 
     F, k, R, B = 100_000_000, 16, 8, 32768
     ref = FMContext(F, k, seed=5, init_sd=0.01)
-    engines = [HipShardEngine(F, k, r, R, fuse=fuse) for r in range(R)]
+    engines = [HipShardEngine(F, k, r, R) for r in range(R)]
     for t in (1, 2):
         parts = [synthetic_batch(B, F, batch_index=100 * t + r) for r in range(R)]
         cat = _concat([R_.CSR(p.row_ptr, p.col, p.val, p.label) for p in parts])

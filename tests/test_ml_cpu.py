@@ -140,3 +140,75 @@ def test_resident_loop_orders_gather_prepare_step_per_buffer(caplog):
             live[e[1]] = e[2]
         elif e[0] == "step":
             assert live.pop(e[1]) == e[2]
+
+
+def test_split_loop_orders_view_prepare_step_per_buffer(caplog):
+    """run_minibatch_sgd_splits' host schedule on a recording context: iteration i steps split i of
+    the split-ordered dataset through a view, prepared before its step; a view is re-pointed only
+    after the step that read it was enqueued; empty splits (and the trailing split of unsampled rows)
+    are not stepped, the empty ones logged with the reference's warning; losses in iteration order."""
+    import logging
+
+    import numpy as np
+
+    from fm_spark_amd.ml import run_minibatch_sgd_splits
+
+    events = []
+
+    class View:
+        def __init__(self, n):
+            self.id, self.open = n, True
+
+        def prepare(self):
+            events.append(("prepare", self.id, self.split))
+
+        def close(self):
+            self.open = False
+
+    class Data:
+        split_rows = np.array([0, 2, 2, 3, 6, 7, 7, 9, 10, 40])  # 8 iterations + 30 unsampled rows
+
+    class Ctx:
+        epoch = 3
+        made = []
+
+        def split_view(self, data, split, into=None):
+            b = into if into is not None else View(len(self.made))
+            if into is None:
+                self.made.append(b)
+            b.split = split
+            events.append(("view", b.id, split))
+            return b
+
+        def step_batch(self, b, it, step, reg, sync=True):
+            assert sync is False
+            events.append(("step", b.id, b.split, it))
+
+        def sync(self):
+            events.append(("sync",))
+
+        def loss_history(self):
+            return [None] * 3 + [10.0 * (j + 1) for j in range(64)]
+
+    ctx = Ctx()
+    with caplog.at_level(logging.WARNING):
+        out = run_minibatch_sgd_splits(ctx, Data(), 1.0, 0.0, n_iter=8)
+    work = [0, 2, 3, 4, 6, 7]
+    assert out == [10.0 * (j + 1) for j in range(len(work))]
+    assert len(ctx.made) == 2 and not any(b.open for b in ctx.made)
+    assert sum("size of sampled batch is zero" in r.getMessage() for r in caplog.records) == 2
+    steps = [e for e in events if e[0] == "step"]
+    assert [(e[2], e[3]) for e in steps] == [(i, i + 1) for i in work]
+    assert events[-1] == ("sync",)
+    for i in work:
+        v = events.index(next(e for e in events if e[0] == "view" and e[2] == i))
+        p = events.index(next(e for e in events if e[0] == "prepare" and e[2] == i))
+        s = events.index(next(e for e in events if e[0] == "step" and e[2] == i))
+        assert v < p < s
+    live = {}
+    for e in events:
+        if e[0] == "view":
+            assert e[1] not in live, "view re-pointed before its step"
+            live[e[1]] = e[2]
+        elif e[0] == "step":
+            assert live.pop(e[1]) == e[2]

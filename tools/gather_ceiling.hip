@@ -7,6 +7,15 @@
 // Every variant is its own kernel instantiation (the MODE argument only names it), launched 2 + 10
 // times; the tool prints the event time per launch; tools/gather_ceiling.py joins it with the
 // TCC_HIT + TCC_MISS counts of a rocprofv3 --pmc pass over the same binary.
+//
+// With a stream file (argv[2], tools/c3_stream.py: one c3 batch's row_ptr and feature ids in CSR
+// order, bit 31 = the id has one entry in the batch) two more variants replay c3's own forward
+// address stream: MODE 2 gathers its ids in CSR order (as the uniform variants do), MODE 3
+// (`gather_skel`) is the fused forward's memory skeleton without its arithmetic -- one wave per
+// sample, its row_ptr, ids and x read, every row's whole 128-B record gathered (8 lanes x 16 B, all
+// of a 39-entry sample's rows in flight), the singleton rows' records written back (one 8-lane
+// store each) and the sample's 128-B S record written.  Its time is the floor of the forward's
+// own access stream on this chip.
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -70,6 +79,75 @@ void run(const float4* tab, const uint32_t* idx, int64_t n, float4* out, hipStre
   CK(hipEventDestroy(b));
 }
 
+
+// MODE 3: the fused forward's memory skeleton over c3's own stream (see the header)
+template <int LPR, int U, int STRIDE, int MODE>
+__global__ __launch_bounds__(256) void gather_skel(float4* __restrict__ tab, const int64_t* __restrict__ rp,
+                                                   const uint32_t* __restrict__ col, const float* __restrict__ xs,
+                                                   int64_t B, float4* __restrict__ srec) {
+  constexpr int Q = STRIDE / 4;
+  constexpr int RPP = 64 / LPR;  // rows per pass of the wave
+  const int lane = threadIdx.x & 63;
+  const int g = lane % LPR, row_in = lane / LPR;
+  const int64_t wave = ((int64_t)blockIdx.x * 256 + threadIdx.x) / 64;
+  const int64_t nwaves = (int64_t)gridDim.x * 256 / 64;
+  for (int64_t s = wave; s < B; s += nwaves) {
+    const int64_t e0 = rp[s], e1 = rp[s + 1];
+    uint32_t id[U];
+    float x[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t e = e0 + u * RPP + row_in;
+      id[u] = e < e1 ? col[e] : 0xFFFFFFFFu;
+      x[u] = e < e1 ? xs[e] : 0.f;
+    }
+    float4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      v[u] = id[u] != 0xFFFFFFFFu ? tab[(int64_t)(id[u] & 0x7FFFFFFFu) * Q + g] : make_float4(0, 0, 0, 0);
+    float4 acc = make_float4(0, 0, 0, 0);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      acc.x += v[u].x * x[u];
+      acc.y += v[u].y * x[u];
+      acc.z += v[u].z * x[u];
+      acc.w += v[u].w * x[u];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (id[u] != 0xFFFFFFFFu && (id[u] >> 31)) {
+        float4 w = v[u];
+        w.x += 1e-7f * acc.x;
+        tab[(int64_t)(id[u] & 0x7FFFFFFFu) * Q + g] = w;
+      }
+    if (lane < Q) srec[s * Q + lane] = acc;
+  }
+}
+
+template <int LPR, int U, int STRIDE, int MODE>
+void run_skel(float4* tab, const int64_t* rp, const uint32_t* col, const float* xs, int64_t B, int64_t n,
+              float4* srec, hipStream_t st) {
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  const int grid = 2048;
+  for (int w = 0; w < 2; ++w)
+    hipLaunchKernelGGL((gather_skel<LPR, U, STRIDE, MODE>), dim3(grid), dim3(256), 0, st, tab, rp, col, xs, B, srec);
+  CK(hipEventRecord(a, st));
+  const int R = 10;
+  for (int r = 0; r < R; ++r)
+    hipLaunchKernelGGL((gather_skel<LPR, U, STRIDE, MODE>), dim3(grid), dim3(256), 0, st, tab, rp, col, xs, B, srec);
+  CK(hipEventRecord(b, st));
+  CK(hipEventSynchronize(b));
+  float ms;
+  CK(hipEventElapsedTime(&ms, a, b));
+  ms /= R;
+  printf("VARIANT gather<%d, %d, %d, %d> ms=%.5f rows=%ld\\n", LPR, U, STRIDE, MODE, ms, (long)n);
+  fflush(stdout);
+  CK(hipEventDestroy(a));
+  CK(hipEventDestroy(b));
+}
+
 int main(int argc, char** argv) {
   const int64_t rows = argc > 1 ? atoll(argv[1]) : 100000000;
   const int64_t n = 10223616;  // a c3 batch's entries (256K rows x 39)
@@ -102,6 +180,51 @@ int main(int argc, char** argv) {
       run<4, 8, 16, 1>(tab, idx, n, out, st);
       run<1, 8, 32, 1>(tab, idx, n, out, st);
     }
+  }
+  if (argc > 2) {  // c3's own stream (tools/c3_stream.py)
+    FILE* f = fopen(argv[2], "rb");
+    if (!f) {
+      printf("cannot open %s\n", argv[2]);
+      return 1;
+    }
+    int64_t hdr[2];
+    if (fread(hdr, sizeof(int64_t), 2, f) != 2) return 1;
+    const int64_t B = hdr[0], N = hdr[1];
+    if (N > n || B < 1) return 1;  // the index buffer holds a c3 batch's entries
+    std::vector<int64_t> hrp(B + 1);
+    std::vector<uint32_t> hcol(N);
+    std::vector<float> hxs(N);
+    if (fread(hrp.data(), sizeof(int64_t), B + 1, f) != (size_t)(B + 1) || fread(hcol.data(), 4, N, f) != (size_t)N ||
+        fread(hxs.data(), 4, N, f) != (size_t)N)
+      return 1;
+    fclose(f);
+    for (int64_t e = 0; e < N; ++e)
+      if ((int64_t)(hcol[e] & 0x7FFFFFFFu) >= rows) return 1;
+    int64_t* drp;
+    uint32_t* dcol;
+    float* dxs;
+    float4* srec;
+    CK(hipMalloc(&drp, 8 * (B + 1)));
+    CK(hipMalloc(&dcol, 4 * N));
+    CK(hipMalloc(&dxs, 4 * N));
+    CK(hipMalloc(&srec, 128 * B));
+    CK(hipMemcpy(drp, hrp.data(), 8 * (B + 1), hipMemcpyHostToDevice));
+    CK(hipMemcpy(dcol, hcol.data(), 4 * N, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dxs, hxs.data(), 4 * N, hipMemcpyHostToDevice));
+    int64_t nsingle = 0;
+    for (int64_t e = 0; e < N; ++e) {
+      nsingle += hcol[e] >> 31;
+      h[e] = hcol[e] & 0x7FFFFFFFu;
+    }
+    printf("STREAM rows=%ld entries=%ld singleton_entries=%ld\n", (long)B, (long)N, (long)nsingle);
+    CK(hipMemcpy(idx, h.data(), 4 * N, hipMemcpyHostToDevice));
+    run<4, 8, 32, 2>(tab, idx, N, out, st);  // c3's ids in CSR order: 64 B of each 128-B record
+    run<8, 4, 32, 2>(tab, idx, N, out, st);  // the whole record
+    run_skel<8, 5, 32, 3>(tab, drp, dcol, dxs, B, N, srec, st);  // the fused forward's memory skeleton
+    CK(hipFree(drp));
+    CK(hipFree(dcol));
+    CK(hipFree(dxs));
+    CK(hipFree(srec));
   }
   CK(hipFree(tab));
   CK(hipFree(out));

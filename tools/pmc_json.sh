@@ -1,5 +1,5 @@
 #!/bin/bash
-# profiles/pmc_*.json from the raw PMC passes of tools/r04_pmc2.sh (run here, on the passes merged back
+# profiles/pmc_*.json from the raw PMC passes of tools/pmc.sh (run here, on the passes merged back
 # under gpurun_out/): tools/pmc_json.sh <base dir> <tag> [config:sort ...]
 set -eu
 cd "$(dirname "$0")/.."

@@ -4,6 +4,11 @@ tensor slicing, as in tests/test_gpu_shard.py).  Shows the R = 8 shapes (about z
 (sample, owner) pair) that a world-1 run cannot.
 
   python tools/shard_sim_bench.py [--ranks 8] [--rows 262144] [--features 100000000] [--k 16] [--steps 5]
+                                  [--reps 3]
+
+--reps: repeated runs on the same host batches, each with fresh shard contexts.  (Round 5 timed the
+fused owner step here against the unfused one, alternating, at R = 8: 1.23-1.24 against 0.92-0.93 ms
+per rank-step, profiles/r05_a/sim8.log; the fused owner step was removed.)
 """
 
 import argparse
@@ -42,18 +47,25 @@ def main():
     ap.add_argument("--features", type=int, default=100_000_000)
     ap.add_argument("--k", type=int, default=16)
     ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--reps", type=int, default=1)
     a = ap.parse_args()
+    from fm_spark_amd.data import synthetic_batch
+
+    hb = [synthetic_batch(a.rows, a.features, batch_index=r) for r in range(a.ranks)]
+    for rep in range(a.reps):
+        run(a, hb, rep)
+
+
+def run(a, hb, rep):
     import torch
 
     from fm_spark_amd._native import CSRHost
-    from fm_spark_amd.data import synthetic_batch
     from fm_spark_amd.distributed import HipShardEngine
 
     R, F, k, B = a.ranks, a.features, a.k, a.rows
     engines = [HipShardEngine(F, k, r, R, seed=20261015) for r in range(R)]
     for e in engines:
         e.init_random_range(0, F)
-    hb = [synthetic_batch(B, F, batch_index=r) for r in range(R)]
     bs = [e.batch(CSRHost(b.row_ptr, b.col, b.val, b.label)) for e, b in zip(engines, hb)]
     W = engines[0].width
     kp = engines[0].kp
@@ -96,10 +108,18 @@ def main():
             x[0] += ms
             x[1] += n
     P = [int(sum(pair_cnt[r])) for r in range(R)]
-    print(f"R={R} rows/rank={B} pairs/rank={np.mean(P):.0f} entries/pair={B * 39 / np.mean(P):.2f} "
-          f"wire MB/rank/direction={np.mean(P) * W * 4 / 1e6:.1f}")
+    print(f"R={R} rep={rep} rows/rank={B} pairs/rank={np.mean(P):.0f} "
+          f"entries/pair={B * 39 / np.mean(P):.2f} wire MB/rank/direction={np.mean(P) * W * 4 / 1e6:.1f}")
+    owner = 0.0
     for name, (ms, n) in tot.items():
         print(f"  {name:14s} {ms / n:.3f} ms per rank-step")
+        if name.startswith("owner_") and name != "owner_prepare":
+            owner += ms / n
+    print(f"  owner phases (forward + update, critical path) {owner:.3f} ms per rank-step", flush=True)
+    for e in engines:
+        e.ctx.close()
+    del engines, bs
+    torch.cuda.synchronize()
 
 
 if __name__ == "__main__":
