@@ -89,9 +89,6 @@ def parse():
                    help="single table, k <= 16: the fused step (the forward updates the rows whose feature has one "
                         "entry in the batch; fm_config.fuse_single): auto = the library's default (tables larger "
                         "than the 256-MB Infinity Cache), on, off")
-    p.add_argument("--sort", default="default", choices=["default", "lsd", "bucket"],
-                   help="how a batch's entries are grouped by feature (fm_config.sort_algo): default = the library's "
-                        "choice (the bucket sort for batches of 2^20+ entries), lsd, bucket")
     p.add_argument("--trainer", default="lib", choices=["lib", "torch"],
                    help="N > 1: 'lib' = the multi-GPU fm_ctx, every exchange inside libfm_hip over RCCL (the "
                         "C-ABI path); 'torch' (torch.distributed.run only) = the torch.distributed test harness "
@@ -261,7 +258,7 @@ except (OSError, ValueError, KeyError, TypeError):
 
 
 def _pmc_files(F, k, B, fused, mode, world, group=None):
-    """The committed PMC files of this workload; with `group` ("lsd" / "bucket"), those counted
+    """The committed PMC files of this workload; with `group` ("lsd"), those counted
     with that grouping sort first, then those that do not say."""
     import glob
 
@@ -313,17 +310,6 @@ def requests_roof(req, seconds):
                               "the best variant, 40 % of the gathers on 1000 hot rows; and uniformly random rows)"}
 
 
-def grouping(sort, n, num_rows):
-    """Which sort groups a batch of n entries by feature slot (fm_capi.hip bucket_on, fm_sort.hip
-    bucket_hi_bits): "bucket" or "lsd"."""
-    kb = max(1, int(num_rows - 1).bit_length())
-    H = 9
-    while H < 11 and n // (1 << H) > 30 * 512 // 3:  # buckets of about a third of the 15K-entry LDS image
-        H += 1
-    fits = 0 < n < 2**32 - 1 and kb >= H + 1 and kb - H <= 18
-    return "bucket" if sort == "bucket" and fits else "lsd"
-
-
 def sort_passes(num_rows):
     """Digit passes of the feature-slot radix sort (fm_sort.hip digit_bits: at most 10-bit digits,
     spread evenly, never narrower than 9 bits)."""
@@ -333,41 +319,26 @@ def sort_passes(num_rows):
     return -(-kb // rb)
 
 
-def step_kernels(F, n, sort, fused):
+def step_kernels(F, fused):
     """Launches per single-table step of each kernel (fm_capi.hip step_impl / fm_batch_prepare,
-    fm_sort.hip): the forward, update and combine; the grouping sort's -- LSD: count / chunk scan /
-    chunk top / scatter per digit pass (+ the split kernels at the step, which tag the multi rows,
-    fused); bucket: the top-bit pass, the big path's one or two passes, the plan and the phase-2
-    kernel (+ the big path's split, the compaction and the tag pass, fused)."""
+    fm_sort.hip): the forward, update and combine; count / chunk scan / chunk top / scatter per
+    digit pass of the LSD sort (+ the split kernels at the step, which tag the multi rows, fused)."""
     ps = {"k_forward": 1, "k_segment_update": 1, "k_segment_combine": 1}
-    if grouping(sort, n, F) == "lsd":
-        passes = sort_passes(F)
-        if fused:  # the split at the step, its count pass writing the multi tags
-            ps.update({"k_split_count": 1, "k_split_scan": 1, "k_split_scatter": 1})
-    else:
-        if fused:
-            ps["k_tag_runs"] = 1
-        kb = max(1, int(F - 1).bit_length())
-        H = 9
-        while H < 11 and n // (1 << H) > 30 * 512 // 3:
-            H += 1
-        passes = 1 + (1 if kb - H <= 11 else 2)
-        ps.update({"k_big_plan": 1, "k_bucket_sort": 1})
-        if fused:
-            ps.update({"k_big_split_count": 1, "k_big_split_scan": 1, "k_big_split_write": 1,
-                       "k_bucket_offsets": 1, "k_bucket_compact": 1})
+    passes = sort_passes(F)
+    if fused:  # the split at the step, its count pass writing the multi tags
+        ps.update({"k_split_count": 1, "k_split_scan": 1, "k_split_scatter": 1})
     ps.update({"k_radix_count": passes, "k_radix_chunk_scan": passes, "k_radix_chunk_top": passes,
                "k_radix_scatter": passes})
     return ps
 
 
-def step_traffic(F, k, B, fused, n, sort):
+def step_traffic(F, k, B, fused):
     """Counted HBM bytes and L2 requests of one whole single-table step: every kernel's per-launch
     figures in the committed PMC passes of this workload times its launches per step (the file's
     "per_step" map when it has one, else step_kernels).  None unless every kernel of the step was
     counted."""
-    per_step = step_kernels(F, n, sort, fused)
-    for f, d in _pmc_files(F, k, B, fused, "single", 1, grouping(sort, n, F)):
+    per_step = step_kernels(F, fused)
+    for f, d in _pmc_files(F, k, B, fused, "single", 1, "lsd"):
         ks = d.get("kernels", {})
         ps = d.get("per_step", per_step)
         if all("traffic_bytes" in ks.get(kn, {}) for kn in ps):
@@ -551,7 +522,7 @@ def main():
     xg = None
     if mode == "single":
         ctx = FMContext(F, k, device=local_rank, seed=20261015, init_sd=INIT_SD,
-                        fuse={"auto": None, "on": True, "off": False}[args.fuse], sort=args.sort)
+                        fuse={"auto": None, "on": True, "off": False}[args.fuse])
         # launch on a torch stream of our own so torch events can bracket every step on it
         main_stream = torch.cuda.Stream()
         torch.cuda.set_stream(main_stream)
@@ -647,7 +618,7 @@ def main():
             cid = bytes(idt.tolist())
         ctx = FMContext(F, k, seed=20261015, init_sd=INIT_SD, parallel=par, n_gpus=L, devices=pl["devices"],
                         transport="rccl", n_procs=world if mode == "procs" else 1, proc_rank=rank, comm_id=cid,
-                        fuse={"auto": None, "on": True, "off": False}[args.fuse], sort=args.sort)
+                        fuse={"auto": None, "on": True, "off": False}[args.fuse])
         main_stream = None
         if L == 1:  # launch on a torch stream so torch events time each step on it
             main_stream = torch.cuda.Stream()
@@ -806,8 +777,7 @@ def main():
             "config": {"workload": f"{args.config}: {desc}", "num_features": F, "k": k, "batch_rows_per_gpu": B,
                        "global_batch": B * world, "nnz_per_row": z, "rows_updated_per_gpu": U_mean,
                        "step_size": STEP_SIZE, "reg_param": REG_PARAM, "parallelism": parallelism,
-                       "launch": mode,
-                       "grouping": grouping(args.sort, int(z * B), F // max(world, 1) if mode != "single" else F)},
+                       "launch": mode},
             "loss_sum_all_steps": float(np.sum(losses)),
         }
         if args.trainer == "lib" and not args.host_path and not args.no_prefetch:
@@ -881,7 +851,7 @@ def main():
                                      "achieved_GBs": step_bytes / (ms_per_step * 1e-3) / 1e9,
                                      "frac": step_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS}
             if mode == "single":
-                st_t, st_r, st_src = step_traffic(F, k, B, fused, int(z * B), args.sort)
+                st_t, st_r, st_src = step_traffic(F, k, B, fused)
                 if st_t:  # every kernel of the step, counted (PMC), against the step's time
                     line["step_roofline"].update(traffic=st_t, traffic_GBs=st_t / (ms_per_step * 1e-3) / 1e9,
                                                  traffic_frac=st_t / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS,

@@ -261,15 +261,6 @@ bool fuse_rule(const fm_ctx* ctx) {
 
 static bool fuse_on(const fm_ctx* ctx) { return ctx->cfg.shard_count == 1 && fuse_rule(ctx); }
 
-// The bucket sort (fm_sort.hip) for a batch of N entries of this context, or the LSD passes
-// (fm_config.sort_algo; both stable, so the step is bitwise the same)
-bool bucket_on(const fm_ctx* ctx, int64_t N) {
-  // the bucket sort on request only: in the step it measured slower than the LSD passes at c3, c2
-  // and c5 (its top-bit pass scatters 1024-2048 digits per tile, runs of 2-4 entries, and phase 2
-  // gathers payloads by index: more L2 requests than the passes it saves)
-  return ctx->cfg.sort_algo == FM_SORT_BUCKET && bucket_hi_bits(N, bits_for(ctx->rows - 1)) != 0;
-}
-
 static bool batch_fits(const fm_batch* b, const Staged& g) {
   return b->dev.row_ptr.bytes >= sizeof(int64_t) * (g.B + 1) &&
          b->dev.col.bytes >= sizeof(uint32_t) * std::max<int64_t>(g.N, 4) + 16 &&
@@ -388,38 +379,24 @@ int step_impl(fm_ctx* ctx, fm_batch* b, int32_t t, double step_size, double reg_
     FM_HIP_CHECK(hipEventRecord(ctx->ev_fork, ctx->stream));
     FM_HIP_CHECK(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
     hipEvent_t es = ctx->prof_begin(ctx->side);
-    if (bucket_on(ctx, N)) {
-      SortWork& sw = ctx->work.sort;
-      sw.ensure(N);
-      bucket_sort_pairs64(sw, b->dev.col.as<uint32_t>(), b->dev.ent.as<uint2>(), N, bits_for(ctx->rows - 1), ctx->side,
-                          sw.keys_b.as<uint32_t>(), sw.vals_b.as<uint2>(), nullptr);
-      skeys = sw.keys_b.as<uint32_t>();
-      sents = sw.vals_b.as<uint2>();
-    } else {
-      radix_sort_pairs64(ctx->work.sort, b->dev.col.as<uint32_t>(), b->dev.ent.as<uint2>(), N,
-                         bits_for(ctx->rows - 1), ctx->side, &skeys, &sents);
-    }
+    radix_sort_pairs64(ctx->work.sort, b->dev.col.as<uint32_t>(), b->dev.ent.as<uint2>(), N, bits_for(ctx->rows - 1),
+                       ctx->side, &skeys, &sents);
     ctx->prof_end("sort", es, ctx->side);
     FM_HIP_CHECK(hipEventRecord(ctx->ev_join, ctx->side));
   }
   hipEvent_t e0 = nullptr;
   FwdOut fx{};
   if (fused) {
-    // the batch's multi view (fm_batch_prepare, a step or more ahead on the side stream: sorted,
-    // singleton runs dropped)
+    // the batch's sorted view (fm_batch_prepare, a step ahead on the side stream) split here, on the
+    // main stream: its runs of two or more entries into the multi view, each multi run's row tagged
+    // with this step's epoch by the count pass as it finds the run (the split on the side stream with a
+    // separate tag pass at the step measured 0.968-0.971 against 0.924-0.931 ms per c3 step, three
+    // alternating reps, profiles/r04_i)
     FM_HIP_CHECK(hipStreamWaitEvent(ctx->stream, b->ready, 0));
-    // each multi run's row tagged with this step's epoch (so here, at the step, on the main stream):
-    // with the LSD view, by the split pass as it finds the runs; with the bucket sort's split view,
-    // by a pass over it
     e0 = ctx->prof_begin(ctx->stream);
-    if (b->split_at_step) {
-      launch_split(b->fkeys.as<uint32_t>(), b->fents.as<uint2>(), N, ctx->split_work, b->skeys.as<uint32_t>(),
-                   b->sents.as<uint2>(), b->split_n.as<int64_t>(), ctx->stream, &T, p.epoch);
-      ctx->prof_end("split", e0, ctx->stream);
-    } else {
-      launch_tag_runs(T, b->skeys.as<uint32_t>(), b->split_n.as<int64_t>(), N, p.epoch, ctx->stream);
-      ctx->prof_end("tag", e0, ctx->stream);
-    }
+    launch_split(b->fkeys.as<uint32_t>(), b->fents.as<uint2>(), N, ctx->split_work, b->skeys.as<uint32_t>(),
+                 b->sents.as<uint2>(), b->split_n.as<int64_t>(), ctx->stream, T, p.epoch);
+    ctx->prof_end("split", e0, ctx->stream);
     fx.fused = true;
   }
   e0 = ctx->prof_begin(ctx->stream);
@@ -470,8 +447,6 @@ int fm_create(const fm_config* cfg, fm_ctx** out) {
     FM_REQUIRE(cfg->init_sd >= 0.0, "init_sd must be >= 0");
     FM_REQUIRE(cfg->fuse_single == FM_FUSE_DEFAULT || cfg->fuse_single == FM_FUSE_ON || cfg->fuse_single == FM_FUSE_OFF,
                "fuse_single must be FM_FUSE_DEFAULT, FM_FUSE_ON or FM_FUSE_OFF");
-    FM_REQUIRE(cfg->sort_algo == FM_SORT_DEFAULT || cfg->sort_algo == FM_SORT_LSD || cfg->sort_algo == FM_SORT_BUCKET,
-               "sort_algo must be FM_SORT_DEFAULT, FM_SORT_LSD or FM_SORT_BUCKET");
     int ndev = 0;
     FM_HIP_CHECK(hipGetDeviceCount(&ndev));
     FM_REQUIRE(cfg->device >= 0 && cfg->device < ndev, "device ordinal out of range");
@@ -745,28 +720,18 @@ int fm_batch_prepare(fm_ctx* ctx, fm_batch* b) {
     const uint32_t* sk = nullptr;
     const uint2* sv = nullptr;
     b->split = fuse_on(ctx);
-    b->split_at_step = false;
     const int kb = bits_for(ctx->rows - 1);
     const uint32_t* col = b->dev.col.as<uint32_t>();
     const uint2* ent = b->dev.ent.as<uint2>();
     if (b->split) {
-      // the fused step's view: only the runs of two or more entries (skeys / sents), with
-      // {their count, the number of singleton runs} in split_n -- the bucket sort keeps them as it
-      // orders each bucket; the LSD passes leave the whole view (fkeys / fents) to the step's split
+      // the fused step's batch: the whole sorted view (fkeys / fents), which the step splits into the
+      // multi view (skeys / sents, {their count, the number of singleton runs} in split_n)
       b->split_n.ensure(2 * sizeof(int64_t));
-      if (!(bucket_on(ctx, N) && bucket_sort_pairs64(ctx->work.sort, col, ent, N, kb, ctx->side, b->skeys.as<uint32_t>(),
-                                                     b->sents.as<uint2>(), b->split_n.as<int64_t>()))) {
-        b->fkeys.ensure_slack(sizeof(uint32_t) * N);
-        b->fents.ensure_slack(sizeof(uint2) * N);
-        radix_sort_pairs64(ctx->work.sort, col, ent, N, kb, ctx->side, &sk, &sv, b->fkeys.as<uint32_t>(),
-                           b->fents.as<uint2>());
-        // the step splits this view on the main stream, its count pass tagging the multi rows: c3
-        // 0.924-0.931 ms per step against 0.968-0.971 with the split here on the side stream and a
-        // separate tag pass at the step (three alternating reps, profiles/r04_i)
-        b->split_at_step = true;
-      }
-    } else if (!(bucket_on(ctx, N) && bucket_sort_pairs64(ctx->work.sort, col, ent, N, kb, ctx->side,
-                                                          b->skeys.as<uint32_t>(), b->sents.as<uint2>(), nullptr))) {
+      b->fkeys.ensure_slack(sizeof(uint32_t) * N);
+      b->fents.ensure_slack(sizeof(uint2) * N);
+      radix_sort_pairs64(ctx->work.sort, col, ent, N, kb, ctx->side, &sk, &sv, b->fkeys.as<uint32_t>(),
+                         b->fents.as<uint2>());
+    } else {
       radix_sort_pairs64(ctx->work.sort, col, ent, N, kb, ctx->side, &sk, &sv, b->skeys.as<uint32_t>(),
                          b->sents.as<uint2>());
     }
@@ -1187,7 +1152,7 @@ int fm_vector_sum_by_key(fm_ctx* ctx, const int32_t* keys, int64_t n, const doub
     FM_HIP_CHECK(hipMemcpy(out_sums, dos.p, sizeof(double) * nu * k, hipMemcpyDeviceToHost));
     *n_out = nu;
     DevBuf* bufs[] = {&dk, &dvec, &dok, &dos, &drun, &dn, &sw.keys_a, &sw.keys_b, &sw.vals_a, &sw.vals_b,
-                      &sw.counts, &sw.digit_tot, &sw.bscratch, &sw.bstat, &sw.bplan};
+                      &sw.counts, &sw.digit_tot};
     for (auto* bb : bufs) bb->release();
     return FM_OK;
   });

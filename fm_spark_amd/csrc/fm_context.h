@@ -101,13 +101,13 @@ struct fm_batch {
   int64_t max_id = -1;
   DevBuf up;  // device image of the host staging (fm_capi.hip copy_staged)
   // feature-major view produced by fm_batch_prepare (consumed once by the next step): the whole
-  // sorted view, or -- split = true -- only the runs of two or more entries, split_n = {their
-  // count, the number of singleton runs} on the device (the fused step, fm_kernels.hip)
+  // sorted view in skeys / sents, or -- split = true, the fused step -- the whole sorted view in
+  // fkeys / fents, which the step splits into the runs of two or more entries (skeys / sents) with
+  // split_n = {their count, the number of singleton runs} on the device (fm_kernels.hip)
   DevBuf skeys, sents;
-  DevBuf fkeys, fents;  // the LSD-sorted whole view a split pass reduces to the multi view (bucket sort: unused)
+  DevBuf fkeys, fents;
   DevBuf split_n;
   bool split = false;
-  bool split_at_step = false;     // the LSD view in fkeys / fents, split (and tagged) by the step
   hipEvent_t ready = nullptr;     // recorded on the side stream after the prepared sort
   hipEvent_t last_use = nullptr;  // recorded on the main stream after a step read the batch
   bool prepared = false;
@@ -314,9 +314,7 @@ struct fm_ctx {
                       &route_sort.keys_a, &route_sort.keys_b, &route_sort.vals_a, &route_sort.vals_b,
                       &route_sort.counts, &route_sort.digit_tot,
                       &sh_okey, &sh_mask, &sh_tcnt, &sh_tot, &sh_pay, &sh_skey, &sh_ent2, &repl_cnt,
-                      &split_work.cnt, &split_work.off, &work.sort.bscratch, &work.sort.bstat, &work.sort.bplan,
-                      &side_sort.bscratch, &side_sort.bstat, &side_sort.bplan, &route_sort.bscratch,
-                      &route_sort.bstat, &route_sort.bplan};
+                      &split_work.cnt, &split_work.off};
     for (auto* b : bufs) b->release();
     if (own_stream && stream) (void)hipStreamDestroy(stream);
   }
@@ -391,11 +389,10 @@ inline int bits_for(int64_t max_value) {
 
 // shared host helpers (fm_capi.hip)
 // the fused step's rule (fm_config.fuse_single, kp <= 16, tables above 256 MB unless FUSE_ON) for the
-// single table; and whether a batch of N entries takes the bucket sort (fm_config.sort_algo)
+// single table
 bool fuse_rule(const fm_ctx* ctx);
 // stream st waits until a batch refilled by fm_batch_from_rows has been gathered (copy stream)
 void wait_built(const fm_batch* b, hipStream_t st);
-bool bucket_on(const fm_ctx* ctx, int64_t N);
 void upload_batch(fm_ctx* ctx, const fm_csr* c, fm_batch* b, bool check_range);
 void reserve_work(fm_ctx* ctx, int64_t B, int64_t N);
 

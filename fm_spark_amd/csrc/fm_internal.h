@@ -89,8 +89,6 @@ struct DevBuf {
 // ------------------------------------------------------------------- radix sort
 struct SortWork {
   DevBuf keys_a, keys_b, vals_a, vals_b, counts, digit_tot;
-  DevBuf bscratch, bstat, bplan;  // bucket sort: the big path's middle pass, per-bucket counts and
-                                  // offsets, the big path's segments / tiles
   int64_t cap = 0;
   void ensure(int64_t n);
 };
@@ -107,14 +105,6 @@ void radix_sort_pairs64(SortWork& w, const uint32_t* keys_in, const uint2* vals_
                         int key_bits, hipStream_t st, const uint32_t** keys_out,
                         const uint2** vals_out, uint32_t* final_keys = nullptr,
                         uint2* final_vals = nullptr);
-// Two-phase bucket sort (fm_sort.hip) of the same pairs, the whole key of key_bits bits, into
-// final_keys / final_vals: split_out == nullptr -> the whole sorted view; else only the entries of
-// runs of two or more (the fused step's multi view), split_out[0] = their count, split_out[1] = the
-// number of singleton runs (device).  Returns false (nothing enqueued) when the sizes do not suit
-// it (bucket_hi_bits == 0): the caller sorts with the LSD passes.
-int bucket_hi_bits(int64_t n, int key_bits);
-bool bucket_sort_pairs64(SortWork& w, const uint32_t* keys_in, const uint2* vals_in, int64_t n, int key_bits,
-                         hipStream_t st, uint32_t* final_keys, uint2* final_vals, int64_t* split_out);
 // Stable sort by key bits [lo_bit, hi_bit) only (the bits below ride along), output written to
 // final_keys / final_vals.
 void radix_sort_pairs64_bits(SortWork& w, const uint32_t* keys_in, const uint2* vals_in, int64_t n, int lo_bit,
@@ -204,18 +194,15 @@ struct SegSource {
 void launch_segment_update(const TableView& T, const BatchDev& b, StepWork& w, const StepParams& p,
                            const uint32_t* skeys, const uint2* sents, int64_t n_fwd_blocks,
                            double* stats_out, hipStream_t st, float* emit = nullptr, const int64_t* n_dev = nullptr);
-// fm_batch_prepare's singleton split of a sorted view (fm_kernels.hip "Singleton rows"): the entries
-// of runs of two or more, in order, into mkeys / ments (capacity N); n_out[0] = their count,
-// n_out[1] = the number of singleton runs (device)
+// the fused step's singleton split of a prepared sorted view, at the step (fm_kernels.hip "Singleton
+// rows"): the entries of runs of two or more, in order, into mkeys / ments (capacity N); n_out[0] =
+// their count, n_out[1] = the number of singleton runs (device); each multi run's row in tag_T gets
+// the epoch's multi tag
 struct SplitWork {
   DevBuf cnt, off;
 };
 void launch_split(const uint32_t* skeys, const uint2* sents, int64_t N, SplitWork& sw, uint32_t* mkeys, uint2* ments,
-                  int64_t* n_out, hipStream_t st,
-                  const TableView* tag_T = nullptr, int32_t epoch = 0);
-// the fused step's multi tags for the runs of a prepared multi view (n_dev[0] <= n_max entries)
-void launch_tag_runs(const TableView& T, const uint32_t* mkeys, const int64_t* n_dev, int64_t n_max, int32_t epoch,
-                     hipStream_t st);
+                  int64_t* n_out, hipStream_t st, const TableView& tag_T, int32_t epoch);
 void launch_segment_update(const TableView& T, int64_t N, const SegSource& src, StepWork& w, const StepParams& p,
                            const uint32_t* skeys, const uint2* sents, int64_t n_loss_blocks, double* stats_out,
                            hipStream_t st, float* emit = nullptr);

@@ -1665,9 +1665,8 @@ __device__ __forceinline__ bool split_multi(const uint32_t* __restrict__ skeys, 
   return p < N && (prev == key || next == key);
 }
 
-// TAG (the split at the step's start, main stream): the first entry of every multi run also writes
-// the epoch's multi tag into its row's header
-template <bool TAG>
+// (the split at the step's start, main stream) the first entry of every multi run also writes the
+// epoch's multi tag into its row's header
 __global__ __launch_bounds__(kBlock) void k_split_count(const uint32_t* __restrict__ skeys, int64_t N,
                                                         uint2* __restrict__ cnt, int64_t nchunks, TableView T,
                                                         int32_t epoch) {
@@ -1680,7 +1679,7 @@ __global__ __launch_bounds__(kBlock) void k_split_count(const uint32_t* __restri
     const uint32_t key = p < N ? skeys[p] : 0xFFFFFFFEu;
     bool first = false;
     const bool m = split_multi(skeys, N, p, key, lane, &first);
-    if (TAG && m && first) {
+    if (m && first) {
       int32_t* t = &T.hdr(key)->t;
       *t = multi_tag(epoch, *t >= 0);
     }
@@ -1777,30 +1776,8 @@ __global__ __launch_bounds__(kBlock) void k_split_scatter(const uint32_t* __rest
   }
 }
 
-// The fused step's tags (main stream, at the step: they name its epoch): the first entry of every
-// run of the batch's multi view (prepared by fm_batch_prepare, n_dev[0] entries) writes the epoch's
-// multi tag into its row's header (4 B read-modify-write of one row per multi run).
-__global__ __launch_bounds__(kBlock) void k_tag_runs(const uint32_t* __restrict__ mkeys, const int64_t* __restrict__ n_dev,
-                                                    TableView T, int32_t epoch) {
-  const int64_t M = n_dev[0];
-  for (int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x; p < M; p += (int64_t)gridDim.x * kBlock) {
-    const uint32_t key = mkeys[p];
-    if (p == 0 || mkeys[p - 1] != key) {
-      int32_t* t = &T.hdr(key)->t;
-      *t = multi_tag(epoch, *t >= 0);
-    }
-  }
-}
-
-void launch_tag_runs(const TableView& T, const uint32_t* mkeys, const int64_t* n_dev, int64_t n_max, int32_t epoch,
-                     hipStream_t st) {
-  if (n_max <= 0) return;
-  hipLaunchKernelGGL(k_tag_runs, dim3(grid_for(n_max, kBlock, 256 * 8)), dim3(kBlock), 0, st, mkeys, n_dev, T, epoch);
-  FM_HIP_CHECK(hipGetLastError());
-}
-
 void launch_split(const uint32_t* skeys, const uint2* sents, int64_t N, SplitWork& sw, uint32_t* mkeys, uint2* ments,
-                  int64_t* n_out, hipStream_t st, const TableView* tag_T, int32_t epoch) {
+                  int64_t* n_out, hipStream_t st, const TableView& tag_T, int32_t epoch) {
   const int64_t nchunks = (N + kSplitChunk - 1) / kSplitChunk;
   sw.cnt.ensure_slack(sizeof(uint2) * (size_t)std::max<int64_t>(nchunks, 1));
   sw.off.ensure_slack(sizeof(int64_t) * (size_t)std::max<int64_t>(nchunks, 1));
@@ -1809,12 +1786,8 @@ void launch_split(const uint32_t* skeys, const uint2* sents, int64_t N, SplitWor
     return;
   }
   const unsigned blocks = (unsigned)((nchunks + kBlock / 64 - 1) / (kBlock / 64));
-  if (tag_T)
-    hipLaunchKernelGGL(k_split_count<true>, dim3(blocks), dim3(kBlock), 0, st, skeys, N, sw.cnt.as<uint2>(), nchunks,
-                       *tag_T, epoch);
-  else
-    hipLaunchKernelGGL(k_split_count<false>, dim3(blocks), dim3(kBlock), 0, st, skeys, N, sw.cnt.as<uint2>(), nchunks,
-                       TableView{}, 0);
+  hipLaunchKernelGGL(k_split_count, dim3(blocks), dim3(kBlock), 0, st, skeys, N, sw.cnt.as<uint2>(), nchunks, tag_T,
+                     epoch);
   hipLaunchKernelGGL(k_split_scan, dim3(1), dim3(kSplitScanNT), 0, st, sw.cnt.as<uint2>(), nchunks, sw.off.as<int64_t>(), n_out);
   hipLaunchKernelGGL(k_split_scatter, dim3(blocks), dim3(kBlock), 0, st, skeys, sents, N, sw.off.as<int64_t>(), nchunks,
                      mkeys, ments);

@@ -611,10 +611,7 @@ int fm_shard_owner_prepare(fm_ctx* ctx, fm_batch* b, const void* recv_slot, cons
       const uint2* sv = nullptr;
       const uint32_t* keys = reinterpret_cast<const uint32_t*>(recv_slot);
       const int kb = bits_for(std::max<int64_t>(ctx->rows - 1, 1));
-      if (!(bucket_on(ctx, n) &&
-            bucket_sort_pairs64(ctx->side_sort, keys, ent2, n, kb, st, S.skeys.as<uint32_t>(), S.sents.as<uint2>(),
-                                nullptr)))
-        radix_sort_pairs64(ctx->side_sort, keys, ent2, n, kb, st, &sk, &sv, S.skeys.as<uint32_t>(), S.sents.as<uint2>());
+      radix_sort_pairs64(ctx->side_sort, keys, ent2, n, kb, st, &sk, &sv, S.skeys.as<uint32_t>(), S.sents.as<uint2>());
     }
     FM_HIP_CHECK(hipEventRecord(S.ready_upd, st));
     ctx->prof_end("owner_prepare", e0, st);

@@ -39,14 +39,14 @@ class HipShardEngine:
     """The HIP phase functions of one rank (its own fm_ctx with shard_index = rank)."""
 
     def __init__(self, num_features: int, k: int, rank: int, world: int, *, device: int = 0, seed: int = 0,
-                 init_sd: float = 0.01, w0: float = 0.0, sort: str = "default"):
+                 init_sd: float = 0.01, w0: float = 0.0):
         import torch
 
         self.torch = torch
         self.device = torch.device("cuda", device)
         self.R = world
         self.ctx = FMContext(num_features, k, device=device, seed=seed, init_sd=init_sd, w0=w0, shard_index=rank,
-                             shard_count=world, sort=sort)
+                             shard_count=world)
         # launch on torch's streams so the C-ABI kernels and the collectives are stream-ordered:
         # the iteration on the current stream, batch-only preparation on a side stream
         self.main_stream = torch.cuda.current_stream(self.device)

@@ -50,9 +50,6 @@ extern "C" {
 #define FM_FUSE_DEFAULT 0 /* fm_config.fuse_single: the library's choice (tables above 256 MB) */
 #define FM_FUSE_ON 1
 #define FM_FUSE_OFF (-1)
-#define FM_SORT_DEFAULT 0 /* fm_config.sort_algo: the library's choice (the LSD sort; measured faster in the step) */
-#define FM_SORT_LSD 1     /* three-pass stable LSD radix sort */
-#define FM_SORT_BUCKET 2  /* two-phase bucket sort whenever the key width allows it */
 
 typedef struct fm_ctx fm_ctx;
 typedef struct fm_batch fm_batch;
@@ -88,12 +85,6 @@ typedef struct fm_batch fm_batch;
  * xchg_chunks  : sharded step with R > 1: the owners' partial pass runs in this many chunks, each
  *                sent while the next is computed (0 = the default, 4; 1 = one pass then one
  *                all-to-all; at most 64).  Every process of a job must pass the same value.
- * sort_algo    : how a single-table batch's entries are grouped by feature (FM_SORT_*): both sorts
- *                are stable, so the step is bitwise the same either way.  FM_SORT_DEFAULT takes the
- *                LSD passes; FM_SORT_BUCKET the bucket sort (one radix pass on the top bits, each
- *                bucket ordered in LDS, the oversized ones by LSD passes across the chip, the fused
- *                step's singleton split folded in), which sorts uniform keys faster alone but
- *                measured slower inside the c3 / c2 / c5 steps.
  * Zero-initialise the struct: every field's 0 is its default. */
 typedef struct fm_config {
   int64_t num_features;
@@ -113,7 +104,6 @@ typedef struct fm_config {
   uint8_t comm_id[128];
   int32_t fuse_single;
   int32_t xchg_chunks;
-  int32_t sort_algo;
 } fm_config;
 
 /* One mini-batch in CSR form: the result of explode(udfVecToMap(features))

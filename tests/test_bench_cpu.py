@@ -134,21 +134,6 @@ def test_sort_passes_follow_the_digit_plan():
     assert bench.sort_passes(1 << 31) == 4
 
 
-def test_grouping_rule_follows_the_library():
-    """bench.grouping restates fm_capi.hip bucket_on / fm_sort.hip bucket_hi_bits: the LSD passes
-    unless "bucket" is asked for and the key width allows one radix pass on the top 9-11 bits with
-    at most 18 low bits."""
-    import bench
-
-    assert bench.grouping("default", 10_223_616, 100_000_000) == "lsd"      # c3: the default is LSD
-    assert bench.grouping("bucket", 10_223_616, 100_000_000) == "bucket"    # c3: 27-bit slots
-    assert bench.grouping("bucket", 2_555_904, 1_000_000) == "bucket"       # c2 / c5: 20 bits
-    assert bench.grouping("bucket", 500_000, 1_000_000) == "bucket"
-    assert bench.grouping("lsd", 10_223_616, 100_000_000) == "lsd"
-    assert bench.grouping("bucket", 1000, 500) == "lsd"                     # 9-bit keys: one pass does it
-    assert bench.grouping("bucket", 20_000_000, 2**31 - 1) == "lsd"         # 31 bits: 21 low bits, too many
-
-
 def test_step_traffic_covers_every_kernel_of_the_default_steps():
     """The committed PMC files (profiles/pmc_*.json) count every kernel bench.step_kernels says a c3
     (fused, LSD), c2 and c5 step launches, so the line's step_roofline carries traffic and
@@ -156,11 +141,11 @@ def test_step_traffic_covers_every_kernel_of_the_default_steps():
     step with its scatter, no separate tag pass)."""
     import bench
 
-    ps = bench.step_kernels(100_000_000, 10_223_616, "default", True)
+    ps = bench.step_kernels(100_000_000, True)
     assert ps["k_radix_scatter"] == 3 and ps["k_split_scatter"] == 1 and "k_tag_runs" not in ps
-    assert bench.step_kernels(1_000_000, 2_555_904, "default", False)["k_radix_count"] == 2
+    assert bench.step_kernels(1_000_000, False)["k_radix_count"] == 2
     for cfg, fused in (("c3", True), ("c2", False), ("c5", False)):
         F, k, B, _, _ = bench.CONFIGS[cfg]
-        t, r, src = bench.step_traffic(F, k, B, fused, int(39 * B), "default")
+        t, r, src = bench.step_traffic(F, k, B, fused)
         assert t and r and src, cfg
         assert 1e8 < t < 1e10 and 1e6 < r < 1e8

@@ -79,11 +79,9 @@ def test_group_sharded_step_matches_oracle(gpu, R, k, F, hot, transport):
     ctx.close()
 
 
-@pytest.mark.parametrize("R,k,sort,transport", [
-    (1, 16, "bucket", "copy"), (2, 8, "lsd", "copy"), (3, 16, "lsd", "copy"), (8, 16, "bucket", "copy"),
-    (1, 16, "bucket", "rccl"),
-])
-def test_group_sharded_step_ignores_fuse(gpu, R, k, sort, transport):
+@pytest.mark.parametrize("R,k,transport", [(1, 16, "copy"), (2, 8, "copy"), (3, 16, "copy"), (8, 16, "copy"),
+                                           (1, 16, "rccl")])
+def test_group_sharded_step_ignores_fuse(gpu, R, k, transport):
     """A sharded group never fuses (fm_fuse_active 0 whatever fm_config.fuse_single says: the fused
     owner step measured slower at R = 8 and at world 1 and was removed): with fuse on
     and off the steps are bitwise the same and match the fp64 oracle, from host CSRs and from prepared
@@ -96,7 +94,7 @@ def test_group_sharded_step_ignores_fuse(gpu, R, k, sort, transport):
     model.load(keep, w[keep], V[keep])
     out = {}
     for fuse in (True, False):
-        ctx = _ctx(F, k, R, transport=transport, fuse=fuse, sort=sort)
+        ctx = _ctx(F, k, R, transport=transport, fuse=fuse)
         assert not ctx.fuse_active
         ctx.load_tables(keep, w[keep], V[keep])
         res = []

@@ -7,7 +7,7 @@ entries that all eight ranks' 256K-row batches route to it (tests/c4_emul.py emu
 other ranks between the phases).  The phases' device times come from fm_profile (HIP events on
 the launch streams); run under rocprofv3 --kernel-trace --stats for the per-kernel view.
 
-  python tools/c4_rank_bench.py [--iters 5] [--sort default|lsd|bucket]
+  python tools/c4_rank_bench.py [--iters 5]
 """
 
 import argparse
@@ -29,8 +29,6 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--sort", default="default", choices=["default", "lsd", "bucket"],
-                    help="the owner's slot sort (fm_config.sort_algo)")
     args = ap.parse_args()
     import torch
 
@@ -40,7 +38,7 @@ def main():
     from fm_spark_amd.distributed import HipShardEngine
 
     t0 = time.perf_counter()
-    eng = HipShardEngine(F_C4, K_C4, 0, R_C4, seed=20261015, init_sd=0.01, sort=args.sort)
+    eng = HipShardEngine(F_C4, K_C4, 0, R_C4, seed=20261015, init_sd=0.01)
     eng.init_random_range(0, F_C4)
     eng.ctx.sync()
     t_init = time.perf_counter() - t0
@@ -90,7 +88,7 @@ def main():
     line = {
         "workload": "c4 per rank: F = 2^31 - 1, k = 32, rank 0 of 8 (268,435,456 rows x 256 B resident), "
                     "eight 256K-row batches routed to it per iteration",
-        "iters": args.iters, "sort": args.sort, "entries_in": n_in, "pairs_in": P, "rows_updated": n_upd,
+        "iters": args.iters, "entries_in": n_in, "pairs_in": P, "rows_updated": n_upd,
         "table_bytes": int(eng.ctx.num_features // R_C4 + 1) * 256,
         "phases": phases, "roofline": roof,
         "critical_path_kernels_ms": crit,

@@ -98,16 +98,11 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&fk, 4 * n));
   CK(hipMalloc(&fv, 8 * n));
   CK(hipMalloc(&dn, 16));
-  for (int mode = 0; mode < 3; ++mode) {
+  for (int mode = 0; mode < 1; ++mode) {  // (modes 1-2 timed the bucket sort, removed in round 5)
     fmhip::SortWork sw;
     const uint32_t* ok = fk;
     const uint2* ov = fv;
-    auto run = [&] {
-      if (mode == 0)
-        fmhip::radix_sort_pairs64(sw, dk, dv, n, bits, st, &ok, &ov);
-      else if (!fmhip::bucket_sort_pairs64(sw, dk, dv, n, bits, st, fk, fv, mode == 2 ? dn : nullptr))
-        printf("bucket sort not applicable\n");
-    };
+    auto run = [&] { fmhip::radix_sort_pairs64(sw, dk, dv, n, bits, st, &ok, &ov); };
     for (int w = 0; w < 3; ++w) run();
     CK(hipEventRecord(a, st));
     for (int r = 0; r < R; ++r) run();
