@@ -124,6 +124,59 @@ __global__ __launch_bounds__(256) void gather_skel(float4* __restrict__ tab, con
   }
 }
 
+
+// MODE 4: the same skeleton in the forward's lane shape -- 4 lanes per row carry the 64-B V quads, the
+// 16-B header is a second load (every lane of the group), a singleton's record leaves as V (4 lanes)
+// plus header + pad (4 lanes) in two stores: what the shape costs against the 8-lane whole-record one
+template <int LPR, int U, int STRIDE, int MODE>
+__global__ __launch_bounds__(256) void gather_skel4(float4* __restrict__ tab, const int64_t* __restrict__ rp,
+                                                    const uint32_t* __restrict__ col, const float* __restrict__ xs,
+                                                    int64_t B, float4* __restrict__ srec) {
+  constexpr int Q = STRIDE / 4;
+  constexpr int RPP = 64 / LPR;
+  const int lane = threadIdx.x & 63;
+  const int g = lane % LPR, row_in = lane / LPR;
+  const int64_t wave = ((int64_t)blockIdx.x * 256 + threadIdx.x) / 64;
+  const int64_t nwaves = (int64_t)gridDim.x * 256 / 64;
+  for (int64_t s = wave; s < B; s += nwaves) {
+    const int64_t e0 = rp[s], e1 = rp[s + 1];
+    uint32_t id[U];
+    float x[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t e = e0 + u * RPP + row_in;
+      id[u] = e < e1 ? col[e] : 0xFFFFFFFFu;
+      x[u] = e < e1 ? xs[e] : 0.f;
+    }
+    float4 v[U], h[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const bool ok = id[u] != 0xFFFFFFFFu;
+      const int64_t r = (int64_t)(id[u] & 0x7FFFFFFFu) * Q;
+      h[u] = ok ? tab[r + 4] : make_float4(0, 0, 0, 0);
+      v[u] = ok ? tab[r + g] : make_float4(0, 0, 0, 0);
+    }
+    float4 acc = make_float4(0, 0, 0, 0);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      acc.x += v[u].x * x[u] + h[u].x;
+      acc.y += v[u].y * x[u];
+      acc.z += v[u].z * x[u];
+      acc.w += v[u].w * x[u];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (id[u] != 0xFFFFFFFFu && (id[u] >> 31)) {
+        const int64_t r = (int64_t)(id[u] & 0x7FFFFFFFu) * Q;
+        float4 w = v[u];
+        w.x += 1e-7f * acc.x;
+        tab[r + g] = w;
+        tab[r + 4 + g] = g == 0 ? h[u] : make_float4(0, 0, 0, 0);
+      }
+    if (lane < Q) srec[s * Q + lane] = acc;
+  }
+}
+
 template <int LPR, int U, int STRIDE, int MODE>
 void run_skel(float4* tab, const int64_t* rp, const uint32_t* col, const float* xs, int64_t B, int64_t n,
               float4* srec, hipStream_t st) {
@@ -131,18 +184,22 @@ void run_skel(float4* tab, const int64_t* rp, const uint32_t* col, const float* 
   CK(hipEventCreate(&a));
   CK(hipEventCreate(&b));
   const int grid = 2048;
-  for (int w = 0; w < 2; ++w)
-    hipLaunchKernelGGL((gather_skel<LPR, U, STRIDE, MODE>), dim3(grid), dim3(256), 0, st, tab, rp, col, xs, B, srec);
+  auto launch = [&] {
+    if (MODE == 4)
+      hipLaunchKernelGGL((gather_skel4<LPR, U, STRIDE, MODE>), dim3(grid), dim3(256), 0, st, tab, rp, col, xs, B, srec);
+    else
+      hipLaunchKernelGGL((gather_skel<LPR, U, STRIDE, MODE>), dim3(grid), dim3(256), 0, st, tab, rp, col, xs, B, srec);
+  };
+  for (int w = 0; w < 2; ++w) launch();
   CK(hipEventRecord(a, st));
   const int R = 10;
-  for (int r = 0; r < R; ++r)
-    hipLaunchKernelGGL((gather_skel<LPR, U, STRIDE, MODE>), dim3(grid), dim3(256), 0, st, tab, rp, col, xs, B, srec);
+  for (int r = 0; r < R; ++r) launch();
   CK(hipEventRecord(b, st));
   CK(hipEventSynchronize(b));
   float ms;
   CK(hipEventElapsedTime(&ms, a, b));
   ms /= R;
-  printf("VARIANT gather<%d, %d, %d, %d> ms=%.5f rows=%ld\\n", LPR, U, STRIDE, MODE, ms, (long)n);
+  printf("VARIANT gather<%d, %d, %d, %d> ms=%.5f rows=%ld\n", LPR, U, STRIDE, MODE, ms, (long)n);
   fflush(stdout);
   CK(hipEventDestroy(a));
   CK(hipEventDestroy(b));
@@ -221,6 +278,7 @@ int main(int argc, char** argv) {
     run<4, 8, 32, 2>(tab, idx, N, out, st);  // c3's ids in CSR order: 64 B of each 128-B record
     run<8, 4, 32, 2>(tab, idx, N, out, st);  // the whole record
     run_skel<8, 5, 32, 3>(tab, drp, dcol, dxs, B, N, srec, st);  // the fused forward's memory skeleton
+    run_skel<4, 3, 32, 4>(tab, drp, dcol, dxs, B, N, srec, st);  // the same in the forward's lane shape
     CK(hipFree(drp));
     CK(hipFree(dcol));
     CK(hipFree(dxs));

@@ -47,7 +47,7 @@ ceil_uni = max(uni, key=lambda v: v["l2_requests_per_s"]) if uni else None
 # c3's own forward address stream (tools/c3_stream.py): its ids gathered in CSR order (MODE 2), and
 # the fused forward's memory skeleton (MODE 3: CSR stream, whole-record gathers, singleton write-back,
 # S records), whose time is the floor of the forward's access stream
-c3 = {k: v for k, v in variants.items() if k.endswith(",2>") or k.endswith(",3>")}
+c3 = {k: v for k, v in variants.items() if k.endswith(",2>") or k.endswith(",3>") or k.endswith(",4>")}
 res = {"what": "L2 requests (TCC_HIT_sum + TCC_MISS_sum) per second of random row gathers "
                "(tools/gather_ceiling.hip: 10.2M gathers over a 100M-record table; <LPR lanes, U in flight, "
                "record floats, 0 uniform / 1 40 % hot>)",
@@ -58,7 +58,8 @@ res = {"what": "L2 requests (TCC_HIT_sum + TCC_MISS_sum) per second of random ro
                              "<4,8,32,2> / <8,4,32,2> its ids gathered in CSR order (64 B / the whole 128-B record); "
                              "<8,5,32,3> the fused forward's memory skeleton (row_ptr, ids and x read, every row's "
                              "128-B record gathered, the singleton rows' records written back, the 128-B S record "
-                             "written; no arithmetic)",
+                             "written; no arithmetic); <4,3,32,4> the same skeleton in the forward's lane shape "
+                             "(4 lanes of V quads + a header load per row, the record written back in two stores)",
                      "variants": c3} if c3 else None,
        "source": {"log": log, "pmc": pmc}}
 open(out, "w").write(json.dumps(res, indent=1, sort_keys=True) + "\n")
