@@ -402,6 +402,9 @@ int step_impl(fm_ctx* ctx, fm_batch* b, int32_t t, double step_size, double reg_
   e0 = ctx->prof_begin(ctx->stream);
   launch_forward(T, b->dev, ctx->work, p, ctx->stream, &nfwd, nullptr, fused ? &fx : nullptr);
   ctx->prof_end("forward", e0, ctx->stream);
+  // (the prepared batch's wait moved before the forward, where its sort has long finished, measured
+  // 0.170-0.173 against 0.167-0.168 ms at c2 and 0.191-0.192 against 0.187-0.190 at c5, three
+  // alternating reps, profiles/r05_h/ab: not taken)
   if (!fused) FM_HIP_CHECK(hipStreamWaitEvent(ctx->stream, prepared ? b->ready : ctx->ev_join, 0));
   e0 = ctx->prof_begin(ctx->stream);
   double* stats = ctx->loss_hist.as<double>() + 3 * (int64_t)ctx->epoch;

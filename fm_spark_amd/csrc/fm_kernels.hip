@@ -491,230 +491,6 @@ void k_forward(TableView T, const int64_t* __restrict__ row_ptr,
   }
 }
 
-#ifdef FM_FWD_WHOLE
-// The fused forward on whole-record gathers (kTrainFused, kp <= 16).  One wave per sample: the
-// LR = stride / 4 lanes of a row group gather its whole 64- or 128-B record in ONE load instruction
-// -- lanes g < NQ the V quads, lane NQ the header {w, t, cum}, the lanes past it the zero pad --
-// RPP = 64 / LR rows per pass, U passes in flight (all of a 39-entry sample's rows at k = 16: 8 x 5).
-// The header reaches the group's V lanes by ds_swizzle.  c3's own stream replayed in this shape
-// takes 0.367 ms against 0.429 in k_forward's (4 lanes of V quads + a header load per row, the
-// record written back in two stores; tools/gather_ceiling.hip, profiles/r05_f).  The arithmetic is
-// k_forward<kTrainFused>'s: lazy L1 caught up in fp64 on the values, fp64 sums, and every untagged
-// (singleton) row kept raw in LDS, updated after the sample's reduction with the segmented update's
-// arithmetic on the same fp32 S, r, yhat, and written back -- one store instruction per record,
-// header and pad included -- during the next sample, after its ids and before its gathers.
-template <int LR, int NQ>
-__device__ __forceinline__ int hdr_lane(int v) {  // lane NQ of each LR-lane group (ds_swizzle bitmask mode)
-  return __builtin_amdgcn_ds_swizzle(v, (0x1F & ~(LR - 1)) | (NQ << 5));
-}
-
-template <int NQ, int U, int TEAM>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5)))
-void k_forward_whole(TableView T, const int64_t* __restrict__ row_ptr, const uint32_t* __restrict__ col,
-                     const float* __restrict__ xs, const double* __restrict__ label, int64_t B, double w0,
-                     float* __restrict__ S_out, float2* __restrict__ yl_out, int64_t sstr, int64_t ystr,
-                     double2* __restrict__ loss_part, StepParams sp) {
-  constexpr int LR = NQ + 1 <= 4 ? 4 : 8;  // lanes per record: 64-B (kp <= 12) or 128-B records
-  constexpr int RPP = TEAM / LR;           // rows per pass of the team
-  constexpr int WPB = kBlock / TEAM;       // teams (samples in flight) per block
-  constexpr int NS = RPP >= 8 ? kFuseNS : 8;  // singleton rows a lane group keeps per sample
-  constexpr int MZ = NS * RPP;
-  __shared__ float4 st[WPB][MZ][LR];       // stashed records: V quads, header (x in the t word), pad
-  __shared__ uint32_t st_id[WPB][MZ];
-  const int tid = threadIdx.x, lane = tid % TEAM, wv = tid / TEAM;
-  const int g = lane % LR, rs = lane / LR;
-  const bool vl = g < NQ, hl = g == NQ;
-  const double cumE = sp.cumE;
-  const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
-  const float4 absent4 = make_float4(0.f, __int_as_float(-1), 0.f, 0.f);  // an absent row's header
-  double loss_acc = 0.0, nloss = 0.0;
-  int pend = 0;  // updated records of the previous sample waiting in slots rs + j RPP, j < pend
-  auto flush = [&]() {
-    for (int j = 0; j < pend; ++j) {
-      const int i = rs + j * RPP;
-      st_row4(T.v(st_id[wv][i]) + 4 * g, st[wv][i][g]);  // the group's LR lanes: the whole record
-    }
-    pend = 0;
-  };
-  for (int64_t s = (int64_t)blockIdx.x * WPB + wv; s < B; s += (int64_t)gridDim.x * WPB) {
-    const int64_t e0 = row_ptr[s], e1 = row_ptr[s + 1];
-    const double ys = label[s];
-    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0, vv = 0.0, wx = 0.0;
-    int nst = 0;  // singletons of this sample met by the lane group
-    if (e0 + rs >= e1) flush();  // no entry of this sample for the group: nothing to wait behind
-    for (int64_t eb = e0 + rs; eb < e1; eb += U * RPP) {
-      uint32_t id[U];
-      float x[U];
-      bool ok[U];
-      // every load unconditional (a slot past the sample's end reads its first entry, then is masked):
-      // guarded loads compile to a branch and a wait each, and the rows would be gathered one by one
-#pragma unroll
-      for (int j = 0; j < U; ++j) {
-        const int64_t e = eb + j * RPP;
-        ok[j] = e < e1;
-        const int64_t ec = ok[j] ? e : eb;
-        id[j] = col[ec];
-        x[j] = ok[j] ? xs[ec] : 0.f;
-      }
-      if (eb == e0 + rs) flush();  // the previous sample's rows: ids in, gathers not yet issued
-      float4 q[U];
-#pragma unroll
-      for (int j = 0; j < U; ++j) q[j] = reinterpret_cast<const float4*>(T.v(id[j]))[g];
-#pragma unroll
-      for (int j = 0; j < U; ++j)
-        if (!ok[j]) q[j] = hl ? absent4 : zero4;
-#pragma unroll
-      for (int j = 0; j < U; ++j) {
-        const int32_t t = hdr_lane<LR, NQ>(__float_as_int(q[j].y));
-        // a singleton row (untagged): kept raw, with x in place of t in its header (group-uniform)
-        if (ok[j] && !is_multi(t, sp.epoch)) {
-          if (nst < NS) {
-            const int i = rs + nst * RPP;
-            st[wv][i][g] = hl ? make_float4(q[j].x, x[j], q[j].z, q[j].w) : (vl ? q[j] : zero4);
-            if (g == 0) st_id[wv][i] = id[j];
-          }
-          ++nst;
-        }
-        if (t >= 0) {
-          const double cum = __hiloint2double(hdr_lane<LR, NQ>(__float_as_int(q[j].w)),
-                                              hdr_lane<LR, NQ>(__float_as_int(q[j].z)));
-          const double a = cumE - cum;
-          if (a > 0.0) {
-            if (vl) q[j] = shrink4(q[j], a);
-            if (hl) q[j].x = shrink_f(q[j].x, a);
-          }
-        } else if (vl) {
-          q[j] = zero4;
-        }
-        const double xd = x[j];
-        if (vl) {
-          // vfxi = v * x (Model.scala:179), VectorSum over the sample (:191); vi2xi2 (:256-258)
-          a0 += (double)q[j].x * xd; a1 += (double)q[j].y * xd;
-          a2 += (double)q[j].z * xd; a3 += (double)q[j].w * xd;
-          const double v2 = (double)q[j].x * q[j].x + (double)q[j].y * q[j].y + (double)q[j].z * q[j].z +
-                            (double)q[j].w * q[j].w;
-          vv += v2 * xd * xd;
-        }
-        if (hl && t >= 0) wx += (double)q[j].x * xd;  // wixi (Model.scala:178)
-      }
-    }
-    // sum the row slots (lanes with equal g), then the whole wave for the scalars
-#pragma unroll
-    for (int o = LR; o < TEAM; o <<= 1) {
-      a0 += __shfl_xor(a0, o); a1 += __shfl_xor(a1, o);
-      a2 += __shfl_xor(a2, o); a3 += __shfl_xor(a3, o);
-    }
-#pragma unroll
-    for (int o = 1; o < TEAM; o <<= 1) {
-      vv += __shfl_xor(vv, o);
-      wx += __shfl_xor(wx, o);
-    }
-    double ss = vl ? a0 * a0 + a1 * a1 + a2 * a2 + a3 * a3 : 0.0;
-#pragma unroll
-    for (int o = 1; o < LR; o <<= 1) ss += __shfl_xor(ss, o);
-    // sumVx + wixiSum + w0 (Model.scala:221, :260-262)
-    const double yhat = 0.5 * (ss - vv) + wx + w0;
-    if (rs == 0 && vl)
-      *reinterpret_cast<float4*>(S_out + s * sstr + g * 4) = make_float4((float)a0, (float)a1, (float)a2, (float)a3);
-    // the singleton rows of this sample (SGD.scala:145-181 over a run of one entry), from the values the
-    // update kernel would read back: S, r and yhat rounded to fp32 as stored, x from the batch
-    const float r32 = (float)(yhat - ys), yh32 = (float)yhat;
-    const double rj = (double)r32, yh = (double)yh32;
-    const float4 Sq = make_float4((float)a0, (float)a1, (float)a2, (float)a3);
-    const float lamf = (float)sp.lam;
-    const int zc = nst < NS ? nst : NS;
-    for (int jj = 0; jj < zc; ++jj) {
-      const int i = rs + jj * RPP;
-      const float4 hq = st[wv][i][NQ];
-      const RowHdr h = *reinterpret_cast<const RowHdr*>(&hq);
-      const double xd = (double)__int_as_float(h.t);  // the stash keeps x in the t word
-      const float acf = (float)(sp.cumE - h.cum);  // pending L1 of the row
-      const double tt = xd * rj, b = (xd * xd) * rj;
-      const double gwe = (xd - 1.0) * yh + rj;  // x yhat - y (SGD.scala:145)
-      if (vl) {
-        const float4 v = shrink4f(st[wv][i][g], acf);
-        const double g0 = fma((double)Sq.x, tt, 0.0) - (double)v.x * b, g1 = fma((double)Sq.y, tt, 0.0) - (double)v.y * b;
-        const double g2 = fma((double)Sq.z, tt, 0.0) - (double)v.z * b, g3 = fma((double)Sq.w, tt, 0.0) - (double)v.w * b;
-        const float4 u = make_float4((float)fma(g0, -sp.scale_v, (double)v.x), (float)fma(g1, -sp.scale_v, (double)v.y),
-                                     (float)fma(g2, -sp.scale_v, (double)v.z), (float)fma(g3, -sp.scale_v, (double)v.w));
-        st[wv][i][g] = shrink4f(u, lamf);
-      }
-      if (hl) {
-        RowHdr o;
-        o.w = upd_w(shrink1f(h.w, acf), 0.0 + gwe, sp);  // SGD.scala:150, :171
-        o.t = sp.epoch + 1;
-        o.cum = sp.cum_next;
-        st[wv][i][NQ] = *reinterpret_cast<const float4*>(&o);
-      }
-    }
-    pend = zc;
-    // singletons beyond the group's NS (long samples): the group walks its entries again, and rows
-    // past the first NS singletons are read again (nobody else reads or writes a singleton row in
-    // this step) and updated straight away
-    int seen = 0;
-    for (int64_t e = e0 + rs; nst > NS && e < e1; e += RPP) {
-      const uint32_t id = col[e];
-      float4 q = reinterpret_cast<const float4*>(T.v(id))[g];
-      const int32_t t = hdr_lane<LR, NQ>(__float_as_int(q.y));
-      if (is_multi(t, sp.epoch)) continue;
-      if (++seen <= NS) continue;  // stashed
-      const double cum = __hiloint2double(hdr_lane<LR, NQ>(__float_as_int(q.w)), hdr_lane<LR, NQ>(__float_as_int(q.z)));
-      const double xd = (double)xs[e];
-      const float acf = (float)(sp.cumE - cum);  // pending L1 of the row
-      const double tt = xd * rj, b = (xd * xd) * rj;
-      const double gwe = (xd - 1.0) * yh + rj;
-      float4 out = zero4;
-      if (vl) {
-        const float4 v = shrink4f(q, acf);
-        const double g0 = fma((double)Sq.x, tt, 0.0) - (double)v.x * b, g1 = fma((double)Sq.y, tt, 0.0) - (double)v.y * b;
-        const double g2 = fma((double)Sq.z, tt, 0.0) - (double)v.z * b, g3 = fma((double)Sq.w, tt, 0.0) - (double)v.w * b;
-        const float4 u = make_float4((float)fma(g0, -sp.scale_v, (double)v.x), (float)fma(g1, -sp.scale_v, (double)v.y),
-                                     (float)fma(g2, -sp.scale_v, (double)v.z), (float)fma(g3, -sp.scale_v, (double)v.w));
-        out = shrink4f(u, lamf);
-      }
-      if (hl) {
-        RowHdr o;
-        o.w = upd_w(shrink1f(q.x, acf), 0.0 + gwe, sp);
-        o.t = sp.epoch + 1;
-        o.cum = sp.cum_next;
-        out = *reinterpret_cast<const float4*>(&o);
-      }
-      st_row4(T.v(id) + 4 * g, out);  // the whole record (V, header, pad) in one store
-    }
-    if (lane == 0) {
-      // r = pred - label in fp64 (SGD.scala:146), rounded once
-      yl_out[s * ystr] = make_float2((float)(yhat - ys), (float)yhat);
-      if (e1 > e0) {
-        const double d = yhat - ys;
-        loss_acc += d * d;  // pow(pred - label, 2.0), Model.scala:230
-        nloss += 1.0;
-      }
-    }
-  }
-  flush();  // the last sample's rows
-  // deterministic block reduction of the loss partials
-  __shared__ double red[2][kBlock / 64];
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    loss_acc += __shfl_xor(loss_acc, o);
-    nloss += __shfl_xor(nloss, o);
-  }
-  if ((tid & 63) == 0) {
-    red[0][tid >> 6] = loss_acc;
-    red[1][tid >> 6] = nloss;
-  }
-  __syncthreads();
-  if (tid == 0) {
-    double l = 0.0, c = 0.0;
-    for (int w = 0; w < kBlock / 64; ++w) {
-      l += red[0][w];
-      c += red[1][w];
-    }
-    loss_part[blockIdx.x] = make_double2(l, c);
-  }
-}
-#endif
-
 // -------------------------------------------------------------- segmented update
 struct SegArgs {
   TableView T;
@@ -1545,32 +1321,6 @@ void launch_fwd_t(const TableView& T, const BatchDev& b, StepWork& w, const Step
                        nullptr, (int64_t)T.kp, (int64_t)1, nullptr, *xo);
     return;
   }
-#ifdef FM_FWD_WHOLE
-  if constexpr (GS <= 4) {
-    if (xo && xo->fused) {  // kp <= 16: one wave per sample, whole-record gathers
-      constexpr int WPB = kBlock / FM_FWD_WHOLE;  // teams per block
-      int64_t wb = (b.n_rows + WPB - 1) / WPB;
-      if (wb > kFwdGrid) wb = kFwdGrid;
-      if (wb < 1) wb = 1;
-      *nblk = wb;
-      w.loss_part.ensure(sizeof(double2) * wb);
-      const dim3 gw((unsigned)wb);
-      auto go = [&](auto kern) {
-        hipLaunchKernelGGL(kern, gw, blk, 0, st, T, b.row_ptr.as<int64_t>(), b.col.as<uint32_t>(), b.xs.as<float>(),
-                           b.label.as<double>(), b.n_rows, p.w0, w.S.as<float>(),
-                           reinterpret_cast<float2*>(w.S.as<float>() + T.kp), (int64_t)s_rec_floats(T.kp),
-                           (int64_t)s_rec_floats(T.kp) / 2, w.loss_part.as<double2>(), p);
-      };
-      switch (T.kp / 4) {  // V quads of a row: 64-B records carry 3 passes of 16 rows, 128-B 5 of 8
-        case 1: go(k_forward_whole<1, 3 * 64 / FM_FWD_WHOLE, FM_FWD_WHOLE>); break;
-        case 2: go(k_forward_whole<2, 3 * 64 / FM_FWD_WHOLE, FM_FWD_WHOLE>); break;
-        case 3: go(k_forward_whole<3, 3 * 64 / FM_FWD_WHOLE, FM_FWD_WHOLE>); break;
-        default: go(k_forward_whole<4, (FM_FWD_WHOLE == 64 ? 5 : 6), FM_FWD_WHOLE>); break;
-      }
-      return;
-    }
-  }
-#endif
   w.loss_part.ensure(sizeof(double2) * blocks);
   FwdOut tr = xo ? *xo : none;  // train mode: xo->fused = the singleton rows' updates in the forward
   auto kern = k_forward<GS, TEAM, kTrain, U>;

@@ -5,7 +5,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=${PMC_OUT:-gpurun_out/pmc}
 mkdir -p $OUT
-ARGS="${BENCH_ARGS:---steps 5 --warmup 2 --no-cpu-baseline --profile-kernels 0 --host-path-steps 0}"
+ARGS="${BENCH_ARGS:---steps 5 --warmup 2 --no-cpu-baseline --profile-kernels 0 --host-path-steps 0 --fit-iters 0}"
 REGEX="${KREGEX:-k_segment_update|k_forward|k_radix_scatter|k_radix_count|k_radix_chunk|k_segment_combine|k_split|k_pack_srec}"
 CMD="${PMC_CMD:-python bench.py $ARGS}"
 GROUPS_DEFAULT=("FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU"
