@@ -58,6 +58,8 @@ def test_null_arguments_are_errors_not_crashes():
     assert lib.fm_create(None, None) == -1
     assert b"null" in lib.fm_last_error()
     assert lib.fm_step(None, None, 1, 1.0, 0.0, None) == -1
+    assert lib.fm_batch_create_splits(None, None, 1, None, None) == -1
+    assert lib.fm_batch_split_view(None, None, 0, None) == -1
     assert lib.fm_epoch(None) == -1
     lib.fm_destroy(None)
     lib.fm_batch_destroy(None)

@@ -349,3 +349,37 @@ def test_split_views_on_a_multi_gpu_context(gpu, mode):
     assert a[0] == b[0]
     for x, y in zip(a[1], b[1]):
         assert np.array_equal(x, y)
+
+
+@pytest.mark.parametrize("mode", ["sharded", "replicated"])
+def test_pipelined_resident_loop_on_a_multi_gpu_context(gpu, mode):
+    """run_minibatch_sgd_resident (enqueue-only steps; each batch refilled by fm_batch_from_rows two
+    iterations ahead while earlier steps may still be queued) on a 3-rank context (COPY transport):
+    the losses and the table bitwise those of synchronous steps on the host CSRs of the same rows.
+    A refill must wait for the sharded iteration that last read the batch (its combine reads the
+    labels, its route the entries)."""
+    from fm_spark_amd.engine import FMContext
+    from fm_spark_amd.ml import run_minibatch_sgd_resident
+
+    F, k, R = 3000, 8, 3
+    data, ids, w, V = make_problem(1216, 2400, F, k, 9, hot=4)
+    rng = np.random.default_rng(14)
+    splits = [rng.permutation(2400)[: 300 + 40 * i] for i in range(7)]
+
+    def ctx_():
+        c = FMContext(F, k, parallel=mode, n_gpus=R, devices=[0] * R, transport="copy")
+        c.load_tables(ids, w, V)
+        return c
+
+    a = ctx_()
+    d = a.batch(to_host(data))
+    la = run_minibatch_sgd_resident(a, d, splits, 0.3, 1e-3)
+    ta = a.export_tables()
+    b = ctx_()
+    lb = [b.step(to_host(_select(data, s)), i + 1, 0.3, 1e-3).loss_sum for i, s in enumerate(splits)]
+    tb = b.export_tables()
+    assert la == lb
+    for x, y in zip(ta, tb):
+        assert np.array_equal(x, y)
+    a.close()
+    b.close()

@@ -25,7 +25,7 @@ meta = json.loads(sys.argv[3]) if len(sys.argv) > 3 else {}
 # meta "timed_steps": N keeps only the last N launches of the once-per-step kernels of the main
 # stream (bench.py's warmup and U-count steps run unprepared batches, i.e. the unfused variant)
 timed = int(meta.get("timed_steps", 0))
-PER_STEP = ("k_forward", "k_segment_update", "k_segment_combine", "k_tag_runs", "k_owner_single", "k_pack_srec")
+PER_STEP = ("k_forward", "k_segment_update", "k_segment_combine", "k_pack_srec")
 acc = defaultdict(lambda: defaultdict(list))
 for f in sorted(glob.glob(os.path.join(src, "p*", "run_counter_collection.csv")) +
                 glob.glob(os.path.join(src, "p*_counters.csv"))):

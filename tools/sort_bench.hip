@@ -1,6 +1,5 @@
-// Measurement tool (not product): time the library's sorts (LSD passes, bucket sort, bucket sort
-// with the singleton split) against rocPRIM's device radix sort on the same 10M (uint32 key,
-// uint64 payload) pairs, 27-bit keys, and check their output against it.
+// Measurement tool (not product): time the library's LSD sort against rocPRIM's device radix sort
+// on the same 10M (uint32 key, uint64 payload) pairs, 27-bit keys, and check its output against it.
 #include <hip/hip_runtime.h>
 #include <cstring>
 #include <rocprim/device/device_radix_sort.hpp>
@@ -73,8 +72,7 @@ int main(int argc, char** argv) {
   float ms;
   CK(hipEventElapsedTime(&ms, a, b));
   printf("rocprim radix_sort_pairs n=%lld bits=%d: %.3f ms\n", (long long)n, bits, ms / R);
-  // ours: the LSD passes, the bucket sort (whole view) and the bucket sort's split (the fused step's
-  // multi view: only the entries of keys that occur twice or more, checked against rocPRIM's output)
+  // ours: the LSD passes (mode 0; the multi-view check below served the bucket sort's split, removed)
   std::vector<uint32_t> k1(n), k2(n);
   std::vector<uint2> v1(n), v2(n);
   CK(hipMemcpy(k1.data(), dk2, 4 * n, hipMemcpyDeviceToHost));
