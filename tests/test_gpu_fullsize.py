@@ -271,3 +271,48 @@ def test_c3_whole_table_parity_against_c_oracle(gpu):
         ctx.close()
     finally:
         lib.oracle_destroy(m)
+
+
+def test_c3_split_views_bitwise_equal_host_batches(gpu):
+    """c3 at full size through the estimator's loop: three 256K-row mini-batches laid out as one
+    split-ordered resident dataset (fm_batch_create_splits) and stepped in place through two views
+    re-pointed in turn, sorted on the side stream one iteration ahead, every step only enqueued
+    (ml.run_minibatch_sgd_splits, the fit path), against a second context stepping the same rows
+    uploaded as host batches, prepared and stepped synchronously: the loss sums and every one of the
+    100M rows (fm_export_rows in id-range chunks) bitwise equal."""
+    import bench
+    from fm_spark_amd import ml
+    from fm_spark_amd.data import synthetic_batch
+    from fm_spark_amd.engine import FMContext
+
+    F, k, B, n, seed, sd = 100_000_000, 16, 262144, 3, 20261015, 0.01
+    hb = [synthetic_batch(B, F, batch_index=50 + i) for i in range(n)]
+    lay = bench.concat_batches(hb)
+    split_rows = np.arange(n + 1, dtype=np.int64) * B
+
+    a = FMContext(F, k, seed=seed, init_sd=sd)
+    a.init_random_range(0, F)
+    data = a.batch_splits(_host(lay), split_rows)
+    la = ml.run_minibatch_sgd_splits(a, data, STEP, REG)
+    a.sync()
+
+    b = FMContext(F, k, seed=seed, init_sd=sd)
+    b.init_random_range(0, F)
+    lb = []
+    for t, h in enumerate(hb, start=1):
+        db = b.batch(_host(h))
+        db.prepare()
+        lb.append(b.step_batch(db, t, STEP, REG, sync=True).loss_sum)
+        db.close()
+    assert list(la) == lb
+
+    chunk = 1 << 23
+    for s in range(0, F, chunk):
+        ids = np.arange(s, min(F, s + chunk), dtype=np.int32)
+        wa, Va, pa = a.export_rows(ids)
+        wb, Vb, pb = b.export_rows(ids)
+        assert pa.all() and pb.all()
+        assert np.array_equal(wa, wb) and np.array_equal(Va, Vb)
+    data.close()
+    a.close()
+    b.close()
