@@ -910,18 +910,19 @@ __device__ __forceinline__ RowCur row_current(const SegArgs& a, uint32_t key) {
   if (r.ac > 0.0) r.w = shrink_f(r.w, r.ac);
   return r;
 }
+// column c of the run's update from the row's stored value vraw (read whatever the row's presence)
+__device__ __forceinline__ void close_col(const SegArgs& a, uint32_t key, const RowCur& rc, int c, float vraw, double b,
+                                          double sum) {
+  float v = rc.present ? vraw : 0.f;
+  if (rc.ac > 0.0) v = shrink_f(v, rc.ac);
+  const double gv = sum - (double)v * b;
+  if (a.emit) a.emit[(int64_t)key * (a.T.kp + 4) + c] = (float)gv;
+  else a.T.v(key)[c] = upd_v(v, gv, a.p);
+}
 __device__ __forceinline__ void close_cols(const SegArgs& a, uint32_t key, const RowCur& rc, int c_lo, int c_hi,
                                            int c_step, double b, const double* sums) {
-  const int kp = a.T.kp;
-  float* vrow = a.T.v(key);
-  float* gr = a.emit ? a.emit + (int64_t)key * (kp + 4) : nullptr;
-  for (int c = c_lo, j = 0; c < c_hi; c += c_step, ++j) {
-    float v = rc.present ? vrow[c] : 0.f;
-    if (rc.ac > 0.0) v = shrink_f(v, rc.ac);
-    const double gv = sums[j] - (double)v * b;
-    if (gr) gr[c] = (float)gv;
-    else vrow[c] = upd_v(v, gv, a.p);
-  }
+  const float* vrow = a.T.v(key);
+  for (int c = c_lo, j = 0; c < c_hi; c += c_step, ++j) close_col(a, key, rc, c, vrow[c], b, sums[j]);
 }
 __device__ __forceinline__ void close_hdr(const SegArgs& a, uint32_t key, const RowCur& rc, double gw) {
   const int kp = a.T.kp;
@@ -936,6 +937,8 @@ __device__ __forceinline__ void close_hdr(const SegArgs& a, uint32_t key, const 
   }
 }
 
+constexpr int kStatLd = 8;     // block 0's stats loads in flight per thread
+constexpr int kCombCols = 10;  // long-run columns a lane sums at once (even; W = kp + 2: k = 8 in one pass)
 __global__ __launch_bounds__(kBlock) void k_segment_combine(SegArgs a, const double2* __restrict__ loss_part,
                                                             int64_t n_loss_blocks, int64_t n_ucnt,
                                                             double* __restrict__ stats_out) {
@@ -948,14 +951,36 @@ __global__ __launch_bounds__(kBlock) void k_segment_combine(SegArgs a, const dou
   if (blockIdx.x == 0) {
     __shared__ double rl[kBlock], rc[kBlock], ru[kBlock];
     double l = 0.0, c = 0.0, u = 0.0;
-    for (int64_t i = tid; i < n_loss_blocks; i += kBlock) {
-      l += loss_part[i].x;
-      c += loss_part[i].y;
+    // each thread's partials in index order as ever, their loads issued kStatLd at a time from
+    // clamped addresses (a plain loop waits one memory round trip per element: this block closed
+    // the kernel 20-30 us after the others)
+    for (int64_t i0 = tid; i0 < n_loss_blocks; i0 += kStatLd * kBlock) {
+      double2 v[kStatLd];
+#pragma unroll
+      for (int j = 0; j < kStatLd; ++j) {
+        const int64_t i = i0 + j * kBlock;
+        v[j] = loss_part[i < n_loss_blocks ? i : n_loss_blocks - 1];
+      }
+#pragma unroll
+      for (int j = 0; j < kStatLd; ++j) {
+        const bool in = i0 + j * kBlock < n_loss_blocks;
+        l += in ? v[j].x : 0.0;
+        c += in ? v[j].y : 0.0;
+      }
     }
     // update blocks that held entries (a device count leaves the grid's tail without any)
     const int64_t per_blk = (int64_t)kWaveEnt * (kBlock / 64);
     const int64_t nu = a.n_dev ? min(n_ucnt, (N + per_blk - 1) / per_blk) : n_ucnt;
-    for (int64_t i = tid; i < nu; i += kBlock) u += (double)a.ucnt[i];
+    for (int64_t i0 = tid; i0 < nu; i0 += kStatLd * kBlock) {
+      uint32_t v[kStatLd];
+#pragma unroll
+      for (int j = 0; j < kStatLd; ++j) {
+        const int64_t i = i0 + j * kBlock;
+        v[j] = a.ucnt[i < nu ? i : nu - 1];
+      }
+#pragma unroll
+      for (int j = 0; j < kStatLd; ++j) u += i0 + j * kBlock < nu ? (double)v[j] : 0.0;
+    }
     if (a.n_dev && tid == 0) u += (double)a.n_dev[1];  // the singleton rows the forward updated
     rl[tid] = l;
     rc[tid] = c;
@@ -979,33 +1004,40 @@ __global__ __launch_bounds__(kBlock) void k_segment_combine(SegArgs a, const dou
   const int64_t chunk = ((int64_t)blockIdx.x * kBlock + tid) / 16;  // range index
   const int f = tid & 15;
   const int64_t L = a.L;
-  bool owner = false;
+  bool owner = false, two = false;
   uint32_t key = 0;
   if (chunk < nranges) {
     const int64_t p0 = chunk * L;
     const int64_t p1 = p0 + L < N ? p0 + L : N;
     if (p1 < N) {
-      key = a.skeys[p1 - 1];
+      // every key the two tests need, loaded together (clamped addresses: no load waits behind
+      // another's comparison)
+      const int64_t p2 = (chunk + 2) * L;
+      const uint32_t kl = a.skeys[p1 - 1], kn = a.skeys[p1], kf = a.skeys[p0];
+      const uint32_t kb = a.skeys[p0 > 0 ? p0 - 1 : 0], k2 = a.skeys[p2 < N ? p2 : N - 1];
+      key = kl;
       // the range's last run continues into the next range and starts inside this range
-      owner = a.skeys[p1] == key && !(a.skeys[p0] == key && p0 > 0 && a.skeys[p0 - 1] == key);
+      owner = kn == kl && !(kf == kl && p0 > 0 && kb == kl);
+      // common case: the run ends inside the next range -> its two partials
+      two = owner && !(p2 < N && k2 == kl);
     }
-  }
-  // common case: the run ends inside the next range -> its two partials
-  bool two = false;
-  if (owner) {
-    const int64_t c2 = chunk + 2;
-    two = !(c2 < nranges && a.skeys[c2 * L] == key);
   }
   if (owner && two) {
     const double* pt = a.part + (chunk * 2 + 1) * W;
     const double* ph = a.part + ((chunk + 1) * 2) * W;
-    const double b = pt[kp + 1] + ph[kp + 1];
+    // the two pieces' scalars and first column, the row's header and V column: one round trip
+    const int cf = f < kp ? f : kp - 1;
+    const double bt = pt[kp + 1], bh = ph[kp + 1], wt = pt[0], wh = ph[0];
+    const double st = pt[1 + cf], sh = ph[1 + cf];
+    const float vf = a.T.v(key)[cf];
     const RowCur rc = row_current(a, key);
-    for (int c = f; c < kp; c += 16) {
+    const double b = bt + bh;
+    if (f < kp) close_col(a, key, rc, f, vf, b, st + sh);
+    for (int c = f + 16; c < kp; c += 16) {
       const double sm = pt[1 + c] + ph[1 + c];
       close_cols(a, key, rc, c, c + 1, 1, b, &sm);
     }
-    if (f == 0) close_hdr(a, key, rc, pt[0] + ph[0]);
+    if (f == 0) close_hdr(a, key, rc, wt + wh);
   }
   // long runs (hot features): one wave per run, lanes over the factor columns, range order
   uint64_t owners = __ballot(owner && !two && f == 0);
@@ -1028,29 +1060,38 @@ __global__ __launch_bounds__(kBlock) void k_segment_combine(SegArgs a, const dou
       break;
     }
     // the run's pieces = the owner range's tail + the head pieces of ranges c0+1 .. cend-1, each a
-    // row of W = kp + 2 doubles [g_w | sum S*x*r (kp) | sum x*x*r].  The wave sums them as 8 column
-    // lanes x 8 range groups (range group rg takes ranges c0+1+rg, +8, ...), then combines the 8
-    // groups by a fixed xor tree and adds the tail: a fixed order, so the step stays bitwise
-    // reproducible, with every lane loading (hot runs at R = 8 span hundreds of ranges).
-    const int cl = lane & 7, rg = lane >> 3;
-    for (int col0 = 0; col0 < (int)W; col0 += 8) {
-      const int col = col0 + cl;
-      double s = 0.0;
-      if (col < (int)W) {
-        int64_t c = c0 + 1 + rg;
-        for (; c + 8 < cend; c += 16) {  // two loads in flight per lane
-          const double g0 = a.part[(c * 2) * W + col];
-          const double g1 = a.part[((c + 8) * 2) * W + col];
-          s += g0;
-          s += g1;
+    // row of W = kp + 2 doubles [g_w | sum S*x*r (kp) | sum x*x*r].  Lane l sums the pieces of
+    // ranges c0+1+l, +64, ... kCombCols columns at a time (a piece's columns are contiguous, loaded
+    // unconditionally from clamped addresses: one round trip per 64 ranges), then a fixed xor tree
+    // over the 64 lanes, then the tail: a fixed order, so the step stays bitwise reproducible.
+    for (int col0 = 0; col0 < (int)W; col0 += kCombCols) {
+      double s[kCombCols];
+#pragma unroll
+      for (int j = 0; j < kCombCols; ++j) s[j] = 0.0;
+      for (int64_t c = c0 + 1 + lane; c < cend; c += 64) {
+        const double* pr = a.part + (c * 2) * W;
+#pragma unroll
+        for (int j = 0; j < kCombCols / 2; ++j) {
+          const int cc = col0 + 2 * j;
+          const double2 v = *reinterpret_cast<const double2*>(pr + (cc < (int)W ? cc : (int)W - 2));
+          s[2 * j] += cc < (int)W ? v.x : 0.0;
+          s[2 * j + 1] += cc < (int)W ? v.y : 0.0;
         }
-        for (; c < cend; c += 8) s += a.part[(c * 2) * W + col];
       }
-      s += __shfl_xor(s, 8);
-      s += __shfl_xor(s, 16);
-      s += __shfl_xor(s, 32);
-      if (col < (int)W && rg == 0) run_sum[wave][col] = a.part[(c0 * 2 + 1) * W + col] + s;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1)
+#pragma unroll
+        for (int j = 0; j < kCombCols; ++j) s[j] += __shfl_xor(s[j], o);
+      if (lane == 0) {
+#pragma unroll
+        for (int j = 0; j < kCombCols; ++j)
+          if (col0 + j < (int)W) run_sum[wave][col0 + j] = s[j];
+      }
     }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int col = lane; col < (int)W; col += 64) run_sum[wave][col] = a.part[(c0 * 2 + 1) * W + col] + run_sum[wave][col];
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1648,43 +1689,78 @@ __global__ __launch_bounds__(kBlock) void k_split_rebase(const int64_t* __restri
 // The sorted view of a batch -> the entries of its runs of two or more (stable: the order the
 // segmented update needs) and the number of singleton runs.  One wave per chunk of 1024 sorted
 // entries: count, one-block scan of the chunk counts, then each wave writes its multi entries at
-// its offset in order (ballot ranks).  Integer work only: deterministic.  Loading a wave's whole
-// chunk at once (16 independent loads, not a round trip per row) made both passes twice as fast and
-// the c3 step 4-30 us slower: their bursts land on the side stream's sort (profiles/r04_z, r04_za).
+// its offset in order (ballot ranks).  Integer work only: deterministic.  Each pass loads a wave's
+// whole chunk at once (16 independent loads, not a round trip per row): in round 4 that made both
+// passes twice as fast and the step slower, their bursts landing on the side stream's sort
+// (profiles/r04_z, r04_za); once the sort's own latency chains were cut (round 5), the step is
+// faster with it ("Latency chains").
 constexpr int kSplitChunk = 1024;
 
-// entry p of the sorted view belongs to a run of two or more (multi); *first: it opens its run
-__device__ __forceinline__ bool split_multi(const uint32_t* __restrict__ skeys, int64_t N, int64_t p, uint32_t key,
-                                            int lane, bool* first = nullptr) {
-  uint32_t prev = __shfl_up(key, 1), next = __shfl_down(key, 1);
-  if (lane == 0) prev = p > 0 && p <= N ? skeys[p - 1] : 0xFFFFFFFFu;
-  if (lane == 63) next = p + 1 < N ? skeys[p + 1] : 0xFFFFFFFFu;
-  if (p == 0) prev = 0xFFFFFFFFu;      // (lane 0 only)
-  if (p + 1 >= N) next = 0xFFFFFFFFu;  // the last entry has no successor
-  if (first) *first = prev != key;
-  return p < N && (prev == key || next == key);
+// A wave's whole chunk of the sorted keys, loaded at once: row r's key per lane (clamped addresses,
+// every load issued before any is used) and the keys just before and after the chunk; then per row
+// whether the entry belongs to a run of two or more (multi) and whether it opens its run.
+constexpr int kSplitRows = kSplitChunk / 64;
+constexpr uint32_t kSplitNone = 0xFFFFFFFFu;
+struct SplitChunk {
+  uint32_t key[kSplitRows];
+  uint32_t multi = 0, first = 0;  // bit r: row r's entry is multi / opens its run
+};
+__device__ __forceinline__ void split_chunk(const uint32_t* __restrict__ skeys, int64_t N, int64_t c, int lane,
+                                            SplitChunk& sc) {
+  const int64_t base = c * kSplitChunk;
+#pragma unroll
+  for (int r = 0; r < kSplitRows; ++r) {
+    const int64_t p = base + r * 64 + lane;
+    sc.key[r] = skeys[p < N ? p : N - 1];
+  }
+  // the keys just before and after the chunk, in one more load per lane (lane 0: before, the
+  // others: after), unconditional so that it is issued with the rows' and not sunk into a branch
+  const int64_t eb = lane == 0 ? (base > 0 ? base - 1 : 0) : (base + kSplitChunk < N ? base + kSplitChunk : N - 1);
+  const uint32_t edge = skeys[eb];
+  const uint32_t before = base > 0 ? __shfl(edge, 0) : kSplitNone;
+  const uint32_t after = base + kSplitChunk < N ? __shfl(edge, 1) : kSplitNone;
+#pragma unroll
+  for (int r = 0; r < kSplitRows; ++r) {
+    const int64_t p = base + r * 64 + lane;
+    const uint32_t up = __shfl_up(sc.key[r], 1), dn = __shfl_down(sc.key[r], 1);
+    const uint32_t pl = r > 0 ? __shfl(sc.key[r > 0 ? r - 1 : 0], 63) : before;
+    const uint32_t nf = r + 1 < kSplitRows ? __shfl(sc.key[r + 1 < kSplitRows ? r + 1 : r], 0) : after;
+    const uint32_t prev = lane == 0 ? pl : up;
+    const uint32_t next = p + 1 >= N ? kSplitNone : (lane == 63 ? nf : dn);
+    const bool valid = p < N;
+    sc.multi |= (uint32_t)(valid && (prev == sc.key[r] || next == sc.key[r])) << r;
+    sc.first |= (uint32_t)(valid && prev != sc.key[r]) << r;
+  }
 }
 
 // (the split at the step's start, main stream) the first entry of every multi run also writes the
-// epoch's multi tag into its row's header
+// epoch's multi tag into its row's header: the headers' t words are read for all rows of the chunk
+// before any tag is written
 __global__ __launch_bounds__(kBlock) void k_split_count(const uint32_t* __restrict__ skeys, int64_t N,
                                                         uint2* __restrict__ cnt, int64_t nchunks, TableView T,
                                                         int32_t epoch) {
   const int lane = threadIdx.x & 63;
   const int64_t c = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
   if (c >= nchunks) return;  // wave-uniform
+  SplitChunk sc;
+  split_chunk(skeys, N, c, lane, sc);
+  const uint32_t tag = sc.multi & sc.first;
+  // every lane loads a t word per row, unconditionally (a guarded load waits out its round trip
+  // before the next is issued): the run's row where it tags one, else row 0's (one shared line)
+  int32_t tv[kSplitRows];
+#pragma unroll
+  for (int r = 0; r < kSplitRows; ++r) tv[r] = T.hdr((tag >> r) & 1u ? sc.key[r] : 0u)->t;
+#pragma unroll
+  for (int r = 0; r < kSplitRows; ++r)
+    if ((tag >> r) & 1u) T.hdr(sc.key[r])->t = multi_tag(epoch, tv[r] >= 0);
   uint32_t nm = 0, ns = 0;
-  for (int r = 0; r < kSplitChunk / 64; ++r) {
-    const int64_t p = c * kSplitChunk + r * 64 + lane;
-    const uint32_t key = p < N ? skeys[p] : 0xFFFFFFFEu;
-    bool first = false;
-    const bool m = split_multi(skeys, N, p, key, lane, &first);
-    if (m && first) {
-      int32_t* t = &T.hdr(key)->t;
-      *t = multi_tag(epoch, *t >= 0);
-    }
+  const int64_t base = c * kSplitChunk;
+#pragma unroll
+  for (int r = 0; r < kSplitRows; ++r) {
+    const bool valid = base + r * 64 + lane < N;
+    const bool m = (sc.multi >> r) & 1u;
     nm += (uint32_t)__popcll(__ballot(m));
-    ns += (uint32_t)__popcll(__ballot(p < N && !m));
+    ns += (uint32_t)__popcll(__ballot(valid && !m));
   }
   if (lane == 0) cnt[c] = make_uint2(nm, ns);
 }
@@ -1692,7 +1768,8 @@ __global__ __launch_bounds__(kBlock) void k_split_count(const uint32_t* __restri
 // one block: exclusive scan of the chunks' multi counts -> off[c]; totals -> n_out[0] (multi
 // entries), n_out[1] (singleton runs).  It sits on the step's critical path (main stream, before
 // the forward), so each thread loads its kSplitPer consecutive chunk counts of a round at once: one
-// memory round trip per 12K chunks (a 12.6M-entry batch: all of a c3 batch), not one per 1024.
+// memory round trip per 12K chunks (a 12.6M-entry batch: all of a c3 batch), not one per 1024
+// (from clamped addresses: as guarded loads they compiled to 48 round trips).
 // 48 against 16 (three rounds at c3): c3 step 0.971-0.975 against 0.976-0.977 ms, three alternating
 // reps (profiles/r04_x); 222 VGPRs, no scratch.
 constexpr int kSplitPer = 48;
@@ -1713,7 +1790,10 @@ __global__ __launch_bounds__(kSplitScanNT) void k_split_scan(const uint2* __rest
     const int64_t i0 = b + (int64_t)threadIdx.x * kSplitPer;
     uint2 v[kSplitPer];
 #pragma unroll
-    for (int j = 0; j < kSplitPer; ++j) v[j] = i0 + j < nchunks ? cnt[i0 + j] : make_uint2(0u, 0u);
+    for (int j = 0; j < kSplitPer; ++j) v[j] = cnt[i0 + j < nchunks ? i0 + j : nchunks - 1];  // clamped: one round trip
+#pragma unroll
+    for (int j = 0; j < kSplitPer; ++j)
+      if (i0 + j >= nchunks) v[j] = make_uint2(0u, 0u);
     int64_t t = 0, sg = 0;
 #pragma unroll
     for (int j = 0; j < kSplitPer; ++j) {
@@ -1761,16 +1841,26 @@ __global__ __launch_bounds__(kBlock) void k_split_scatter(const uint32_t* __rest
   const int64_t c = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
   if (c >= nchunks) return;  // wave-uniform
   const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+  const int64_t base = c * kSplitChunk;
+  // the chunk's payloads with its keys, all loads in one round trip (the payload rows are read
+  // whole: a row of multi entries touches the same lines)
+  uint2 en[kSplitRows];
+#pragma unroll
+  for (int r = 0; r < kSplitRows; ++r) {
+    const int64_t p = base + r * 64 + lane;
+    en[r] = sents[p < N ? p : N - 1];
+  }
   int64_t o = off[c];
-  for (int r = 0; r < kSplitChunk / 64; ++r) {
-    const int64_t p = c * kSplitChunk + r * 64 + lane;
-    const uint32_t key = p < N ? skeys[p] : 0xFFFFFFFEu;
-    const bool m = split_multi(skeys, N, p, key, lane);
+  SplitChunk sc;
+  split_chunk(skeys, N, c, lane, sc);
+#pragma unroll
+  for (int r = 0; r < kSplitRows; ++r) {
+    const bool m = (sc.multi >> r) & 1u;
     const uint64_t bm = __ballot(m);
     if (m) {
       const int64_t d = o + __popcll(bm & lt);
-      mkeys[d] = key;
-      ments[d] = sents[p];
+      mkeys[d] = sc.key[r];
+      ments[d] = en[r];
     }
     o += __popcll(bm);
   }

@@ -78,26 +78,40 @@ __global__ __launch_bounds__(kBlock) void k_radix_count(const uint32_t* __restri
   __shared__ uint32_t hist[R];
   TileGeo g;
   if (!tile_geo(g, n, ntiles)) return;  // block-uniform
-  for (int d = threadIdx.x; d < R; d += kBlock) hist[d] = 0;
-  lds_barrier();
   const int64_t base = g.base;
+  // the tile's keys are loaded first, all together (from clamped addresses: a guarded load waits
+  // out its round trip before the next is issued), and in flight while the histogram is cleared;
   // uint4 reads of whole tiles when the keys are 16-byte aligned (a split view of a dataset starts
   // anywhere)
-  if (vec && base + kTile <= g.end) {
+  constexpr int NV = kTile / (4 * kBlock), NS = kTile / kBlock;
+  const bool wide = vec && base + kTile <= g.end;  // block-uniform
+  uint4 q[NV];
+  uint32_t kk[NS];
+  if (wide) {
     const uint4* k4 = reinterpret_cast<const uint4*>(keys + base);
 #pragma unroll
-    for (int i = 0; i < kTile / (4 * kBlock); ++i) {
-      const uint4 q = k4[i * kBlock + threadIdx.x];
-      atomicAdd(&hist[(q.x >> shift) & M], 1u);
-      atomicAdd(&hist[(q.y >> shift) & M], 1u);
-      atomicAdd(&hist[(q.z >> shift) & M], 1u);
-      atomicAdd(&hist[(q.w >> shift) & M], 1u);
+    for (int i = 0; i < NV; ++i) q[i] = k4[i * kBlock + threadIdx.x];
+  } else {
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+      const int64_t idx = base + (int64_t)i * kBlock + threadIdx.x;
+      kk[i] = keys[idx < g.end ? idx : g.end - 1];
+    }
+  }
+  for (int d = threadIdx.x; d < R; d += kBlock) hist[d] = 0;
+  lds_barrier();
+  if (wide) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      atomicAdd(&hist[(q[i].x >> shift) & M], 1u);
+      atomicAdd(&hist[(q[i].y >> shift) & M], 1u);
+      atomicAdd(&hist[(q[i].z >> shift) & M], 1u);
+      atomicAdd(&hist[(q[i].w >> shift) & M], 1u);
     }
   } else {
-    for (int i = 0; i < kTile / kBlock; ++i) {
-      const int64_t idx = base + (int64_t)i * kBlock + threadIdx.x;
-      if (idx < g.end) atomicAdd(&hist[(keys[idx] >> shift) & M], 1u);
-    }
+#pragma unroll
+    for (int i = 0; i < NS; ++i)
+      if (base + (int64_t)i * kBlock + threadIdx.x < g.end) atomicAdd(&hist[(kk[i] >> shift) & M], 1u);
   }
   lds_barrier();
   for (int d = threadIdx.x; d < R; d += kBlock) counts[g.tile * R + d] = hist[d];
@@ -152,9 +166,16 @@ __global__ __launch_bounds__(256) void k_radix_chunk_top(uint32_t* __restrict__ 
   const int64_t nch = nchunks;
   const int64_t per = (nch + kSl - 1) / kSl;
   const int64_t c0 = min(nch, sl * per), c1 = min(nch, c0 + per);
+  // kTopLd chunks' sums loaded together per round trip (clamped addresses), in chunk order
+  constexpr int kTopLd = 8;
   uint32_t s = 0;
-#pragma unroll 8
-  for (int64_t c = c0; c < c1; ++c) s += csum[c * R + d];
+  for (int64_t cb = c0; cb < c1; cb += kTopLd) {
+    uint32_t x[kTopLd];
+#pragma unroll
+    for (int j = 0; j < kTopLd; ++j) x[j] = csum[(cb + j < c1 ? cb + j : c1 - 1) * R + d];
+#pragma unroll
+    for (int j = 0; j < kTopLd; ++j) s += cb + j < c1 ? x[j] : 0u;
+  }
   part[sl][dl] = s;
   __syncthreads();
   if (sl == 0) {
@@ -169,11 +190,15 @@ __global__ __launch_bounds__(256) void k_radix_chunk_top(uint32_t* __restrict__ 
   }
   __syncthreads();
   uint32_t run = part[sl][dl];
-#pragma unroll 8
-  for (int64_t c = c0; c < c1; ++c) {
-    const uint32_t x = csum[c * R + d];
-    csum[c * R + d] = run;
-    run += x;
+  for (int64_t cb = c0; cb < c1; cb += kTopLd) {
+    uint32_t x[kTopLd];
+#pragma unroll
+    for (int j = 0; j < kTopLd; ++j) x[j] = csum[(cb + j < c1 ? cb + j : c1 - 1) * R + d];
+#pragma unroll
+    for (int j = 0; j < kTopLd; ++j) {
+      if (cb + j < c1) csum[(cb + j) * R + d] = run;
+      run += cb + j < c1 ? x[j] : 0u;
+    }
   }
 }
 
@@ -208,7 +233,10 @@ __device__ __forceinline__ uint2 implicit_payload<uint2>(int64_t idx) {
   return make_uint2((uint32_t)idx, 0u);
 }
 
-template <class P, int RB>
+// IMPLICIT: the payload is each key's index (vals_in is null, the first pass of a sort); a template
+// parameter, so every instantiation issues a fixed number of loads and the block scan waits only
+// for its own
+template <class P, int RB, bool IMPLICIT>
 __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint32_t* __restrict__ keys_in,
                                                           const P* __restrict__ vals_in,
                                                           uint32_t* __restrict__ keys_out,
@@ -220,7 +248,8 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint32_t* __rest
   constexpr int R = 1 << RB;
   constexpr uint32_t M = R - 1;
   constexpr int D = digits_per_thread<R>();  // digits per thread in the block scans
-  const bool own = (int)threadIdx.x * D < R;  // this thread holds digits in the block scans
+  const bool own = R >= kBlock || (int)threadIdx.x * D < R;  // this thread holds digits in the block scans (all of
+  // them when R >= kBlock: no branch, so the digit loads below are issued where they stand)
   // per-wave digit counts and their prefixes stay below the 4096-key tile: 16-bit counters for the
   // 10-bit digits keep the block at 74 KB of LDS, two blocks per CU (32-bit: 90 KB, one block)
   using HistT = typename std::conditional<(RB >= 10), uint16_t, uint32_t>::type;
@@ -241,29 +270,44 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint32_t* __rest
   const int64_t wbase = tile_base + (int64_t)wave * (kTile / kWaves);
   uint32_t my_key[kRounds], my_rank[kRounds];
   P my_val[kRounds];
-  // the tile's loads first: in flight while the digit offsets below are read and scanned
+  // the digit offsets' loads first (the block scan below waits for them; clamped addresses, no
+  // branch around them), then the tile's, in flight through the scan
+  uint32_t tot[D], pcs[D], pct[D];
+#pragma unroll
+  for (int i = 0; i < D; ++i) {
+    const int d = own ? tid * D + i : 0;
+    tot[i] = digit_tot[d];
+    pcs[i] = csum[(tile / kChunk) * R + d];
+    pct[i] = counts[tile * R + d];
+  }
+  // (from clamped addresses, unguarded: a lane past the end loads the last key and is left out of
+  // every ballot and store below by its own validity test)
 #pragma unroll
   for (int r = 0; r < kRounds; ++r) {
     const int64_t idx = wbase + (int64_t)r * 64 + lane;
-    const bool valid = idx < g.end;
-    my_key[r] = valid ? keys_in[idx] : 0u;
-    my_val[r] = valid ? (vals_in ? vals_in[idx] : implicit_payload<P>(idx)) : P{};
+    my_key[r] = keys_in[idx < g.end ? idx : g.end - 1];
   }
+#pragma unroll
+  for (int r = 0; r < kRounds; ++r) {
+    const int64_t idx = wbase + (int64_t)r * 64 + lane;
+    if constexpr (IMPLICIT) my_val[r] = P{};  // made at the staging store
+    else my_val[r] = vals_in[idx < g.end ? idx : g.end - 1];
+  }
+  __builtin_amdgcn_sched_barrier(0);  // keep the loads above in this order, ahead of the scan
 #pragma unroll
   for (int w = 0; w < kWaves; ++w)
     for (int d = tid; d < R; d += kBlock) wave_hist[w][d] = 0;
 
   // global base of (digit, this tile): exclusive scan of digit totals + the tile's running prefix
   // of the digit (its chunk's prefix + its own prefix within the chunk)
-  auto prefix = [&](int64_t t, int d) { return csum[(t / kChunk) * R + d] + counts[t * R + d]; };
   {
     uint32_t v[D];
 #pragma unroll
-    for (int i = 0; i < D; ++i) v[i] = own ? digit_tot[tid * D + i] : 0u;
+    for (int i = 0; i < D; ++i) v[i] = own ? tot[i] : 0u;
     block_excl_scan<D>(v, wsum, lane, wave);
 #pragma unroll
     for (int i = 0; i < D; ++i)
-      if (own) glob_off[tid * D + i] = v[i] + prefix(tile, tid * D + i);
+      if (own) glob_off[tid * D + i] = v[i] + (pcs[i] + pct[i]);
   }
   lds_barrier();
 
@@ -323,7 +367,7 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint32_t* __rest
       const uint32_t d = (my_key[r] >> shift) & M;
       const uint32_t pos = tile_start[d] + wave_hist[wave][d] + my_rank[r];
       s_keys[pos] = my_key[r];
-      s_vals[pos] = my_val[r];
+      s_vals[pos] = IMPLICIT ? implicit_payload<P>(wbase + (int64_t)r * 64 + lane) : my_val[r];
     }
   }
   lds_barrier();
@@ -380,8 +424,9 @@ static void radix_pass_impl(const uint32_t* kin, const P* vin, uint32_t* ko, P* 
                      ntiles, csum);
   hipLaunchKernelGGL(k_radix_chunk_top, dim3((1u << RB) / 32), dim3(256), 0, st, csum, nchunks, 1 << RB,
                      w.digit_tot.as<uint32_t>());
-  hipLaunchKernelGGL((k_radix_scatter<P, RB>), dim3((unsigned)blocks_for_tiles(ntiles)), dim3(kBlock), 0, st, kin,
-                     vin, ko, vo, n, shift, (const uint32_t*)counts, (const uint32_t*)csum,
+  auto scatter = vin ? k_radix_scatter<P, RB, false> : k_radix_scatter<P, RB, true>;
+  hipLaunchKernelGGL(scatter, dim3((unsigned)blocks_for_tiles(ntiles)), dim3(kBlock), 0, st, kin, vin, ko, vo, n,
+                     shift, (const uint32_t*)counts, (const uint32_t*)csum,
                      (const uint32_t*)w.digit_tot.as<uint32_t>(), ntiles);
   FM_HIP_CHECK(hipGetLastError());
 }
