@@ -108,17 +108,39 @@ __global__ __launch_bounds__(kBlock) void k_route_keys(const uint32_t* __restric
                                                        int64_t N, uint32_t R, int sb, uint64_t F,
                                                        const int32_t* __restrict__ pairidx, uint32_t* __restrict__ key,
                                                        uint2* __restrict__ pay) {
-  for (int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x; e < N; e += (int64_t)gridDim.x * kBlock) {
-    const uint32_t id = col[e];
-    const uint2 en = ent[e];
-    if (id >= F) {
-      key[e] = R << sb;
-      pay[e] = make_uint2(0u, en.y);
-      continue;
+  // kRkU entries per thread at once: their ids and entries, then their pair indices, each a single
+  // round trip (clamped indices)
+  constexpr int kRkU = 4;
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  for (int64_t e0 = (int64_t)blockIdx.x * kBlock + threadIdx.x; e0 < N; e0 += kRkU * stride) {
+    uint32_t id[kRkU];
+    uint2 en[kRkU];
+#pragma unroll
+    for (int u = 0; u < kRkU; ++u) {
+      const int64_t e = e0 + u * stride;
+      const int64_t ec = e < N ? e : N - 1;
+      id[u] = col[ec];
+      en[u] = ent[ec];
     }
-    const uint32_t o = id % R;
-    key[e] = (o << sb) | (id / R);
-    pay[e] = make_uint2((uint32_t)pairidx[(int64_t)en.x * R + o], en.y);
+    int32_t px[kRkU];
+#pragma unroll
+    for (int u = 0; u < kRkU; ++u) {
+      const uint32_t o = id[u] < F ? id[u] % R : 0u;
+      px[u] = pairidx[(int64_t)en[u].x * R + o];
+    }
+#pragma unroll
+    for (int u = 0; u < kRkU; ++u) {
+      const int64_t e = e0 + u * stride;
+      if (e >= N) break;
+      if (id[u] >= F) {
+        key[e] = R << sb;
+        pay[e] = make_uint2(0u, en[u].y);
+        continue;
+      }
+      const uint32_t o = id[u] % R;
+      key[e] = (o << sb) | (id[u] / R);
+      pay[e] = make_uint2((uint32_t)px[u], en[u].y);
+    }
   }
 }
 
@@ -223,16 +245,38 @@ __global__ __launch_bounds__(kBlock) void k_pair_index(const uint64_t* __restric
 // index within that source's block: ent2 = {pair = pbase[source] + local, x}, and the first
 // entry of every pair opens it in pair_ptr (one pass, no scan).
 // ent2 == nullptr (one source: its pairs start at 0, so ent2 would equal ent): the pair table only.
-__global__ void k_pair_table(const uint2* __restrict__ ent, int64_t n, const int64_t* __restrict__ src_off,
-                             const int64_t* __restrict__ pbase, int R, int64_t* __restrict__ pair_ptr,
-                             uint2* __restrict__ ent2) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    int r = 0;
-    while (r + 1 < R && src_off[r + 1] <= i) ++r;
-    const uint2 e = ent[i];
-    const uint32_t pair = (uint32_t)pbase[r] + e.x;
-    if (ent2) ent2[i] = make_uint2(pair, e.y);
-    if (i == src_off[r] || ent[i - 1].x != e.x) pair_ptr[pair] = i;
+__global__ __launch_bounds__(kBlock) void k_pair_table(const uint2* __restrict__ ent, int64_t n,
+                                                       const int64_t* __restrict__ src_off,
+                                                       const int64_t* __restrict__ pbase, int R,
+                                                       int64_t* __restrict__ pair_ptr, uint2* __restrict__ ent2) {
+  // the source offsets and pair bases in LDS (a loop of dependent global loads per entry otherwise);
+  // an entry and its predecessor loaded together (clamped index), kPtU entries per thread at once
+  constexpr int kPtU = 4;
+  __shared__ int64_t so[kMaxR + 1], pb[kMaxR];
+  for (int t = threadIdx.x; t <= R; t += kBlock) so[t] = src_off[t];
+  for (int t = threadIdx.x; t < R; t += kBlock) pb[t] = pbase[t];
+  __syncthreads();
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  for (int64_t i0 = (int64_t)blockIdx.x * kBlock + threadIdx.x; i0 < n; i0 += kPtU * stride) {
+    uint2 e[kPtU];
+    uint32_t px[kPtU];
+#pragma unroll
+    for (int u = 0; u < kPtU; ++u) {
+      const int64_t i = i0 + u * stride;
+      const int64_t ic = i < n ? i : n - 1;
+      e[u] = ent[ic];
+      px[u] = ent[ic > 0 ? ic - 1 : 0].x;
+    }
+#pragma unroll
+    for (int u = 0; u < kPtU; ++u) {
+      const int64_t i = i0 + u * stride;
+      if (i >= n) break;
+      int r = 0;
+      while (r + 1 < R && so[r + 1] <= i) ++r;
+      const uint32_t pair = (uint32_t)pb[r] + e[u].x;
+      if (ent2) ent2[i] = make_uint2(pair, e[u].y);
+      if (i == so[r] || px[u] != e[u].x) pair_ptr[pair] = i;
+    }
   }
 }
 
@@ -242,7 +286,11 @@ __global__ void k_pair_table(const uint2* __restrict__ ent, int64_t n, const int
 // (FactorizationMachinesModel.scala:221, :260-262), the loss partial (:230), and the S rows
 // sent back to every owner holding entries of the sample.  Wire layout (structure of arrays):
 // part_vec / s_vec [pair][kp], part_sc / s_sc [pair] float2 ({sum v^2 x^2, sum w x} / {yhat, y}).
-template <int GS>
+// OW > 0 (R <= OW owners): the sample's pair slots live in registers and every owner's loads of a
+// pass are issued before any is used (clamped owner indices; a pair the sample lacks reads poff's
+// first bytes and is masked out) -- as guarded loads, one per owner, each waited out its round trip
+// before the next: 2R + R round trips per sample.  OW = 0: any R up to kMaxR, owner by owner.
+template <int GS, int OW>
 __global__ __launch_bounds__(kBlock) void k_shard_combine(const int32_t* __restrict__ pairidx,
                                                           const int64_t* __restrict__ poff, int R, int64_t B,
                                                           const float* __restrict__ part_vec,
@@ -258,6 +306,64 @@ __global__ __launch_bounds__(kBlock) void k_shard_combine(const int32_t* __restr
     const int32_t* pi = pairidx + s * R;
     double vv = 0.0, wx = 0.0, ss = 0.0;
     bool any = false;
+    if constexpr (OW > 0) {
+      int32_t ix[OW];
+      int64_t pj[OW];  // the sample's pair slot in owner o's block, -1: none
+#pragma unroll
+      for (int o = 0; o < OW; ++o) {
+        const int oc = o < R ? o : R - 1;
+        ix[o] = pi[oc];
+        pj[o] = poff[oc];
+      }
+      float2 t[OW];
+#pragma unroll
+      for (int o = 0; o < OW; ++o) {
+        pj[o] = o < R && ix[o] >= 0 ? pj[o] + ix[o] : -1;
+        t[o] = *(pj[o] >= 0 ? part_sc + pj[o] : reinterpret_cast<const float2*>(poff));
+      }
+#pragma unroll
+      for (int o = 0; o < OW; ++o) {  // owner order, as the loop below
+        vv += pj[o] >= 0 ? (double)t[o].x : 0.0;
+        wx += pj[o] >= 0 ? (double)t[o].y : 0.0;
+        any = any || pj[o] >= 0;
+      }
+      for (int qc = 0; qc < nq; qc += GS) {
+        const int q = qc + g;
+        if (q >= nq) break;  // (q grows with qc)
+        float4 tv[OW];
+#pragma unroll
+        for (int o = 0; o < OW; ++o)
+          tv[o] = pj[o] >= 0 ? reinterpret_cast<const float4*>(part_vec + pj[o] * kp)[q]
+                             : *reinterpret_cast<const float4*>(poff);
+        double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+#pragma unroll
+        for (int o = 0; o < OW; ++o) {
+          const bool ok = pj[o] >= 0;
+          a0 += ok ? (double)tv[o].x : 0.0; a1 += ok ? (double)tv[o].y : 0.0;
+          a2 += ok ? (double)tv[o].z : 0.0; a3 += ok ? (double)tv[o].w : 0.0;
+        }
+        ss += a0 * a0 + a1 * a1 + a2 * a2 + a3 * a3;
+        const float4 sq = make_float4((float)a0, (float)a1, (float)a2, (float)a3);
+#pragma unroll
+        for (int o = 0; o < OW; ++o)
+          if (pj[o] >= 0) reinterpret_cast<float4*>(s_vec + pj[o] * kp)[q] = sq;
+      }
+#pragma unroll
+      for (int o = 1; o < GS; o <<= 1) ss += __shfl_xor(ss, o);
+      const double yhat = 0.5 * (ss - vv) + wx + w0;
+      if (g == 0) {
+        const double y = label[s];
+#pragma unroll
+        for (int o = 0; o < OW; ++o)
+          if (pj[o] >= 0) s_sc[pj[o]] = make_float2((float)(yhat - y), (float)yhat);  // {r, yhat}
+        if (any) {
+          const double d = yhat - y;
+          loss_acc += d * d;
+          nloss += 1.0;
+        }
+      }
+      continue;
+    }
     for (int o = 0; o < R; ++o) {
       const int32_t ix = pi[o];
       if (ix >= 0) {
@@ -740,12 +846,22 @@ int fm_shard_combine(fm_ctx* ctx, fm_batch* b, const void* partials_in, void* s_
     double2* lp = ctx->work.loss_part.as<double2>();
     const double w0 = ctx->cfg.w0;
     const dim3 grid((unsigned)blocks), blk(kBlock);
-    switch (GS) {
-      case 1: hipLaunchKernelGGL(k_shard_combine<1>, grid, blk, 0, st, pi, poff, R, B, pin, psc, lab, kp, w0, so, ssc, lp); break;
-      case 2: hipLaunchKernelGGL(k_shard_combine<2>, grid, blk, 0, st, pi, poff, R, B, pin, psc, lab, kp, w0, so, ssc, lp); break;
-      case 4: hipLaunchKernelGGL(k_shard_combine<4>, grid, blk, 0, st, pi, poff, R, B, pin, psc, lab, kp, w0, so, ssc, lp); break;
-      case 8: hipLaunchKernelGGL(k_shard_combine<8>, grid, blk, 0, st, pi, poff, R, B, pin, psc, lab, kp, w0, so, ssc, lp); break;
-      default: hipLaunchKernelGGL(k_shard_combine<16>, grid, blk, 0, st, pi, poff, R, B, pin, psc, lab, kp, w0, so, ssc, lp); break;
+    if (R <= 8) {
+      switch (GS) {
+        case 1: hipLaunchKernelGGL((k_shard_combine<1, 8>), grid, blk, 0, st, pi, poff, R, B, pin, psc, lab, kp, w0, so, ssc, lp); break;
+        case 2: hipLaunchKernelGGL((k_shard_combine<2, 8>), grid, blk, 0, st, pi, poff, R, B, pin, psc, lab, kp, w0, so, ssc, lp); break;
+        case 4: hipLaunchKernelGGL((k_shard_combine<4, 8>), grid, blk, 0, st, pi, poff, R, B, pin, psc, lab, kp, w0, so, ssc, lp); break;
+        case 8: hipLaunchKernelGGL((k_shard_combine<8, 8>), grid, blk, 0, st, pi, poff, R, B, pin, psc, lab, kp, w0, so, ssc, lp); break;
+        default: hipLaunchKernelGGL((k_shard_combine<16, 8>), grid, blk, 0, st, pi, poff, R, B, pin, psc, lab, kp, w0, so, ssc, lp); break;
+      }
+    } else {
+      switch (GS) {
+        case 1: hipLaunchKernelGGL((k_shard_combine<1, 0>), grid, blk, 0, st, pi, poff, R, B, pin, psc, lab, kp, w0, so, ssc, lp); break;
+        case 2: hipLaunchKernelGGL((k_shard_combine<2, 0>), grid, blk, 0, st, pi, poff, R, B, pin, psc, lab, kp, w0, so, ssc, lp); break;
+        case 4: hipLaunchKernelGGL((k_shard_combine<4, 0>), grid, blk, 0, st, pi, poff, R, B, pin, psc, lab, kp, w0, so, ssc, lp); break;
+        case 8: hipLaunchKernelGGL((k_shard_combine<8, 0>), grid, blk, 0, st, pi, poff, R, B, pin, psc, lab, kp, w0, so, ssc, lp); break;
+        default: hipLaunchKernelGGL((k_shard_combine<16, 0>), grid, blk, 0, st, pi, poff, R, B, pin, psc, lab, kp, w0, so, ssc, lp); break;
+      }
     }
     FM_HIP_CHECK(hipGetLastError());
     ctx->prof_end("combine", e0, st);
