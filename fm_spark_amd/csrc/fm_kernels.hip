@@ -267,10 +267,24 @@ void k_forward(TableView T, const int64_t* __restrict__ row_ptr,
       for (int j = 0; j < U; ++j) {
         const int64_t e = eb + j * RPP;
         ok[j] = e < e1;
-        id[j] = ok[j] ? col[e] : 0u;
-        if (MODE == kPredict) ok[j] = ok[j] && id[j] < (uint64_t)T.rows;
-        // the batch's x stream (4 B per entry); the partial pass's entries carry x themselves
-        x[j] = ok[j] ? (PARTIAL ? __uint_as_float(ent[e].y) : xs[e]) : 0.f;
+        if constexpr (MODE == kTrainFused) {
+          // (the fused forward issues these guarded loads together already; its 5-wave register
+          // budget allocates the unguarded form below differently: c3 within the noise, slower)
+          id[j] = ok[j] ? col[e] : 0u;
+          x[j] = ok[j] ? xs[e] : 0.f;
+        } else {
+          // loaded from a clamped index, unguarded (eb < e1 here): every id and x of the round in
+          // flight at once (a guarded load, or one behind the predict's id test, waits out its round
+          // trip first -- the partial pass's were issued in three groups: R = 8 owner forward 0.356
+          // -> 0.277 ms, profiles/r05_q)
+          const int64_t ec = ok[j] ? e : e1 - 1;
+          const uint32_t idl = col[ec];
+          // the batch's x stream (4 B per entry); the partial pass's entries carry x themselves
+          const float xl = PARTIAL ? __uint_as_float(ent[ec].y) : xs[ec];
+          id[j] = ok[j] ? idl : 0u;
+          if (MODE == kPredict) ok[j] = ok[j] && id[j] < (uint64_t)T.rows;
+          x[j] = ok[j] ? xl : 0.f;
+        }
       }
       if (STASH && eb == e0 + rs) flush(pp_s);  // the previous sample's rows: ids in, gathers not yet issued
       RowHdr h[U];
