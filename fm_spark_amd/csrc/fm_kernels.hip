@@ -810,13 +810,18 @@ __global__ __launch_bounds__(kBlock, NF == 1 ? kUpdMinW : 1) void k_segment_upda
           open = false;
         }
         }
-        if (kPairCfg && paired) flush_pair();  // converged: every lane of the wave
+        // converged: every lane of the wave (with one entry per step, after the next step's
+        // loads: see the loop below)
+        if (kPairCfg && paired && D > 1) flush_pair();
       }
     };
 #pragma unroll 1
     for (int b0 = D; b0 <= RL; b0 += D) {  // the first step's loads are in flight already
       consume(b0 - D, Sp0, Vp0, Hp0, Yp0);
       if (b0 < RL) prefetch(b0, Sp0, Vp0, Hp0, Yp0);
+      // the closed rows' stores after the next step's loads: issued before them, the loads had to
+      // wait for the stores to complete (their destination registers held the stores' data)
+      if (kPairCfg && paired && D == 1) flush_pair();
     }
     const bool tail = open && started;  // the open piece began in this group
     if (open && !started) {             // the head piece runs through the group's end
