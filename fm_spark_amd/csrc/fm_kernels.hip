@@ -128,14 +128,14 @@ __device__ __forceinline__ bool is_multi(int32_t t, int32_t epoch) {
   return t >= kTagPresent ? t - kTagPresent == e : (t <= -2 && -2 - t == e);
 }
 
-// The fused forward at 5 waves per SIMD (96 VGPRs, a few spilled; 107 and 4 waves unbounded):
-// c3 step 0.98 against 1.03 ms in three alternating A/B pairs on one box, 0.989 against 1.003-1.009
-// on another; 6 waves (80 VGPRs, more spills) 1.066 (profiles/r03_v9/ab, r03_v10/ab).  Its
-// latency-bound gathers want waves in flight more than registers.  The other modes keep the
-// compiler's choice.
+// The fused forward at 4 waves per SIMD (107 VGPRs, no spill).  Round 3 measured 5 waves (96
+// VGPRs, a few spilled) faster: c3 step 0.98 against 1.03 ms (profiles/r03_v9/ab, r03_v10/ab);
+// with the small kernels' latency chains cut (round 5) the spills cost more than the fifth wave
+// buys: 0.881-0.882 against 0.892-0.894 ms, five alternating reps (profiles/r05_w2).  6 waves (80
+// VGPRs, more spills) measured 1.066 in round 3.  The other modes keep the compiler's choice.
 template <int MODE, int GS>
-constexpr int fwd_min_waves() { return MODE == kTrainFused && GS == 4 ? 5 : 1; }  // k = 9..16 (smaller
-// k: the stash's LDS holds the block count below 5 waves anyway)
+constexpr int fwd_min_waves() { return MODE == kTrainFused && GS == 4 ? 4 : 1; }  // k = 9..16 (smaller
+// k: the stash's LDS holds the block count below 4 waves anyway)
 template <int GS, int TEAM, int MODE, int U>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(fwd_min_waves<MODE, GS>())))
 void k_forward(TableView T, const int64_t* __restrict__ row_ptr,
@@ -268,8 +268,8 @@ void k_forward(TableView T, const int64_t* __restrict__ row_ptr,
         const int64_t e = eb + j * RPP;
         ok[j] = e < e1;
         if constexpr (MODE == kTrainFused) {
-          // (the fused forward issues these guarded loads together already; its 5-wave register
-          // budget allocates the unguarded form below differently: c3 within the noise, slower)
+          // (the fused forward issues these guarded loads together already; under its register
+          // budget the unguarded form below came out c3 within the noise, slower: profiles/r05_q)
           id[j] = ok[j] ? col[e] : 0u;
           x[j] = ok[j] ? xs[e] : 0.f;
         } else {
