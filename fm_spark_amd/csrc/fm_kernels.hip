@@ -103,10 +103,11 @@ constexpr int kFwdTeam = 32, kFwdU = 2;
 // (profiles/r04_o)
 constexpr int kFwdUNarrow = 3;
 constexpr int kFwdGrid = 2048;  // forward blocks at most (grid-stride over samples beyond)
-// the fused forward (kTrainFused): 3 passes in flight (24 rows per sample at k = 16, so a 39-entry
-// sample takes two rounds instead of three); c3 step -2 to -4 % against 2 passes, 4 passes slower
-// (tools/r03_xp2.sh, profiles/r03_v7/ab)
-constexpr int kFuseU = 3;
+// the fused forward (kTrainFused): 5 passes in flight (40 rows per sample at k = 16, so a 39-entry
+// c3 sample takes one round instead of two): round 5 at 4 waves per SIMD, c3 0.869-0.872 against
+// 0.878-0.883 ms for 3 passes, 4 passes slower (profiles/r05_x); round 3 had taken 3 (-2 to -4 %
+// against 2, 4 slower under the 5-wave cap: profiles/r03_v7/ab)
+constexpr int kFuseU = 5;
 
 // Singleton rows.  fm_batch_prepare sorts the batch (side stream); at the start of the step the
 // split (k_split_*, main stream) keeps the runs of two or more entries (the only ones that need a
