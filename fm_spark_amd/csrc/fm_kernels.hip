@@ -102,7 +102,10 @@ constexpr int kFwdTeam = 32, kFwdU = 2;
 // 0.173 against 0.175 / 0.174 ms per step (median 0.162 against 0.165), at c5 (k = 16) slower
 // (profiles/r04_o)
 constexpr int kFwdUNarrow = 3;
-constexpr int kFwdGrid = 2048;  // forward blocks at most (grid-stride over samples beyond)
+// forward blocks at most (grid-stride over samples beyond): 8192 (four samples per team at c3, one at
+// c2 / c5) against 2048 in round 5, c3 0.859-0.863 against 0.867-0.869 ms, c2 0.161-0.163 against
+// 0.163-0.168, c5 0.178-0.181 against 0.182-0.185 (profiles/r05_ab, r05_ac; 1024 and 32768 slower)
+constexpr int kFwdGrid = 8192;
 // the fused forward (kTrainFused): 5 passes in flight (40 rows per sample at k = 16, so a 39-entry
 // c3 sample takes one round instead of two): round 5 at 4 waves per SIMD, c3 0.869-0.872 against
 // 0.878-0.883 ms for 3 passes, 4 passes slower (profiles/r05_x); round 3 had taken 3 (-2 to -4 %
