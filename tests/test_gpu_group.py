@@ -42,7 +42,7 @@ def _check_tables(ctx, model):
 
 @pytest.mark.parametrize("R,k,F,hot,transport", [
     (1, 8, 503, 11, "copy"), (2, 16, 503, 11, "copy"), (3, 5, 401, 7, "copy"), (4, 32, 513, 512, "copy"),
-    (8, 16, 1031, 1030, "copy"), (1, 16, 300, 2, "rccl"),
+    (8, 16, 1031, 1030, "copy"), (12, 8, 1031, 1030, "copy"), (1, 16, 300, 2, "rccl"),
 ])
 def test_group_sharded_step_matches_oracle(gpu, R, k, F, hot, transport):
     _, ids, w, V = make_problem(3, 1, F, k, 1)

@@ -80,10 +80,11 @@ def _simulated_step(engines, batches, t, step_size, reg):
 # slot (id F - 1, made hot) needs one more key bit than a rank with fewer rows would give it
 @pytest.mark.parametrize("R,k,F,hot", [(1, 8, 503, 11), (2, 16, 503, 11), (3, 5, 503, 11), (4, 32, 503, 11),
                                        (2, 8, 513, 512), (4, 4, 513, 512), (1, 16, 503, 11), (3, 8, 503, 11),
-                                       (8, 16, 1031, 7)])
+                                       (8, 16, 1031, 7), (12, 16, 1031, 7)])
 def test_hip_shard_phases_match_single_table(gpu, R, k, F, hot):
     """The fm_shard_* phases driven one by one (the all-to-alls done by slicing) against the fp64
-    oracle step over the concatenated batches."""
+    oracle step over the concatenated batches (R = 12: the combine's any-R path; R <= 8 keeps each
+    sample's pair slots in registers)."""
     from fm_spark_amd._native import CSRHost
     from fm_spark_amd.distributed import HipShardEngine
 
