@@ -1790,19 +1790,17 @@ __global__ __launch_bounds__(kBlock) void k_split_count(const uint32_t* __restri
 
 // one block: exclusive scan of the chunks' multi counts -> off[c]; totals -> n_out[0] (multi
 // entries), n_out[1] (singleton runs).  It sits on the step's critical path (main stream, before
-// the forward), so each thread loads its kSplitPer consecutive chunk counts of a round at once: one
-// memory round trip per 12K chunks (a 12.6M-entry batch: all of a c3 batch), not one per 1024
-// (from clamped addresses: as guarded loads they compiled to 48 round trips).
-// 48 against 16 (three rounds at c3): c3 step 0.971-0.975 against 0.976-0.977 ms, three alternating
-// reps (profiles/r04_x); 222 VGPRs, no scratch.
-constexpr int kSplitPer = 48;
-// one 256-thread block: it finds room on a CU beside the
-// sort's blocks sooner than a 1024-thread one -- c3 step 0.971-0.975 against 0.992-0.995 ms (1024)
-// and 0.978-0.982 (64), three alternating reps (profiles/r03_v13/ab).  Scanning in the count pass's
-// last block instead (a device-scope counter, a release fence per block) cost 1.355 against 0.973 ms:
-// each fence writes back the XCD's L2 (profiles/r04_v); no scan at all, each scatter block summing
-// the count pass's block totals before it, 1.025 against 0.976 ms (profiles/r04_w)
-constexpr int kSplitScanNT = 256;
+// the forward), so each thread loads its kSplitPer consecutive chunk counts of a round at once
+// (from clamped addresses: as guarded loads they compiled to one round trip each):
+// one memory round trip per 12K chunks (a 12.6M-entry batch: all of a c3 batch).  1024 threads x 12
+// counts since round 5 (c3 0.852-0.856 against 0.856-0.862 ms for 256 x 48, four alternating reps,
+// profiles/r05_aj); in round 3, with its loads still chained, 256 threads had been the faster block
+// (profiles/r03_v13/ab).  Scanning in the count pass's last block instead (a device-scope counter, a
+// release fence per block) cost 1.355 against 0.973 ms: each fence writes back the XCD's L2
+// (profiles/r04_v); no scan at all, each scatter block summing the count pass's block totals before
+// it, 1.025 against 0.976 ms (profiles/r04_w)
+constexpr int kSplitPer = 12;
+constexpr int kSplitScanNT = 1024;
 __global__ __launch_bounds__(kSplitScanNT) void k_split_scan(const uint2* __restrict__ cnt, int64_t nchunks,
                                                              int64_t* __restrict__ off, int64_t* __restrict__ n_out) {
   constexpr int NW = kSplitScanNT / 64;
