@@ -85,6 +85,9 @@ def parse():
                         "sharded, routed (and its entries exchanged and slot-sorted) on the side streams; 0 = 1 for "
                         "the single table (c3, 20-step runs: 0.990-0.997 against 1.000-1.004 ms for 2, 1.017-1.024 for "
                         "3; profiles/r03_v15/depth), 2 for a group (two-phase prepare: each route gets a step)")
+    p.add_argument("--sort", default="default", choices=["default", "lsd"],
+                   help="grouping by feature: the two-level grouping (default) or the LSD radix passes "
+                        "(fm_config.sort_algo)")
     p.add_argument("--fuse", default="auto", choices=["auto", "on", "off"],
                    help="single table, k <= 16: the fused step (the forward updates the rows whose feature has one "
                         "entry in the batch; fm_config.fuse_single): auto = the library's default (tables larger "
@@ -522,7 +525,7 @@ def main():
     xg = None
     if mode == "single":
         ctx = FMContext(F, k, device=local_rank, seed=20261015, init_sd=INIT_SD,
-                        fuse={"auto": None, "on": True, "off": False}[args.fuse])
+                        fuse={"auto": None, "on": True, "off": False}[args.fuse], sort=args.sort)
         # launch on a torch stream of our own so torch events can bracket every step on it
         main_stream = torch.cuda.Stream()
         torch.cuda.set_stream(main_stream)
@@ -618,7 +621,7 @@ def main():
             cid = bytes(idt.tolist())
         ctx = FMContext(F, k, seed=20261015, init_sd=INIT_SD, parallel=par, n_gpus=L, devices=pl["devices"],
                         transport="rccl", n_procs=world if mode == "procs" else 1, proc_rank=rank, comm_id=cid,
-                        fuse={"auto": None, "on": True, "off": False}[args.fuse])
+                        fuse={"auto": None, "on": True, "off": False}[args.fuse], sort=args.sort)
         main_stream = None
         if L == 1:  # launch on a torch stream so torch events time each step on it
             main_stream = torch.cuda.Stream()

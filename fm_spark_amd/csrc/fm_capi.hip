@@ -394,8 +394,17 @@ int step_impl(fm_ctx* ctx, fm_batch* b, int32_t t, double step_size, double reg_
     // alternating reps, profiles/r04_i)
     FM_HIP_CHECK(hipStreamWaitEvent(ctx->stream, b->ready, 0));
     e0 = ctx->prof_begin(ctx->stream);
-    launch_split(b->fkeys.as<uint32_t>(), b->fents.as<uint2>(), N, ctx->split_work, b->skeys.as<uint32_t>(),
-                 b->sents.as<uint2>(), b->split_n.as<int64_t>(), ctx->stream, T, p.epoch);
+    if (b->msd.ok) {
+      // the two-level grouping's second level (fm_msd.hip): each level-1 bucket sorted in LDS and split,
+      // the multi view compacted across buckets, the tags written as the runs are found
+      const bool one = b->msd.hb == 0;  // one bucket: the batch itself
+      msd_split(b->msd, one ? b->dev.col.as<uint32_t>() : b->fkeys.as<uint32_t>(),
+                one ? b->dev.ent.as<uint2>() : b->fents.as<uint2>(), b->btot.as<uint32_t>(), N, ctx->msd_main,
+                b->skeys.as<uint32_t>(), b->sents.as<uint2>(), b->split_n.as<int64_t>(), ctx->stream, &T, p.epoch);
+    } else {
+      launch_split(b->fkeys.as<uint32_t>(), b->fents.as<uint2>(), N, ctx->split_work, b->skeys.as<uint32_t>(),
+                   b->sents.as<uint2>(), b->split_n.as<int64_t>(), ctx->stream, T, p.epoch);
+    }
     ctx->prof_end("split", e0, ctx->stream);
     fx.fused = true;
   }
@@ -450,6 +459,8 @@ int fm_create(const fm_config* cfg, fm_ctx** out) {
     FM_REQUIRE(cfg->init_sd >= 0.0, "init_sd must be >= 0");
     FM_REQUIRE(cfg->fuse_single == FM_FUSE_DEFAULT || cfg->fuse_single == FM_FUSE_ON || cfg->fuse_single == FM_FUSE_OFF,
                "fuse_single must be FM_FUSE_DEFAULT, FM_FUSE_ON or FM_FUSE_OFF");
+    FM_REQUIRE(cfg->sort_algo == FM_SORT_DEFAULT || cfg->sort_algo == FM_SORT_LSD,
+               "sort_algo must be FM_SORT_DEFAULT or FM_SORT_LSD");
     int ndev = 0;
     FM_HIP_CHECK(hipGetDeviceCount(&ndev));
     FM_REQUIRE(cfg->device >= 0 && cfg->device < ndev, "device ordinal out of range");
@@ -726,17 +737,39 @@ int fm_batch_prepare(fm_ctx* ctx, fm_batch* b) {
     const int kb = bits_for(ctx->rows - 1);
     const uint32_t* col = b->dev.col.as<uint32_t>();
     const uint2* ent = b->dev.ent.as<uint2>();
+    b->msd = ctx->cfg.sort_algo == FM_SORT_LSD ? MsdPlan{} : msd_plan(N, kb);
+    SortWork& w = ctx->work.sort;
     if (b->split) {
-      // the fused step's batch: the whole sorted view (fkeys / fents), which the step splits into the
-      // multi view (skeys / sents, {their count, the number of singleton runs} in split_n)
+      // the fused step's batch, which the step splits into the multi view (skeys / sents, {their count,
+      // the number of singleton runs} in split_n): the level-1 buckets and their sizes (fkeys / fents,
+      // btot; nothing for a one-bucket batch) or, with the LSD passes, the whole sorted view
       b->split_n.ensure(2 * sizeof(int64_t));
-      b->fkeys.ensure_slack(sizeof(uint32_t) * N);
-      b->fents.ensure_slack(sizeof(uint2) * N);
-      radix_sort_pairs64(ctx->work.sort, col, ent, N, kb, ctx->side, &sk, &sv, b->fkeys.as<uint32_t>(),
-                         b->fents.as<uint2>());
+      if (!b->msd.ok || b->msd.hb > 0) {
+        b->fkeys.ensure_slack(sizeof(uint32_t) * N);
+        b->fents.ensure_slack(sizeof(uint2) * N);
+      }
+      if (b->msd.ok && b->msd.hb > 0) {
+        b->btot.ensure(sizeof(uint32_t) * kMaxBuckets);
+        radix_partition_pairs64(w, col, ent, N, b->msd.sh, b->msd.hb, ctx->side, b->fkeys.as<uint32_t>(),
+                                b->fents.as<uint2>(), b->btot.as<uint32_t>());
+      } else if (!b->msd.ok) {
+        radix_sort_pairs64(w, col, ent, N, kb, ctx->side, &sk, &sv, b->fkeys.as<uint32_t>(), b->fents.as<uint2>());
+      }
+    } else if (b->msd.ok) {
+      // the whole sorted view by the two levels, both here (side stream)
+      if (b->msd.hb > 0) {
+        w.ensure(N);
+        radix_partition_pairs64(w, col, ent, N, b->msd.sh, b->msd.hb, ctx->side, w.keys_a.as<uint32_t>(),
+                                w.vals_a.as<uint2>(), w.digit_tot.as<uint32_t>());
+        msd_sort_full(b->msd, w.keys_a.as<uint32_t>(), w.vals_a.as<uint2>(), w.keys_b.as<uint32_t>(),
+                      w.vals_b.as<uint2>(), w.digit_tot.as<uint32_t>(), N, b->skeys.as<uint32_t>(),
+                      b->sents.as<uint2>(), ctx->side);
+      } else {
+        msd_sort_full(b->msd, col, ent, nullptr, nullptr, nullptr, N, b->skeys.as<uint32_t>(), b->sents.as<uint2>(),
+                      ctx->side);
+      }
     } else {
-      radix_sort_pairs64(ctx->work.sort, col, ent, N, kb, ctx->side, &sk, &sv, b->skeys.as<uint32_t>(),
-                         b->sents.as<uint2>());
+      radix_sort_pairs64(w, col, ent, N, kb, ctx->side, &sk, &sv, b->skeys.as<uint32_t>(), b->sents.as<uint2>());
     }
     ctx->prof_end("sort", es, ctx->side);
     FM_HIP_CHECK(hipEventRecord(b->ready, ctx->side));

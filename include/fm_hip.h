@@ -50,6 +50,8 @@ extern "C" {
 #define FM_FUSE_DEFAULT 0 /* fm_config.fuse_single: the library's choice (tables above 256 MB) */
 #define FM_FUSE_ON 1
 #define FM_FUSE_OFF (-1)
+#define FM_SORT_DEFAULT 0 /* fm_config.sort_algo: the two-level grouping where it applies, else LSD */
+#define FM_SORT_LSD 1     /* the stable LSD radix passes only */
 
 typedef struct fm_ctx fm_ctx;
 typedef struct fm_batch fm_batch;
@@ -85,6 +87,11 @@ typedef struct fm_batch fm_batch;
  * xchg_chunks  : sharded step with R > 1: the owners' partial pass runs in this many chunks, each
  *                sent while the next is computed (0 = the default, 4; 1 = one pass then one
  *                all-to-all; at most 64).  Every process of a job must pass the same value.
+ * sort_algo    : how a prepared batch is grouped by feature (the reference's groupBy featureId,
+ *                SGD.scala:148-155).  FM_SORT_DEFAULT: one radix pass on the slot's top bits, then each
+ *                bucket sorted in LDS (and, for the fused step, split into its runs of two or more at
+ *                the step); FM_SORT_LSD: the LSD radix passes.  Both are stable sorts by slot, so the
+ *                step's tables are bitwise the same either way.
  * Zero-initialise the struct: every field's 0 is its default. */
 typedef struct fm_config {
   int64_t num_features;
@@ -104,6 +111,7 @@ typedef struct fm_config {
   uint8_t comm_id[128];
   int32_t fuse_single;
   int32_t xchg_chunks;
+  int32_t sort_algo;
 } fm_config;
 
 /* One mini-batch in CSR form: the result of explode(udfVecToMap(features))
