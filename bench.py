@@ -85,9 +85,9 @@ def parse():
                         "sharded, routed (and its entries exchanged and slot-sorted) on the side streams; 0 = 1 for "
                         "the single table (c3, 20-step runs: 0.990-0.997 against 1.000-1.004 ms for 2, 1.017-1.024 for "
                         "3; profiles/r03_v15/depth), 2 for a group (two-phase prepare: each route gets a step)")
-    p.add_argument("--sort", default="default", choices=["default", "lsd"],
-                   help="grouping by feature: the two-level grouping (default) or the LSD radix passes "
-                        "(fm_config.sort_algo)")
+    p.add_argument("--copy-ranks", type=int, default=0,
+                   help="measurement only: run an R-rank group job on GPU 0 (COPY transport), e.g. to time the "
+                        "one host thread's per-iteration enqueue at R = 8; the line is not a multi-GPU result")
     p.add_argument("--fuse", default="auto", choices=["auto", "on", "off"],
                    help="single table, k <= 16: the fused step (the forward updates the rows whose feature has one "
                         "entry in the batch; fm_config.fuse_single): auto = the library's default (tables larger "
@@ -177,12 +177,16 @@ def fit_leg(ctx, F, B, zipf_s, lab, iters, parts=16):
     ds = concat_batches([synthetic_batch(B, F, batch_index=7000 + i, zipf_s=zipf_s, **lab) for i in range(iters)])
     n = ds.n_rows
     sizes = [n * (i + 1) // parts - n * i // parts for i in range(parts)]
+    t_gen = time.perf_counter() - t0
+    t0 = time.perf_counter()
     split_of, _, order = random_split_csr(sizes, ds.label, ds.row_ptr, ds.col, ds.val, F, [0.1] * iters, 1234)
+    t_sampler = time.perf_counter() - t0
+    t0 = time.perf_counter()
     splits = [order[split_of[order] == i] for i in range(iters)]
     rest = order[split_of[order] < 0]
     lay = _select_csr(ds.row_ptr, ds.col, ds.val, ds.label, np.concatenate(splits + [rest]).astype(np.int64))
     split_rows = np.concatenate([[0], np.cumsum([len(r) for r in splits] + [len(rest)])])
-    t_split = time.perf_counter() - t0
+    t_layout = time.perf_counter() - t0
     t0 = time.perf_counter()
     data = ctx.batch_splits(lay, split_rows)
     ctx.sync()
@@ -204,7 +208,8 @@ def fit_leg(ctx, F, B, zipf_s, lab, iters, parts=16):
             "fit_ms_per_iter_steady": 1e3 * (dt - dt_half) / (iters - half) if iters > half else None,
             "samples_per_s": float(np.sum(rows)) / dt, "dataset_rows": n, "partitions": parts,
             "finite_losses": bool(np.all(np.isfinite(losses))),
-            "setup_s": {"generate_and_split": t_split, "upload_once": t_upload},
+            "setup_s": {"generate": t_gen, "random_split": t_sampler, "layout": t_layout, "upload_once": t_upload,
+                        "random_split_threads": sampler_threads()},
             "what": "FactorizationMachinesSGD.fit's mini-batch loop on the resident dataset laid out split after "
                     "split (fm_batch_create_splits): each randomSplit split stepped in place through a view "
                     "(fm_batch_split_view: no copy, no gather) and sorted on the side stream while the previous split "
@@ -215,6 +220,11 @@ def fit_leg(ctx, F, B, zipf_s, lab, iters, parts=16):
 
 def log(msg):
     print(msg, file=sys.stderr, flush=True)
+
+
+def sampler_threads():
+    # fm_random_split's partitions run on the library's host pool: min(16, hardware threads)
+    return min(16, os.cpu_count() or 1)
 
 
 def algorithmic_bytes(F, k, B, z, U):
@@ -424,6 +434,11 @@ def plan_run(args, env, n_visible):
                 "parallel": par, "devices": list(range(args.gpus))}
     if n_visible < 1:
         raise PlanError("no GPU visible")
+    if args.copy_ranks > 1:
+        # measurement only: an R-rank job on this one GPU (COPY transport: device copies between the
+        # ranks' buffers), e.g. the one host thread's enqueue and prepare cost at R = 8
+        return {"mode": "group", "world": args.copy_ranks, "rank": 0, "local_rank": 0, "n_local": args.copy_ranks,
+                "parallel": par, "devices": [0] * args.copy_ranks}
     if args.force_sharded or args.parallel != "auto":
         return {"mode": "group", "world": 1, "rank": 0, "local_rank": 0, "n_local": 1, "parallel": par,
                 "devices": [0]}
@@ -525,7 +540,7 @@ def main():
     xg = None
     if mode == "single":
         ctx = FMContext(F, k, device=local_rank, seed=20261015, init_sd=INIT_SD,
-                        fuse={"auto": None, "on": True, "off": False}[args.fuse], sort=args.sort)
+                        fuse={"auto": None, "on": True, "off": False}[args.fuse])
         # launch on a torch stream of our own so torch events can bracket every step on it
         main_stream = torch.cuda.Stream()
         torch.cuda.set_stream(main_stream)
@@ -620,8 +635,9 @@ def main():
             dist.broadcast(idt, src=0)
             cid = bytes(idt.tolist())
         ctx = FMContext(F, k, seed=20261015, init_sd=INIT_SD, parallel=par, n_gpus=L, devices=pl["devices"],
-                        transport="rccl", n_procs=world if mode == "procs" else 1, proc_rank=rank, comm_id=cid,
-                        fuse={"auto": None, "on": True, "off": False}[args.fuse], sort=args.sort)
+                        transport="copy" if args.copy_ranks > 1 else "rccl", n_procs=world if mode == "procs" else 1,
+                        proc_rank=rank, comm_id=cid,
+                        fuse={"auto": None, "on": True, "off": False}[args.fuse])
         main_stream = None
         if L == 1:  # launch on a torch stream so torch events time each step on it
             main_stream = torch.cuda.Stream()
@@ -788,7 +804,12 @@ def main():
                                   f"timed region: the pipeline in its steady state, each step preparing the batch "
                                   f"{depth} steps ahead (the first {depth} timed steps' batches were prepared before it)")
         if prof:
-            kern = {name: {"avg_ms": ms / max(n, 1), "launches": n} for name, (ms, n) in prof.items()}
+            # "host_*": the one-thread multi-GPU driver's host time per phase (fm_group.hip HostClock)
+            hostp = {name: ms / max(n, 1) for name, (ms, n) in prof.items() if name.startswith("host_")}
+            if hostp:
+                line.setdefault("host_trace", {})["phases_ms"] = hostp
+            kern = {name: {"avg_ms": ms / max(n, 1), "launches": n} for name, (ms, n) in prof.items()
+                    if not name.startswith("host_")}
             line["kernels"] = kern
             if args.trainer == "lib" and not args.host_path:
                 line["kernels_sampled"] = f"HIP events on every {max(1, args.profile_every)}. timed step (launch streams)"
@@ -880,7 +901,7 @@ def main():
                                                                 (XGMI_LINK_GBS * (world - 1)) if world > 1 else None),
                                         vs_step_algorithmic_bytes=xg["allreduce_B"] / max(fwd_b + upd_b, 1.0))
         if host_trace:
-            line["host_trace"] = host_trace
+            line["host_trace"] = {**host_trace, **line.get("host_trace", {})}
         if host_path:
             line["host_path_ms_per_step"] = host_path["median_ms_per_step"]
             line["host_path"] = host_path

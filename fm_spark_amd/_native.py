@@ -20,7 +20,6 @@ FM_PARALLEL_NONE, FM_PARALLEL_SHARDED, FM_PARALLEL_REPLICATED = 0, 1, 2
 FM_TRANSPORT_AUTO, FM_TRANSPORT_RCCL, FM_TRANSPORT_COPY = 0, 1, 2
 FM_MAX_LOCAL = 16
 FM_FUSE_DEFAULT, FM_FUSE_ON, FM_FUSE_OFF = 0, 1, -1
-FM_SORT_DEFAULT, FM_SORT_LSD = 0, 1
 
 
 class FMError(RuntimeError):
@@ -46,7 +45,6 @@ class fm_config(C.Structure):
         ("comm_id", C.c_uint8 * 128),
         ("fuse_single", C.c_int32),
         ("xchg_chunks", C.c_int32),
-        ("sort_algo", C.c_int32),
     ]
 
 

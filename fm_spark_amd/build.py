@@ -16,9 +16,9 @@ INCLUDE = PKG.parent / "include"
 ARCH = os.environ.get("FM_HIP_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
-SOURCES = ["fm_kernels.hip", "fm_sort.hip", "fm_msd.hip", "fm_capi.hip", "fm_shard.hip", "fm_group.hip", "fm_sampler.cpp",
+SOURCES = ["fm_kernels.hip", "fm_sort.hip", "fm_capi.hip", "fm_shard.hip", "fm_group.hip", "fm_sampler.cpp",
            "fm_libsvm.cpp"]
-HEADERS = ["fm_internal.h", "fm_device.h", "fm_context.h"]
+HEADERS = ["fm_internal.h", "fm_device.h", "fm_context.h", "fm_hostpool.h"]
 
 CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function", "-Wno-unused-variable"]
 

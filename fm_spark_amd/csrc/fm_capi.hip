@@ -16,6 +16,7 @@
 #include <utility>
 
 #include "fm_context.h"
+#include "fm_hostpool.h"
 
 namespace fmhip {
 
@@ -47,89 +48,6 @@ void DevBuf::release() {
   p = nullptr;
   bytes = 0;
 }
-
-// A persistent pool of host threads (up to 16: the GPU box's CPU share per GPU) for the host passes
-// of fm_step's upload and fm_batch_from_rows: spawning the threads per call cost about as much as
-// the work.  One job at a time (callers serialise on run_mu); the calling thread works too.
-// at most 16 threads (the GPU box's CPU share per GPU; 8 measured the same in the fit loop)
-constexpr int kHostThreadsMax = 16;
-class HostPool {
- public:
-  static HostPool& get() {
-    static HostPool p;
-    return p;
-  }
-  int threads() const { return (int)workers_.size() + 1; }
-  // f(i) for every i in [0, n)
-  void run(int n, const std::function<void(int)>& f) {
-    if (n <= 0) return;
-    std::lock_guard<std::mutex> job_lk(run_mu_);
-    if (n == 1 || workers_.empty()) {
-      for (int i = 0; i < n; ++i) f(i);
-      return;
-    }
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      job_ = &f;
-      njobs_ = n;
-      next_.store(0);
-      done_ = 0;
-      ++gen_;
-    }
-    cv_.notify_all();
-    work();
-    std::unique_lock<std::mutex> lk(mu_);
-    done_cv_.wait(lk, [&] { return done_ == njobs_; });
-    job_ = nullptr;
-  }
-  ~HostPool() {
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      stop_ = true;
-    }
-    cv_.notify_all();
-    for (auto& t : workers_) t.join();
-  }
-
- private:
-  HostPool() {
-    const int hw = std::max(1, (int)std::thread::hardware_concurrency());
-    const int T = std::min(kHostThreadsMax, hw);
-    for (int t = 1; t < T; ++t) workers_.emplace_back([this] { loop(); });
-  }
-  void work() {
-    int mine = 0;
-    for (int i = next_.fetch_add(1); i < njobs_; i = next_.fetch_add(1)) {
-      (*job_)(i);
-      ++mine;
-    }
-    if (mine) {
-      std::lock_guard<std::mutex> lk(mu_);
-      done_ += mine;
-      if (done_ == njobs_) done_cv_.notify_all();
-    }
-  }
-  void loop() {
-    uint64_t seen = 0;
-    for (;;) {
-      {
-        std::unique_lock<std::mutex> lk(mu_);
-        cv_.wait(lk, [&] { return stop_ || (gen_ != seen && job_ != nullptr); });
-        if (stop_) return;
-        seen = gen_;
-      }
-      work();
-    }
-  }
-  std::vector<std::thread> workers_;
-  std::mutex run_mu_, mu_;
-  std::condition_variable cv_, done_cv_;
-  const std::function<void(int)>* job_ = nullptr;
-  int njobs_ = 0, done_ = 0;
-  std::atomic<int> next_{0};
-  uint64_t gen_ = 0;
-  bool stop_ = false;
-};
 
 // How many contiguous chunks parallel_chunks cuts [0, n) into (one per pool thread, at least
 // min_per_thread items each).
@@ -394,17 +312,8 @@ int step_impl(fm_ctx* ctx, fm_batch* b, int32_t t, double step_size, double reg_
     // alternating reps, profiles/r04_i)
     FM_HIP_CHECK(hipStreamWaitEvent(ctx->stream, b->ready, 0));
     e0 = ctx->prof_begin(ctx->stream);
-    if (b->msd.ok) {
-      // the two-level grouping's second level (fm_msd.hip): each level-1 bucket sorted in LDS and split,
-      // the multi view compacted across buckets, the tags written as the runs are found
-      const bool one = b->msd.hb == 0;  // one bucket: the batch itself
-      msd_split(b->msd, one ? b->dev.col.as<uint32_t>() : b->fkeys.as<uint32_t>(),
-                one ? b->dev.ent.as<uint2>() : b->fents.as<uint2>(), b->btot.as<uint32_t>(), N, ctx->msd_main,
-                b->skeys.as<uint32_t>(), b->sents.as<uint2>(), b->split_n.as<int64_t>(), ctx->stream, &T, p.epoch);
-    } else {
-      launch_split(b->fkeys.as<uint32_t>(), b->fents.as<uint2>(), N, ctx->split_work, b->skeys.as<uint32_t>(),
-                   b->sents.as<uint2>(), b->split_n.as<int64_t>(), ctx->stream, T, p.epoch);
-    }
+    launch_split(b->fkeys.as<uint32_t>(), b->fents.as<uint2>(), N, ctx->split_work, b->skeys.as<uint32_t>(),
+                 b->sents.as<uint2>(), b->split_n.as<int64_t>(), ctx->stream, T, p.epoch);
     ctx->prof_end("split", e0, ctx->stream);
     fx.fused = true;
   }
@@ -459,8 +368,6 @@ int fm_create(const fm_config* cfg, fm_ctx** out) {
     FM_REQUIRE(cfg->init_sd >= 0.0, "init_sd must be >= 0");
     FM_REQUIRE(cfg->fuse_single == FM_FUSE_DEFAULT || cfg->fuse_single == FM_FUSE_ON || cfg->fuse_single == FM_FUSE_OFF,
                "fuse_single must be FM_FUSE_DEFAULT, FM_FUSE_ON or FM_FUSE_OFF");
-    FM_REQUIRE(cfg->sort_algo == FM_SORT_DEFAULT || cfg->sort_algo == FM_SORT_LSD,
-               "sort_algo must be FM_SORT_DEFAULT or FM_SORT_LSD");
     int ndev = 0;
     FM_HIP_CHECK(hipGetDeviceCount(&ndev));
     FM_REQUIRE(cfg->device >= 0 && cfg->device < ndev, "device ordinal out of range");
@@ -737,39 +644,17 @@ int fm_batch_prepare(fm_ctx* ctx, fm_batch* b) {
     const int kb = bits_for(ctx->rows - 1);
     const uint32_t* col = b->dev.col.as<uint32_t>();
     const uint2* ent = b->dev.ent.as<uint2>();
-    b->msd = ctx->cfg.sort_algo == FM_SORT_LSD ? MsdPlan{} : msd_plan(N, kb);
-    SortWork& w = ctx->work.sort;
     if (b->split) {
-      // the fused step's batch, which the step splits into the multi view (skeys / sents, {their count,
-      // the number of singleton runs} in split_n): the level-1 buckets and their sizes (fkeys / fents,
-      // btot; nothing for a one-bucket batch) or, with the LSD passes, the whole sorted view
+      // the fused step's batch: the whole sorted view (fkeys / fents), which the step splits into the
+      // multi view (skeys / sents, {their count, the number of singleton runs} in split_n)
       b->split_n.ensure(2 * sizeof(int64_t));
-      if (!b->msd.ok || b->msd.hb > 0) {
-        b->fkeys.ensure_slack(sizeof(uint32_t) * N);
-        b->fents.ensure_slack(sizeof(uint2) * N);
-      }
-      if (b->msd.ok && b->msd.hb > 0) {
-        b->btot.ensure(sizeof(uint32_t) * kMaxBuckets);
-        radix_partition_pairs64(w, col, ent, N, b->msd.sh, b->msd.hb, ctx->side, b->fkeys.as<uint32_t>(),
-                                b->fents.as<uint2>(), b->btot.as<uint32_t>());
-      } else if (!b->msd.ok) {
-        radix_sort_pairs64(w, col, ent, N, kb, ctx->side, &sk, &sv, b->fkeys.as<uint32_t>(), b->fents.as<uint2>());
-      }
-    } else if (b->msd.ok) {
-      // the whole sorted view by the two levels, both here (side stream)
-      if (b->msd.hb > 0) {
-        w.ensure(N);
-        radix_partition_pairs64(w, col, ent, N, b->msd.sh, b->msd.hb, ctx->side, w.keys_a.as<uint32_t>(),
-                                w.vals_a.as<uint2>(), w.digit_tot.as<uint32_t>());
-        msd_sort_full(b->msd, w.keys_a.as<uint32_t>(), w.vals_a.as<uint2>(), w.keys_b.as<uint32_t>(),
-                      w.vals_b.as<uint2>(), w.digit_tot.as<uint32_t>(), N, b->skeys.as<uint32_t>(),
-                      b->sents.as<uint2>(), ctx->side);
-      } else {
-        msd_sort_full(b->msd, col, ent, nullptr, nullptr, nullptr, N, b->skeys.as<uint32_t>(), b->sents.as<uint2>(),
-                      ctx->side);
-      }
+      b->fkeys.ensure_slack(sizeof(uint32_t) * N);
+      b->fents.ensure_slack(sizeof(uint2) * N);
+      radix_sort_pairs64(ctx->work.sort, col, ent, N, kb, ctx->side, &sk, &sv, b->fkeys.as<uint32_t>(),
+                         b->fents.as<uint2>());
     } else {
-      radix_sort_pairs64(w, col, ent, N, kb, ctx->side, &sk, &sv, b->skeys.as<uint32_t>(), b->sents.as<uint2>());
+      radix_sort_pairs64(ctx->work.sort, col, ent, N, kb, ctx->side, &sk, &sv, b->skeys.as<uint32_t>(),
+                         b->sents.as<uint2>());
     }
     ctx->prof_end("sort", es, ctx->side);
     FM_HIP_CHECK(hipEventRecord(b->ready, ctx->side));

@@ -108,10 +108,6 @@ struct fm_batch {
   DevBuf fkeys, fents;
   DevBuf split_n;
   bool split = false;
-  // the two-level grouping (fm_msd.hip): msd.ok when it applies; fkeys / fents then hold the level-1
-  // buckets (hb > 0) and btot their sizes, which the fused step's split groups and splits
-  MsdPlan msd;
-  DevBuf btot;
   hipEvent_t ready = nullptr;     // recorded on the side stream after the prepared sort
   hipEvent_t last_use = nullptr;  // recorded on the main stream after a step read the batch
   bool prepared = false;
@@ -156,7 +152,6 @@ struct fm_batch {
     fkeys.release();
     fents.release();
     split_n.release();
-    btot.release();
     up.release();
     dev.row_ptr.release();
     dev.col.release();
@@ -211,7 +206,6 @@ struct fm_ctx {
   // the split of an LSD-sorted view into its multi runs: only the single-table fused step runs it, at
   // the step (main stream, step_impl), so one stream uses the workspace
   SplitWork split_work;
-  MsdWork msd_main;  // the two-level split at the step (main stream)
   Pinned side_pinned;  // route counts (device -> host)
   // replicated step state (fm_repl_*)
   DevBuf repl_cnt;            // touched-row counts per apply block (uint32)
@@ -253,6 +247,17 @@ struct fm_ctx {
     FM_HIP_CHECK(hipEventRecord(e1, s));
     pending.push_back({name, {e0, e1}});
     if (pending.size() > 4096) resolve_profile();
+  }
+  // host time of a phase (the multi-GPU driver's enqueue, fm_group.hip), beside the device phases
+  void prof_host(const char* name, double ms) {
+    if (!prof) return;
+    auto it = prof_acc.find(name);
+    if (it == prof_acc.end()) {
+      prof_order.push_back(name);
+      it = prof_acc.emplace(name, ProfEntry{}).first;
+    }
+    it->second.ms += ms;
+    it->second.n += 1;
   }
   void resolve_profile() {
     if (pending.empty()) return;
@@ -320,7 +325,7 @@ struct fm_ctx {
                       &route_sort.keys_a, &route_sort.keys_b, &route_sort.vals_a, &route_sort.vals_b,
                       &route_sort.counts, &route_sort.digit_tot,
                       &sh_okey, &sh_mask, &sh_tcnt, &sh_tot, &sh_pay, &sh_skey, &sh_ent2, &repl_cnt,
-                      &split_work.cnt, &split_work.off, &msd_main.keys, &msd_main.vals, &msd_main.status};
+                      &split_work.cnt, &split_work.off};
     for (auto* b : bufs) b->release();
     if (own_stream && stream) (void)hipStreamDestroy(stream);
   }

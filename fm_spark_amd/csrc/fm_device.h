@@ -68,26 +68,6 @@ __device__ __forceinline__ void store_hdr(const TableView& T, int64_t slot, cons
   for (int i = 0; i < pad; i += 4) *reinterpret_cast<float4*>(r + 4 + i) = make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
-// Singleton rows.  fm_batch_prepare groups the batch by slot (side stream); at the start of the step
-// the split (fm_msd.hip k_msd_buckets, or k_split_* after the LSD passes; main stream) keeps the runs
-// of two or more entries (the only ones that need a per-feature reduction) and marks every such row
-// in the row header's t field, the word that otherwise only says present (t >= 0) or absent (t = -1):
-//   present, multi at epoch E : t = kTagPresent + (E & kTagMask)   (>= 2^30; normal t < 2^30)
-//   absent,  multi at epoch E : t = -2 - (E & kTagMask)            (<= -2: still "absent")
-// so every reader that asks t >= 0 is unchanged, and the fused forward, which loads the header of
-// every entry's row anyway, knows which rows it may update in place: nobody else reads them in
-// this step.  The segmented update then walks the multi runs only and rewrites their headers
-// (t = E + 1), clearing the tags.
-constexpr int32_t kTagPresent = 1 << 30;
-constexpr int32_t kTagMask = (1 << 29) - 1;
-__device__ __forceinline__ int32_t multi_tag(int32_t epoch, bool present) {
-  return present ? kTagPresent + (epoch & kTagMask) : -2 - (epoch & kTagMask);
-}
-__device__ __forceinline__ bool is_multi(int32_t t, int32_t epoch) {
-  const int32_t e = epoch & kTagMask;
-  return t >= kTagPresent ? t - kTagPresent == e : (t <= -2 && -2 - t == e);
-}
-
 // Row update of SGD.scala:150-181, fp64:
 //   vec' = S_lambda(vec - sum * (eta / m));  strength' = S_lambda(strength - (sum / m) * eta)
 __device__ __forceinline__ float upd_v(float v, double g, const StepParams& p) {

@@ -28,6 +28,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <chrono>
 #include <numeric>
 
 #include "fm_context.h"
@@ -574,6 +575,19 @@ void fill_out(Group& g, fm_ctx* ctx, int64_t e, int64_t global_rows, fm_step_out
   out->n_rows = global_rows;
 }
 
+// Host time of a phase of the one-thread driver (enqueue only: nothing here waits for the GPU
+// unless the phase says so), recorded with rank 0's profile as "host_<phase>" when profiling is on.
+struct HostClock {
+  fm_ctx* m;
+  const char* name;
+  std::chrono::steady_clock::time_point t0;
+  HostClock(Group& g, const char* n)
+      : m(g.ranks[0].m->prof ? g.ranks[0].m : nullptr), name(n), t0(std::chrono::steady_clock::now()) {}
+  ~HostClock() {
+    if (m) m->prof_host(name, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+  }
+};
+
 // Chunks of the owners' partial pass whose exchange overlaps the next chunk's compute
 // (fm_config.xchg_chunks, default 4; 1 = one pass, then one all-to-all).  Only with R > 1.
 int xchg_chunks(const Group& g) {
@@ -657,29 +671,42 @@ int step_sharded(fm_ctx* ctx, Group& g, GroupBatch& gb, int32_t t, double step_s
   const bool self = g.R == 1;
   for (int l = 0; self && l < L; ++l) FM_REQUIRE(Pin[l] == Pout[l], "one-rank job: pair counts differ");
   const int C = xchg_chunks(g);
-  if (C > 1) {
-    forward_exchange_chunked(g, gb, kp, C, Pin, Pout);
-  } else {
-    // owners: partial sums per received pair
-    for (int l = 0; l < L; ++l)
-      mcheck(fm_shard_owner_forward(g.ranks[l].m, gb.parts[l].b, g.ranks[l].partials.p), "fm_shard_owner_forward");
-    // back to the requesters (owner l -> requester p: the pair_in[l][p] pairs it got from p)
-    if (!self) a2a_pairs(g, kp, parts, Pin, part_in, Pout, pin, pout);
+  {
+    HostClock hc(g, "host_forward_xchg");
+    if (C > 1) {
+      forward_exchange_chunked(g, gb, kp, C, Pin, Pout);
+    } else {
+      // owners: partial sums per received pair
+      for (int l = 0; l < L; ++l)
+        mcheck(fm_shard_owner_forward(g.ranks[l].m, gb.parts[l].b, g.ranks[l].partials.p), "fm_shard_owner_forward");
+      // back to the requesters (owner l -> requester p: the pair_in[l][p] pairs it got from p)
+      if (!self) a2a_pairs(g, kp, parts, Pin, part_in, Pout, pin, pout);
+    }
   }
-  for (int l = 0; l < L; ++l) {
-    Rank& r = g.ranks[l];
-    mcheck(fm_shard_combine(r.m, gb.parts[l].b, (self ? r.partials : r.part_in).p, r.s_send.p), "fm_shard_combine");
+  {
+    HostClock hc(g, "host_combine");
+    for (int l = 0; l < L; ++l) {
+      Rank& r = g.ranks[l];
+      mcheck(fm_shard_combine(r.m, gb.parts[l].b, (self ? r.partials : r.part_in).p, r.s_send.p), "fm_shard_combine");
+    }
   }
   // S rows to the owners
-  if (!self) a2a_pairs(g, kp, s_send, Pout, s_recv, Pin, pout, pin);
-  for (int l = 0; l < L; ++l) {
-    Rank& r = g.ranks[l];
-    mcheck(fm_shard_owner_update(r.m, gb.parts[l].b, (self ? r.s_send : r.s_recv).p, t, step_size, reg_param,
-                                 gb.global_rows),
-           "fm_shard_owner_update");
+  if (!self) {
+    HostClock hc(g, "host_s_xchg");
+    a2a_pairs(g, kp, s_send, Pout, s_recv, Pin, pout, pin);
+  }
+  {
+    HostClock hc(g, "host_update");
+    for (int l = 0; l < L; ++l) {
+      Rank& r = g.ranks[l];
+      mcheck(fm_shard_owner_update(r.m, gb.parts[l].b, (self ? r.s_send : r.s_recv).p, t, step_size, reg_param,
+                                   gb.global_rows),
+             "fm_shard_owner_update");
+    }
   }
   gb.prefetched = false;
   const int64_t e = g.ranks[0].m->epoch - 1;
+  HostClock hc(g, "host_stats");
   reduce_stats(g, e);
   ctx->epoch = (int32_t)(e + 1);
   fill_out(g, ctx, e, gb.global_rows, out);
@@ -690,11 +717,15 @@ int step_replicated(fm_ctx* ctx, Group& g, GroupBatch& gb, int32_t t, double ste
                     fm_step_out* out) {
   const int L = g.L;
   const int64_t n = g.ranks[0].m->rows * (int64_t)(ctx->kp + 4);
-  for (int l = 0; l < L; ++l) {
-    Rank& r = g.ranks[l];
-    ensure_on(r.device, r.grad, sizeof(float) * n);
-    mcheck(fm_repl_grad(r.m, gb.parts[l].b, r.grad.p), "fm_repl_grad");
+  {
+    HostClock hc(g, "host_grad");
+    for (int l = 0; l < L; ++l) {
+      Rank& r = g.ranks[l];
+      ensure_on(r.device, r.grad, sizeof(float) * n);
+      mcheck(fm_repl_grad(r.m, gb.parts[l].b, r.grad.p), "fm_repl_grad");
+    }
   }
+  HostClock hc_ar(g, "host_allreduce_apply");
   if (g.rccl) {
     FM_RCCL_CHECK(ncclGroupStart());
     for (auto& r : g.ranks) {
@@ -902,9 +933,12 @@ int group_batch_create(fm_ctx* ctx, const fm_csr* csr, fm_batch** out) {
 
 namespace {
 
-// Local rank l's full copy of the group batch dg (its parts copied from every rank's device): the
-// source of that rank's fm_batch_from_rows gathers.  Made once per dataset.
-fm_batch* dataset_replica(Group& g, GroupBatch& dg, int l) {
+// Local rank l's full copy of the group batch dg (its parts copied from every rank's device), rows in
+// the dataset's order: the source of that rank's fm_batch_from_rows gathers.  A dataset made by
+// fm_batch_create_splits holds split s of the dataset as every rank's share of it (rank 0's rows of
+// split s, then rank 1's, ...: group_batch_create_splits), so its copy is assembled split by split,
+// rank by rank, and row i of the copy is row i of the caller's CSR.  Made once per dataset.
+fm_batch* dataset_replica(Group& g, GroupBatch& dg, int l, const std::vector<int64_t>& split_rows) {
   if ((int)dg.full.size() != g.L) dg.full.assign(g.L, nullptr);
   if (dg.full[l]) return dg.full[l];
   Rank& r = g.ranks[l];
@@ -912,15 +946,35 @@ fm_batch* dataset_replica(Group& g, GroupBatch& dg, int l) {
   f->owner = r.m;
   f->device = r.device;
   const int64_t B = dg.rows, N = dg.nnz;
+  // the dataset's rows as segments {part, first row, end row} of the parts, in dataset order
+  struct Seg {
+    int part;
+    int64_t a, z;
+  };
+  std::vector<Seg> segs;
+  const int ns = split_rows.empty() ? 1 : (int)split_rows.size() - 1;
+  for (int sp = 0; sp < ns; ++sp) {
+    for (int q = 0; q < (int)dg.parts.size(); ++q) {
+      const GPart& pq = dg.parts[q];
+      FM_REQUIRE((int64_t)pq.b->host_rp.size() == pq.rows + 1, "group dataset part without its host row_ptr");
+      if (split_rows.empty()) {
+        segs.push_back({q, 0, pq.rows});
+      } else {
+        const std::vector<int64_t>& msr = pq.b->split_rows;
+        FM_REQUIRE((int)msr.size() == ns + 1, "group dataset part without its split boundaries");
+        segs.push_back({q, msr[sp], msr[sp + 1]});
+      }
+    }
+  }
   std::vector<int64_t> rp;
   rp.reserve(B + 1);
   int64_t off = 0, mx = -1;
-  for (const GPart& q : dg.parts) {
-    FM_REQUIRE((int64_t)q.b->host_rp.size() == q.rows + 1, "group dataset part without its host row_ptr");
-    for (int64_t i = 0; i < q.rows; ++i) rp.push_back(off + q.b->host_rp[i]);
-    off += q.nnz;
-    mx = std::max(mx, q.b->max_id);
+  for (const Seg& sg : segs) {
+    const std::vector<int64_t>& hrp = dg.parts[sg.part].b->host_rp;
+    for (int64_t i = sg.a; i < sg.z; ++i) rp.push_back(off + hrp[i] - hrp[sg.a]);
+    off += hrp[sg.z] - hrp[sg.a];
   }
+  for (const GPart& q : dg.parts) mx = std::max(mx, q.b->max_id);
   rp.push_back(off);
   FM_REQUIRE(off == N && (int64_t)rp.size() == B + 1, "group dataset parts do not add up");
   on(r, [&] {
@@ -933,16 +987,20 @@ fm_batch* dataset_replica(Group& g, GroupBatch& dg, int l) {
     f->dev.label.ensure(sizeof(double) * std::max<int64_t>(B, 4) + 16);
     FM_HIP_CHECK(hipMemcpy(f->dev.row_ptr.p, rp.data(), sizeof(int64_t) * (B + 1), hipMemcpyHostToDevice));
     int64_t e = 0, row = 0;
-    for (const GPart& q : dg.parts) {
-      if (q.nnz > 0) {
-        FM_HIP_CHECK(hipMemcpyPeer(f->dev.col.as<uint32_t>() + e, r.device, q.b->dev.col.p, q.device, sizeof(uint32_t) * q.nnz));
-        FM_HIP_CHECK(hipMemcpyPeer(f->dev.xs.as<float>() + e, r.device, q.b->dev.xs.p, q.device, sizeof(float) * q.nnz));
+    for (const Seg& sg : segs) {
+      const GPart& q = dg.parts[sg.part];
+      const int64_t e0 = q.b->host_rp[sg.a], ne = q.b->host_rp[sg.z] - e0, nr = sg.z - sg.a;
+      if (ne > 0) {
+        FM_HIP_CHECK(hipMemcpyPeer(f->dev.col.as<uint32_t>() + e, r.device, q.b->dev.col.as<uint32_t>() + e0, q.device,
+                                   sizeof(uint32_t) * ne));
+        FM_HIP_CHECK(hipMemcpyPeer(f->dev.xs.as<float>() + e, r.device, q.b->dev.xs.as<float>() + e0, q.device,
+                                   sizeof(float) * ne));
       }
-      if (q.rows > 0)
-        FM_HIP_CHECK(hipMemcpyPeer(f->dev.label.as<double>() + row, r.device, q.b->dev.label.p, q.device,
-                                   sizeof(double) * q.rows));
-      e += q.nnz;
-      row += q.rows;
+      if (nr > 0)
+        FM_HIP_CHECK(hipMemcpyPeer(f->dev.label.as<double>() + row, r.device, q.b->dev.label.as<double>() + sg.a,
+                                   q.device, sizeof(double) * nr));
+      e += ne;
+      row += nr;
     }
   });
   f->host_rp.swap(rp);
@@ -963,7 +1021,8 @@ int group_batch_from_rows(fm_ctx* ctx, const fm_batch* data, const int64_t* rows
     fresh.reset(new_group_batch(ctx));
     b = fresh.get();
   }
-  FM_REQUIRE(b->owner == ctx && b->grp && b != data, "out must be a batch of this context other than data");
+  FM_REQUIRE(b->owner == ctx && b->grp && b != data && b->split_rows.empty(),
+             "out must be a batch of this context other than data");
   GroupBatch& gb = *b->grp;
   drop_route(g, gb);  // a routed plan of the old contents is dropped before its buffers are reused
   // a former dataset refilled as a selection: its per-rank full copies describe the old contents
@@ -979,7 +1038,7 @@ int group_batch_from_rows(fm_ctx* ctx, const fm_batch* data, const int64_t* rows
     Rank& r = g.ranks[l];
     GPart& p = gb.parts[l];
     const int64_t r0 = n * l / g.L, r1 = n * (l + 1) / g.L;  // the split's rows by rows, as upload_parts
-    fm_batch* src = dataset_replica(g, dg, l);
+    fm_batch* src = dataset_replica(g, dg, l, data->split_rows);
     mcheck(fm_batch_from_rows(r.m, src, rows + r0, r1 - r0, &p.b), "fm_batch_from_rows");
     p.device = r.device;
     p.rows = r1 - r0;
@@ -1119,8 +1178,12 @@ int group_batch_prepare(fm_ctx* ctx, fm_batch* b) {
   if (g.sharded()) {
     // phase 2 of the batch prepared before this one (its routes ran beside the steps enqueued
     // since), then phase 1 of this one: the host waits only for route work an iteration old
-    if (g.pending && g.pending != &gb) finish_routes(g, *g.pending);
+    if (g.pending && g.pending != &gb) {
+      HostClock hc(g, "host_prepare_finish");  // waits for route counts an iteration old
+      finish_routes(g, *g.pending);
+    }
     if (!gb.prefetched && !gb.routed) {
+      HostClock hc(g, "host_prepare_route");
       launch_routes(g, gb);
       gb.g = &g;
       g.pending = &gb;
@@ -1177,11 +1240,13 @@ int group_init_from_batch(fm_ctx* ctx, fm_batch* b, int64_t* n_present) {
   GroupBatch& gb = gbatch(ctx, b);
   if (g.sharded() && !b->split_rows.empty()) {
     // a dataset laid out by splits: its entries' sample indices count from their split's first row,
-    // so the owner routing runs split by split (the draw depends on (seed, id, factor) only)
+    // so the owner routing runs split by split (the draw depends on (seed, id, factor) only).  Every
+    // split is routed, also one with no entries in this process: the routing's exchanges are
+    // collectives of the whole job, and another process may hold entries of that split
     fm_batch* v = nullptr;
     for (int32_t s = 0; s + 1 < (int32_t)b->split_rows.size(); ++s) {
       group_batch_split_view(ctx, b, s, &v);
-      if (v->grp->nnz > 0) group_init_from_batch(ctx, v, nullptr);
+      group_init_from_batch(ctx, v, nullptr);
     }
     if (v) {
       group_sync(ctx);

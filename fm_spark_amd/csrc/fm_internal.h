@@ -109,38 +109,6 @@ void radix_sort_pairs64(SortWork& w, const uint32_t* keys_in, const uint2* vals_
 // final_keys / final_vals.
 void radix_sort_pairs64_bits(SortWork& w, const uint32_t* keys_in, const uint2* vals_in, int64_t n, int lo_bit,
                              int hi_bit, hipStream_t st, uint32_t* final_keys, uint2* final_vals);
-// One stable radix pass on key bits [shift, shift + rb) (6 <= rb <= 10): the pairs grouped by that
-// digit into keys_out / vals_out, the digit totals -> tot[2^rb] (device).
-void radix_partition_pairs64(SortWork& w, const uint32_t* keys_in, const uint2* vals_in, int64_t n, int shift, int rb,
-                             hipStream_t st, uint32_t* keys_out, uint2* vals_out, uint32_t* tot);
-
-// ------------------------------------------------- two-level grouping (fm_msd.hip)
-// level 1: one radix pass on the slot's top hb bits (radix_partition_pairs64) -> 2^hb buckets;
-// level 2: each bucket sorted by its low sh bits in LDS (32K entries; larger buckets through global
-// memory), then written back (msd_sort_full) or split into its runs of two or more (msd_split).
-// hb == 0: one bucket (n <= 32K, key_bits <= 17), no level-1 pass.  ok == false: the LSD passes.
-constexpr int kMaxBuckets = 1024;
-struct MsdPlan {
-  bool ok = false;
-  int hb = 0, sh = 0, nbk = 0;
-};
-MsdPlan msd_plan(int64_t n, int key_bits);
-struct MsdWork {
-  DevBuf keys, vals;  // oversized buckets' second buffer (split mode)
-  DevBuf status;      // look-back words, ticket, error word
-  int64_t cap = 0;
-  void ensure(int64_t n, int nbk);
-};
-// the whole sorted view: keys / vals = the level-1 output (or the batch itself when hb == 0),
-// keys_b / vals_b a buffer of n pairs (oversized buckets), btot the bucket sizes
-void msd_sort_full(const MsdPlan& pl, const uint32_t* keys, const uint2* vals, uint32_t* keys_b, uint2* vals_b,
-                   const uint32_t* btot, int64_t n, uint32_t* okeys, uint2* ovals, hipStream_t st);
-// the fused step's split at the step: the entries of runs of two or more, in order, into mkeys / ments;
-// n_out[0] = their count, n_out[1] = the number of singleton runs (device); each multi run's row in
-// tag_T gets the epoch's multi tag.  keys / vals (level-1 output) may be overwritten.
-void msd_split(const MsdPlan& pl, const uint32_t* keys, const uint2* vals, const uint32_t* btot, int64_t n,
-               MsdWork& mw, uint32_t* mkeys, uint2* ments, int64_t* n_out, hipStream_t st, const TableView* tag_T,
-               int32_t epoch);
 
 // ---------------------------------------------------------------- step kernels
 // A device-resident mini-batch: the exploded (sampleId, featureId, featureValue) rows of

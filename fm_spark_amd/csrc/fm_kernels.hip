@@ -112,7 +112,25 @@ constexpr int kFwdGrid = 8192;
 // against 2, 4 slower under the 5-wave cap: profiles/r03_v7/ab)
 constexpr int kFuseU = 5;
 
-// Singleton rows and their multi tags: fm_device.h.
+// Singleton rows.  fm_batch_prepare sorts the batch (side stream); at the start of the step the
+// split (k_split_*, main stream) keeps the runs of two or more entries (the only ones that need a
+// per-feature reduction) and marks every such row in the row header's t field, the word that
+// otherwise only says present (t >= 0) or absent (t = -1):
+//   present, multi at epoch E : t = kTagPresent + (E & kTagMask)   (>= 2^30; normal t < 2^30)
+//   absent,  multi at epoch E : t = -2 - (E & kTagMask)            (<= -2: still "absent")
+// so every reader that asks t >= 0 is unchanged, and the fused forward, which loads the header of
+// every entry's row anyway, knows which rows it may update in place: nobody else reads them in
+// this step.  The segmented update then walks the multi runs only and rewrites their headers
+// (t = E + 1), clearing the tags.
+constexpr int32_t kTagPresent = 1 << 30;
+constexpr int32_t kTagMask = (1 << 29) - 1;
+__device__ __forceinline__ int32_t multi_tag(int32_t epoch, bool present) {
+  return present ? kTagPresent + (epoch & kTagMask) : -2 - (epoch & kTagMask);
+}
+__device__ __forceinline__ bool is_multi(int32_t t, int32_t epoch) {
+  const int32_t e = epoch & kTagMask;
+  return t >= kTagPresent ? t - kTagPresent == e : (t <= -2 && -2 - t == e);
+}
 
 // The fused forward at 4 waves per SIMD (107 VGPRs, no spill).  Round 3 measured 5 waves (96
 // VGPRs, a few spilled) faster: c3 step 0.98 against 1.03 ms (profiles/r03_v9/ab, r03_v10/ab);

@@ -9,7 +9,9 @@
 // scala 2.11 MurmurHash3.bytesHash.  None of that code is vendored in the reference; this
 // restates it (see oracle/spark_sampler.py for the line-by-line derivation).  The sampler is
 // host work by nature (a sequential RNG stream per partition and a lexicographic sort of
-// variable-length rows, run once per fit rather than once per step).
+// variable-length rows, run once per fit rather than once per step).  Partitions are independent
+// (each its own sort, its own XORShiftRandom(seed + p)), so they run on the library's host thread
+// pool: the same rows, splits and order as one thread, partition after partition.
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
@@ -19,6 +21,7 @@
 #include <vector>
 
 #include "../../include/fm_hip.h"
+#include "fm_hostpool.h"
 
 namespace fmhip {
 void set_error(const std::string& msg);
@@ -189,39 +192,51 @@ int fm_random_split(int32_t n_parts, const int64_t* part_ptr, const char* column
     std::vector<double> cum(n_weights + 1, 0.0);  // weights.map(_ / sum).scanLeft(0.0d)(_ + _)
     for (int32_t i = 0; i < n_weights; ++i) cum[i + 1] = cum[i] + weights[i] / total;
     const Rows R{label, vec_type, vec_size, vec_ptr, vec_idx, vec_val, extra};
-    std::vector<int64_t> ord;
-    for (int32_t p = 0; p < n_parts; ++p) {
-      const int64_t r0 = part_ptr[p], r1 = part_ptr[p + 1];
-      if (r1 < r0) { fmhip::set_error("part_ptr must be non-decreasing"); return FM_ERR_ARG; }
-      for (int64_t r = r0; r < r1; ++r) sample_id[r] = ((int64_t)p << 33) + (r - r0);
-      ord.resize(r1 - r0);
-      std::iota(ord.begin(), ord.end(), r0);
-      std::sort(ord.begin(), ord.end(), [&](int64_t a, int64_t b) {
-        for (char c : cols) {
-          int x = 0;
-          if (c == 'L') x = cmp_double(label[a], label[b]);
-          else if (c == 'F') x = cmp_vector(R, a, b);
-          else x = cmp_val<int64_t>(extra[a], extra[b]);
-          if (x) return x < 0;
-        }
-        return sample_id[a] < sample_id[b];
-      });
-      XorShift rng(seed + p);  // BernoulliCellSampler.setSeed(seed + index)
-      for (int64_t j = 0; j < (int64_t)ord.size(); ++j) {
-        const int64_t r = ord[j];
-        if (order) order[r0 + j] = r;
-        const double x = rng.next_double();
-        int32_t sp = -1;
-        for (int32_t i = 0; i < n_weights; ++i) {
-          const double lb = cum[i], ub = cum[i + 1];
-          if (ub - lb <= 0.0) continue;  // BernoulliCellSampler: empty range keeps nothing
-          if (x >= lb && x < ub) {
-            sp = i;
-            break;
+    for (int32_t p = 0; p < n_parts; ++p)
+      if (part_ptr[p + 1] < part_ptr[p]) { fmhip::set_error("part_ptr must be non-decreasing"); return FM_ERR_ARG; }
+    // one job per partition on the host pool (no exception leaves a worker: a failed partition is
+    // reported after the join)
+    std::atomic<bool> failed{false};
+    const std::function<void(int)> job = [&](int p) {
+      try {
+        const int64_t r0 = part_ptr[p], r1 = part_ptr[p + 1];
+        for (int64_t r = r0; r < r1; ++r) sample_id[r] = ((int64_t)p << 33) + (r - r0);
+        std::vector<int64_t> ord(r1 - r0);
+        std::iota(ord.begin(), ord.end(), r0);
+        std::sort(ord.begin(), ord.end(), [&](int64_t a, int64_t b) {
+          for (char c : cols) {
+            int x = 0;
+            if (c == 'L') x = cmp_double(label[a], label[b]);
+            else if (c == 'F') x = cmp_vector(R, a, b);
+            else x = cmp_val<int64_t>(extra[a], extra[b]);
+            if (x) return x < 0;
           }
+          return ((int64_t)p << 33) + (a - r0) < ((int64_t)p << 33) + (b - r0);  // monotonically_increasing_id
+        });
+        XorShift rng(seed + p);  // BernoulliCellSampler.setSeed(seed + index)
+        for (int64_t j = 0; j < (int64_t)ord.size(); ++j) {
+          const int64_t r = ord[j];
+          if (order) order[r0 + j] = r;
+          const double x = rng.next_double();
+          int32_t sp = -1;
+          for (int32_t i = 0; i < n_weights; ++i) {
+            const double lb = cum[i], ub = cum[i + 1];
+            if (ub - lb <= 0.0) continue;  // BernoulliCellSampler: empty range keeps nothing
+            if (x >= lb && x < ub) {
+              sp = i;
+              break;
+            }
+          }
+          split_of[r] = sp;
         }
-        split_of[r] = sp;
+      } catch (...) {
+        failed.store(true);
       }
+    };
+    fmhip::HostPool::get().run(n_parts, job);
+    if (failed.load()) {
+      fmhip::set_error("fm_random_split: host allocation failed");
+      return FM_ERR_OOM;
     }
     return FM_OK;
   } catch (const std::exception& e) {

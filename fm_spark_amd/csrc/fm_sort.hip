@@ -407,8 +407,7 @@ void SortWork::ensure(int64_t n) {
 
 template <class P, int RB>
 static void radix_pass_impl(const uint32_t* kin, const P* vin, uint32_t* ko, P* vo, int64_t n, int shift,
-                       SortWork& w, int64_t ntiles, hipStream_t st, uint32_t* tot = nullptr) {
-  uint32_t* dtot = tot ? tot : w.digit_tot.as<uint32_t>();
+                       SortWork& w, int64_t ntiles, hipStream_t st) {
   uint32_t* counts = w.counts.as<uint32_t>();
   uint32_t* csum = counts + (ntiles + 1) * (int64_t(1) << RB);
   const int64_t nchunks = (ntiles + kChunk - 1) / kChunk;
@@ -423,10 +422,12 @@ static void radix_pass_impl(const uint32_t* kin, const P* vin, uint32_t* ko, P* 
   constexpr int TB = (1 << RB) < 256 ? (1 << RB) : 256;
   hipLaunchKernelGGL(k_radix_chunk_scan<RB>, dim3((unsigned)(nchunks * ((1 << RB) / TB))), dim3(TB), 0, st, counts,
                      ntiles, csum);
-  hipLaunchKernelGGL(k_radix_chunk_top, dim3((1u << RB) / 32), dim3(256), 0, st, csum, nchunks, 1 << RB, dtot);
+  hipLaunchKernelGGL(k_radix_chunk_top, dim3((1u << RB) / 32), dim3(256), 0, st, csum, nchunks, 1 << RB,
+                     w.digit_tot.as<uint32_t>());
   auto scatter = vin ? k_radix_scatter<P, RB, false> : k_radix_scatter<P, RB, true>;
   hipLaunchKernelGGL(scatter, dim3((unsigned)blocks_for_tiles(ntiles)), dim3(kBlock), 0, st, kin, vin, ko, vo, n,
-                     shift, (const uint32_t*)counts, (const uint32_t*)csum, (const uint32_t*)dtot, ntiles);
+                     shift, (const uint32_t*)counts, (const uint32_t*)csum,
+                     (const uint32_t*)w.digit_tot.as<uint32_t>(), ntiles);
   FM_HIP_CHECK(hipGetLastError());
 }
 
@@ -505,21 +506,6 @@ void radix_sort_pairs64(SortWork& w, const uint32_t* keys_in, const uint2* vals_
                         hipStream_t st, const uint32_t** keys_out, const uint2** vals_out, uint32_t* final_keys,
                         uint2* final_vals) {
   radix_sort_impl<uint2>(w, keys_in, vals_in, n, key_bits, st, keys_out, vals_out, final_keys, final_vals);
-}
-
-void radix_partition_pairs64(SortWork& w, const uint32_t* keys_in, const uint2* vals_in, int64_t n, int shift, int rb,
-                             hipStream_t st, uint32_t* keys_out, uint2* vals_out, uint32_t* tot) {
-  FM_REQUIRE(n > 0 && n < (int64_t(1) << 32) - 1, "sort size out of range");
-  FM_REQUIRE(rb >= 6 && rb <= kMaxRB && shift >= 0 && shift + rb <= 32, "bad partition digit");
-  w.ensure(n);
-  const int64_t ntiles = (n + kTile - 1) / kTile;
-  switch (rb) {
-    case 6: radix_pass_impl<uint2, 6>(keys_in, vals_in, keys_out, vals_out, n, shift, w, ntiles, st, tot); break;
-    case 7: radix_pass_impl<uint2, 7>(keys_in, vals_in, keys_out, vals_out, n, shift, w, ntiles, st, tot); break;
-    case 8: radix_pass_impl<uint2, 8>(keys_in, vals_in, keys_out, vals_out, n, shift, w, ntiles, st, tot); break;
-    case 9: radix_pass_impl<uint2, 9>(keys_in, vals_in, keys_out, vals_out, n, shift, w, ntiles, st, tot); break;
-    default: radix_pass_impl<uint2, 10>(keys_in, vals_in, keys_out, vals_out, n, shift, w, ntiles, st, tot); break;
-  }
 }
 
 }  // namespace fmhip

@@ -91,8 +91,7 @@ class FMContext:
     ranks on ``devices`` (default device, device + 1, ...) of a job of ``n_procs`` processes and runs
     the multi-GPU step itself (include/fm_hip.h); ``transport`` "auto" | "rccl" | "copy".
     ``fuse`` None (the library's default: on) | True | False: the fused step for prepared batches
-    (fm_config.fuse_single); ``xchg_chunks``: 0 = default (fm_config.xchg_chunks); ``sort`` "default" (the
-    two-level grouping where it applies) | "lsd" (fm_config.sort_algo)."""
+    (fm_config.fuse_single); ``xchg_chunks``: 0 = default (fm_config.xchg_chunks)."""
 
     _PAR = {None: N.FM_PARALLEL_NONE, "none": N.FM_PARALLEL_NONE, "sharded": N.FM_PARALLEL_SHARDED,
             "replicated": N.FM_PARALLEL_REPLICATED}
@@ -101,8 +100,7 @@ class FMContext:
     def __init__(self, num_features: int, k: int, *, device: int = 0, seed: int = 0, init_sd: float = 0.01,
                  w0: float = 0.0, shard_index: int = 0, shard_count: int = 1, parallel: str | None = None,
                  n_gpus: int = 1, devices=None, transport: str = "auto", n_procs: int = 1, proc_rank: int = 0,
-                 comm_id: bytes | None = None, fuse: bool | None = None, xchg_chunks: int = 0,
-                 sort: str = "default"):
+                 comm_id: bytes | None = None, fuse: bool | None = None, xchg_chunks: int = 0):
         self._lib = N.load()
         cfg = N.fm_config(num_features=int(num_features), k=int(k), device=int(device), seed=int(seed) & (2**64 - 1),
                           init_sd=float(init_sd), w0=float(w0), shard_index=int(shard_index),
@@ -119,7 +117,6 @@ class FMContext:
         cfg.transport = self._TR[transport]
         cfg.fuse_single = N.FM_FUSE_DEFAULT if fuse is None else (N.FM_FUSE_ON if fuse else N.FM_FUSE_OFF)
         cfg.xchg_chunks = int(xchg_chunks)
-        cfg.sort_algo = {"default": N.FM_SORT_DEFAULT, "lsd": N.FM_SORT_LSD}[sort]
         cfg.n_procs = int(n_procs)
         cfg.proc_rank = int(proc_rank)
         if comm_id is not None:

@@ -50,8 +50,6 @@ extern "C" {
 #define FM_FUSE_DEFAULT 0 /* fm_config.fuse_single: the library's choice (tables above 256 MB) */
 #define FM_FUSE_ON 1
 #define FM_FUSE_OFF (-1)
-#define FM_SORT_DEFAULT 0 /* fm_config.sort_algo: the two-level grouping where it applies, else LSD */
-#define FM_SORT_LSD 1     /* the stable LSD radix passes only */
 
 typedef struct fm_ctx fm_ctx;
 typedef struct fm_batch fm_batch;
@@ -87,11 +85,6 @@ typedef struct fm_batch fm_batch;
  * xchg_chunks  : sharded step with R > 1: the owners' partial pass runs in this many chunks, each
  *                sent while the next is computed (0 = the default, 4; 1 = one pass then one
  *                all-to-all; at most 64).  Every process of a job must pass the same value.
- * sort_algo    : how a prepared batch is grouped by feature (the reference's groupBy featureId,
- *                SGD.scala:148-155).  FM_SORT_DEFAULT: one radix pass on the slot's top bits, then each
- *                bucket sorted in LDS (and, for the fused step, split into its runs of two or more at
- *                the step); FM_SORT_LSD: the LSD radix passes.  Both are stable sorts by slot, so the
- *                step's tables are bitwise the same either way.
  * Zero-initialise the struct: every field's 0 is its default. */
 typedef struct fm_config {
   int64_t num_features;
@@ -111,7 +104,6 @@ typedef struct fm_config {
   uint8_t comm_id[128];
   int32_t fuse_single;
   int32_t xchg_chunks;
-  int32_t sort_algo;
 } fm_config;
 
 /* One mini-batch in CSR form: the result of explode(udfVecToMap(features))
@@ -222,16 +214,18 @@ int fm_batch_from_rows(fm_ctx* ctx, const fm_batch* data, const int64_t* rows, i
  * hands it to fm_batch_prepare / fm_step_batch with no copy and no gather (fm_batch_from_rows stays
  * for row lists that are not laid out beforehand).  The dataset itself is not stepped or prepared
  * (FM_ERR_ARG; its entries count their sample from their split's first row); fm_init_from_batch
- * (createInitialModel over every row) and fm_batch_from_rows accept it.  A multi-GPU context cuts
- * every split by rows over its local ranks, as it cuts a host CSR.  Synchronous (returns when the
+ * (createInitialModel over every row) and fm_batch_from_rows (row i = row i of csr) accept it.  A
+ * multi-GPU context cuts every split by rows over its local ranks, as it cuts a host CSR.  Synchronous (returns when the
  * dataset is on the device). */
 int fm_batch_create_splits(fm_ctx* ctx, const fm_csr* csr, int32_t n_splits, const int64_t* split_rows,
                            fm_batch** out);
 /* Split `split` of a dataset made by fm_batch_create_splits as a mini-batch: its rows, entries and
  * labels where they lie in data (borrowed -- data must outlive the view and every step queued on
- * it).  *out == NULL: a new batch; otherwise *out (a view, or a batch of this context that becomes
- * one) is re-pointed in place -- host-only, no device work, so a loop re-points the batch it has just
- * stepped while that step still runs (its next fm_batch_prepare waits for it). */
+ * it).  *out == NULL: a new batch; otherwise *out is re-pointed in place.  Re-pointing a view is
+ * host-only, no device work, so a loop re-points the batch it has just stepped while that step still
+ * runs (its next fm_batch_prepare waits for it).  The first conversion of a batch that owns device
+ * buffers (one made by fm_batch_create or fm_batch_from_rows) into a view blocks: it waits for the
+ * batch's queued work, then frees its buffers. */
 int fm_batch_split_view(fm_ctx* ctx, const fm_batch* data, int32_t split, fm_batch** out);
 /* 1 if a batch prepared by fm_batch_prepare on this context takes the fused step (fm_config.fuse_single
  * and the library's rule: a single-table context, k <= 16, table above 256 MB unless FM_FUSE_ON;

@@ -314,6 +314,50 @@ def test_split_dataset_rules(gpu):
 
 
 @pytest.mark.parametrize("mode", ["sharded", "replicated"])
+def test_from_rows_of_a_split_dataset_on_a_multi_gpu_context(gpu, mode):
+    """fm_batch_from_rows over a split dataset on a 3-rank context (COPY): rank l holds its share of
+    every split, so its copy of the dataset is assembled split by split, rank by rank -- row i of the
+    copy is row i of the CSR the dataset was made from.  Row lists over that CSR step bitwise as the
+    host CSR of the same rows; a split dataset is refused as the batch to refill."""
+    from fm_spark_amd._native import FMError
+    from fm_spark_amd.engine import FMContext
+
+    F, k, R = 3000, 8, 3
+    data, ids, w, V = make_problem(1216, 2000, F, k, 9, hot=4)
+    rng = np.random.default_rng(14)
+    lay, split_rows = _layout(data, [rng.permutation(2000)[:700], np.arange(0), rng.permutation(2000)[:1100],
+                                     np.arange(1990, 2000)])
+    n_lay = len(lay.row_ptr) - 1
+    sels = [rng.permutation(n_lay)[:800], np.sort(rng.choice(n_lay, 1000)), np.arange(n_lay)[::-1]]
+
+    def run(use_rows):
+        ctx = FMContext(F, k, parallel=mode, n_gpus=R, devices=[0] * R, transport="copy")
+        ctx.load_tables(ids, w, V)
+        d = ctx.batch_splits(to_host(lay), split_rows)
+        if use_rows:
+            with pytest.raises(FMError, match="other than data"):
+                ctx.batch_from_rows(d, [0, 1], into=ctx.batch_splits(to_host(lay), split_rows))
+        into, out = None, []
+        for t, s in enumerate(sels, start=1):
+            if use_rows:
+                into = ctx.batch_from_rows(d, s, into=into)
+                b = into
+            else:
+                b = ctx.batch(to_host(_select(lay, s)))
+            b.prepare()
+            o = ctx.step_batch(b, t, 0.3, 1e-3)
+            out.append((o.loss_sum, o.n_rows, o.n_loss_rows, o.n_unique))
+        tab = ctx.export_tables()
+        ctx.close()
+        return out, tab
+
+    a, b = run(True), run(False)
+    assert a[0] == b[0]
+    for x, y in zip(a[1], b[1]):
+        assert np.array_equal(x, y)
+
+
+@pytest.mark.parametrize("mode", ["sharded", "replicated"])
 def test_split_views_on_a_multi_gpu_context(gpu, mode):
     """fm_batch_create_splits on a 3-rank context (COPY transport on this GPU): every rank holds its
     contiguous share of every split; each split view steps bitwise as the host CSR of the same rows;

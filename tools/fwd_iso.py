@@ -23,11 +23,10 @@ ap.add_argument("--k", type=int, default=16)
 ap.add_argument("--rows", type=int, default=262144)
 ap.add_argument("--steps", type=int, default=10)
 ap.add_argument("--variants", default="on,off")
-ap.add_argument("--sort", default="default")
 a = ap.parse_args()
 hb = [synthetic_batch(a.rows, a.features, batch_index=i) for i in range(2)]
 for v in a.variants.split(","):
-    ctx = FMContext(a.features, a.k, seed=1, init_sd=0.01, fuse=(v == "on"), sort=a.sort)
+    ctx = FMContext(a.features, a.k, seed=1, init_sd=0.01, fuse=(v == "on"))
     ctx.init_random_range(0, a.features)
     dbs = [ctx.batch(CSRHost(b.row_ptr, b.col, b.val, b.label)) for b in hb]
     for t in range(1, 3):
@@ -42,5 +41,5 @@ for v in a.variants.split(","):
         ctx.step_batch(dbs[t % 2], t, 0.1, 1e-6, sync=True)
     prof = ctx.profile_read()
     ctx.profile_enable(False)
-    print(json.dumps({"fuse": v, "sort": a.sort, "phases_ms": {k: ms / n for k, (ms, n) in prof.items()}}), flush=True)
+    print(json.dumps({"fuse": v, "phases_ms": {k: ms / n for k, (ms, n) in prof.items()}}), flush=True)
     ctx.close()
