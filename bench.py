@@ -398,6 +398,25 @@ class PlanError(SystemExit):
     something other than what was asked (never a silent downgrade to fewer GPUs)."""
 
 
+NNZ_PER_ROW = 39  # the synthetic Criteo-shaped rows (fm_spark_amd/data.py N_FIELDS)
+
+
+def auto_parallel(F, k, B, z, R):
+    """The layout whose per-rank exchange is smaller at R ranks ("c2 at N = 8"): the
+    replicated step all-reduces a dense F x (kp + 4) fp32 buffer (a ring moves 2 (R - 1) / R of it per
+    rank), the sharded step sends every (sample, owner) pair's partial sums and S row, kp + 2 fp32
+    each way (a sample's z ids meet R (1 - (1 - 1/R)^z) owners on average; (R - 1) / R of them
+    remote).  c2 (1M x k = 8, 64K rows) at R = 8: 84 MB against 42 MB per rank: sharded; a 100K-row
+    table: 8.4 MB against 42 MB: replicated."""
+    if R <= 1:
+        return "sharded"
+    kp = (k + 3) // 4 * 4
+    dense = 2.0 * (R - 1) / R * F * (kp + 4) * 4
+    owners = R * (1.0 - (1.0 - 1.0 / R) ** z)
+    pairs = 2.0 * B * owners * (kp + 2) * 4 * (R - 1) / R
+    return "replicated" if dense < pairs else "sharded"
+
+
 def plan_run(args, env, n_visible):
     """How this invocation runs, from the arguments, the launcher's environment and the number of
     visible GPUs (torch.cuda.device_count(), which does not initialise the GPU):
@@ -410,11 +429,13 @@ def plan_run(args, env, n_visible):
                one-GPU group context of an N-rank job (fm_config.n_procs = N)
 
     parallel: "sharded" (rows owned by id % R) or "replicated" (every rank the whole table,
-    gradient all-reduce); "auto" = replicated for c2 (the small-table config), else sharded."""
+    gradient all-reduce); "auto" = auto_parallel's choice for the config at N ranks."""
     world = int(env.get("WORLD_SIZE", "1"))
     rank = int(env.get("RANK", "0"))
     local_rank = int(env.get("LOCAL_RANK", "0"))
-    par = args.parallel if args.parallel != "auto" else ("replicated" if args.config == "c2" else "sharded")
+    n_ranks = max(world, args.gpus, args.copy_ranks, 1)
+    F, k, B = CONFIGS[args.config][:3]
+    par = args.parallel if args.parallel != "auto" else auto_parallel(F, k, B, NNZ_PER_ROW, n_ranks)
     if args.gpus < 1:
         raise PlanError("--gpus must be >= 1")
     if world > 1:

@@ -30,6 +30,11 @@
 #include <cstring>
 #include <chrono>
 #include <numeric>
+#include <thread>
+#include <mutex>
+#include <functional>
+#include <exception>
+#include <condition_variable>
 
 #include "fm_context.h"
 #include "fm_plan.h"
@@ -62,6 +67,34 @@ __global__ void k_slots_to_ids(const uint32_t* __restrict__ slot, int64_t n, uin
 __global__ void k_add_f32(float* __restrict__ dst, const float* __restrict__ src, int64_t n) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     dst[i] += src[i];
+}
+
+// COPY transport with every rank on one device: an all-to-all's blocks copied by one kernel launch
+// (blockIdx.y = block) instead of one hipMemcpyAsync per (source, destination, segment) -- 128 host
+// calls per all-to-all at R = 8, the COPY driver's host time (profiles/r06_host)
+struct CopyDesc {
+  const char* src;
+  char* dst;
+  uint64_t bytes;
+};
+constexpr int kMaxCopyDesc = 128;  // 3 KB of kernel arguments
+struct CopyList {
+  int n;
+  CopyDesc d[kMaxCopyDesc];
+};
+
+__global__ void k_copy_list(CopyList cl) {
+  const CopyDesc d = cl.d[blockIdx.y];
+  const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, nth = (uint64_t)gridDim.x * blockDim.x;
+  if ((((uintptr_t)d.src | (uintptr_t)d.dst | d.bytes) & 15u) == 0) {
+    const uint4* s = reinterpret_cast<const uint4*>(d.src);
+    uint4* t = reinterpret_cast<uint4*>(d.dst);
+    for (uint64_t i = tid; i < d.bytes / 16; i += nth) t[i] = s[i];
+  } else {  // element sizes are multiples of 4 bytes
+    const uint32_t* s = reinterpret_cast<const uint32_t*>(d.src);
+    uint32_t* t = reinterpret_cast<uint32_t*>(d.dst);
+    for (uint64_t i = tid; i < d.bytes / 4; i += nth) t[i] = s[i];
+  }
 }
 
 inline unsigned grid_of(int64_t n) {
@@ -126,6 +159,89 @@ struct GroupBatch {
   ~GroupBatch();
 };
 
+// Host workers of a multi-rank context: one thread per local rank beyond the first (the calling
+// thread takes rank 0).  each(f) runs f(l) for every local rank at once and returns when all have
+// returned; an exception thrown for any rank is rethrown afterwards (the lowest rank's).  The
+// per-rank phases of an iteration (route, owner preparation, owner passes, combine, update) are
+// enqueued this way: one thread enqueueing R ranks' kernels one after another costs R times one
+// rank's host time per phase.  The C-ABI's contract is unchanged -- one caller thread at a time per
+// context (its mutex); the workers only act inside one of that caller's calls, each on its own
+// rank's member context, streams and communicators.
+class RankWorkers {
+ public:
+  void start(int L) {
+    for (int l = 1; l < L; ++l) threads_.emplace_back([this, l] { loop(l); });
+  }
+  void each(int L, const std::function<void(int)>& f) {
+    if (threads_.empty() || L <= 1) {
+      for (int l = 0; l < L; ++l) f(l);
+      return;
+    }
+    std::vector<std::exception_ptr> err(L);
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      job_ = &f;
+      err_ = &err;
+      pending_ = L - 1;
+      ++gen_;
+    }
+    cv_.notify_all();
+    try {
+      f(0);
+    } catch (...) {
+      err[0] = std::current_exception();
+    }
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      done_cv_.wait(lk, [&] { return pending_ == 0; });
+      job_ = nullptr;
+      err_ = nullptr;
+    }
+    for (auto& e : err)
+      if (e) std::rethrow_exception(e);
+  }
+  ~RankWorkers() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : threads_) t.join();
+  }
+
+ private:
+  void loop(int l) {
+    uint64_t seen = 0;
+    for (;;) {
+      const std::function<void(int)>* f;
+      std::vector<std::exception_ptr>* err;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+        if (stop_) return;
+        seen = gen_;
+        f = job_;
+        err = err_;
+      }
+      try {
+        (*f)(l);
+      } catch (...) {
+        (*err)[l] = std::current_exception();
+      }
+      std::lock_guard<std::mutex> lk(mu_);
+      if (--pending_ == 0) done_cv_.notify_all();
+    }
+  }
+  std::vector<std::thread> threads_;
+  std::mutex mu_;
+  std::condition_variable cv_, done_cv_;
+  const std::function<void(int)>* job_ = nullptr;
+  std::vector<std::exception_ptr>* err_ = nullptr;
+  int pending_ = 0;
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+};
+
 struct Group {
   int mode = FM_PARALLEL_SHARDED;
   GroupBatch* pending = nullptr;  // the batch whose sharded prepare waits for its phase 2
@@ -135,7 +251,10 @@ struct Group {
   std::vector<Rank> ranks;
   std::unique_ptr<fm_batch> host_b[2];  // fm_step / fm_predict uploads, used in turn
   int hnext = 0;
+  RankWorkers workers;  // per-rank host workers (L > 1)
   bool sharded() const { return mode == FM_PARALLEL_SHARDED; }
+  // f(l) for every local rank, in parallel on the rank workers
+  void each(const std::function<void(int)>& f) { workers.each(L, f); }
   ~Group() {
     if (pending) pending->g = nullptr;
     for (auto& h : host_b) h.reset();
@@ -271,6 +390,43 @@ void a2a_plan(Group& g, int lane, const std::vector<A2ASeg>& segs, const A2APlan
     FM_RCCL_CHECK(ncclGroupEnd());
     return;
   }
+  bool one_device = true;
+  for (const Rank& r : g.ranks) one_device = one_device && r.device == g.ranks[0].device;
+  if (one_device) {
+    // rank 0's stream waits for every rank's, copies every block in one launch, every rank waits for it
+    Rank& r0 = g.ranks[0];
+    FM_HIP_CHECK(hipSetDevice(r0.device));
+    for (int l = 1; l < g.L; ++l) {
+      FM_HIP_CHECK(hipEventRecord(g.ranks[l].event(lane), g.ranks[l].stream(lane)));
+      FM_HIP_CHECK(hipStreamWaitEvent(r0.stream(lane), g.ranks[l].event(lane), 0));
+    }
+    CopyList cl;
+    cl.n = 0;
+    uint64_t most = 0;
+    auto flush = [&] {
+      if (!cl.n) return;
+      const unsigned gx = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(1024, (most / 16 + 255) / 256));
+      hipLaunchKernelGGL(k_copy_list, dim3(gx, (unsigned)cl.n), dim3(256), 0, r0.stream(lane), cl);
+      FM_HIP_CHECK(hipGetLastError());
+      cl.n = 0;
+      most = 0;
+    };
+    for (const A2ASeg& s : segs)
+      for (int l = 0; l < g.L; ++l)    // destination
+        for (int q = 0; q < g.L; ++q) {  // source (one process: global rank = local rank)
+          FM_REQUIRE(pl.sc[q][l] == pl.rc[l][q], "a2a: send and receive counts differ");
+          const size_t bytes = (size_t)pl.rc[l][q] * s.esize;
+          if (!bytes) continue;
+          cl.d[cl.n++] = CopyDesc{s.send[q] + (size_t)pl.so[q][l] * s.esize, s.recv[l] + (size_t)pl.ro[l][q] * s.esize,
+                                  (uint64_t)bytes};
+          most = std::max<uint64_t>(most, bytes);
+          if (cl.n == kMaxCopyDesc) flush();
+        }
+    flush();
+    FM_HIP_CHECK(hipEventRecord(r0.event(lane), r0.stream(lane)));
+    for (int l = 1; l < g.L; ++l) FM_HIP_CHECK(hipStreamWaitEvent(g.ranks[l].stream(lane), r0.event(lane), 0));
+    return;
+  }
   barrier(g, lane);
   for (const A2ASeg& s : segs) {
     for (int l = 0; l < g.L; ++l) {  // destination
@@ -338,6 +494,19 @@ std::vector<int64_t> allgather(Group& g, const std::vector<std::vector<int64_t>>
   std::memcpy(all.data(), r0.xg_pin.p, br);
   return all;
 }
+
+// Host time of a phase of the one-thread driver (enqueue only: nothing here waits for the GPU
+// unless the phase says so), recorded with rank 0's profile as "host_<phase>" when profiling is on.
+struct HostClock {
+  fm_ctx* m;
+  const char* name;
+  std::chrono::steady_clock::time_point t0;
+  HostClock(Group& g, const char* n)
+      : m(g.ranks[0].m->prof ? g.ranks[0].m : nullptr), name(n), t0(std::chrono::steady_clock::now()) {}
+  ~HostClock() {
+    if (m) m->prof_host(name, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+  }
+};
 
 void drop_route(Group& g, GroupBatch& gb);
 
@@ -408,13 +577,13 @@ void sync_group_batch_view(fm_batch* b) {  // fm_batch_rows / fm_batch_nnz of th
 void launch_routes(Group& g, GroupBatch& gb) {
   const int R = g.R, L = g.L;
   const size_t row = sizeof(unsigned long long) * 2 * R;
-  for (int l = 0; l < L; ++l) {
+  g.each([&](int l) {
     Rank& r = g.ranks[l];
     GPart& p = gb.parts[l];
     ensure_on(r.device, p.send_slot, sizeof(uint32_t) * p.nnz);
     ensure_on(r.device, p.send_ent, sizeof(uint2) * p.nnz);
     on(r, [&] { shard_route_launch(r.m, p.b, p.send_slot.p, p.send_ent.p, r.m->side); });
-  }
+  });
   gb.cnt_pin.ensure(row * R);
   if ((int)gb.ev_cnt.size() != L) {
     gb.ev_cnt.assign(L, nullptr);
@@ -465,20 +634,23 @@ void drop_route(Group& g, GroupBatch& gb) {
 // and every owner's pair table and slot order.
 void finish_routes(Group& g, GroupBatch& gb) {
   const int R = g.R, L = g.L;
-  for (int l = 0; l < L; ++l) {
-    FM_HIP_CHECK(hipSetDevice(g.ranks[l].device));
-    FM_HIP_CHECK(hipEventSynchronize(gb.ev_cnt[l]));
+  {
+    HostClock hc(g, "host_prepare_wait");  // the host waiting for the route counts (GPU time, not host work)
+    for (int l = 0; l < L; ++l) {
+      FM_HIP_CHECK(hipSetDevice(g.ranks[l].device));
+      FM_HIP_CHECK(hipEventSynchronize(gb.ev_cnt[l]));
+    }
   }
   if (g.pending == &gb) g.pending = nullptr;
   gb.routed = false;
   const unsigned long long* rc = reinterpret_cast<const unsigned long long*>(gb.cnt_pin.p);  // [source][pairs | entries]
-  std::vector<int64_t> counts(2 * R);
   std::vector<const char*> ss(L), se(L);
   std::vector<char*> rs(L), re(L);
   std::vector<const int64_t*> out(L), in(L);
-  for (int l = 0; l < L; ++l) {
+  g.each([&](int l) {
     Rank& r = g.ranks[l];
     GPart& p = gb.parts[l];
+    std::vector<int64_t> counts(2 * R);
     on(r, [&] { shard_route_finish(r.m, p.b, rc + (size_t)r.global * 2 * R, counts.data()); });
     plan::RouteCounts c = plan::route_counts(rc, R, r.global);
     p.ent_out = std::move(c.ent_out);
@@ -498,15 +670,15 @@ void finish_routes(Group& g, GroupBatch& gb) {
     re[l] = p.recv_ent.as<char>();
     out[l] = p.ent_out.data();
     in[l] = p.ent_in.data();
-  }
+  });
   if (R > 1) a2a_multi(g, true, {A2ASeg{ss, rs, sizeof(uint32_t)}, A2ASeg{se, re, sizeof(uint2)}}, out, in);
-  for (int l = 0; l < L; ++l) {
+  g.each([&](int l) {
     Rank& r = g.ranks[l];
     GPart& p = gb.parts[l];
     const int64_t n_in = std::accumulate(p.ent_in.begin(), p.ent_in.end(), int64_t(0));
     mcheck(fm_shard_owner_prepare(r.m, p.b, p.in_slot, p.in_ent, n_in, p.ent_in.data(), p.pair_in.data()),
            "fm_shard_owner_prepare");
-  }
+  });
   gb.prefetched = true;
 }
 
@@ -575,18 +747,6 @@ void fill_out(Group& g, fm_ctx* ctx, int64_t e, int64_t global_rows, fm_step_out
   out->n_rows = global_rows;
 }
 
-// Host time of a phase of the one-thread driver (enqueue only: nothing here waits for the GPU
-// unless the phase says so), recorded with rank 0's profile as "host_<phase>" when profiling is on.
-struct HostClock {
-  fm_ctx* m;
-  const char* name;
-  std::chrono::steady_clock::time_point t0;
-  HostClock(Group& g, const char* n)
-      : m(g.ranks[0].m->prof ? g.ranks[0].m : nullptr), name(n), t0(std::chrono::steady_clock::now()) {}
-  ~HostClock() {
-    if (m) m->prof_host(name, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
-  }
-};
 
 // Chunks of the owners' partial pass whose exchange overlaps the next chunk's compute
 // (fm_config.xchg_chunks, default 4; 1 = one pass, then one all-to-all).  Only with R > 1.
@@ -622,15 +782,15 @@ void forward_exchange_chunked(Group& g, GroupBatch& gb, int kp, int C, const std
   }
   for (int c = 0; c < C; ++c) {
     A2APlan pl;
-    for (int l = 0; l < L; ++l) {
+    for (int l = 0; l < L; ++l) pl.add(plan::chunk(gb.parts[l].pair_in.data(), gb.parts[l].pair_out.data(), R, c, C));
+    g.each([&](int l) {
       Rank& r = g.ranks[l];
       on(r, [&] {
         shard_owner_partials(r.m, gb.parts[l].b, r.partials.p, nullptr, c, C);
         FM_HIP_CHECK(hipEventRecord(r.ev_fwd, r.m->stream));
         FM_HIP_CHECK(hipStreamWaitEvent(r.xstream, r.ev_fwd, 0));
       });
-      pl.add(plan::chunk(gb.parts[l].pair_in.data(), gb.parts[l].pair_out.data(), R, c, C));
-    }
+    });
     a2a_plan(g, kLaneXchg, {A2ASeg{sv, rv, sizeof(float) * kp}, A2ASeg{sc, rc, sizeof(float) * 2}}, pl);
   }
   for (auto& r : g.ranks) {  // the combine reads what the exchange stream received
@@ -677,18 +837,19 @@ int step_sharded(fm_ctx* ctx, Group& g, GroupBatch& gb, int32_t t, double step_s
       forward_exchange_chunked(g, gb, kp, C, Pin, Pout);
     } else {
       // owners: partial sums per received pair
-      for (int l = 0; l < L; ++l)
+      g.each([&](int l) {
         mcheck(fm_shard_owner_forward(g.ranks[l].m, gb.parts[l].b, g.ranks[l].partials.p), "fm_shard_owner_forward");
+      });
       // back to the requesters (owner l -> requester p: the pair_in[l][p] pairs it got from p)
       if (!self) a2a_pairs(g, kp, parts, Pin, part_in, Pout, pin, pout);
     }
   }
   {
     HostClock hc(g, "host_combine");
-    for (int l = 0; l < L; ++l) {
+    g.each([&](int l) {
       Rank& r = g.ranks[l];
       mcheck(fm_shard_combine(r.m, gb.parts[l].b, (self ? r.partials : r.part_in).p, r.s_send.p), "fm_shard_combine");
-    }
+    });
   }
   // S rows to the owners
   if (!self) {
@@ -697,12 +858,12 @@ int step_sharded(fm_ctx* ctx, Group& g, GroupBatch& gb, int32_t t, double step_s
   }
   {
     HostClock hc(g, "host_update");
-    for (int l = 0; l < L; ++l) {
+    g.each([&](int l) {
       Rank& r = g.ranks[l];
       mcheck(fm_shard_owner_update(r.m, gb.parts[l].b, (self ? r.s_send : r.s_recv).p, t, step_size, reg_param,
                                    gb.global_rows),
              "fm_shard_owner_update");
-    }
+    });
   }
   gb.prefetched = false;
   const int64_t e = g.ranks[0].m->epoch - 1;
@@ -719,11 +880,11 @@ int step_replicated(fm_ctx* ctx, Group& g, GroupBatch& gb, int32_t t, double ste
   const int64_t n = g.ranks[0].m->rows * (int64_t)(ctx->kp + 4);
   {
     HostClock hc(g, "host_grad");
-    for (int l = 0; l < L; ++l) {
+    g.each([&](int l) {
       Rank& r = g.ranks[l];
       ensure_on(r.device, r.grad, sizeof(float) * n);
       mcheck(fm_repl_grad(r.m, gb.parts[l].b, r.grad.p), "fm_repl_grad");
-    }
+    });
   }
   HostClock hc_ar(g, "host_allreduce_apply");
   if (g.rccl) {
@@ -749,8 +910,9 @@ int step_replicated(fm_ctx* ctx, Group& g, GroupBatch& gb, int32_t t, double ste
       FM_HIP_CHECK(hipMemcpyAsync(g.ranks[l].grad.p, r0.grad.p, sizeof(float) * n, hipMemcpyDefault, r0.m->stream));
     barrier(g, false);
   }
-  for (int l = 0; l < L; ++l)
+  g.each([&](int l) {
     mcheck(fm_repl_apply(g.ranks[l].m, g.ranks[l].grad.p, t, step_size, reg_param, gb.global_rows), "fm_repl_apply");
+  });
   const int64_t e = g.ranks[0].m->epoch - 1;
   reduce_stats(g, e);
   ctx->epoch = (int32_t)(e + 1);
@@ -916,6 +1078,7 @@ int group_create(const fm_config* cfg, fm_ctx** out) {
       FM_RCCL_CHECK(ncclGroupEnd());
     }
   }
+  g.workers.start(L);
   *out = c.release();
   return FM_OK;
 }

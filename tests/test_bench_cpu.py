@@ -11,7 +11,7 @@ import bench
 
 
 def _args(**kw):
-    base = dict(gpus=1, config="c3", parallel="auto", force_sharded=False, trainer="lib")
+    base = dict(gpus=1, config="c3", parallel="auto", force_sharded=False, trainer="lib", copy_ranks=0)
     base.update(kw)
     return argparse.Namespace(**base)
 
@@ -33,10 +33,24 @@ def test_one_process_drives_n_gpus():
     pl = bench.plan_run(_args(gpus=8), {}, 8)
     assert pl["mode"] == "group" and pl["world"] == 8 and pl["n_local"] == 8
     assert pl["devices"] == list(range(8)) and pl["parallel"] == "sharded"
-    pl = bench.plan_run(_args(gpus=2, config="c2"), {}, 8)
-    assert pl["parallel"] == "replicated"  # c2: the replicated-table config
-    pl = bench.plan_run(_args(gpus=2, parallel="sharded", config="c2"), {}, 2)
-    assert pl["parallel"] == "sharded"
+    pl = bench.plan_run(_args(gpus=8, config="c2"), {}, 8)
+    assert pl["parallel"] == "sharded"  # c2 at R = 8: the pairs move less than the dense all-reduce
+    pl = bench.plan_run(_args(gpus=2, parallel="replicated", config="c2"), {}, 2)
+    assert pl["parallel"] == "replicated"
+
+
+def test_auto_layout_follows_the_exchange_projection():
+    """per rank, the dense all-reduce (2 (R-1)/R F (kp+4) 4 B) against the pairs'
+    partial sums and S rows (2 B R(1-(1-1/R)^z) (kp+2) 4 (R-1)/R B)."""
+    assert bench.auto_parallel(1_000_000, 8, 65536, 39, 8) == "sharded"     # c2: 84 MB against 36 MB
+    assert bench.auto_parallel(100_000, 8, 65536, 39, 8) == "replicated"    # 8.4 MB against 36 MB
+    assert bench.auto_parallel(100_000_000, 16, 262144, 39, 8) == "sharded"  # c3
+    assert bench.auto_parallel(1_000_000, 8, 65536, 39, 1) == "sharded"
+
+
+def test_copy_ranks_run_on_one_gpu():
+    pl = bench.plan_run(_args(copy_ranks=8), {}, 1)
+    assert pl["mode"] == "group" and pl["world"] == 8 and pl["devices"] == [0] * 8
 
 
 def test_launcher_one_process_per_gpu():
