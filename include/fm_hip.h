@@ -313,7 +313,9 @@ int fm_read_libsvm(const char* path, int64_t cap_rows, int64_t cap_nnz, double* 
  * vec_ptr[n+1], vec_idx (sparse only; ignored for dense), vec_val.
  * Outputs: split_of[n] (-1 = in no split), sample_id[n] = (partition << 33) + row index
  * (monotonically_increasing_id, Model.scala:268-272), order[n] = row indices in sorted
- * (per-partition) order. */
+ * (per-partition) order.  Partitions are sorted and sampled in parallel on the library's host
+ * thread pool (each writes only its own rows; the result does not depend on the thread count);
+ * an allocation failure is FM_ERR_OOM. */
 int fm_random_split(int32_t n_parts, const int64_t* part_ptr, const char* column_order,
                     const double* label, const int8_t* vec_type, const int32_t* vec_size,
                     const int64_t* vec_ptr, const int32_t* vec_idx, const double* vec_val,
