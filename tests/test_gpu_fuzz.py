@@ -1,0 +1,85 @@
+"""GPU parity over seeded random problems: the step against the fp64 oracle on configurations
+drawn at random -- k from 1 to 40, 5 to 60000 features, 0 to 3000 rows of 1 to 50 entries (empty
+rows and explicit zeros included), with or without a hot feature, binary or regression labels,
+step sizes and L1 strengths across their ranges -- through each way the library runs a step: the
+host CSR (fm_step), a prepared device batch with the fused step on and off, and the three-rank
+sharded and replicated contexts (COPY transport on this GPU).  Tolerance: north_star's 1e-5
+relative, the counts exact; the absolute floor for values the L1 drives to (near) zero is 1e-8 on
+one table, and on the three-rank paths 4 fp32 ulps of the table's largest value: their wire
+carries each owner's partial sums (sharded) or each rank's gradient sums (replicated) in fp32
+(DESIGN.md §6), so a value left near zero by the L1 keeps a few ulps of the value it was shrunk
+from (case 39, sharded: 2.1e-8 at a value of 3.9e-5, the table's largest 0.68).  The cases are
+fixed by their seeds, so a failure reproduces."""
+
+import numpy as np
+import pytest
+
+from oracle import fm_ref as R
+from problems import make_problem
+from test_gpu_parity import ATOL, RTOL, to_host
+
+pytestmark = pytest.mark.gpu
+
+N_CASES = 40
+PATHS = ["host", "fused", "unfused", "sharded3", "replicated3"]
+
+
+def draw(seed):
+    rng = np.random.default_rng(seed)
+    k = int(rng.integers(1, 41))
+    F = int(np.exp(rng.uniform(np.log(5), np.log(60000))))
+    rows = int(rng.integers(0, 3001))
+    nnz = int(rng.integers(1, 51))
+    hot = int(rng.integers(0, F)) if rng.random() < 0.5 else None
+    labels = "binary" if rng.random() < 0.5 else "regression"
+    step = float(rng.uniform(0.05, 1.0))
+    reg = float(rng.choice([0.0, 1e-6, 1e-4, 1e-3]))
+    batches = [make_problem(seed * 10 + i, rows, F, k, nnz, hot=hot, labels=labels,
+                            empty_frac=float(rng.uniform(0, 0.3)))[0] for i in range(3)]
+    _, ids, w, V = make_problem(seed * 10 + 9, 1, F, k, 1)
+    return dict(k=k, F=F, rows=rows, nnz=nnz, hot=hot, labels=labels, step=step, reg=reg), batches, ids, w, V
+
+
+def run_path(path, cfg, batches, ids, w, V):
+    from fm_spark_amd.engine import FMContext
+
+    F, k = cfg["F"], cfg["k"]
+    if path in ("sharded3", "replicated3"):
+        ctx = FMContext(F, k, parallel=path[:-1], n_gpus=3, devices=[0] * 3, transport="copy")
+    else:
+        ctx = FMContext(F, k, fuse={"fused": True, "unfused": False}.get(path))
+    ctx.load_tables(ids, w, V)
+    outs = []
+    dbs = [ctx.batch(to_host(c)) for c in batches] if path != "host" else None
+    for t, c in enumerate(batches, start=1):
+        if path == "host":
+            o = ctx.step(to_host(c), t, cfg["step"], cfg["reg"])
+        else:
+            dbs[t - 1].prepare()
+            o = ctx.step_batch(dbs[t - 1], t, cfg["step"], cfg["reg"])
+        outs.append(o)
+    tabs = ctx.export_tables()
+    ctx.close()
+    return outs, tabs
+
+
+@pytest.mark.parametrize("case", range(N_CASES))
+def test_random_problems_every_path(gpu, case):
+    cfg, batches, ids, w, V = draw(2027 + case)
+    model = R.Model.empty(cfg["F"], cfg["k"])
+    model.load(ids, w, V)
+    ref = [R.sgd_step_fast(model, c, t, cfg["step"], cfg["reg"]) for t, c in enumerate(batches, start=1)]
+    pids = np.nonzero(model.present)[0]
+    ulp4 = 4 * 2.0 ** -24 * max(float(np.max(np.abs(model.V[pids]), initial=0.0)),
+                                float(np.max(np.abs(model.w[pids]), initial=0.0)))
+    for path in PATHS:
+        atol = ATOL if path in ("host", "fused", "unfused") else max(ATOL, ulp4)
+        outs, (gids, gw, gV) = run_path(path, cfg, batches, ids, w, V)
+        for o, r in zip(outs, ref):
+            assert o.executed == r.executed, (path, cfg)
+            if r.executed:
+                assert (o.n_rows, o.n_loss_rows, o.n_unique) == (r.n_rows, r.n_loss_rows, r.n_unique), (path, cfg)
+                assert o.loss_sum == pytest.approx(r.loss_sum, rel=RTOL, abs=1e-9), (path, cfg)
+        np.testing.assert_array_equal(gids, pids, err_msg=f"{path} {cfg}")
+        np.testing.assert_allclose(gw, model.w[pids], rtol=RTOL, atol=atol, err_msg=f"{path} {cfg}")
+        np.testing.assert_allclose(gV, model.V[pids], rtol=RTOL, atol=atol, err_msg=f"{path} {cfg}")
