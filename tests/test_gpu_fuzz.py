@@ -1,7 +1,8 @@
 """GPU parity over seeded random problems: the step against the fp64 oracle on configurations
 drawn at random -- k from 1 to 40, 5 to 60000 features, 0 to 3000 rows of 1 to 50 entries (empty
 rows and explicit zeros included), with or without a hot feature, binary or regression labels,
-step sizes and L1 strengths across their ranges -- through each way the library runs a step: the
+step sizes and L1 strengths across their ranges -- through each way the library runs a step (and
+then transform / predict on the trained model): the
 host CSR (fm_step), a prepared device batch with the fused step on and off, and the three-rank
 sharded and replicated contexts (COPY transport on this GPU).  Tolerance: north_star's 1e-5
 relative, the counts exact; the absolute floor for values the L1 drives to (near) zero is 1e-8 on
@@ -40,6 +41,23 @@ def draw(seed):
     return dict(k=k, F=F, rows=rows, nnz=nnz, hot=hot, labels=labels, step=step, reg=reg), batches, ids, w, V
 
 
+def score_terms(model, csr):
+    """Per row, the magnitude of the terms a score sums: |w x| over the entries, and per factor the
+    square of the |v x| sum and the v^2 x^2 sum (Model.scala:173-221)."""
+    n = csr.n_rows
+    row = np.repeat(np.arange(n), np.diff(csr.row_ptr))
+    ok = csr.col < len(model.w)
+    row, col, x = row[ok], csr.col[ok], csr.val[ok]
+    aw = np.zeros(n)
+    np.add.at(aw, row, np.abs(model.w[col] * x))
+    vx = np.abs(model.V[col] * x[:, None])
+    s1 = np.zeros((n, model.k))
+    np.add.at(s1, row, vx)
+    s2 = np.zeros(n)
+    np.add.at(s2, row, (vx * vx).sum(axis=1))
+    return aw + 0.5 * ((s1 * s1).sum(axis=1) + s2)
+
+
 def run_path(path, cfg, batches, ids, w, V):
     from fm_spark_amd.engine import FMContext
 
@@ -59,8 +77,9 @@ def run_path(path, cfg, batches, ids, w, V):
             o = ctx.step_batch(dbs[t - 1], t, cfg["step"], cfg["reg"])
         outs.append(o)
     tabs = ctx.export_tables()
+    pred = ctx.predict(to_host(batches[0]), -2.0, 3.0)  # transform of the first batch with the trained model
     ctx.close()
-    return outs, tabs
+    return outs, tabs, pred
 
 
 @pytest.mark.parametrize("case", range(N_CASES))
@@ -74,7 +93,7 @@ def test_random_problems_every_path(gpu, case):
                                 float(np.max(np.abs(model.w[pids]), initial=0.0)))
     for path in PATHS:
         atol = ATOL if path in ("host", "fused", "unfused") else max(ATOL, ulp4)
-        outs, (gids, gw, gV) = run_path(path, cfg, batches, ids, w, V)
+        outs, (gids, gw, gV), pred = run_path(path, cfg, batches, ids, w, V)
         for o, r in zip(outs, ref):
             assert o.executed == r.executed, (path, cfg)
             if r.executed:
@@ -83,3 +102,16 @@ def test_random_problems_every_path(gpu, case):
         np.testing.assert_array_equal(gids, pids, err_msg=f"{path} {cfg}")
         np.testing.assert_allclose(gw, model.w[pids], rtol=RTOL, atol=atol, err_msg=f"{path} {cfg}")
         np.testing.assert_allclose(gV, model.V[pids], rtol=RTOL, atol=atol, err_msg=f"{path} {cfg}")
+        # the transform's arithmetic against the oracle's on the tables this path trained (the tables
+        # themselves are checked above; a score near zero is a cancellation of terms that carry the
+        # tables' fp32 rounding, so the trained oracle model is not the reference for it)
+        trained = R.Model.empty(cfg["F"], cfg["k"])
+        trained.load(gids, gw, gV)
+        ref_pred = R.predict(trained, batches[0], -2.0, 3.0, num_features=cfg["F"])
+        if path in ("host", "fused", "unfused"):
+            np.testing.assert_allclose(pred, ref_pred, rtol=RTOL, atol=1e-7, err_msg=f"predict {path} {cfg}")
+        else:
+            # the three-rank transform sums each owner's fp32 partial sums: a score that cancels keeps
+            # a few fp32 ulps of the terms it cancels (8 ulps of their magnitude per row)
+            bound = RTOL * np.abs(ref_pred) + np.maximum(1e-7, 8 * 2.0 ** -24 * score_terms(trained, batches[0]))
+            assert np.all(np.abs(pred - ref_pred) <= bound), (path, cfg, float(np.max(np.abs(pred - ref_pred) - bound)))
