@@ -115,3 +115,31 @@ def test_random_problems_every_path(gpu, case):
             # a few fp32 ulps of the terms it cancels (8 ulps of their magnitude per row)
             bound = RTOL * np.abs(ref_pred) + np.maximum(1e-7, 8 * 2.0 ** -24 * score_terms(trained, batches[0]))
             assert np.all(np.abs(pred - ref_pred) <= bound), (path, cfg, float(np.max(np.abs(pred - ref_pred) - bound)))
+
+
+@pytest.mark.parametrize("case", range(10))
+def test_random_create_initial_model_every_path(gpu, case):
+    """createInitialModel over a random batch (SGD.scala:218-252): the rows present afterwards are
+    the batch's distinct ids, and the seeded draw is the same table on one GPU and on the
+    three-rank sharded and replicated contexts, bit for bit."""
+    from fm_spark_amd.engine import FMContext
+
+    cfg, batches, _, _, _ = draw(4051 + case)
+    F, k = cfg["F"], cfg["k"]
+    csr = batches[0]
+    tabs = []
+    for path in ("single", "sharded3", "replicated3"):
+        if path == "single":
+            ctx = FMContext(F, k, seed=77)
+        else:
+            ctx = FMContext(F, k, seed=77, parallel=path[:-1], n_gpus=3, devices=[0] * 3, transport="copy")
+        n = ctx.init_from_batch(ctx.batch(to_host(csr)))
+        tabs.append((n, ctx.export_tables()))
+        ctx.close()
+    distinct = np.unique(csr.col)
+    for n, (gids, gw, gV) in tabs:
+        assert n == len(distinct), cfg
+        np.testing.assert_array_equal(gids, distinct)
+    for n, t in tabs[1:]:
+        for x, y in zip(t, tabs[0][1]):
+            assert np.array_equal(x, y), cfg
