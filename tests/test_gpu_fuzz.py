@@ -143,3 +143,52 @@ def test_random_create_initial_model_every_path(gpu, case):
     for n, t in tabs[1:]:
         for x, y in zip(t, tabs[0][1]):
             assert np.array_equal(x, y), cfg
+
+
+@pytest.mark.parametrize("case", range(8))
+def test_random_resident_splits_every_path(gpu, case):
+    """fit()'s resident dataset on random data: laid out split by split (ragged, empty and
+    repeated-row splits), every split stepped through its in-place view and, on the same context, a
+    random row list gathered from the dataset by fm_batch_from_rows -- bitwise the steps on the host
+    CSRs of the same rows, on one GPU (fused and unfused) and on three sharded or replicated ranks."""
+    from fm_spark_amd.engine import FMContext
+    from test_gpu_resident_fit import _layout, _select
+
+    cfg, batches, ids, w, V = draw(6073 + case)
+    F, k = cfg["F"], cfg["k"]
+    data = batches[0]
+    n = data.n_rows
+    rng = np.random.default_rng(case)
+    sels = [rng.permutation(n)[: int(rng.integers(0, n + 1))] for _ in range(int(rng.integers(1, 5)))]
+    sels.append(np.sort(rng.choice(n, int(rng.integers(0, n + 1)), replace=True)) if n else np.arange(0))
+    lay, split_rows = _layout(data, sels)
+    picks = np.sort(rng.choice(max(n, 1), int(rng.integers(0, n + 1)), replace=True)) if n else np.arange(0)
+
+    def run(path, views):
+        kw = dict(fuse={"fused": True, "unfused": False}[path]) if path in ("fused", "unfused") else dict(
+            parallel=path[:-1], n_gpus=3, devices=[0] * 3, transport="copy")
+        ctx = FMContext(F, k, **kw)
+        ctx.load_tables(ids, w, V)
+        d = ctx.batch_splits(to_host(lay), split_rows) if views else None
+        plain = ctx.batch(to_host(data)) if views else None
+        out, into = [], None
+        for t, s in enumerate(sels, start=1):
+            b = ctx.split_view(d, t - 1, into=into) if views else ctx.batch(to_host(_select(lay, np.arange(split_rows[t - 1], split_rows[t]))))
+            into = b if views else None
+            b.prepare()
+            o = ctx.step_batch(b, t, cfg["step"], cfg["reg"])
+            out.append((o.executed, o.loss_sum, o.n_rows, o.n_loss_rows, o.n_unique))
+        t = len(sels) + 1
+        g = ctx.batch_from_rows(plain, picks) if views else ctx.batch(to_host(_select(data, picks)))
+        g.prepare()
+        o = ctx.step_batch(g, t, cfg["step"], cfg["reg"])
+        out.append((o.executed, o.loss_sum, o.n_rows, o.n_loss_rows, o.n_unique))
+        tab = ctx.export_tables()
+        ctx.close()
+        return out, tab
+
+    for path in ("fused", "unfused", "sharded3", "replicated3"):
+        a, b = run(path, True), run(path, False)
+        assert a[0] == b[0], (path, cfg)
+        for x, y in zip(a[1], b[1]):
+            assert np.array_equal(x, y), (path, cfg)
