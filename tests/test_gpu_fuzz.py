@@ -192,3 +192,35 @@ def test_random_resident_splits_every_path(gpu, case):
         assert a[0] == b[0], (path, cfg)
         for x, y in zip(a[1], b[1]):
             assert np.array_equal(x, y), (path, cfg)
+
+
+@pytest.mark.parametrize("case", range(10))
+def test_random_loss_grad_and_vector_sum(gpu, case):
+    """calcLossGrad (Model.scala:135-234) per entry on random problems against the oracle, and
+    VectorSum by key (FactorizationMachines.scala:45-81) on random keys and widths, bitwise the
+    oracle's sequential sums."""
+    from fm_spark_amd.engine import FMContext
+
+    cfg, batches, ids, w, V = draw(8089 + case)
+    F, k = cfg["F"], cfg["k"]
+    model = R.Model.empty(F, k)
+    model.load(ids, w, V)
+    ctx = FMContext(F, k)
+    ctx.load_tables(ids, w, V)
+    csr = batches[1]
+    if csr.nnz:
+        gp, gl, gdw, gdv = ctx.loss_grad(to_host(csr))
+        rp, rl, rdw, rdv = R.loss_grad(model, csr)
+        np.testing.assert_allclose(gp, rp, rtol=1e-6, atol=1e-9, err_msg=str(cfg))
+        np.testing.assert_allclose(gl, rl, rtol=1e-5, atol=1e-9, err_msg=str(cfg))
+        np.testing.assert_array_equal(gdw, rdw)
+        np.testing.assert_allclose(gdv, rdv, rtol=1e-5, atol=1e-9, err_msg=str(cfg))
+    rng = np.random.default_rng(case)
+    n, width = int(rng.integers(1, 50000)), int(rng.integers(1, 40))
+    keys = rng.integers(0, int(rng.integers(1, 5000)), n).astype(np.int32)
+    vecs = rng.normal(size=(n, width)) * 10.0 ** rng.uniform(-3, 3, size=(n, 1))
+    gk, gs = ctx.vector_sum_by_key(keys, vecs)
+    rk, rs = R.vector_sum_by_key(keys, vecs)
+    np.testing.assert_array_equal(gk, rk)
+    assert np.array_equal(gs, rs)
+    ctx.close()
