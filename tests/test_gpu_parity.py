@@ -452,3 +452,40 @@ def test_host_step_async_matches_sync(gpu):
     for x, y in zip(a, b):
         assert np.array_equal(x, y)
     assert np.array_equal(la, lb) and len(la) == len(csrs)
+
+
+def test_prepared_pipeline_at_c2_scale_bitwise(gpu):
+    """The bench's pipeline at c2's shape (1M features, k = 8, 64K rows of 39 entries, four batches
+    cycled, each prepared -- sorted on the side stream -- right after the step before it is enqueued,
+    no host synchronisation): bit for bit the steps whose sorts run inline.  A step that started its
+    segmented update before its batch's sort had finished would read a partly written view."""
+    from oracle.fm_ref import CSR
+    from fm_spark_amd.engine import FMContext
+
+    F, k, B, z, steps = 1_000_000, 8, 65_536, 39, 40
+    rng = np.random.default_rng(2028)
+    csrs = []
+    for _ in range(4):
+        col = np.minimum((F * rng.random((B, z)) ** 3).astype(np.int64), F - 1)
+        col.sort(axis=1)
+        val = np.where(rng.random((B, z)) < 0.6, 1.0, f32(rng.random((B, z))))
+        csrs.append(CSR(row_ptr=np.arange(0, B * z + 1, z, dtype=np.int64), col=col.ravel().astype(np.int32),
+                        val=val.ravel(), label=(rng.random(B) < 0.25).astype(np.float64)))
+    outs = []
+    for prep in (True, False):
+        ctx = FMContext(F, k, fuse=False, seed=5)
+        ctx.init_random_range(0, F)
+        dbs = [ctx.batch(to_host(c)) for c in csrs]
+        if prep:
+            dbs[0].prepare()
+        for i in range(steps):
+            ctx.step_batch(dbs[i % 4], i + 1, 0.1, 1e-6, sync=False)
+            if prep:
+                dbs[(i + 1) % 4].prepare()
+        ctx.sync()
+        outs.append((ctx.export_tables(), ctx.loss_history()))
+        ctx.close()
+    (a, la), (b, lb) = outs
+    assert np.array_equal(la, lb)
+    for x, y in zip(a, b):
+        assert np.array_equal(x, y)
